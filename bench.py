@@ -1,0 +1,235 @@
+"""Headline benchmark: device-resident Mpps of example/xdp-counter over 64-B
+packets (BASELINE.json metric, configs[1] at N=1; configs[3]'s per-GPU shard
+at N>1).  One step = one ebpf_exec_batch of the loaded xdp-counter bytecode
+over the whole resident batch (2^24 packets per GPU).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PKT = 64
+ALGO_BYTES_PER_PKT = 28  # 12 B MAC read + 12 B MAC write + 4 B verdict
+HBM_PEAK_GBS = 8000.0    # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log2n", type=int, default=24, help="packets per GPU = 2^log2n")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--unchecked", action="store_true", help="skip the global-window check")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        # control plane only (barrier, timing max, map-shard gather) over gloo;
+        # the data path has no collective.  torch is imported
+        # before libbpftime_amd so one HIP runtime is loaded.
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    import numpy as np
+
+    from bpftime_amd import gen, isa, programs
+    from bpftime_amd import vm as dev
+
+    if dev.lib().bpftime_amd_set_device(local_rank) != 0:
+        raise SystemExit(f"rank {rank}: cannot select GPU {local_rank}")
+
+    n = 1 << args.log2n
+    first = rank * n  # contiguous shard of the global packet stream (configs[3])
+    dev.reset_runtime()
+    ctl = dev.Map(isa.BPF_MAP_TYPE_ARRAY, 4, 4, 2, name="ctl_array")
+    bss = dev.Map(isa.BPF_MAP_TYPE_ARRAY, 4, 4096, 1, flags=isa.BPF_F_MMAPABLE, name=".bss")
+    code = programs.xdp_counter(ctl.fd, bss.fd)
+    vm = dev.VM()
+    vm.load(code)
+    info = vm.info()
+
+    pkts = dev.DeviceBuffer(n * PKT)
+    if dev.lib().bpftime_amd_gen_xdp(pkts.ptr, n, PKT, PKT, gen.SEED_CFG2, first, None) != 0:
+        raise SystemExit("generator failed")
+    verd = dev.DeviceBuffer(4 * n)
+    init_bss = bss.snapshot()
+    flags = dev.BATCH_UNCHECKED if args.unchecked else 0
+
+    def step():
+        vm.exec_batch(dev.CTX_XDP, pkts, n, PKT, fixed_len=PKT, verdicts=verd, flags=flags, first_unit=first)
+
+    for _ in range(args.warmup):
+        step()
+    dev.lib().bpftime_amd_sync()
+    if dist:
+        dist.barrier()
+    dev.lib().bpftime_amd_sync()
+    evs = [dev.Event() for _ in range(args.steps + 1)]
+    t0 = time.perf_counter()
+    evs[0].record()
+    for i in range(args.steps):
+        step()
+        evs[i + 1].record()
+    dev.lib().bpftime_amd_sync()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    wall = t1 - t0
+    kern_ms = [evs[i].elapsed_ms(evs[i + 1]) for i in range(args.steps)]
+    kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
+
+    # ---- parity of the timed run (size-independent properties) ----
+    total_runs = args.warmup + args.steps
+    v = verd.download(np.uint32)
+    ok_verdicts = bool((v == isa.XDP_TX).all())
+    cnt = np.frombuffer(bss.lookup(b"\0\0\0\0"), dtype=np.uint64)
+    ok_counter = int(cnt[0]) == total_runs * n and not cnt[1:].any()
+    sample = min(n, 1 << 16)
+    ref = gen.xdp_packets(sample, PKT, gen.SEED_CFG2, first)
+    got = pkts.download(count=sample * PKT).reshape(sample, PKT)
+    exp = ref.copy()
+    if total_runs % 2:
+        exp[:, :6], exp[:, 6:12] = ref[:, 6:12], ref[:, :6]
+    ok_bytes = bool((got == exp).all())
+
+    shard = bss.snapshot()
+    times = [wall]
+    shards = [shard]
+    oks = [ok_verdicts and ok_counter and ok_bytes]
+    if dist:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (wall, shard.tobytes(), oks[0]))
+        times = [g[0] for g in gathered]
+        shards = [np.frombuffer(g[1], dtype=np.uint8) for g in gathered]
+        oks = [g[2] for g in gathered]
+    if rank != 0:
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    # host merge of per-GPU map shards: final = init + sum(shard - init)
+    merged = init_bss.copy()
+    for s in shards:
+        dev.lib().bpftime_amd_merge_delta_u64(merged.ctypes.data, init_bss.ctypes.data, s.ctypes.data,
+                                              merged.nbytes)
+    merged_cnt = int(merged.view(np.uint64)[0])
+    parity = all(oks) and merged_cnt == world * total_runs * n
+
+    tmax = max(times)
+    value = world * n * args.steps / tmax / 1e6
+    achieved_gbs = ALGO_BYTES_PER_PKT * n / kern_avg_s / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            if pmc.get("packets") == n and pmc.get("program") == "xdp-counter":
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds)
+
+    out = {
+        "metric": "device-resident Mpps, 64B pkts, example/xdp-counter XDP prog",
+        "value": round(value, 3),
+        "unit": "Mpps",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(tmax / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (seeded splitmix64 64-B Eth frames, seed 0x5EED0002)",
+        "config": {
+            "workload": "example/xdp-counter (hand-assembled, SURVEY.md App. A) over 2^%d device-resident "
+                        "64-B packets per GPU, BPF_MAP_TYPE_ARRAY maps (BASELINE configs[1]; configs[3] shards "
+                        "at N>1)" % args.log2n,
+            "packets_per_gpu": n,
+            "pkt_bytes": PKT,
+            "parallelism": "dp%d (contiguous packet shards, host-merged map shards, no collective)" % world,
+            "interp": {"stack_bytes_per_lane": info["stack_size"], "fused_rmw": info["fused_rmw"],
+                       "checked": not args.unchecked},
+        },
+        "parity": {"verdicts_all_tx": ok_verdicts, "counter_exact": ok_counter, "mac_swap_sample": ok_bytes,
+                   "merged_counter": merged_cnt, "ok": parity},
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved_gbs, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved_gbs / HBM_PEAK_GBS, 5),
+            "traffic": traffic,
+            "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
+            "algo_bytes_per_pkt": ALGO_BYTES_PER_PKT,
+        },
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out))
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(budget_s):
+    """The oracle (restated reference CPU interpreter, -O2, 1 pinned thread)
+    over a bounded sample of the same workload."""
+    import numpy as np
+
+    from bpftime_amd import gen, isa, programs
+    from oracle import pyoracle as po
+
+    po.reset()
+    ctl = po.OracleMap(isa.BPF_MAP_TYPE_ARRAY, 4, 4, 2)
+    bss = po.OracleMap(isa.BPF_MAP_TYPE_ARRAY, 4, 4096, 1)
+    ovm = po.OracleVM()
+    ovm.load(programs.xdp_counter(ctl.fd, bss.fd))
+    sample_n = 1 << 22
+    pk = gen.xdp_packets(sample_n, PKT, gen.SEED_CFG2, 0)
+    secs, done = 0.0, 0
+    while secs < budget_s and done < 64 * sample_n:
+        secs += ovm.time_xdp(pk, PKT, pin_cpu=0)
+        done += sample_n
+    cnt = int(np.frombuffer(bss.lookup(b"\0\0\0\0"), dtype=np.uint64)[0])
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(done / secs / 1e6, 3),
+        "unit": "Mpps",
+        "cores": 1,
+        "kind": "port",
+        "sample": "%d passes x 2^22 64-B packets of the same stream (%.1f s, counter %s), cpu %s, pinned core 0"
+                  % (done // sample_n, secs, "ok" if cnt == done else "MISMATCH", cpu_model),
+    }
+
+
+if __name__ == "__main__":
+    main()

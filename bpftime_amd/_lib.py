@@ -1,0 +1,129 @@
+"""ctypes binding of libbpftime_amd.so (the C ABI in include/ebpf-vm.h and
+include/bpftime_amd.h).  The library is built in-tree by ``build()`` in
+__graft_entry__.py (bpftime_amd/csrc/Makefile) and MUST be present: there is
+no CPU fallback anywhere in the product path."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libbpftime_amd.so")
+
+u8p = C.POINTER(C.c_uint8)
+u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
+
+
+class BpfMapAttr(C.Structure):  # runtime/include/bpftime_shm.hpp:27-46
+    _fields_ = [("type", C.c_int), ("key_size", C.c_uint32), ("value_size", C.c_uint32),
+                ("max_ents", C.c_uint32), ("flags", C.c_uint64), ("ifindex", C.c_uint32),
+                ("btf_vmlinux_value_type_id", C.c_uint32), ("btf_id", C.c_uint32),
+                ("btf_key_type_id", C.c_uint32), ("btf_value_type_id", C.c_uint32),
+                ("map_extra", C.c_uint64), ("kernel_bpf_map_id", C.c_uint32),
+                ("gpu_thread_count", C.c_uint64)]
+
+
+class BpfLinkCreateArgs(C.Structure):  # bpftime_shm.hpp:250-301
+    _fields_ = [("prog_fd", C.c_uint32), ("target_fd", C.c_uint32), ("attach_type", C.c_uint32),
+                ("flags", C.c_uint32), ("attach_union", C.c_uint64 * 4)]
+
+
+class EbpfBatch(C.Structure):  # include/ebpf-vm.h struct ebpf_batch
+    _fields_ = [("ctx_kind", C.c_uint32), ("flags", C.c_uint32), ("count", C.c_uint64),
+                ("data", C.c_void_p), ("stride", C.c_uint64), ("lens", C.c_void_p),
+                ("fixed_len", C.c_uint32), ("ingress_ifindex", C.c_uint32),
+                ("rx_queue_index", C.c_uint32), ("head", C.c_uint32), ("verdicts", C.c_void_p),
+                ("rets", C.c_void_p), ("data_off_out", C.c_void_p), ("len_out", C.c_void_p),
+                ("first_unit", C.c_uint64), ("stream", C.c_void_p)]
+
+
+# (name, restype, argtypes) for every exported symbol of include/*.h
+SIGNATURES = [
+    # include/ebpf-vm.h
+    ("ebpf_create", C.c_void_p, [C.c_char_p]),
+    ("ebpf_destroy", None, [C.c_void_p]),
+    ("ebpf_get_vm_name", C.c_char_p, [C.c_void_p]),
+    ("ebpf_toggle_bounds_check", C.c_bool, [C.c_void_p, C.c_bool]),
+    ("ebpf_set_error_print", None, [C.c_void_p, C.c_void_p]),
+    ("ebpf_register", C.c_int, [C.c_void_p, C.c_uint, C.c_char_p, C.c_void_p]),
+    ("ebpf_load", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]),
+    ("ebpf_unload_code", None, [C.c_void_p]),
+    ("ebpf_exec", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, u64p]),
+    ("ebpf_compile", C.c_void_p, [C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("ebpf_set_unwind_function_index", C.c_int, [C.c_void_p, C.c_uint]),
+    ("ebpf_set_pointer_secret", C.c_int, [C.c_void_p, C.c_uint64]),
+    ("ebpf_set_lddw_helpers", None, [C.c_void_p] + [C.c_void_p] * 5),
+    ("ebpf_load_aot_object", C.c_void_p, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("ebpf_exec_batch", C.c_int, [C.c_void_p, C.POINTER(EbpfBatch)]),
+    ("ebpf_set_ctx_kind", C.c_int, [C.c_void_p, C.c_uint32]),
+    # include/bpftime_amd.h
+    ("bpftime_maps_create", C.c_int, [C.c_int, C.c_char_p, BpfMapAttr]),
+    ("bpftime_map_lookup_elem", C.c_void_p, [C.c_int, C.c_void_p]),
+    ("bpftime_map_update_elem", C.c_long, [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64]),
+    ("bpftime_map_delete_elem", C.c_long, [C.c_int, C.c_void_p]),
+    ("bpftime_map_get_next_key", C.c_int, [C.c_int, C.c_void_p, C.c_void_p]),
+    ("bpftime_map_value_size_from_syscall", C.c_uint32, [C.c_int]),
+    ("bpftime_is_map_fd", C.c_int, [C.c_int]),
+    ("bpftime_is_array_map", C.c_int, [C.c_int]),
+    ("bpftime_is_prog_fd", C.c_int, [C.c_int]),
+    ("bpftime_find_minimal_unused_fd", C.c_int, []),
+    ("bpftime_close", None, [C.c_int]),
+    ("bpftime_progs_create", C.c_int, [C.c_int, C.c_void_p, C.c_size_t, C.c_char_p, C.c_int]),
+    ("bpftime_link_create", C.c_int, [C.c_int, C.POINTER(BpfLinkCreateArgs)]),
+    ("bpftime_amd_map_ptr_by_fd", C.c_uint64, [C.c_uint32]),
+    ("bpftime_amd_map_val", C.c_uint64, [C.c_uint64]),
+    ("bpftime_amd_map_device_ptr", C.c_uint64, [C.c_int, u64p]),
+    ("bpftime_amd_map_snapshot", C.c_int, [C.c_int, C.c_void_p, C.c_uint64]),
+    ("bpftime_amd_map_restore", C.c_int, [C.c_int, C.c_void_p, C.c_uint64]),
+    ("bpftime_amd_map_geometry", C.c_int, [C.c_int, u64p, u32p, u32p, u32p, u32p]),
+    ("bpftime_amd_map_count", C.c_uint64, [C.c_int]),
+    ("bpftime_amd_set_ncpu", None, [C.c_uint32]),
+    ("bpftime_amd_get_ncpu", C.c_uint32, []),
+    ("bpftime_amd_reset", None, []),
+    ("bpftime_amd_xdp_links", C.c_int, [C.POINTER(C.c_int), C.POINTER(C.c_int), u32p, C.c_int]),
+    ("bpftime_amd_prog_instantiate", C.c_void_p, [C.c_int, C.POINTER(C.c_void_p)]),
+    ("bpftime_amd_register_default_helpers", C.c_int, [C.c_void_p]),
+    ("bpftime_amd_vm_info", C.c_int, [C.c_void_p, u32p, C.POINTER(C.c_int), u32p, u32p]),
+    ("bpftime_amd_set_step_limit", None, [C.c_void_p, C.c_uint64]),
+    ("bpftime_amd_merge_delta_u64", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
+    ("bpftime_amd_device_count", C.c_int, []),
+    ("bpftime_amd_set_device", C.c_int, [C.c_int]),
+    ("bpftime_amd_dev_alloc", C.c_void_p, [C.c_uint64]),
+    ("bpftime_amd_dev_free", None, [C.c_void_p]),
+    ("bpftime_amd_memcpy_htod", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    ("bpftime_amd_memcpy_dtoh", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    ("bpftime_amd_memset", C.c_int, [C.c_void_p, C.c_int, C.c_uint64]),
+    ("bpftime_amd_sync", C.c_int, []),
+    ("bpftime_amd_host_alloc", C.c_void_p, [C.c_uint64]),
+    ("bpftime_amd_host_free", None, [C.c_void_p]),
+    ("bpftime_amd_event_create", C.c_void_p, []),
+    ("bpftime_amd_event_destroy", None, [C.c_void_p]),
+    ("bpftime_amd_event_record", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("bpftime_amd_event_elapsed_ms", C.c_float, [C.c_void_p, C.c_void_p]),
+    ("bpftime_amd_last_error", C.c_char_p, []),
+    ("bpftime_amd_gen_xdp", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64,
+                                       C.c_uint64, C.c_void_p]),
+]
+
+# symbols outside include/*.h that the Python layer also uses
+EXTRA = [
+    ("bpftime_amd_vm_error", C.c_char_p, [C.c_void_p]),
+]
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load the product library; raise loudly if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback exists)")
+        l = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES + EXTRA:
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = l
+    return _lib

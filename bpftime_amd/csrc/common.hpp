@@ -1,0 +1,121 @@
+// bpftime_amd: data structures shared by the host loader/runtime and the
+// gfx950 interpreter kernel.  Everything here is plain-old-data so it can be
+// hipMemcpy'd and read with scalar loads on the device.
+#pragma once
+#include <stdint.h>
+
+namespace bpftime_amd {
+
+constexpr uint32_t kMaxInsts = 65536;   // vm/vm-core/include/ebpf-vm.h:33-35
+constexpr uint32_t kStackSize = 512;    // ebpf-vm.h:47-49
+constexpr uint32_t kMaxFds = 1024;      // device map table size
+constexpr uint32_t kBlock = 256;        // threads per workgroup (4 waves)
+constexpr uint32_t kLdsStackMax = 64;   // per-lane stack bytes kept in LDS
+
+// Internal (pre-decoded) opcodes.  The device switch dispatches on these; the
+// set is dense so the compiler's binary search over cases stays shallow.
+enum XOp : uint8_t {
+  X_BAD = 0,
+  // ALU, same result for 32/64 after masking with `mask` (see DInsn::aux)
+  X_ADD, X_SUB, X_MUL, X_OR, X_AND, X_XOR, X_MOV,
+  // 64-bit only forms
+  X_DIV64, X_MOD64, X_LSH64, X_RSH64, X_ARSH64, X_NEG64,
+  // 32-bit only forms
+  X_DIV32, X_MOD32, X_LSH32, X_RSH32, X_ARSH32, X_NEG32,
+  X_LE, X_BE,
+  // memory
+  X_LDX, X_ST, X_STX, X_ATOMIC, X_LDDW,
+  // fused "ldx r,[b+o]; add r,v; stx [b+o],r" with r dead afterwards
+  X_RMW_ADD,
+  // control
+  X_JA, X_JEQ, X_JGT, X_JGE, X_JSET, X_JNE, X_JSGT, X_JSGE, X_JLT, X_JLE, X_JSLT, X_JSLE,
+  X_CALL, X_EXIT,
+  X_NOP,  // second slot of lddw (never executed)
+  X_COUNT
+};
+
+// DInsn::aux bits
+constexpr uint8_t A_SRCREG = 0x01;  // second operand is a register
+constexpr uint8_t A_W32 = 0x02;     // 32-bit ALU / JMP32
+constexpr uint8_t A_SIZE_SHIFT = 4; // memory access size = 1 << ((aux >> 4) & 3)
+
+// 16-byte pre-decoded instruction: fetched with one s_load_dwordx4.
+struct DInsn {
+  uint8_t op;
+  uint8_t dst;
+  uint8_t src;
+  uint8_t aux;
+  int16_t off;
+  uint16_t tgt;   // absolute jump target / next pc for fused ops
+  int32_t imm;    // sign-extended immediate, or low half of lddw
+  int32_t hi;     // high half of lddw, helper id (CALL), atomic op (ATOMIC)
+};
+static_assert(sizeof(DInsn) == 16, "DInsn must be 16 bytes");
+
+// Map types (linux/bpf.h)
+constexpr uint32_t MT_HASH = 1;
+constexpr uint32_t MT_ARRAY = 2;
+constexpr uint32_t MT_PERCPU_HASH = 5;
+constexpr uint32_t MT_PERCPU_ARRAY = 6;
+
+// Device-side map descriptor (64 B), indexed by fd.
+//   ARRAY          data = value_size * max_entries, stride value_size
+//   PERCPU_ARRAY   data = [idx][cpu][value_size]  (per_cpu_array_map.hpp:25-28)
+//   HASH/PERCPU_HASH  nbuckets = next_prime(max_entries) slots of slot_size:
+//                  [u32 state][u32 pad][key, padded to 8][value(s), padded to 8]
+//                  state 0 = empty, 1 = filled, 2 = being written
+struct DMap {
+  uint32_t type;
+  uint32_t key_size;
+  uint32_t value_size;
+  uint32_t max_entries;
+  uint64_t data;        // device address
+  uint64_t nbuckets;
+  uint32_t slot_size;
+  uint32_t key_off;     // = 8
+  uint32_t val_off;     // = 8 + round8(key_size)
+  uint32_t ncpu;        // per-CPU slot count
+  uint64_t count_addr;  // device address of the u64 element counter (hash)
+  uint64_t reserved;
+};
+static_assert(sizeof(DMap) == 64, "DMap must be 64 bytes");
+
+// Context kinds for a batch
+constexpr uint32_t CTX_RAW = 0;      // r1 = unit memory, r2 = length
+constexpr uint32_t CTX_XDP = 1;      // r1 = xdp_md_userspace (48 B, LDS)
+constexpr uint32_t CTX_SYSCALL = 2;  // r1 = 64-B trace_event_raw_sys_enter record
+
+// Kernel launch parameters (passed by value).
+struct KParams {
+  const DInsn *prog;
+  const DMap *maps;
+  uint8_t *data;          // base of unit slots (device)
+  const uint32_t *lens;   // per-unit lengths or nullptr
+  uint32_t *verdicts;     // u32 r0 per unit (nullable)
+  uint64_t *rets;         // u64 r0 per unit (nullable)
+  int32_t *out_data_off;  // XDP: data - slot after the program (nullable)
+  uint32_t *out_len;      // XDP: data_end - data after the program (nullable)
+  uint32_t *err_count;    // device counter of units whose exec failed
+  uint64_t n;
+  uint64_t stride;
+  uint64_t first_unit;    // global index of unit 0 (virtual-cpu assignment)
+  uint64_t data_lo, data_hi;    // allowed global window #1 (the batch)
+  uint64_t arena_lo, arena_hi;  // allowed global window #2 (map arena)
+  uint64_t step_limit;    // max executed insns per unit
+  uint32_t fixed_len;
+  uint32_t stack_size;    // per-lane stack bytes (multiple of 8)
+  uint32_t ncpu;          // virtual CPU count (helper 8, per-CPU maps)
+  uint32_t ifindex;
+  uint32_t rxq;
+  uint32_t checked;       // 1 = confine global accesses to the two windows
+  uint32_t head;          // XDP: initial data offset inside each slot
+  uint32_t ordered;       // 1 = a single lane runs the units in index order
+};
+
+// Error codes recorded per unit (err_count counts units with any error)
+constexpr uint32_t E_OK = 0;
+constexpr uint32_t E_OOB = 1;
+constexpr uint32_t E_STEPS = 2;
+constexpr uint32_t E_BADOP = 3;
+
+}  // namespace bpftime_amd

@@ -1,0 +1,592 @@
+// bpftime_amd: program loader (patch -> validate -> pre-decode -> analyse).
+//
+// Load-time semantics follow bpftime_ubpf_vm::load_code
+// (vm/compat/ubpf-vm/compat_ubpf.cpp:61-200): every opcode 0x85 is a helper
+// call resolved through the registration map (:75-95, error strings kept),
+// lddw src 1..6 are patched through the lddw helpers (:97-190).  Validation
+// restates ubpf_load's checks (ubpf itself is absent from the reference).
+// The device-specific steps -- decoding to DInsn, fusing ldx/add/stx
+// read-modify-writes into one atomic add, sizing the per-lane stack -- are
+// described in DESIGN.md §3.
+#include "loader.hpp"
+
+#include <errno.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+
+namespace bpftime_amd {
+
+bool device_helper_supported(uint32_t id) {
+  switch (id) {
+    case 1: case 2: case 3: case 5: case 7: case 8: case 28: case 44: case 65: case 189:
+      return true;
+  }
+  return false;
+}
+
+static std::string fmt(const char *f, ...) __attribute__((format(printf, 1, 2)));
+static std::string fmt(const char *f, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, f);
+  vsnprintf(buf, sizeof(buf), f, ap);
+  va_end(ap);
+  return buf;
+}
+
+static inline uint8_t cls(uint8_t c) { return c & 7; }
+enum { C_LD = 0, C_LDX, C_ST, C_STX, C_ALU, C_JMP, C_JMP32, C_ALU64 };
+
+static bool opcode_known(uint8_t c) {
+  uint8_t k = cls(c), op = c & 0xf0;
+  switch (k) {
+    case C_ALU:
+    case C_ALU64:
+      if (op > 0xd0) return false;
+      if (op == 0xd0) return k == C_ALU;
+      if (op == 0x80) return (c & 0x08) == 0;
+      return true;
+    case C_JMP:
+    case C_JMP32:
+      if (op > 0xd0) return false;
+      if (k == C_JMP32 && (op == 0x00 || op == 0x80 || op == 0x90)) return false;
+      if (op == 0x00 || op == 0x80 || op == 0x90) return (c & 0x08) == 0;
+      return true;
+    case C_LDX:
+    case C_ST:
+      return (c & 0xe0) == 0x60;
+    case C_STX:
+      return (c & 0xe0) == 0x60 ||
+             ((c & 0xe0) == 0xc0 && ((c & 0x18) == 0x00 || (c & 0x18) == 0x18));
+    case C_LD:
+      return c == 0x18;
+  }
+  return false;
+}
+
+static bool writes_dst(uint8_t c) {
+  uint8_t k = cls(c);
+  return k == C_ALU || k == C_ALU64 || k == C_LDX || c == 0x18;
+}
+
+static bool atomic_imm_ok(int32_t imm) {
+  switch (imm) {
+    case 0x00: case 0x01: case 0x40: case 0x41: case 0x50: case 0x51: case 0xa0: case 0xa1:
+    case 0xe1: case 0xf1:
+      return true;
+  }
+  return false;
+}
+
+static int validate(const std::vector<RawInsn> &in, std::string &err) {
+  const uint32_t n = (uint32_t)in.size();
+  for (uint32_t i = 0; i < n; i++) {
+    const RawInsn d = in[i];
+    if (!opcode_known(d.code)) {
+      err = fmt("unknown opcode 0x%02x at PC %u", d.code, i);
+      return -1;
+    }
+    if (d.src > 10) {
+      err = fmt("invalid source register at PC %u", i);
+      return -1;
+    }
+    if (d.dst > 10 || (d.dst == 10 && writes_dst(d.code))) {
+      err = fmt("invalid destination register at PC %u", i);
+      return -1;
+    }
+    const uint8_t k = cls(d.code);
+    if ((k == C_JMP || k == C_JMP32) && d.code != 0x85 && d.code != 0x95) {
+      int64_t t = (int64_t)i + 1 + d.off;
+      if (t < 0 || t >= (int64_t)n) {
+        err = fmt("jump out of bounds at PC %u", i);
+        return -1;
+      }
+      if (t > 0 && in[t - 1].code == 0x18 && in[t].code == 0) {
+        err = fmt("jump to middle of lddw at PC %u", i);
+        return -1;
+      }
+    }
+    if (k == C_STX && (d.code & 0xe0) == 0xc0 && !atomic_imm_ok(d.imm)) {
+      err = fmt("unknown atomic operation 0x%x at PC %u", (unsigned)d.imm, i);
+      return -1;
+    }
+    if (d.code == 0x18) {
+      if (i + 1 >= n || in[i + 1].code != 0) {
+        err = fmt("incomplete lddw at PC %u", i);
+        return -1;
+      }
+      i++;
+    }
+  }
+  return 0;
+}
+
+// ---- pre-decoding ----------------------------------------------------------
+static uint8_t size_code(uint8_t c) {
+  switch (c & 0x18) {
+    case 0x10: return 0;  // B
+    case 0x08: return 1;  // H
+    case 0x00: return 2;  // W
+    default: return 3;    // DW
+  }
+}
+
+static DInsn decode_one(const std::vector<RawInsn> &in, uint32_t i) {
+  const RawInsn r = in[i];
+  DInsn d{};
+  d.dst = r.dst;
+  d.src = r.src;
+  d.off = r.off;
+  d.imm = r.imm;
+  d.tgt = 0;
+  d.hi = 0;
+  const uint8_t k = cls(r.code), op = r.code & 0xf0;
+  const bool srcreg = (r.code & 0x08) != 0;
+  if (k == C_ALU || k == C_ALU64) {
+    const bool w32 = k == C_ALU;
+    d.aux = (srcreg ? A_SRCREG : 0) | (w32 ? A_W32 : 0);
+    switch (op) {
+      case 0x00: d.op = X_ADD; break;
+      case 0x10: d.op = X_SUB; break;
+      case 0x20: d.op = X_MUL; break;
+      case 0x40: d.op = X_OR; break;
+      case 0x50: d.op = X_AND; break;
+      case 0xa0: d.op = X_XOR; break;
+      case 0xb0: d.op = X_MOV; break;
+      case 0x30: d.op = w32 ? X_DIV32 : X_DIV64; break;
+      case 0x90: d.op = w32 ? X_MOD32 : X_MOD64; break;
+      case 0x60: d.op = w32 ? X_LSH32 : X_LSH64; break;
+      case 0x70: d.op = w32 ? X_RSH32 : X_RSH64; break;
+      case 0xc0: d.op = w32 ? X_ARSH32 : X_ARSH64; break;
+      case 0x80: d.op = w32 ? X_NEG32 : X_NEG64; d.aux &= ~A_SRCREG; break;
+      case 0xd0: d.op = srcreg ? X_BE : X_LE; d.aux = 0; break;
+      default: d.op = X_BAD;
+    }
+    return d;
+  }
+  if (k == C_JMP || k == C_JMP32) {
+    d.aux = (srcreg ? A_SRCREG : 0) | (k == C_JMP32 ? A_W32 : 0);
+    d.tgt = (uint16_t)(i + 1 + r.off);
+    switch (op) {
+      case 0x00: d.op = X_JA; d.aux = 0; break;
+      case 0x10: d.op = X_JEQ; break;
+      case 0x20: d.op = X_JGT; break;
+      case 0x30: d.op = X_JGE; break;
+      case 0x40: d.op = X_JSET; break;
+      case 0x50: d.op = X_JNE; break;
+      case 0x60: d.op = X_JSGT; break;
+      case 0x70: d.op = X_JSGE; break;
+      case 0xa0: d.op = X_JLT; break;
+      case 0xb0: d.op = X_JLE; break;
+      case 0xc0: d.op = X_JSLT; break;
+      case 0xd0: d.op = X_JSLE; break;
+      case 0x80: d.op = X_CALL; d.hi = r.imm; d.aux = 0; d.tgt = 0; break;
+      case 0x90: d.op = X_EXIT; d.aux = 0; d.tgt = 0; break;
+      default: d.op = X_BAD;
+    }
+    return d;
+  }
+  const uint8_t sz = (uint8_t)(size_code(r.code) << A_SIZE_SHIFT);
+  if (k == C_LDX) {
+    d.op = X_LDX;
+    d.aux = sz;
+    return d;
+  }
+  if (k == C_ST) {
+    d.op = X_ST;
+    d.aux = sz;
+    return d;
+  }
+  if (k == C_STX) {
+    if ((r.code & 0xe0) == 0xc0) {
+      d.op = X_ATOMIC;
+      d.aux = sz;
+      d.hi = r.imm;
+    } else {
+      d.op = X_STX;
+      d.aux = sz;
+    }
+    return d;
+  }
+  if (r.code == 0x18) {
+    d.op = X_LDDW;
+    d.imm = r.imm;
+    d.hi = in[i + 1].imm;
+    return d;
+  }
+  d.op = X_BAD;
+  return d;
+}
+
+// ---- analysis --------------------------------------------------------------
+typedef uint16_t RegSet;  // bit per register r0..r10
+
+static void use_def(const DInsn &d, RegSet &use, RegSet &def) {
+  use = def = 0;
+  auto U = [&](int r) { use |= (RegSet)(1u << r); };
+  auto D = [&](int r) { def |= (RegSet)(1u << r); };
+  switch (d.op) {
+    case X_MOV:
+      if (d.aux & A_SRCREG) U(d.src);
+      D(d.dst);
+      break;
+    case X_ADD: case X_SUB: case X_MUL: case X_OR: case X_AND: case X_XOR: case X_DIV64:
+    case X_MOD64: case X_LSH64: case X_RSH64: case X_ARSH64: case X_DIV32: case X_MOD32:
+    case X_LSH32: case X_RSH32: case X_ARSH32:
+      U(d.dst);
+      if (d.aux & A_SRCREG) U(d.src);
+      D(d.dst);
+      break;
+    case X_NEG64: case X_NEG32: case X_LE: case X_BE:
+      U(d.dst);
+      D(d.dst);
+      break;
+    case X_LDX: U(d.src); D(d.dst); break;
+    case X_ST: U(d.dst); break;
+    case X_STX: U(d.dst); U(d.src); break;
+    case X_ATOMIC:
+      U(d.dst);
+      U(d.src);
+      if (d.hi == 0xf1) {
+        U(0);
+        D(0);
+      } else if (d.hi & 1) {
+        D(d.src);
+      }
+      break;
+    case X_LDDW: D(d.dst); break;
+    case X_JA: break;
+    case X_JEQ: case X_JGT: case X_JGE: case X_JSET: case X_JNE: case X_JSGT: case X_JSGE:
+    case X_JLT: case X_JLE: case X_JSLT: case X_JSLE:
+      U(d.dst);
+      if (d.aux & A_SRCREG) U(d.src);
+      break;
+    case X_CALL:
+      for (int r = 1; r <= 5; r++) U(r);
+      D(0);
+      break;
+    case X_EXIT: U(0); break;
+    default: break;
+  }
+}
+
+static void successors(const std::vector<DInsn> &p, uint32_t i, uint32_t s[2], int &ns) {
+  const DInsn &d = p[i];
+  ns = 0;
+  switch (d.op) {
+    case X_EXIT: return;
+    case X_JA: s[ns++] = d.tgt; return;
+    case X_LDDW: if (i + 2 < p.size()) s[ns++] = i + 2; return;
+    case X_JEQ: case X_JGT: case X_JGE: case X_JSET: case X_JNE: case X_JSGT: case X_JSGE:
+    case X_JLT: case X_JLE: case X_JSLT: case X_JSLE:
+      if (i + 1 < p.size()) s[ns++] = i + 1;
+      s[ns++] = d.tgt;
+      return;
+    default:
+      if (i + 1 < p.size()) s[ns++] = i + 1;
+  }
+}
+
+// Stack lattice per register: UNDEF, FP+k, OTHER, TOP
+struct SVal {
+  uint8_t kind;  // 0 undef, 1 fp, 2 other, 3 top
+  int32_t k;
+  bool operator==(const SVal &o) const { return kind == o.kind && (kind != 1 || k == o.k); }
+};
+static SVal join(SVal a, SVal b) {
+  if (a.kind == 0) return b;
+  if (b.kind == 0) return a;
+  if (a == b) return a;
+  if (a.kind == 2 && b.kind == 2) return a;
+  return SVal{3, 0};
+}
+
+// Returns per-lane stack bytes needed, or -1 if accesses cannot be bounded.
+static int stack_depth(const std::vector<DInsn> &p, const std::vector<bool> &reach) {
+  const uint32_t n = (uint32_t)p.size();
+  std::vector<std::vector<SVal>> in(n, std::vector<SVal>(11, SVal{0, 0}));
+  std::vector<bool> queued(n, false);
+  std::vector<uint32_t> work;
+  for (int r = 0; r < 11; r++) in[0][r] = SVal{2, 0};
+  in[0][10] = SVal{1, 0};
+  work.push_back(0);
+  queued[0] = true;
+  int64_t lowest = 0;  // most negative byte offset from fp touched
+  bool escape = false;
+  auto touch = [&](int64_t lo) { lowest = std::min(lowest, lo); };
+  while (!work.empty()) {
+    uint32_t i = work.back();
+    work.pop_back();
+    queued[i] = false;
+    std::vector<SVal> st = in[i];
+    const DInsn &d = p[i];
+    auto base_access = [&](int reg, int sz) {
+      SVal b = st[reg];
+      if (b.kind == 1) touch((int64_t)b.k + d.off);
+      else if (b.kind == 3) escape = true;
+      (void)sz;
+    };
+    switch (d.op) {
+      case X_MOV:
+        st[d.dst] = (d.aux & A_SRCREG) ? ((d.aux & A_W32) ? SVal{2, 0} : st[d.src]) : SVal{2, 0};
+        break;
+      case X_ADD:
+      case X_SUB:
+        if (st[d.dst].kind == 1 && !(d.aux & A_SRCREG) && !(d.aux & A_W32)) {
+          int64_t k = (int64_t)st[d.dst].k + (d.op == X_ADD ? (int64_t)d.imm : -(int64_t)d.imm);
+          if (k < -65536 || k > 65536) escape = true;
+          st[d.dst] = SVal{1, (int32_t)k};
+          touch(k);
+        } else {
+          if (st[d.dst].kind == 1 || st[d.dst].kind == 3) escape = true;
+          if ((d.aux & A_SRCREG) && (st[d.src].kind == 1 || st[d.src].kind == 3)) escape = true;
+          st[d.dst] = SVal{2, 0};
+        }
+        break;
+      case X_LDX:
+        base_access(d.src, 0);
+        st[d.dst] = SVal{2, 0};
+        break;
+      case X_ST:
+        base_access(d.dst, 0);
+        break;
+      case X_STX:
+        base_access(d.dst, 0);
+        if (st[d.src].kind == 1 || st[d.src].kind == 3) escape = true;  // fp value spilled
+        break;
+      case X_ATOMIC:
+        base_access(d.dst, 0);
+        if (st[d.src].kind == 1 || st[d.src].kind == 3) escape = true;
+        if (d.hi == 0xf1) st[0] = SVal{2, 0};
+        else if (d.hi & 1) st[d.src] = SVal{2, 0};
+        break;
+      case X_CALL:
+        for (int r = 1; r <= 5; r++)
+          if (st[r].kind == 1) touch(st[r].k);
+          else if (st[r].kind == 3) escape = true;
+        st[0] = SVal{2, 0};
+        break;
+      case X_EXIT:
+      case X_JA:
+        break;
+      case X_JEQ: case X_JGT: case X_JGE: case X_JSET: case X_JNE: case X_JSGT: case X_JSGE:
+      case X_JLT: case X_JLE: case X_JSLT: case X_JSLE:
+        break;
+      default: {
+        RegSet u, df;
+        use_def(d, u, df);
+        for (int r = 0; r < 11; r++)
+          if (df & (1u << r)) {
+            if (st[r].kind == 1 || st[r].kind == 3) {
+              // an fp-derived value transformed by other arithmetic
+              if (u & (1u << r)) escape = true;
+            }
+            st[r] = SVal{2, 0};
+          }
+        break;
+      }
+    }
+    uint32_t s[2];
+    int ns;
+    successors(p, i, s, ns);
+    for (int j = 0; j < ns; j++) {
+      uint32_t t = s[j];
+      bool changed = false;
+      for (int r = 0; r < 11; r++) {
+        SVal nv = join(in[t][r], st[r]);
+        if (!(nv == in[t][r])) {
+          in[t][r] = nv;
+          changed = true;
+        }
+      }
+      if (changed && !queued[t]) {
+        queued[t] = true;
+        work.push_back(t);
+      }
+    }
+  }
+  (void)reach;
+  if (escape) return -1;
+  int64_t depth = -lowest;
+  if (depth > kStackSize) return -1;
+  return (int)depth;
+}
+
+int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &helper_id_map,
+                 const std::map<size_t, std::string> &helper_names, const LddwHelpers &lddw,
+                 LoadOut &out, std::string &err) {
+  if (n > kMaxInsts) {
+    err = fmt("too many instructions (max %u)", kMaxInsts);
+    return -1;
+  }
+  std::vector<RawInsn> in(code, code + n);
+  // compat_ubpf.cpp:72-190
+  for (size_t i = 0; i < n; i++) {
+    RawInsn &cur = in[i];
+    if (cur.code == 0x85) {
+      if (helper_id_map.find((size_t)(uint32_t)cur.imm) == helper_id_map.end() || cur.imm < 0) {
+        if (cur.imm >= 64) {
+          err = "invalid call immediate at PC " + std::to_string(i);
+        } else {
+          err = "call to nonexistent function " + std::to_string(cur.imm) + " at PC " + std::to_string(i);
+        }
+        return -EINVAL;
+      }
+      if (!device_helper_supported((uint32_t)cur.imm)) {
+        auto it = helper_names.find((size_t)cur.imm);
+        err = "helper " + std::to_string(cur.imm) + " (" + (it != helper_names.end() ? it->second : "?") +
+              ") has no device implementation at PC " + std::to_string(i);
+        return -EINVAL;
+      }
+    } else if (cur.code == 0x18) {
+      if (i + 1 == n) {
+        err = "Unable to patch lddw instructions at " + std::to_string(i) + ", it's the last instruction";
+        return -EINVAL;
+      }
+      RawInsn &nx = in[i + 1];
+      uint64_t imm;
+      const std::string at = "Unable to patch lddw instruction at " + std::to_string(i);
+      switch (cur.src) {
+        case 0:
+          imm = (uint64_t)(uint32_t)cur.imm | ((uint64_t)(uint32_t)nx.imm << 32);
+          break;
+        case 1:
+          if (!lddw.map_by_fd) { err = at + ", map_by_fd not defined"; return -EINVAL; }
+          imm = lddw.map_by_fd((uint32_t)cur.imm);
+          break;
+        case 2:
+          if (!lddw.map_by_fd || !lddw.map_val) { err = at + ", map_by_fd or map_val not defined"; return -EINVAL; }
+          imm = lddw.map_val(lddw.map_by_fd((uint32_t)cur.imm)) + (uint64_t)(int64_t)nx.imm;
+          break;
+        case 3:
+          if (!lddw.var_addr) { err = at + ", var_addr not defined"; return -EINVAL; }
+          imm = lddw.var_addr((uint32_t)cur.imm);
+          break;
+        case 4:
+          if (!lddw.code_addr) { err = at + ", code_addr not defined"; return -EINVAL; }
+          imm = lddw.code_addr((uint32_t)cur.imm);
+          break;
+        case 5:
+          if (!lddw.map_by_idx) { err = at + ", map_by_idx not defined"; return -EINVAL; }
+          imm = lddw.map_by_idx((uint32_t)cur.imm);
+          break;
+        case 6:
+          if (!lddw.map_by_idx || !lddw.map_val) { err = at + ", map_by_idx or map_val not defined"; return -EINVAL; }
+          imm = lddw.map_val(lddw.map_by_idx((uint32_t)cur.imm)) + (uint64_t)(int64_t)nx.imm;
+          break;
+        default:
+          err = at + ", unsupported src_reg " + std::to_string(cur.src);
+          return -EINVAL;
+      }
+      cur.imm = (int32_t)(uint32_t)(imm & 0xffffffffu);
+      nx.imm = (int32_t)(uint32_t)(imm >> 32);
+      cur.src = 0;
+      i++;
+    }
+  }
+  if (validate(in, err) < 0) return -1;
+  if (n == 0) {
+    err = "no instructions";
+    return -1;
+  }
+
+  // pre-decode
+  std::vector<DInsn> p(n);
+  for (uint32_t i = 0; i < n; i++) {
+    if (in[i].code == 0x18) {
+      p[i] = decode_one(in, i);
+      p[i + 1] = DInsn{};
+      p[i + 1].op = X_NOP;
+      i++;
+    } else {
+      p[i] = decode_one(in, i);
+    }
+  }
+
+  // reachability + jump-target marks
+  std::vector<bool> reach(n, false), is_target(n, false);
+  {
+    std::vector<uint32_t> st{0};
+    reach[0] = true;
+    while (!st.empty()) {
+      uint32_t i = st.back();
+      st.pop_back();
+      uint32_t s[2];
+      int ns;
+      successors(p, i, s, ns);
+      for (int j = 0; j < ns; j++) {
+        if (s[j] != i + 1 && !(p[i].op == X_LDDW && s[j] == i + 2)) is_target[s[j]] = true;
+        if (!reach[s[j]]) {
+          reach[s[j]] = true;
+          st.push_back(s[j]);
+        }
+      }
+    }
+  }
+
+  // liveness (backward, to fixpoint)
+  std::vector<RegSet> live_in(n, 0), live_out(n, 0);
+  for (bool changed = true; changed;) {
+    changed = false;
+    for (int64_t i = (int64_t)n - 1; i >= 0; i--) {
+      if (!reach[i]) continue;
+      uint32_t s[2];
+      int ns;
+      successors(p, (uint32_t)i, s, ns);
+      RegSet o = 0;
+      for (int j = 0; j < ns; j++) o |= live_in[s[j]];
+      RegSet u, d;
+      use_def(p[i], u, d);
+      RegSet li = (RegSet)(u | (o & ~d));
+      if (li != live_in[i] || o != live_out[i]) {
+        live_in[i] = li;
+        live_out[i] = o;
+        changed = true;
+      }
+    }
+  }
+
+  // RMW fusion: ldx r,[b+o]; add r,v; stx [b+o],r  with r dead after the stx
+  uint32_t fused = 0;
+  for (uint32_t i = 0; i + 2 < n; i++) {
+    const DInsn &a = p[i], &b = p[i + 1], &c = p[i + 2];
+    if (a.op != X_LDX || b.op != X_ADD || c.op != X_STX) continue;
+    const uint32_t sz = (a.aux >> A_SIZE_SHIFT) & 3;
+    if (sz < 2) continue;                                   // 4 / 8 byte counters
+    if (sz == 3 && (b.aux & A_W32)) continue;               // 32-bit add on a u64 value
+    if (((c.aux >> A_SIZE_SHIFT) & 3) != sz) continue;
+    const uint8_t r = a.dst, base = a.src;
+    if (r == base || b.dst != r || c.src != r || c.dst != base || c.off != a.off) continue;
+    if ((b.aux & A_SRCREG) && b.src == r) continue;
+    if (is_target[i + 1] || is_target[i + 2]) continue;
+    if (live_out[i + 2] & (1u << r)) continue;
+    DInsn f{};
+    f.op = X_RMW_ADD;
+    f.dst = base;
+    f.off = a.off;
+    f.aux = (uint8_t)((sz << A_SIZE_SHIFT) | (b.aux & A_SRCREG));
+    f.src = b.src;
+    f.imm = b.imm;
+    f.tgt = (uint16_t)(i + 3);
+    p[i] = f;
+    fused++;
+    i += 2;
+  }
+
+  int depth = stack_depth(p, reach);
+  if (depth < 0 || depth > (int)kLdsStackMax) {
+    out.big_stack = true;
+    out.stack_size = kStackSize;
+  } else {
+    out.big_stack = false;
+    out.stack_size = (uint32_t)std::max(8, (depth + 7) & ~7);
+  }
+  out.fused_rmw = fused;
+  out.prog = std::move(p);
+  return 0;
+}
+
+}  // namespace bpftime_amd

@@ -1,0 +1,619 @@
+// bpftime_amd: device-resident maps and the prog / link records.
+//
+// Map semantics (syscall side, from_syscall = true) follow
+// runtime/src/handler/map_handler.cpp:109-330 over
+//   array_map.cpp:19-81, fix_hash_map.cpp:16-84 + bpftime_hash_map.hpp,
+//   per_cpu_array_map.cpp:97-145, per_cpu_hash_map.cpp:141-216,
+// with storage in one device arena (HBM) whose layout is described by the
+// DMap records the interpreter reads (csrc/common.hpp).  Host-side ops copy
+// the touched slots over PCIe: they are control-plane operations and must not
+// race a running batch (the reference's syscall path likewise takes the map
+// lock, map_handler.hpp:45-62).
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/bpftime_amd.h"
+#include "runtime.hpp"
+
+namespace bpftime_amd {
+
+Runtime &rt() {
+  static Runtime *r = new Runtime();
+  return *r;
+}
+
+void set_error(const std::string &e) { rt().last_error = e; }
+
+static thread_local std::vector<uint8_t> tl_lookup_buf;
+
+int Runtime::ensure_device() {
+  if (d_maptab) return 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    set_error("no HIP device");
+    return -1;
+  }
+  device = dev;
+  const char *mb = getenv("BPFTIME_AMD_ARENA_MB");
+  arena_size = (uint64_t)(mb ? atoll(mb) : 256) << 20;
+  if (hipMalloc((void **)&arena, arena_size) != hipSuccess) {
+    set_error("hipMalloc(arena) failed");
+    arena = nullptr;
+    return -1;
+  }
+  if (hipMemset(arena, 0, arena_size) != hipSuccess) return -1;
+  if (hipMalloc((void **)&d_maptab, sizeof(DMap) * kMaxFds) != hipSuccess) {
+    set_error("hipMalloc(map table) failed");
+    return -1;
+  }
+  if (hipMemset(d_maptab, 0, sizeof(DMap) * kMaxFds) != hipSuccess) return -1;
+  arena_used = 0;
+  return 0;
+}
+
+uint64_t Runtime::arena_alloc(uint64_t bytes) {
+  uint64_t off = (arena_used + 255) & ~255ull;
+  if (off + bytes > arena_size) return 0;
+  arena_used = off + bytes;
+  return (uint64_t)(uintptr_t)arena + off;
+}
+
+int Runtime::push_map(int fd) {
+  return hipMemcpy(d_maptab + fd, &maps[fd].d, sizeof(DMap), hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+
+// bpftime_hash_map.hpp:14-38
+static uint64_t next_prime(uint64_t n) {
+  auto is_prime = [](uint64_t v) {
+    if (v <= 1) return false;
+    if (v <= 3) return true;
+    if (v % 2 == 0 || v % 3 == 0) return false;
+    for (uint64_t i = 5; i * i <= v; i += 6)
+      if (v % i == 0 || v % (i + 2) == 0) return false;
+    return true;
+  };
+  while (!is_prime(n)) ++n;
+  return n;
+}
+
+static uint64_t hash_bytes(const void *key, uint32_t n) {
+  uint64_t h = 0;
+  for (uint32_t i = 0; i < n; i++) h = h * 31 + ((const uint8_t *)key)[i];
+  return h;
+}
+
+static MapRec *map_of(int fd) {
+  Runtime &r = rt();
+  if (fd < 0 || fd >= (int)kMaxFds || r.kind[fd] != HKind::MAP) {
+    errno = ENOENT;
+    return nullptr;
+  }
+  return &r.maps[fd];
+}
+
+static int alloc_fd(int fd) {
+  Runtime &r = rt();
+  if (fd < 0) {
+    for (fd = 3; fd < (int)kMaxFds && r.kind[fd] != HKind::NONE; fd++) {
+    }
+  }
+  if (fd < 0 || fd >= (int)kMaxFds || r.kind[fd] != HKind::NONE) {
+    errno = EBADF;
+    return -1;
+  }
+  return fd;
+}
+
+// --- device slot helpers (hash maps) ---
+static bool read_slot(const MapRec &m, uint64_t idx, std::vector<uint8_t> &buf) {
+  buf.resize(m.d.slot_size);
+  return hipMemcpy(buf.data(), (void *)(m.d.data + idx * m.d.slot_size), m.d.slot_size,
+                   hipMemcpyDeviceToHost) == hipSuccess;
+}
+static bool write_slot(const MapRec &m, uint64_t idx, const std::vector<uint8_t> &buf) {
+  return hipMemcpy((void *)(m.d.data + idx * m.d.slot_size), buf.data(), m.d.slot_size,
+                   hipMemcpyHostToDevice) == hipSuccess;
+}
+static uint64_t read_count(const MapRec &m) {
+  uint64_t c = 0;
+  hipMemcpy(&c, (void *)m.d.count_addr, 8, hipMemcpyDeviceToHost);
+  return c;
+}
+static void write_count(const MapRec &m, uint64_t c) {
+  hipMemcpy((void *)m.d.count_addr, &c, 8, hipMemcpyHostToDevice);
+}
+
+// probe like bpftime_hash_map::elem_lookup; returns bucket or -1
+static int64_t host_hash_find(const MapRec &m, const void *key, std::vector<uint8_t> &slot,
+                              int64_t *first_empty) {
+  const uint64_t nb = m.d.nbuckets;
+  uint64_t idx = hash_bytes(key, m.key_size) % nb, start = idx;
+  if (first_empty) *first_empty = -1;
+  do {
+    if (!read_slot(m, idx, slot)) return -1;
+    uint32_t st;
+    memcpy(&st, slot.data(), 4);
+    if (st == 0) {
+      if (first_empty) *first_empty = (int64_t)idx;
+      return -1;
+    }
+    if (memcmp(slot.data() + m.d.key_off, key, m.key_size) == 0) return (int64_t)idx;
+    idx = (idx + 1) % nb;
+  } while (idx != start);
+  return -1;
+}
+
+}  // namespace bpftime_amd
+
+using namespace bpftime_amd;
+
+extern "C" {
+
+const char *bpftime_amd_last_error(void) { return rt().last_error.c_str(); }
+
+void bpftime_amd_set_ncpu(uint32_t ncpu) { rt().ncpu = ncpu ? ncpu : 1; }
+uint32_t bpftime_amd_get_ncpu(void) { return rt().ncpu; }
+
+int bpftime_find_minimal_unused_fd(void) {
+  std::lock_guard<std::mutex> g(rt().mu);
+  return alloc_fd(-1);
+}
+
+int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
+  Runtime &r = rt();
+  std::lock_guard<std::mutex> g(r.mu);
+  if (r.ensure_device() < 0) return -1;
+  fd = alloc_fd(fd);
+  if (fd < 0) return -1;
+  MapRec m;
+  m.name = name ? name : "";
+  m.type = (uint32_t)attr.type;
+  m.key_size = attr.key_size;
+  m.value_size = attr.value_size;
+  m.max_entries = attr.max_ents;
+  m.flags = attr.flags;
+  DMap &d = m.d;
+  d.type = m.type;
+  d.key_size = m.key_size;
+  d.value_size = m.value_size;
+  d.max_entries = m.max_entries;
+  d.ncpu = r.ncpu;
+  switch (m.type) {
+    case MT_ARRAY:
+      m.bytes = (uint64_t)m.value_size * m.max_entries;
+      break;
+    case MT_PERCPU_ARRAY:
+      m.bytes = (uint64_t)m.value_size * m.max_entries * d.ncpu;
+      break;
+    case MT_HASH:
+    case MT_PERCPU_HASH: {
+      if (m.key_size == 0 || m.value_size == 0 || m.max_entries == 0) {
+        errno = EINVAL;
+        set_error("hash map needs key/value size and max_entries");
+        return -1;
+      }
+      d.nbuckets = next_prime(m.max_entries);
+      d.key_off = 8;
+      d.val_off = 8 + ((m.key_size + 7) & ~7u);
+      uint64_t vbytes = (uint64_t)m.value_size * (m.type == MT_PERCPU_HASH ? d.ncpu : 1);
+      d.slot_size = (uint32_t)(d.val_off + ((vbytes + 7) & ~7ull));
+      m.bytes = d.nbuckets * d.slot_size;
+      break;
+    }
+    default:
+      errno = EINVAL;
+      set_error("unsupported map type " + std::to_string(m.type));
+      return -1;
+  }
+  uint64_t extra = (m.type == MT_HASH || m.type == MT_PERCPU_HASH) ? 64 : 0;
+  uint64_t base = r.arena_alloc(m.bytes + extra + 8);
+  if (!base) {
+    errno = ENOMEM;
+    set_error("map arena exhausted (BPFTIME_AMD_ARENA_MB)");
+    return -1;
+  }
+  d.data = base;
+  d.count_addr = extra ? base + ((m.bytes + 63) & ~63ull) : 0;
+  if (hipMemset((void *)base, 0, m.bytes + extra + 8) != hipSuccess) return -1;
+  r.maps[fd] = m;
+  r.kind[fd] = HKind::MAP;
+  if (r.push_map(fd) < 0) return -1;
+  return fd;
+}
+
+int bpftime_is_map_fd(int fd) { return fd >= 0 && fd < (int)kMaxFds && rt().kind[fd] == HKind::MAP; }
+int bpftime_is_prog_fd(int fd) { return fd >= 0 && fd < (int)kMaxFds && rt().kind[fd] == HKind::PROG; }
+int bpftime_is_array_map(int fd) {
+  MapRec *m = map_of(fd);
+  return m && m->type == MT_ARRAY;
+}
+
+uint32_t bpftime_map_value_size_from_syscall(int fd) {
+  MapRec *m = map_of(fd);
+  if (!m) return 0;
+  if (m->type == MT_PERCPU_ARRAY || m->type == MT_PERCPU_HASH) return m->value_size * m->d.ncpu;
+  return m->value_size;  // map_handler.cpp:69-84
+}
+
+const void *bpftime_map_lookup_elem(int fd, const void *key) {
+  MapRec *m = map_of(fd);
+  if (!m) return nullptr;
+  std::vector<uint8_t> &buf = tl_lookup_buf;
+  switch (m->type) {
+    case MT_ARRAY:
+    case MT_PERCPU_ARRAY: {
+      uint32_t k;
+      memcpy(&k, key, 4);
+      if (k >= m->max_entries) {
+        errno = ENOENT;
+        return nullptr;
+      }
+      uint64_t vs = m->type == MT_ARRAY ? m->value_size : (uint64_t)m->value_size * m->d.ncpu;
+      buf.resize(vs);
+      if (hipMemcpy(buf.data(), (void *)(m->d.data + k * vs), vs, hipMemcpyDeviceToHost) != hipSuccess)
+        return nullptr;
+      return buf.data();
+    }
+    case MT_HASH:
+    case MT_PERCPU_HASH: {
+      std::vector<uint8_t> slot;
+      int64_t idx = host_hash_find(*m, key, slot, nullptr);
+      if (idx < 0) {
+        errno = ENOENT;
+        return nullptr;
+      }
+      uint64_t vs = m->type == MT_HASH ? m->value_size : (uint64_t)m->value_size * m->d.ncpu;
+      buf.assign(slot.begin() + m->d.val_off, slot.begin() + m->d.val_off + vs);
+      return buf.data();
+    }
+  }
+  return nullptr;
+}
+
+long bpftime_map_update_elem(int fd, const void *key, const void *value, uint64_t flags) {
+  MapRec *m = map_of(fd);
+  if (!m) return -1;
+  uint64_t b = flags & 0xffffffffull;
+  bool flags_ok = b == 0 || b == 1 || b == 2;  // map_common_def.hpp:83-94
+  switch (m->type) {
+    case MT_ARRAY:
+    case MT_PERCPU_ARRAY: {
+      if (!flags_ok) {
+        errno = EINVAL;
+        return -1;
+      }
+      uint32_t k;
+      memcpy(&k, key, 4);
+      if (k < m->max_entries && flags == 1) {
+        errno = EEXIST;
+        return -1;
+      }
+      if (k >= m->max_entries) {
+        errno = E2BIG;
+        return -1;
+      }
+      uint64_t vs = m->type == MT_ARRAY ? m->value_size : (uint64_t)m->value_size * m->d.ncpu;
+      return hipMemcpy((void *)(m->d.data + k * vs), value, vs, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+    }
+    case MT_HASH: {
+      // fix_hash_map.cpp:34-39 -> bpftime_hash_map::elem_update; returns 0
+      std::vector<uint8_t> slot;
+      int64_t empty;
+      int64_t idx = host_hash_find(*m, key, slot, &empty);
+      if (idx >= 0) {
+        memcpy(slot.data() + m->d.val_off, value, m->value_size);
+        write_slot(*m, (uint64_t)idx, slot);
+      } else if (empty >= 0) {
+        uint64_t c = read_count(*m);
+        if (c < m->max_entries) {
+          std::vector<uint8_t> s(m->d.slot_size, 0);
+          uint32_t st = 1;
+          memcpy(s.data(), &st, 4);
+          memcpy(s.data() + m->d.key_off, key, m->key_size);
+          memcpy(s.data() + m->d.val_off, value, m->value_size);
+          write_slot(*m, (uint64_t)empty, s);
+          write_count(*m, c + 1);
+        }
+      }
+      return 0;
+    }
+    case MT_PERCPU_HASH: {
+      // per_cpu_hash_map.cpp:157-183 (userspace view: ncpu * value_size)
+      if (!flags_ok) {
+        errno = EINVAL;
+        return -1;
+      }
+      std::vector<uint8_t> slot;
+      int64_t empty;
+      int64_t idx = host_hash_find(*m, key, slot, &empty);
+      if (flags == 1 && idx >= 0) {
+        errno = EEXIST;
+        return -1;
+      }
+      if (flags == 2 && idx < 0) {
+        errno = ENOENT;
+        return -1;
+      }
+      uint64_t vs = (uint64_t)m->value_size * m->d.ncpu;
+      if (idx >= 0) {
+        memcpy(slot.data() + m->d.val_off, value, vs);
+        write_slot(*m, (uint64_t)idx, slot);
+        return 0;
+      }
+      uint64_t c = read_count(*m);
+      if (c >= m->max_entries || empty < 0) {
+        errno = E2BIG;
+        return -1;
+      }
+      std::vector<uint8_t> s(m->d.slot_size, 0);
+      uint32_t st = 1;
+      memcpy(s.data(), &st, 4);
+      memcpy(s.data() + m->d.key_off, key, m->key_size);
+      memcpy(s.data() + m->d.val_off, value, vs);
+      write_slot(*m, (uint64_t)empty, s);
+      write_count(*m, c + 1);
+      return 0;
+    }
+  }
+  return -1;
+}
+
+long bpftime_map_delete_elem(int fd, const void *key) {
+  MapRec *m = map_of(fd);
+  if (!m) return -1;
+  switch (m->type) {
+    case MT_ARRAY:
+    case MT_PERCPU_ARRAY:
+      errno = EINVAL;  // array_map.cpp:58-64
+      return -1;
+    case MT_HASH:
+    case MT_PERCPU_HASH: {
+      std::vector<uint8_t> slot;
+      int64_t idx = host_hash_find(*m, key, slot, nullptr);
+      if (idx < 0) {
+        if (m->type == MT_PERCPU_HASH) {
+          errno = ENOENT;
+          return -1;
+        }
+        return 0;  // fix_hash_map.cpp:41-45 returns 0 regardless
+      }
+      uint32_t st = 0;
+      memcpy(slot.data(), &st, 4);
+      write_slot(*m, (uint64_t)idx, slot);
+      write_count(*m, read_count(*m) - 1);
+      return 0;
+    }
+  }
+  return -1;
+}
+
+int bpftime_map_get_next_key(int fd, const void *key, void *next_key) {
+  MapRec *m = map_of(fd);
+  if (!m) return -1;
+  switch (m->type) {
+    case MT_ARRAY:
+    case MT_PERCPU_ARRAY: {  // array_map.cpp:66-81
+      uint32_t k = 0;
+      if (key) memcpy(&k, key, 4);
+      if (!key || k >= m->max_entries) {
+        uint32_t z = 0;
+        memcpy(next_key, &z, 4);
+        return 0;
+      }
+      if (k == m->max_entries - 1) {
+        errno = ENOENT;
+        return -1;
+      }
+      k++;
+      memcpy(next_key, &k, 4);
+      return 0;
+    }
+    case MT_HASH:
+    case MT_PERCPU_HASH: {  // fix_hash_map.cpp:47-84: bucket index order
+      if (!next_key) {
+        errno = EINVAL;
+        return -1;
+      }
+      std::vector<uint8_t> all(m->bytes);
+      if (hipMemcpy(all.data(), (void *)m->d.data, m->bytes, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+      uint64_t from = 0;
+      if (key) {
+        std::vector<uint8_t> slot;
+        int64_t idx = host_hash_find(*m, key, slot, nullptr);
+        if (idx >= 0) from = (uint64_t)idx + 1;
+      }
+      for (uint64_t i = from; i < m->d.nbuckets; i++) {
+        const uint8_t *s = all.data() + i * m->d.slot_size;
+        uint32_t st;
+        memcpy(&st, s, 4);
+        if (st == 1) {
+          memcpy(next_key, s + m->d.key_off, m->key_size);
+          return 0;
+        }
+      }
+      errno = ENOENT;
+      return -1;
+    }
+  }
+  return -1;
+}
+
+void bpftime_close(int fd) {
+  Runtime &r = rt();
+  std::lock_guard<std::mutex> g(r.mu);
+  if (fd < 0 || fd >= (int)kMaxFds) return;
+  if (r.kind[fd] == HKind::MAP) {
+    r.maps[fd] = MapRec();
+    r.push_map(fd);
+  } else if (r.kind[fd] == HKind::PROG) {
+    r.progs[fd] = ProgRec();
+  } else if (r.kind[fd] == HKind::LINK) {
+    r.links[fd] = LinkRec();
+  }
+  r.kind[fd] = HKind::NONE;
+}
+
+void bpftime_amd_reset(void) {
+  Runtime &r = rt();
+  std::lock_guard<std::mutex> g(r.mu);
+  for (uint32_t i = 0; i < kMaxFds; i++) {
+    r.kind[i] = HKind::NONE;
+    r.maps[i] = MapRec();
+    r.progs[i] = ProgRec();
+    r.links[i] = LinkRec();
+  }
+  if (r.d_maptab) hipMemset(r.d_maptab, 0, sizeof(DMap) * kMaxFds);
+  r.arena_used = 0;
+}
+
+// ---- lddw helpers: bpftime_shm.cpp:637-676 --------------------------------
+uint64_t bpftime_amd_map_ptr_by_fd(uint32_t fd) {
+  if (!map_of((int)fd)) {
+    errno = ENOENT;
+    return ~0ull;  // INVALID_MAP_PTR
+  }
+  return fd;
+}
+
+uint64_t bpftime_amd_map_val(uint64_t map_ptr) {
+  int fd = (int)map_ptr;
+  MapRec *m = map_of(fd);
+  if (!m) {
+    errno = ENOENT;
+    return 0;
+  }
+  switch (m->type) {
+    case MT_ARRAY:
+      return m->max_entries ? m->d.data : 0;
+    case MT_PERCPU_ARRAY:
+      return m->max_entries ? m->d.data : 0;  // cpu 0's slot of key 0
+    default: {
+      uint8_t key[512];
+      if (m->key_size > sizeof(key) || bpftime_map_get_next_key(fd, nullptr, key) < 0) {
+        errno = ENOENT;
+        return 0;
+      }
+      std::vector<uint8_t> slot;
+      int64_t idx = host_hash_find(*m, key, slot, nullptr);
+      return idx < 0 ? 0 : m->d.data + (uint64_t)idx * m->d.slot_size + m->d.val_off;
+    }
+  }
+}
+
+uint64_t bpftime_amd_map_device_ptr(int fd, uint64_t *bytes) {
+  MapRec *m = map_of(fd);
+  if (!m) return 0;
+  if (bytes) *bytes = m->bytes;
+  return m->d.data;
+}
+
+int bpftime_amd_map_snapshot(int fd, void *out, uint64_t bytes) {
+  MapRec *m = map_of(fd);
+  if (!m || bytes > m->bytes) return -1;
+  return hipMemcpy(out, (void *)m->d.data, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+
+int bpftime_amd_map_restore(int fd, const void *in, uint64_t bytes) {
+  MapRec *m = map_of(fd);
+  if (!m || bytes > m->bytes) return -1;
+  if (hipMemcpy((void *)m->d.data, in, bytes, hipMemcpyHostToDevice) != hipSuccess) return -1;
+  if (m->d.count_addr) {
+    uint64_t c = 0;
+    for (uint64_t i = 0; i < m->d.nbuckets && (i + 1) * m->d.slot_size <= bytes; i++) {
+      uint32_t st;
+      memcpy(&st, (const uint8_t *)in + i * m->d.slot_size, 4);
+      c += st == 1;
+    }
+    write_count(*m, c);
+  }
+  return 0;
+}
+
+int bpftime_amd_map_geometry(int fd, uint64_t *nbuckets, uint32_t *slot_size, uint32_t *key_off,
+                             uint32_t *val_off, uint32_t *ncpu) {
+  MapRec *m = map_of(fd);
+  if (!m) return -1;
+  if (nbuckets) *nbuckets = m->d.nbuckets;
+  if (slot_size) *slot_size = m->d.slot_size;
+  if (key_off) *key_off = m->d.key_off;
+  if (val_off) *val_off = m->d.val_off;
+  if (ncpu) *ncpu = m->d.ncpu;
+  return 0;
+}
+
+uint64_t bpftime_amd_map_count(int fd) {
+  MapRec *m = map_of(fd);
+  if (!m || !m->d.count_addr) return 0;
+  return read_count(*m);
+}
+
+// ---- prog / link records ---------------------------------------------------
+int bpftime_progs_create(int fd, const void *insns, size_t insn_cnt, const char *prog_name, int prog_type) {
+  Runtime &r = rt();
+  std::lock_guard<std::mutex> g(r.mu);
+  fd = alloc_fd(fd);
+  if (fd < 0) return -1;
+  ProgRec p;
+  p.name = prog_name ? prog_name : "";
+  p.insns.assign((const uint8_t *)insns, (const uint8_t *)insns + insn_cnt * 8);
+  p.type = prog_type;
+  r.progs[fd] = std::move(p);
+  r.kind[fd] = HKind::PROG;
+  return fd;
+}
+
+// bpftime_shm_internal.cpp:566-607: only prog_fd is validated; the target of
+// an XDP link is an ifindex.
+int bpftime_link_create(int fd, struct bpf_link_create_args *args) {
+  Runtime &r = rt();
+  std::lock_guard<std::mutex> g(r.mu);
+  if (!args) {
+    errno = EINVAL;
+    return -1;
+  }
+  if (args->prog_fd >= kMaxFds || r.kind[args->prog_fd] != HKind::PROG) {
+    errno = EBADF;
+    return -1;
+  }
+  fd = alloc_fd(fd);
+  if (fd < 0) return -1;
+  LinkRec l;
+  l.prog_fd = args->prog_fd;
+  l.target = args->target_fd;
+  l.attach_type = args->attach_type;
+  l.flags = args->flags;
+  r.links[fd] = l;
+  r.kind[fd] = HKind::LINK;
+  return fd;
+}
+
+int bpftime_amd_xdp_links(int *link_fds, int *prog_fds, uint32_t *ifindexes, int max) {
+  Runtime &r = rt();
+  std::lock_guard<std::mutex> g(r.mu);
+  int n = 0;
+  for (uint32_t i = 0; i < kMaxFds; i++) {
+    if (r.kind[i] != HKind::LINK || r.links[i].attach_type != BPFTIME_AMD_BPF_XDP) continue;
+    if (n < max) {
+      if (link_fds) link_fds[n] = (int)i;
+      if (prog_fds) prog_fds[n] = (int)r.links[i].prog_fd;
+      if (ifindexes) ifindexes[n] = r.links[i].target;
+    }
+    n++;
+  }
+  return n;
+}
+
+// ---- host merge ------------------------------------------------------------
+int bpftime_amd_merge_delta_u64(void *acc, const void *init, const void *shard, uint64_t bytes) {
+  if (bytes % 8) return -1;
+  uint64_t *a = (uint64_t *)acc;
+  const uint64_t *i0 = (const uint64_t *)init, *s = (const uint64_t *)shard;
+  for (uint64_t k = 0; k < bytes / 8; k++) a[k] += s[k] - i0[k];
+  return 0;
+}
+
+}  // extern "C"

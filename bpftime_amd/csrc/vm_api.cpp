@@ -1,0 +1,475 @@
+// bpftime_amd: the drop-in VM C ABI (include/ebpf-vm.h).
+//
+// Mirrors vm/vm-core/src/ebpf-vm.cpp:6-98 over a single backend class that
+// plays the role of a bpftime::vm::compat::bpftime_vm_impl
+// (vm/compat/include/bpftime_vm_compat.hpp:27-198) registered under the name
+// "mi355x" (the reference registers "ubpf" the same way,
+// vm/compat/ubpf-vm/compat_ubpf.cpp:253-257).
+#include <errno.h>
+#include <hip/hip_runtime_api.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/bpftime_amd.h"
+#include "loader.hpp"
+#include "runtime.hpp"
+
+namespace bpftime_amd {
+extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind, bool big_stack, uint32_t grid,
+                                                uint32_t ordered, hipStream_t stream);
+extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds);
+
+struct HelperReg {
+  std::string name;
+  void *fn;
+};
+
+class Mi355xVm {
+ public:
+  std::string error;
+  // compat_ubpf.hpp:42-44 (bpftime id -> ubpf-style id)
+  std::map<size_t, size_t> helper_id_map;
+  std::map<size_t, std::string> helper_names;
+  size_t next_helper_id = 1;
+  LddwHelpers lddw;
+  bool bounds_check = true;
+  int (*error_print)(FILE *, const char *, ...) = nullptr;
+  int unwind_idx = -1;
+  uint32_t ctx_kind = CTX_RAW;
+  uint64_t step_limit = 1ull << 22;
+
+  bool loaded = false;
+  LoadOut prog;
+  DInsn *d_prog = nullptr;
+  uint32_t *d_err = nullptr;
+  // staging for ebpf_exec
+  uint8_t *d_stage = nullptr;
+  size_t stage_size = 0;
+
+  Mi355xVm() {
+    // bpftime_prog.cpp:126-127 defaults, pointed at the device registry
+    lddw.map_by_fd = bpftime_amd_map_ptr_by_fd;
+    lddw.map_val = bpftime_amd_map_val;
+    const char *sl = getenv("BPFTIME_AMD_STEP_LIMIT");
+    if (sl) step_limit = strtoull(sl, nullptr, 0);
+  }
+  ~Mi355xVm() {
+    unload();
+    if (d_err) hipFree(d_err);
+    if (d_stage) hipFree(d_stage);
+  }
+  void unload() {
+    if (d_prog) hipFree(d_prog);
+    d_prog = nullptr;
+    loaded = false;
+    prog = LoadOut();
+  }
+  int register_external_function(size_t index, const std::string &name, void *fn) {
+    // compat_ubpf.cpp:50-59: allocate the next id; ubpf caps helpers at 64
+    size_t next_id = next_helper_id++;
+    if (next_id >= 64) {
+      error = "too many helpers (ubpf supports 64)";
+      return -1;
+    }
+    helper_id_map[index] = next_id;
+    helper_names[index] = name;
+    (void)fn;
+    return 0;
+  }
+  int load_code(const void *code, size_t code_len) {
+    if (code_len % 8 != 0) {
+      error = "Length of code must be a multiple of 8";
+      return -1;
+    }
+    if (loaded) {
+      error = "code has already been loaded into this VM. Use ebpf_unload_code() if you need to reuse this VM";
+      return -1;
+    }
+    LoadOut out;
+    std::string err;
+    int rc = load_program((const RawInsn *)code, code_len / 8, helper_id_map, helper_names, lddw, out, err);
+    if (rc < 0) {
+      error = err;
+      return rc;
+    }
+    if (rt().ensure_device() < 0) {
+      error = "no HIP device: " + rt().last_error;
+      return -1;
+    }
+    size_t bytes = out.prog.size() * sizeof(DInsn);
+    if (hipMalloc((void **)&d_prog, bytes) != hipSuccess ||
+        hipMemcpy(d_prog, out.prog.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+      error = "device upload failed";
+      return -1;
+    }
+    if (!d_err && hipMalloc((void **)&d_err, 4) != hipSuccess) {
+      error = "device alloc failed";
+      return -1;
+    }
+    prog = std::move(out);
+    loaded = true;
+    return 0;
+  }
+
+  int exec_batch(const ebpf_batch *b);
+  int exec_one(void *mem, size_t mem_len, uint64_t *ret);
+};
+
+int Mi355xVm::exec_batch(const ebpf_batch *b) {
+  if (!loaded) {
+    error = "no program loaded";
+    return -1;
+  }
+  if (!b || b->ctx_kind > CTX_SYSCALL || (b->count && (!b->data || !b->stride))) {
+    error = "invalid batch";
+    return -1;
+  }
+  hipStream_t s = (hipStream_t)b->stream;
+  if (b->count == 0) return 0;
+  Runtime &r = rt();
+  KParams p{};
+  p.prog = d_prog;
+  p.maps = r.d_maptab;
+  p.data = (uint8_t *)b->data;
+  p.lens = b->lens;
+  p.verdicts = b->verdicts;
+  p.rets = b->rets;
+  p.out_data_off = b->data_off_out;
+  p.out_len = b->len_out;
+  p.err_count = d_err;
+  p.n = b->count;
+  p.stride = b->stride;
+  p.first_unit = b->first_unit;
+  p.data_lo = (uint64_t)(uintptr_t)b->data;
+  p.data_hi = p.data_lo + b->count * b->stride;
+  p.arena_lo = (uint64_t)(uintptr_t)r.arena;
+  p.arena_hi = p.arena_lo + r.arena_size;
+  p.step_limit = step_limit;
+  p.fixed_len = b->fixed_len;
+  p.stack_size = prog.stack_size;
+  p.ncpu = r.ncpu;
+  p.ifindex = b->ingress_ifindex;
+  p.rxq = b->rx_queue_index;
+  p.head = b->head;
+  p.checked = (b->flags & EBPF_BATCH_UNCHECKED) ? 0 : 1;
+  if (hipMemsetAsync(d_err, 0, 4, s) != hipSuccess) {
+    error = "hipMemsetAsync failed";
+    return -1;
+  }
+  const bool ordered = (b->flags & EBPF_BATCH_ORDERED) != 0;
+  uint32_t grid = 1;
+  if (!ordered) {
+    static int cus = 0;
+    if (!cus) {
+      hipDeviceProp_t prop;
+      int dev = 0;
+      hipGetDevice(&dev);
+      hipGetDeviceProperties(&prop, dev);
+      cus = prop.multiProcessorCount;
+    }
+    const size_t dyn = kBlock * ((b->ctx_kind == CTX_XDP ? 48 : 0) + (prog.big_stack ? 0 : prog.stack_size));
+    int occ = bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn);
+    if (occ < 1) occ = 1;
+    uint64_t want = (b->count + kBlock - 1) / kBlock;
+    uint64_t cap = (uint64_t)cus * (uint64_t)occ;
+    grid = (uint32_t)(want < cap ? want : cap);
+  }
+  hipError_t e = bpftime_amd_launch_interp(&p, b->ctx_kind, prog.big_stack, grid, ordered ? 1 : 0, s);
+  if (e != hipSuccess) {
+    error = std::string("kernel launch failed: ") + hipGetErrorString(e);
+    return -1;
+  }
+  if (b->flags & EBPF_BATCH_SYNC) {
+    uint32_t failed = 0;
+    if (hipMemcpyAsync(&failed, d_err, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      error = "batch sync failed";
+      return -1;
+    }
+    return (int)failed;
+  }
+  return 0;
+}
+
+// ebpf_exec: one unit, copied to the device and back.
+int Mi355xVm::exec_one(void *mem, size_t mem_len, uint64_t *ret) {
+  if (!loaded) {
+    error = "no program loaded";
+    return -1;
+  }
+  struct XdpMd {
+    uint64_t data, data_end;
+    uint32_t data_meta, ingress_ifindex, rx_queue_index, egress_ifindex;
+    uint64_t buffer_start, buffer_end;
+  };
+  uint8_t *host_base;
+  size_t slot_bytes;
+  uint32_t head = 0, len;
+  XdpMd *x = nullptr;
+  if (ctx_kind == CTX_XDP) {
+    x = (XdpMd *)mem;
+    uint64_t lo = x->buffer_start && x->buffer_start <= x->data ? x->buffer_start : x->data;
+    uint64_t hi = x->buffer_end && x->buffer_end >= x->data_end ? x->buffer_end : x->data_end;
+    host_base = (uint8_t *)(uintptr_t)lo;
+    slot_bytes = hi - lo;
+    head = (uint32_t)(x->data - lo);
+    len = (uint32_t)(x->data_end - x->data);
+  } else {
+    host_base = (uint8_t *)mem;
+    slot_bytes = mem_len;
+    len = (uint32_t)mem_len;
+  }
+  size_t need = ((slot_bytes + 255) & ~(size_t)255) + 64;
+  if (need > stage_size) {
+    if (d_stage) hipFree(d_stage);
+    if (hipMalloc((void **)&d_stage, need) != hipSuccess) {
+      d_stage = nullptr;
+      stage_size = 0;
+      error = "staging alloc failed";
+      return -1;
+    }
+    stage_size = need;
+  }
+  uint8_t *d_slot = d_stage + 64;
+  uint64_t *d_ret = (uint64_t *)d_stage;
+  int32_t *d_off = (int32_t *)(d_stage + 8);
+  uint32_t *d_len = (uint32_t *)(d_stage + 12);
+  if (slot_bytes && hipMemcpy(d_slot, host_base, slot_bytes, hipMemcpyHostToDevice) != hipSuccess) return -1;
+  ebpf_batch b{};
+  b.ctx_kind = ctx_kind;
+  b.flags = EBPF_BATCH_SYNC | EBPF_BATCH_ORDERED;
+  b.count = 1;
+  b.data = d_slot;
+  b.stride = slot_bytes ? slot_bytes : 1;
+  b.fixed_len = len;
+  b.head = head;
+  b.rets = d_ret;
+  if (x) {
+    b.data_off_out = d_off;
+    b.len_out = d_len;
+    b.ingress_ifindex = x->ingress_ifindex;
+    b.rx_queue_index = x->rx_queue_index;
+  }
+  int failed = exec_batch(&b);
+  if (failed < 0) return -1;
+  uint8_t hdr[16];
+  if (hipMemcpy(hdr, d_stage, 16, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (slot_bytes && hipMemcpy(host_base, d_slot, slot_bytes, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (failed) {
+    error = "program execution failed on device";
+    return -1;
+  }
+  uint64_t r0;
+  memcpy(&r0, hdr, 8);
+  if (x) {
+    int32_t off;
+    uint32_t l;
+    memcpy(&off, hdr + 8, 4);
+    memcpy(&l, hdr + 12, 4);
+    x->data = (uint64_t)(uintptr_t)host_base + (uint64_t)(int64_t)off;
+    x->data_end = x->data + l;
+  }
+  *ret = r0;
+  return 0;
+}
+
+}  // namespace bpftime_amd
+
+using namespace bpftime_amd;
+
+// ebpf-vm.cpp's struct ebpf_vm {vm_name; vm_instance} (bpftime_vm_compat.hpp:260-263)
+struct ebpf_vm {
+  std::string vm_name;
+  Mi355xVm *impl;
+};
+
+extern "C" {
+
+struct ebpf_vm *ebpf_create(const char *vm_name) {
+  if (!vm_name || strcmp(vm_name, "mi355x") != 0) return nullptr;
+  ebpf_vm *vm = new ebpf_vm;
+  vm->impl = new Mi355xVm();
+  return vm;
+}
+
+void ebpf_destroy(struct ebpf_vm *vm) {
+  if (!vm) return;
+  delete vm->impl;
+  delete vm;
+}
+
+const char *ebpf_get_vm_name(struct ebpf_vm *vm) { return vm->vm_name.c_str(); }
+
+bool ebpf_toggle_bounds_check(struct ebpf_vm *vm, bool enable) {
+  bool prev = vm->impl->bounds_check;
+  vm->impl->bounds_check = enable;
+  return prev;
+}
+
+void ebpf_set_error_print(struct ebpf_vm *vm, int (*error_printf)(FILE *, const char *, ...)) {
+  vm->impl->error_print = error_printf;
+}
+
+int ebpf_register(struct ebpf_vm *vm, unsigned int index, const char *name, void *fn) {
+  return vm->impl->register_external_function(index, name ? name : "", fn);
+}
+
+int ebpf_load(struct ebpf_vm *vm, const void *code, uint32_t code_len, char **errmsg) {
+  int err = vm->impl->load_code(code, code_len);
+  if (err < 0 && errmsg) *errmsg = strdup(vm->impl->error.c_str());
+  return err;
+}
+
+void ebpf_unload_code(struct ebpf_vm *vm) { vm->impl->unload(); }
+
+int ebpf_exec(const struct ebpf_vm *vm, void *mem, size_t mem_len, uint64_t *bpf_return_value) {
+  return vm->impl->exec_one(mem, mem_len, bpf_return_value);
+}
+
+ebpf_jit_fn ebpf_compile(struct ebpf_vm *vm, char **errmsg) {
+  vm->impl->error = "mi355x is a device interpreter: use ebpf_exec / ebpf_exec_batch";
+  if (errmsg) *errmsg = strdup(vm->impl->error.c_str());
+  return nullptr;
+}
+
+int ebpf_set_unwind_function_index(struct ebpf_vm *vm, unsigned int idx) {
+  vm->impl->unwind_idx = (int)idx;
+  return -1;  // tail-call unwinding is not implemented on the device
+}
+
+int ebpf_set_pointer_secret(struct ebpf_vm *vm, uint64_t secret) {
+  (void)vm;
+  (void)secret;
+  return -1;
+}
+
+void ebpf_set_lddw_helpers(struct ebpf_vm *vm, uint64_t (*map_by_fd)(uint32_t), uint64_t (*map_by_idx)(uint32_t),
+                           uint64_t (*map_val)(uint64_t), uint64_t (*var_addr)(uint32_t),
+                           uint64_t (*code_addr)(uint32_t)) {
+  LddwHelpers &l = vm->impl->lddw;
+  l.map_by_fd = map_by_fd ? map_by_fd : nullptr;
+  l.map_by_idx = map_by_idx;
+  l.map_val = map_val;
+  l.var_addr = var_addr;
+  l.code_addr = code_addr;
+}
+
+ebpf_jit_fn ebpf_load_aot_object(struct ebpf_vm *vm, const void *buf, size_t buf_len) {
+  (void)buf;
+  (void)buf_len;
+  vm->impl->error = "AOT objects are not supported by the mi355x interpreter";
+  return nullptr;
+}
+
+int ebpf_exec_batch(const struct ebpf_vm *vm, const struct ebpf_batch *batch) {
+  if (!vm) return -1;
+  return vm->impl->exec_batch(batch);
+}
+
+int ebpf_set_ctx_kind(struct ebpf_vm *vm, uint32_t ctx_kind) {
+  if (ctx_kind > CTX_SYSCALL) return -1;
+  vm->impl->ctx_kind = ctx_kind;
+  return 0;
+}
+
+// ---- runtime glue ----------------------------------------------------------
+int bpftime_amd_register_default_helpers(struct ebpf_vm *vm) {
+  // kernel helper group + shm maps group subset (bpf_helper.cpp:1177-1401)
+  static const struct {
+    unsigned id;
+    const char *name;
+  } h[] = {{8, "bpf_get_smp_processor_id"}, {28, "bpf_csum_diff"},    {44, "bpf_xdp_adjust_head"},
+           {65, "bpf_xdp_adjust_tail"},      {5, "bpf_ktime_get_ns"}, {7, "bpf_get_prandom_u32"},
+           {1, "bpf_map_lookup_elem"},       {2, "bpf_map_update_elem"}, {3, "bpf_map_delete_elem"}};
+  int err = 0;
+  for (auto &e : h) err |= ebpf_register(vm, e.id, e.name, nullptr);
+  return err ? -1 : 0;
+}
+
+struct ebpf_vm *bpftime_amd_prog_instantiate(int prog_fd, char **errmsg) {
+  Runtime &r = rt();
+  if (prog_fd < 0 || prog_fd >= (int)kMaxFds || r.kind[prog_fd] != HKind::PROG) {
+    if (errmsg) *errmsg = strdup("not a prog fd");
+    return nullptr;
+  }
+  std::vector<uint8_t> insns = r.progs[prog_fd].insns;
+  int type = r.progs[prog_fd].type;
+  ebpf_vm *vm = ebpf_create("mi355x");
+  bpftime_amd_register_default_helpers(vm);
+  if (type == BPFTIME_AMD_PROG_TYPE_XDP) vm->impl->ctx_kind = CTX_XDP;
+  if (type == BPFTIME_AMD_PROG_TYPE_TRACEPOINT) vm->impl->ctx_kind = CTX_SYSCALL;
+  if (ebpf_load(vm, insns.data(), (uint32_t)insns.size(), errmsg) < 0) {
+    ebpf_destroy(vm);
+    return nullptr;
+  }
+  return vm;
+}
+
+int bpftime_amd_vm_info(const struct ebpf_vm *vm, uint32_t *stack_size, int *big_stack, uint32_t *fused_rmw,
+                        uint32_t *n_insns) {
+  if (!vm || !vm->impl->loaded) return -1;
+  if (stack_size) *stack_size = vm->impl->prog.stack_size;
+  if (big_stack) *big_stack = vm->impl->prog.big_stack;
+  if (fused_rmw) *fused_rmw = vm->impl->prog.fused_rmw;
+  if (n_insns) *n_insns = (uint32_t)vm->impl->prog.prog.size();
+  return 0;
+}
+
+void bpftime_amd_set_step_limit(struct ebpf_vm *vm, uint64_t limit) { vm->impl->step_limit = limit; }
+
+const char *bpftime_amd_vm_error(const struct ebpf_vm *vm) { return vm->impl->error.c_str(); }
+
+// ---- device utilities ------------------------------------------------------
+int bpftime_amd_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+int bpftime_amd_set_device(int dev) { return hipSetDevice(dev) == hipSuccess ? 0 : -1; }
+void *bpftime_amd_dev_alloc(uint64_t bytes) {
+  void *p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+  return p;
+}
+void bpftime_amd_dev_free(void *p) {
+  if (p) hipFree(p);
+}
+int bpftime_amd_memcpy_htod(void *dst, const void *src, uint64_t bytes) {
+  return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+int bpftime_amd_memcpy_dtoh(void *dst, const void *src, uint64_t bytes) {
+  return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+int bpftime_amd_memset(void *dst, int v, uint64_t bytes) { return hipMemset(dst, v, bytes) == hipSuccess ? 0 : -1; }
+int bpftime_amd_sync(void) { return hipDeviceSynchronize() == hipSuccess ? 0 : -1; }
+void *bpftime_amd_host_alloc(uint64_t bytes) {
+  void *p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+void bpftime_amd_host_free(void *p) {
+  if (p) hipHostFree(p);
+}
+void *bpftime_amd_event_create(void) {
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return (void *)e;
+}
+void bpftime_amd_event_destroy(void *ev) {
+  if (ev) hipEventDestroy((hipEvent_t)ev);
+}
+int bpftime_amd_event_record(void *ev, void *stream) {
+  return hipEventRecord((hipEvent_t)ev, (hipStream_t)stream) == hipSuccess ? 0 : -1;
+}
+float bpftime_amd_event_elapsed_ms(void *start, void *stop) {
+  float ms = -1;
+  if (hipEventSynchronize((hipEvent_t)stop) != hipSuccess) return -1;
+  if (hipEventElapsedTime(&ms, (hipEvent_t)start, (hipEvent_t)stop) != hipSuccess) return -1;
+  return ms;
+}
+
+}  // extern "C"

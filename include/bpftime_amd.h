@@ -1,0 +1,139 @@
+/*
+ * bpftime_amd runtime C ABI (libbpftime_amd.so): device-resident maps, the
+ * prog / bpf_link records of the XDP attach surface, and device utilities.
+ *
+ * The map / prog / link entry points keep the names, argument meaning and
+ * error conventions of the reference's shared-memory runtime
+ * (runtime/include/bpftime_shm.hpp:220-400, implemented in
+ * runtime/src/bpftime_shm.cpp:69-140 / bpftime_shm_internal.cpp), with the
+ * map storage living in GPU HBM instead of a boost.interprocess segment.
+ */
+#ifndef BPFTIME_AMD_H
+#define BPFTIME_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "ebpf-vm.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* runtime/include/bpftime_shm.hpp:27-46 (same field order, C layout) */
+struct bpf_map_attr {
+	int type;
+	uint32_t key_size;
+	uint32_t value_size;
+	uint32_t max_ents;
+	uint64_t flags;
+	uint32_t ifindex;
+	uint32_t btf_vmlinux_value_type_id;
+	uint32_t btf_id;
+	uint32_t btf_key_type_id;
+	uint32_t btf_value_type_id;
+	uint64_t map_extra;
+	uint32_t kernel_bpf_map_id;
+	uint64_t gpu_thread_count;
+};
+
+/* runtime/include/bpftime_shm.hpp:250-301 (BPF_LINK_CREATE args; 48 B) */
+struct bpf_link_create_args {
+	uint32_t prog_fd;        /* union { prog_fd; map_fd; } */
+	uint32_t target_fd;      /* union { target_fd; target_ifindex; } */
+	uint32_t attach_type;    /* BPF_XDP = 37 (runtime/include/bpftime_epoll.h:1158) */
+	uint32_t flags;
+	uint64_t attach_union[4];
+};
+
+#define BPFTIME_AMD_BPF_XDP 37
+#define BPFTIME_AMD_PROG_TYPE_XDP 6        /* bpftime_shm.hpp:144-151 */
+#define BPFTIME_AMD_PROG_TYPE_TRACEPOINT 5
+
+/* ---- maps: bpftime_shm.hpp:316-345 ---- */
+/* create a map at `fd` (-1: lowest unused fd).  Supported types: HASH (1,
+ * fix-size hash, map_handler.cpp:54-58), ARRAY (2), PERCPU_HASH (5),
+ * PERCPU_ARRAY (6).  Returns fd or -1 (errno set). */
+int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr);
+/* syscall-side ops (from_syscall = true), bpftime_shm.cpp:115-140 */
+const void *bpftime_map_lookup_elem(int fd, const void *key);
+long bpftime_map_update_elem(int fd, const void *key, const void *value, uint64_t flags);
+long bpftime_map_delete_elem(int fd, const void *key);
+int bpftime_map_get_next_key(int fd, const void *key, void *next_key);
+uint32_t bpftime_map_value_size_from_syscall(int fd);
+int bpftime_is_map_fd(int fd);
+int bpftime_is_array_map(int fd);
+int bpftime_is_prog_fd(int fd);
+int bpftime_find_minimal_unused_fd(void);
+void bpftime_close(int fd);
+
+/* ---- progs / links (bpftime_shm.hpp:303-309) ---- */
+int bpftime_progs_create(int fd, const void *insns, size_t insn_cnt, const char *prog_name, int prog_type);
+int bpftime_link_create(int fd, struct bpf_link_create_args *args);
+
+/* ---- lddw helpers for the device VM (bpftime_shm.cpp:637-676) ---- */
+uint64_t bpftime_amd_map_ptr_by_fd(uint32_t fd); /* the fd itself, ~0 if not a map */
+uint64_t bpftime_amd_map_val(uint64_t map_ptr);  /* DEVICE address of the first value */
+
+/* ---- bpftime_amd extensions ---- */
+/* device address / byte size of a map's storage (layout: csrc/common.hpp DMap) */
+uint64_t bpftime_amd_map_device_ptr(int fd, uint64_t *bytes);
+/* raw device-layout copy of the map storage to / from the host */
+int bpftime_amd_map_snapshot(int fd, void *out, uint64_t bytes);
+int bpftime_amd_map_restore(int fd, const void *in, uint64_t bytes);
+/* hash maps: bucket count and device slot geometry */
+int bpftime_amd_map_geometry(int fd, uint64_t *nbuckets, uint32_t *slot_size, uint32_t *key_off,
+                             uint32_t *val_off, uint32_t *ncpu);
+uint64_t bpftime_amd_map_count(int fd);
+/* virtual CPU count for per-CPU maps and helper 8 (default 64) */
+void bpftime_amd_set_ncpu(uint32_t ncpu);
+uint32_t bpftime_amd_get_ncpu(void);
+/* drop every map / prog / link record and free the device arena */
+void bpftime_amd_reset(void);
+
+/* XDP attach surface: enumerate BPF_XDP links -> (link fd, prog fd, ifindex) */
+int bpftime_amd_xdp_links(int *link_fds, int *prog_fds, uint32_t *ifindexes, int max);
+/* instantiate a prog record into a loaded "mi355x" VM with the default
+ * helper groups registered (bpf_attach_ctx.cpp:40-57 equivalent). */
+struct ebpf_vm *bpftime_amd_prog_instantiate(int prog_fd, char **errmsg);
+/* registers the device helper set (ids 1,2,3,5,7,8,28,44,65) on a VM */
+int bpftime_amd_register_default_helpers(struct ebpf_vm *vm);
+/* loader facts: per-lane stack bytes, big (scratch) stack, fused RMW count */
+int bpftime_amd_vm_info(const struct ebpf_vm *vm, uint32_t *stack_size, int *big_stack,
+                        uint32_t *fused_rmw, uint32_t *n_insns);
+void bpftime_amd_set_step_limit(struct ebpf_vm *vm, uint64_t limit);
+
+/* ---- host merge of per-GPU map shards ---- */
+/* acc += shard - init over u64 words (array counters, additive rule) */
+int bpftime_amd_merge_delta_u64(void *acc, const void *init, const void *shard, uint64_t bytes);
+
+/* ---- device utilities (HIP runtime plumbing for callers without one) ---- */
+int bpftime_amd_device_count(void);
+int bpftime_amd_set_device(int dev);
+void *bpftime_amd_dev_alloc(uint64_t bytes);
+void bpftime_amd_dev_free(void *p);
+int bpftime_amd_memcpy_htod(void *dst, const void *src, uint64_t bytes);
+int bpftime_amd_memcpy_dtoh(void *dst, const void *src, uint64_t bytes);
+int bpftime_amd_memset(void *dst, int v, uint64_t bytes);
+int bpftime_amd_sync(void);
+void *bpftime_amd_host_alloc(uint64_t bytes); /* pinned */
+void bpftime_amd_host_free(void *p);
+/* events on a stream: returns elapsed ms between start/stop records */
+void *bpftime_amd_event_create(void);
+void bpftime_amd_event_destroy(void *ev);
+int bpftime_amd_event_record(void *ev, void *stream);
+float bpftime_amd_event_elapsed_ms(void *start, void *stop);
+const char *bpftime_amd_last_error(void);
+
+/* ---- synthetic inputs (seeded splitmix64) ---- */
+/* word k of the stream = splitmix64 output #k for `seed`:
+ *   z = seed + (k+1)*0x9E3779B97F4A7C15; z = (z^(z>>30))*0xBF58476D1CE4E5B9;
+ *   z = (z^(z>>27))*0x94D049BB133111EB; z ^= z>>31 */
+/* n packets in `stride`-byte device slots (first `len` bytes random, bytes
+ * 12..13 = 0x08 0x00); unit i uses words of stream index first+i. */
+int bpftime_amd_gen_xdp(void *dev, uint64_t n, uint64_t stride, uint32_t len, uint64_t seed,
+                        uint64_t first, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

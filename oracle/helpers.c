@@ -1,0 +1,138 @@
+/*
+ * ORACLE (test infrastructure only) -- see oracle.h.
+ *
+ * Helper functions the device path implements, restated from
+ * runtime/src/bpf_helper.cpp:
+ *   1/2/3 map lookup/update/delete   :387-408 (map arg = fd, cast to int)
+ *   5 ktime_get_ns                    :357-362
+ *   7 get_prandom_u32                 :301-304
+ *   8 get_smp_processor_id            :702-710 (sched_getcpu -> orc_set_cpu)
+ *   28 csum_diff                      :713-744
+ *   44 xdp_adjust_head                :748-764
+ *   65 xdp_adjust_tail                :766-776
+ * Registration order follows the kernel + shm-maps helper groups
+ * (bpf_helper.cpp:1177-1401).
+ */
+#include "oracle.h"
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+struct xdp_md_userspace { /* runtime/extension/userspace_xdp.h:6-17 */
+	uint64_t data, data_end;
+	uint32_t data_meta, ingress_ifindex, rx_queue_index, egress_ifindex;
+	uint64_t buffer_start, buffer_end;
+};
+
+static uint64_t h_lookup(uint64_t map, uint64_t key, uint64_t a, uint64_t b, uint64_t c)
+{
+	(void)a, (void)b, (void)c;
+	return (uint64_t)(uintptr_t)orc_map_lookup((int)map, (const void *)(uintptr_t)key);
+}
+
+static uint64_t h_update(uint64_t map, uint64_t key, uint64_t value, uint64_t flags, uint64_t c)
+{
+	(void)c;
+	return (uint64_t)orc_map_update((int)map, (const void *)(uintptr_t)key, (const void *)(uintptr_t)value,
+					flags);
+}
+
+static uint64_t h_delete(uint64_t map, uint64_t key, uint64_t a, uint64_t b, uint64_t c)
+{
+	(void)a, (void)b, (void)c;
+	return (uint64_t)orc_map_delete((int)map, (const void *)(uintptr_t)key);
+}
+
+static uint64_t h_ktime(uint64_t a, uint64_t b, uint64_t c, uint64_t d, uint64_t e)
+{
+	(void)a, (void)b, (void)c, (void)d, (void)e;
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ULL + (uint64_t)ts.tv_nsec;
+}
+
+static uint64_t h_prandom(uint64_t a, uint64_t b, uint64_t c, uint64_t d, uint64_t e)
+{
+	(void)a, (void)b, (void)c, (void)d, (void)e;
+	return (uint32_t)rand();
+}
+
+extern int orc_get_cpu(void);
+static uint64_t h_cpu(uint64_t a, uint64_t b, uint64_t c, uint64_t d, uint64_t e)
+{
+	(void)a, (void)b, (void)c, (void)d, (void)e;
+	return (uint64_t)orc_get_cpu();
+}
+
+/* bpf_helper.cpp:713-744 (from ebpf-for-windows) */
+static uint64_t h_csum_diff(uint64_t from_, uint64_t from_size_, uint64_t to_, uint64_t to_size_,
+			    uint64_t seed_)
+{
+	const void *from = (const void *)(uintptr_t)from_;
+	const void *to = (const void *)(uintptr_t)to_;
+	int from_size = (int)from_size_, to_size = (int)to_size_, seed = (int)seed_;
+	int csum_diff = -EINVAL;
+	if ((from_size % 4 != 0) || (to_size % 4 != 0))
+		goto out;
+	csum_diff = seed;
+	if (to != NULL)
+		for (int i = 0; i < to_size / 2; i++)
+			csum_diff += (uint16_t)(*((const uint16_t *)to + i));
+	if (from != NULL)
+		for (int i = 0; i < from_size / 2; i++)
+			csum_diff += (uint16_t)(~*((const uint16_t *)from + i));
+	if (csum_diff < 0)
+		csum_diff = -EINVAL;
+out:
+	return (uint64_t)(int64_t)csum_diff;
+}
+
+#define ETH_HLEN 14
+/* bpf_helper.cpp:748-764 */
+static uint64_t h_adjust_head(uint64_t ctx, uint64_t off_, uint64_t a, uint64_t b, uint64_t c)
+{
+	(void)a, (void)b, (void)c;
+	struct xdp_md_userspace *xdp = (struct xdp_md_userspace *)(uintptr_t)ctx;
+	int offset = (int)off_;
+	uint64_t data = xdp->data + (int64_t)offset;
+	if (data > xdp->data_end - ETH_HLEN || data > xdp->buffer_end)
+		return (uint64_t)(int64_t)-EINVAL;
+	if (data < xdp->buffer_start) {
+		memmove((void *)(uintptr_t)(xdp->buffer_start + (xdp->buffer_start - data)),
+			(void *)(uintptr_t)xdp->data, xdp->data_end - xdp->data);
+		data = xdp->buffer_start;
+	}
+	xdp->data = data;
+	return 0;
+}
+
+/* bpf_helper.cpp:766-776 */
+static uint64_t h_adjust_tail(uint64_t ctx, uint64_t delta_, uint64_t a, uint64_t b, uint64_t c)
+{
+	(void)a, (void)b, (void)c;
+	struct xdp_md_userspace *x = (struct xdp_md_userspace *)(uintptr_t)ctx;
+	int delta = (int)delta_;
+	uint64_t data = x->data_end + (int64_t)delta;
+	if (data < x->data || data < x->buffer_start || data > x->buffer_end)
+		return (uint64_t)(int64_t)-EINVAL;
+	x->data_end = data;
+	return 0;
+}
+
+int orc_vm_register_default_helpers(struct orc_vm *vm)
+{
+	int err = 0;
+	/* kernel helper group subset (bpf_helper.cpp:1177-1356) */
+	err |= orc_vm_register(vm, 8, "bpf_get_smp_processor_id", h_cpu);
+	err |= orc_vm_register(vm, 28, "bpf_csum_diff", h_csum_diff);
+	err |= orc_vm_register(vm, 44, "bpf_xdp_adjust_head", h_adjust_head);
+	err |= orc_vm_register(vm, 65, "bpf_xdp_adjust_tail", h_adjust_tail);
+	err |= orc_vm_register(vm, 5, "bpf_ktime_get_ns", h_ktime);
+	err |= orc_vm_register(vm, 7, "bpf_get_prandom_u32", h_prandom);
+	/* shm maps helper group (bpf_helper.cpp:1359-1401) */
+	err |= orc_vm_register(vm, 1, "bpf_map_lookup_elem", h_lookup);
+	err |= orc_vm_register(vm, 2, "bpf_map_update_elem", h_update);
+	err |= orc_vm_register(vm, 3, "bpf_map_delete_elem", h_delete);
+	return err ? -1 : 0;
+}

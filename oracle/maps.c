@@ -1,0 +1,568 @@
+/*
+ * ORACLE (test infrastructure only) -- see oracle.h.
+ *
+ * Restatement of bpftime's userspace maps as the helpers see them:
+ *   ARRAY          runtime/src/bpf_map/userspace/array_map.cpp:19-81
+ *   HASH (default) fix_size_hash_map_impl  fix_hash_map.cpp:16-84 over
+ *                  bpftime_hash_map        runtime/src/bpf_map/bpftime_hash_map.hpp:12-205
+ *                  (selected by map_handler.cpp:54-58, 785-798)
+ *   PERCPU_ARRAY   per_cpu_array_map.cpp:17-145 (layout [idx][cpu][value])
+ *   PERCPU_HASH    per_cpu_hash_map.cpp:20-216 (boost unordered_map in the
+ *                  reference; here insertion-ordered, so get_next_key order
+ *                  differs -> compared as key/value sets)
+ *   flags check    map_common_def.hpp:83-94
+ *   fd validity    bpftime_shm_internal.cpp:129-166, 457-466
+ *   lddw helpers   bpftime_shm.cpp:637-676
+ */
+#include "oracle.h"
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+
+enum { T_HASH = 1, T_ARRAY = 2, T_PERCPU_HASH = 5, T_PERCPU_ARRAY = 6 };
+
+struct orc_map {
+	int used;
+	uint32_t type, ksize, vsize, max_entries, flags;
+	/* ARRAY / PERCPU_ARRAY */
+	uint8_t *data;
+	uint32_t ncpu;
+	/* HASH: bpftime_hash_map layout [u32 used][key][value] per bucket */
+	uint64_t nbuckets, count;
+	/* PERCPU_HASH: keys[i], vals[i] (ncpu*vsize), insertion ordered */
+	uint8_t *pkeys, *pvals;
+	uint64_t pcount, pcap;
+};
+
+static struct orc_map g_maps[ORC_MAX_FDS];
+static int g_ncpu = 1;
+static int g_cpu = 0;
+static __thread int g_errno;
+
+int orc_last_errno(void)
+{
+	return g_errno;
+}
+
+void orc_set_ncpu(int ncpu)
+{
+	g_ncpu = ncpu > 0 ? ncpu : 1;
+}
+
+void orc_set_cpu(int cpu)
+{
+	g_cpu = cpu;
+}
+
+int orc_get_cpu(void)
+{
+	return g_cpu;
+}
+
+static void free_map(struct orc_map *m)
+{
+	free(m->data);
+	free(m->pkeys);
+	free(m->pvals);
+	memset(m, 0, sizeof(*m));
+}
+
+void orc_maps_reset(void)
+{
+	for (int i = 0; i < ORC_MAX_FDS; i++)
+		free_map(&g_maps[i]);
+}
+
+/* bpftime_hash_map.hpp:14-38 */
+static int is_prime(uint64_t n)
+{
+	if (n <= 1)
+		return 0;
+	if (n <= 3)
+		return 1;
+	if (n % 2 == 0 || n % 3 == 0)
+		return 0;
+	for (uint64_t i = 5; i * i <= n; i += 6)
+		if (n % i == 0 || n % (i + 2) == 0)
+			return 0;
+	return 1;
+}
+
+uint64_t orc_next_prime(uint64_t n)
+{
+	while (!is_prime(n))
+		++n;
+	return n;
+}
+
+/* bpftime_hash_map.hpp:40-47: h = h*31 + byte over size_t */
+uint64_t orc_hash_bytes(const void *key, uint64_t n)
+{
+	uint64_t h = 0;
+	for (uint64_t i = 0; i < n; i++)
+		h = h * 31 + ((const uint8_t *)key)[i];
+	return h;
+}
+
+static struct orc_map *get(int fd)
+{
+	if (fd < 0 || fd >= ORC_MAX_FDS || !g_maps[fd].used) {
+		g_errno = ENOENT;
+		return NULL;
+	}
+	return &g_maps[fd];
+}
+
+int orc_map_create(int fd, uint32_t type, uint32_t ksize, uint32_t vsize, uint32_t max_entries,
+		   uint32_t flags)
+{
+	if (fd < 0) {
+		for (fd = 3; fd < ORC_MAX_FDS && g_maps[fd].used; fd++)
+			;
+	}
+	if (fd >= ORC_MAX_FDS || g_maps[fd].used)
+		return -1;
+	struct orc_map *m = &g_maps[fd];
+	memset(m, 0, sizeof(*m));
+	m->type = type;
+	m->ksize = ksize;
+	m->vsize = vsize;
+	m->max_entries = max_entries;
+	m->flags = flags;
+	switch (type) {
+	case T_ARRAY:
+		m->data = calloc((size_t)vsize * max_entries + 1, 1);
+		break;
+	case T_PERCPU_ARRAY:
+		m->ncpu = (uint32_t)g_ncpu;
+		m->data = calloc((size_t)vsize * max_entries * m->ncpu + 1, 1);
+		break;
+	case T_HASH:
+		m->nbuckets = orc_next_prime(max_entries);
+		m->data = calloc((size_t)m->nbuckets * (4 + ksize + vsize) + 1, 1);
+		break;
+	case T_PERCPU_HASH:
+		m->ncpu = (uint32_t)g_ncpu;
+		break;
+	default:
+		return -1;
+	}
+	m->used = 1;
+	return fd;
+}
+
+/* map_common_def.hpp:83-94 */
+static int check_update_flags(uint64_t flags)
+{
+	uint64_t b = flags & 0xffffffffULL;
+	if (b != 0 && b != 1 && b != 2) {
+		g_errno = EINVAL;
+		return 0;
+	}
+	return 1;
+}
+
+/* ---- fix-size hash (bpftime_hash_map.hpp) ---- */
+static inline uint8_t *slot(struct orc_map *m, uint64_t i)
+{
+	return m->data + i * (4 + m->ksize + m->vsize);
+}
+
+static void *hash_lookup(struct orc_map *m, const void *key)
+{
+	uint64_t idx = orc_hash_bytes(key, m->ksize) % m->nbuckets, start = idx;
+	do {
+		uint8_t *s = slot(m, idx);
+		if (*(uint32_t *)s == 0)
+			return NULL;
+		if (memcmp(s + 4, key, m->ksize) == 0)
+			return s + 4 + m->ksize;
+		idx = (idx + 1) % m->nbuckets;
+	} while (idx != start);
+	return NULL;
+}
+
+static int hash_update(struct orc_map *m, const void *key, const void *val)
+{
+	uint64_t idx = orc_hash_bytes(key, m->ksize) % m->nbuckets, start = idx;
+	do {
+		uint8_t *s = slot(m, idx);
+		if (*(uint32_t *)s == 0) {
+			if (m->count >= m->max_entries)
+				return 0; /* full: reject (:153-156) */
+			memcpy(s + 4, key, m->ksize);
+			memcpy(s + 4 + m->ksize, val, m->vsize);
+			*(uint32_t *)s = 1;
+			m->count++;
+			return 1;
+		} else if (memcmp(s + 4, key, m->ksize) == 0) {
+			memcpy(s + 4 + m->ksize, val, m->vsize);
+			return 1;
+		}
+		idx = (idx + 1) % m->nbuckets;
+	} while (idx != start);
+	return 0;
+}
+
+static int hash_delete(struct orc_map *m, const void *key)
+{
+	uint64_t idx = orc_hash_bytes(key, m->ksize) % m->nbuckets, start = idx;
+	do {
+		uint8_t *s = slot(m, idx);
+		if (*(uint32_t *)s == 0)
+			return 0;
+		if (memcmp(s + 4, key, m->ksize) == 0) {
+			*(uint32_t *)s = 0; /* no tombstone (:182-199) */
+			m->count--;
+			return 1;
+		}
+		idx = (idx + 1) % m->nbuckets;
+	} while (idx != start);
+	return 0;
+}
+
+/* ---- per-cpu hash (per_cpu_hash_map.cpp) ---- */
+static int64_t phash_find(struct orc_map *m, const void *key)
+{
+	for (uint64_t i = 0; i < m->pcount; i++)
+		if (memcmp(m->pkeys + i * m->ksize, key, m->ksize) == 0)
+			return (int64_t)i;
+	return -1;
+}
+
+static uint64_t phash_insert(struct orc_map *m, const void *key)
+{
+	if (m->pcount == m->pcap) {
+		m->pcap = m->pcap ? m->pcap * 2 : 16;
+		m->pkeys = realloc(m->pkeys, m->pcap * m->ksize);
+		m->pvals = realloc(m->pvals, m->pcap * (size_t)m->ncpu * m->vsize);
+	}
+	uint64_t i = m->pcount++;
+	memcpy(m->pkeys + i * m->ksize, key, m->ksize);
+	memset(m->pvals + i * (size_t)m->ncpu * m->vsize, 0, (size_t)m->ncpu * m->vsize);
+	return i;
+}
+
+static void phash_erase(struct orc_map *m, uint64_t i)
+{
+	size_t vs = (size_t)m->ncpu * m->vsize;
+	memmove(m->pkeys + i * m->ksize, m->pkeys + (i + 1) * m->ksize, (m->pcount - i - 1) * m->ksize);
+	memmove(m->pvals + i * vs, m->pvals + (i + 1) * vs, (m->pcount - i - 1) * vs);
+	m->pcount--;
+}
+
+/* ---- helper-side ops (bpf_map_handler::map_*_elem, from_syscall=false) ---- */
+void *orc_map_lookup(int fd, const void *key)
+{
+	struct orc_map *m = get(fd);
+	if (!m)
+		return NULL;
+	switch (m->type) {
+	case T_ARRAY: { /* array_map.cpp:27-35 */
+		uint32_t k = *(const uint32_t *)key;
+		if (k >= m->max_entries) {
+			g_errno = ENOENT;
+			return NULL;
+		}
+		return m->data + (size_t)k * m->vsize;
+	}
+	case T_PERCPU_ARRAY: { /* per_cpu_array_map.cpp:34-48 */
+		if (!key) {
+			g_errno = ENOENT;
+			return NULL;
+		}
+		uint32_t k = *(const uint32_t *)key;
+		if (k >= m->max_entries) {
+			g_errno = ENOENT;
+			return NULL;
+		}
+		return m->data + ((size_t)k * m->ncpu + (size_t)g_cpu) * m->vsize;
+	}
+	case T_HASH:
+		return hash_lookup(m, key);
+	case T_PERCPU_HASH: { /* per_cpu_hash_map.cpp:48-64 */
+		if (!key) {
+			g_errno = ENOENT;
+			return NULL;
+		}
+		int64_t i = phash_find(m, key);
+		if (i < 0) {
+			g_errno = ENOENT;
+			return NULL;
+		}
+		return m->pvals + ((size_t)i * m->ncpu + (size_t)g_cpu) * m->vsize;
+	}
+	}
+	return NULL;
+}
+
+long orc_map_update(int fd, const void *key, const void *value, uint64_t flags)
+{
+	struct orc_map *m = get(fd);
+	if (!m)
+		return -1;
+	switch (m->type) {
+	case T_ARRAY: /* array_map.cpp:37-56 */
+	case T_PERCPU_ARRAY: { /* per_cpu_array_map.cpp:50-73 */
+		if (!check_update_flags(flags))
+			return -1;
+		uint32_t k = *(const uint32_t *)key;
+		if (k < m->max_entries && flags == 1 /*BPF_NOEXIST*/) {
+			g_errno = EEXIST;
+			return -1;
+		}
+		if (k >= m->max_entries) {
+			g_errno = E2BIG;
+			return -1;
+		}
+		uint8_t *dst = m->type == T_ARRAY ? m->data + (size_t)k * m->vsize
+						  : m->data + ((size_t)k * m->ncpu + (size_t)g_cpu) * m->vsize;
+		memcpy(dst, value, m->vsize);
+		return 0;
+	}
+	case T_HASH: /* fix_hash_map.cpp:34-39: flags ignored, always 0 */
+		hash_update(m, key, value);
+		return 0;
+	case T_PERCPU_HASH: { /* per_cpu_hash_map.cpp:66-94: no max-entries check */
+		if (!check_update_flags(flags))
+			return -1;
+		int64_t i = phash_find(m, key);
+		if (i < 0)
+			i = (int64_t)phash_insert(m, key);
+		memcpy(m->pvals + ((size_t)i * m->ncpu + (size_t)g_cpu) * m->vsize, value, m->vsize);
+		return 0;
+	}
+	}
+	return -1;
+}
+
+long orc_map_delete(int fd, const void *key)
+{
+	struct orc_map *m = get(fd);
+	if (!m)
+		return -1;
+	switch (m->type) {
+	case T_ARRAY:
+	case T_PERCPU_ARRAY: /* array_map.cpp:58-64 */
+		g_errno = EINVAL;
+		return -1;
+	case T_HASH: /* fix_hash_map.cpp:41-45 */
+		hash_delete(m, key);
+		return 0;
+	case T_PERCPU_HASH: { /* per_cpu_hash_map.cpp:96-107: zeroes [0, cpu*vsize) */
+		int64_t i = phash_find(m, key);
+		if (i >= 0)
+			memset(m->pvals + (size_t)i * m->ncpu * m->vsize, 0, (size_t)g_cpu * m->vsize);
+		return 0;
+	}
+	}
+	return -1;
+}
+
+/* ---- syscall-side ops (from_syscall=true) ---- */
+void *orc_map_lookup_user(int fd, const void *key)
+{
+	struct orc_map *m = get(fd);
+	if (!m)
+		return NULL;
+	if (m->type == T_PERCPU_ARRAY) { /* per_cpu_array_map.cpp:97-108 */
+		uint32_t k = *(const uint32_t *)key;
+		if (k >= m->max_entries) {
+			g_errno = ENOENT;
+			return NULL;
+		}
+		return m->data + (size_t)k * m->ncpu * m->vsize;
+	}
+	if (m->type == T_PERCPU_HASH) { /* per_cpu_hash_map.cpp:141-155 */
+		int64_t i = phash_find(m, key);
+		if (i < 0) {
+			g_errno = ENOENT;
+			return NULL;
+		}
+		return m->pvals + (size_t)i * m->ncpu * m->vsize;
+	}
+	return orc_map_lookup(fd, key);
+}
+
+long orc_map_update_user(int fd, const void *key, const void *value, uint64_t flags)
+{
+	struct orc_map *m = get(fd);
+	if (!m)
+		return -1;
+	if (m->type == T_PERCPU_ARRAY) { /* per_cpu_array_map.cpp:110-131 */
+		if (!check_update_flags(flags))
+			return -1;
+		uint32_t k = *(const uint32_t *)key;
+		if (k < m->max_entries && flags == 1) {
+			g_errno = EEXIST;
+			return -1;
+		}
+		if (k >= m->max_entries) {
+			g_errno = E2BIG;
+			return -1;
+		}
+		memcpy(m->data + (size_t)k * m->ncpu * m->vsize, value, (size_t)m->ncpu * m->vsize);
+		return 0;
+	}
+	if (m->type == T_PERCPU_HASH) { /* per_cpu_hash_map.cpp:157-183 */
+		if (!check_update_flags(flags))
+			return -1;
+		int64_t i = phash_find(m, key);
+		if (flags == 1 && i >= 0) {
+			g_errno = EEXIST;
+			return -1;
+		}
+		if (flags == 2 && i < 0) {
+			g_errno = ENOENT;
+			return -1;
+		}
+		if (i < 0 && m->pcount == m->max_entries) {
+			g_errno = E2BIG;
+			return -1;
+		}
+		if (i < 0)
+			i = (int64_t)phash_insert(m, key);
+		memcpy(m->pvals + (size_t)i * m->ncpu * m->vsize, value, (size_t)m->ncpu * m->vsize);
+		return 0;
+	}
+	return orc_map_update(fd, key, value, flags);
+}
+
+long orc_map_delete_user(int fd, const void *key)
+{
+	struct orc_map *m = get(fd);
+	if (!m)
+		return -1;
+	if (m->type == T_PERCPU_HASH) { /* per_cpu_hash_map.cpp:184-195 */
+		int64_t i = phash_find(m, key);
+		if (i < 0) {
+			g_errno = ENOENT;
+			return -1;
+		}
+		phash_erase(m, (uint64_t)i);
+		return 0;
+	}
+	return orc_map_delete(fd, key);
+}
+
+int orc_map_get_next_key(int fd, const void *key, void *next_key)
+{
+	struct orc_map *m = get(fd);
+	if (!m)
+		return -1;
+	switch (m->type) {
+	case T_ARRAY:
+	case T_PERCPU_ARRAY: /* array_map.cpp:66-81 */
+		if (!key || *(const uint32_t *)key >= m->max_entries) {
+			*(uint32_t *)next_key = 0;
+			return 0;
+		}
+		if (*(const uint32_t *)key == m->max_entries - 1) {
+			g_errno = ENOENT;
+			return -1;
+		}
+		*(uint32_t *)next_key = *(const uint32_t *)key + 1;
+		return 0;
+	case T_HASH: { /* fix_hash_map.cpp:47-84: bucket index order */
+		uint64_t from = 0;
+		if (key) {
+			uint8_t *v = hash_lookup(m, key);
+			if (v)
+				from = (uint64_t)(v - m->data) / (4 + m->ksize + m->vsize) + 1;
+		}
+		for (uint64_t i = from; i < m->nbuckets; i++) {
+			uint8_t *s = slot(m, i);
+			if (*(uint32_t *)s) {
+				memcpy(next_key, s + 4, m->ksize);
+				return 0;
+			}
+		}
+		g_errno = ENOENT;
+		return -1;
+	}
+	case T_PERCPU_HASH: {
+		int64_t i = key ? phash_find(m, key) : -1;
+		uint64_t nx = i < 0 ? 0 : (uint64_t)i + 1;
+		if (nx >= m->pcount) {
+			g_errno = ENOENT;
+			return -1;
+		}
+		memcpy(next_key, m->pkeys + nx * m->ksize, m->ksize);
+		return 0;
+	}
+	}
+	return -1;
+}
+
+uint32_t orc_map_value_size_user(int fd)
+{
+	struct orc_map *m = get(fd);
+	if (!m)
+		return 0;
+	if (m->type == T_PERCPU_ARRAY || m->type == T_PERCPU_HASH)
+		return m->vsize * m->ncpu; /* map_handler.cpp:69-84 */
+	return m->vsize;
+}
+
+void *orc_map_raw(int fd, size_t *bytes)
+{
+	struct orc_map *m = get(fd);
+	if (!m)
+		return NULL;
+	switch (m->type) {
+	case T_ARRAY:
+		*bytes = (size_t)m->vsize * m->max_entries;
+		return m->data;
+	case T_PERCPU_ARRAY:
+		*bytes = (size_t)m->vsize * m->max_entries * m->ncpu;
+		return m->data;
+	case T_HASH:
+		*bytes = (size_t)m->nbuckets * (4 + m->ksize + m->vsize);
+		return m->data;
+	case T_PERCPU_HASH:
+		*bytes = (size_t)m->pcount * m->ncpu * m->vsize;
+		return m->pvals;
+	}
+	return NULL;
+}
+
+uint64_t orc_map_buckets(int fd)
+{
+	struct orc_map *m = get(fd);
+	return m ? m->nbuckets : 0;
+}
+
+uint64_t orc_map_count(int fd)
+{
+	struct orc_map *m = get(fd);
+	if (!m)
+		return 0;
+	return m->type == T_PERCPU_HASH ? m->pcount : m->count;
+}
+
+/* bpftime_shm.cpp:637-652: the map "pointer" is the fd itself */
+uint64_t orc_map_ptr_by_fd(uint32_t fd)
+{
+	if (!get((int)fd)) {
+		g_errno = ENOENT;
+		return ~0ULL;
+	}
+	return fd;
+}
+
+/* bpftime_shm.cpp:654-676: address of the value at get_next_key(NULL) */
+uint64_t orc_map_val(uint64_t map_ptr)
+{
+	int fd = (int)map_ptr;
+	struct orc_map *m = get(fd);
+	if (!m) {
+		g_errno = ENOENT;
+		return 0;
+	}
+	uint8_t key[256] = {0};
+	if (orc_map_get_next_key(fd, NULL, key) < 0) {
+		g_errno = ENOENT;
+		return 0;
+	}
+	return (uint64_t)(uintptr_t)orc_map_lookup(fd, key);
+}
