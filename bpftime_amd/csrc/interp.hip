@@ -359,6 +359,27 @@ __device__ uint64_t helper_xdp_load_bytes(uint64_t ctx, uint64_t off, uint64_t b
 // ---------------------------------------------------------------------------
 // The interpreter
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return readlane64(x, 0);
+}
+
+// One lane of the wave adds a cached counter delta (wave-uniform arguments).
+__device__ __forceinline__ void flush_delta(uint64_t a, uint32_t sz, uint64_t delta) {
+  if (a == 0 || delta == 0) return;
+  if ((threadIdx.x & 63) == 0) {
+    if (sz == 8)
+      __hip_atomic_fetch_add((uint64_t *)a, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      __hip_atomic_fetch_add((uint32_t *)a, (uint32_t)delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 #define RREG(i) Rf[(uint32_t)(i) * kBlock + tid]
 
 template <uint32_t KIND, bool BIGSTACK>
@@ -371,6 +392,9 @@ __global__ __launch_bounds__(kBlock) void k_interp(KParams p) {
   uint8_t *my_stack = dyn + kBlock * CTXB + tid * p.stack_size;
   uint64_t big_stack[BIGSTACK ? kStackSize / 8 : 1];
   const Win win{p.data_lo, p.data_hi, p.arena_lo, p.arena_hi, p.checked != 0};
+  // per-wave delta cache for fused counters (wave-uniform, lives in SGPRs)
+  uint64_t c0a = 0, c0d = 0, c1a = 0, c1d = 0;
+  uint32_t c0s = 0, c1s = 0;
   const uint64_t stack_top = BIGSTACK ? (uint64_t)(uintptr_t)(big_stack + kStackSize / 8)
                                       : (uint64_t)(uintptr_t)(my_stack + p.stack_size);
 
@@ -548,10 +572,38 @@ __global__ __launch_bounds__(kBlock) void k_interp(KParams p) {
         }
         case X_RMW_ADD: {
           // fused ldx/add/stx (loaded register proven dead by the loader)
+          // Counters hit by a whole wave (e.g. cntrs_array[0]) are summed across
+          // the wave and kept in a per-wave scalar delta cache flushed with one
+          // atomic at the end of the launch; otherwise one atomic per lane.
           const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
+          uint64_t a = 0, v = 0;
           if (sel) {
-            const uint64_t a = RREG(d.dst) + (int64_t)d.off;
-            const uint64_t v = OPB();
+            a = RREG(d.dst) + (int64_t)d.off;
+            v = OPB();
+          }
+          const uint64_t selm = __ballot(sel);
+          const int first = __builtin_ctzll(selm);
+          const uint64_t a0 = readlane64(a, first);
+          if (__ballot(sel && a != a0) == 0 && win.ok(a0, sz) && !is_lds_addr(a0) && !is_scratch_addr(a0)) {
+            const uint64_t v0 = readlane64(v, first);
+            uint64_t total;
+            if (__ballot(sel && v != v0) == 0)
+              total = v0 * (uint64_t)__builtin_popcountll(selm);
+            else
+              total = wave_sum64(sel ? v : 0);
+            if (c0a == a0 && c0s == sz) {
+              c0d += total;
+            } else if (c1a == a0 && c1s == sz) {
+              c1d += total;
+            } else if (c0a == 0) {
+              c0a = a0; c0s = sz; c0d = total;
+            } else if (c1a == 0) {
+              c1a = a0; c1s = sz; c1d = total;
+            } else {
+              flush_delta(c1a, c1s, c1d);
+              c1a = a0; c1s = sz; c1d = total;
+            }
+          } else if (sel) {
             if (win.ok(a, sz)) {
               if (sz == 8)
                 __hip_atomic_fetch_add((uint64_t *)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -706,7 +758,7 @@ __global__ __launch_bounds__(kBlock) void k_interp(KParams p) {
       }
       if (!uni && __ballot(alive) == 0) break;
       if (uni && op >= X_LDX && op <= X_RMW_ADD && __ballot(alive) == 0) break;
-      if (uni && op == X_CALL && __ballot(alive) == 0) break;
+      if (uni && (op == X_CALL || op == X_BAD || op >= X_NOP) && __ballot(alive) == 0) break;
     }
 
     if (active) {
@@ -729,6 +781,8 @@ __global__ __launch_bounds__(kBlock) void k_interp(KParams p) {
       }
     }
   }
+  flush_delta(c0a, c0s, c0d);
+  flush_delta(c1a, c1s, c1d);
 }
 #undef RREG
 

@@ -269,6 +269,10 @@ static void use_def(const DInsn &d, RegSet &use, RegSet &def) {
       D(0);
       break;
     case X_EXIT: U(0); break;
+    case X_RMW_ADD:
+      U(d.dst);
+      if (d.aux & A_SRCREG) U(d.src);
+      break;
     default: break;
   }
 }
@@ -279,6 +283,7 @@ static void successors(const std::vector<DInsn> &p, uint32_t i, uint32_t s[2], i
   switch (d.op) {
     case X_EXIT: return;
     case X_JA: s[ns++] = d.tgt; return;
+    case X_RMW_ADD: if (d.tgt < p.size()) s[ns++] = d.tgt; return;
     case X_LDDW: if (i + 2 < p.size()) s[ns++] = i + 2; return;
     case X_JEQ: case X_JGT: case X_JGE: case X_JSET: case X_JNE: case X_JSGT: case X_JSGE:
     case X_JLT: case X_JLE: case X_JSLT: case X_JSLE:
@@ -352,6 +357,10 @@ static int stack_depth(const std::vector<DInsn> &p, const std::vector<bool> &rea
         break;
       case X_ST:
         base_access(d.dst, 0);
+        break;
+      case X_RMW_ADD:
+        base_access(d.dst, 0);
+        if ((d.aux & A_SRCREG) && (st[d.src].kind == 1 || st[d.src].kind == 3)) escape = true;
         break;
       case X_STX:
         base_access(d.dst, 0);
@@ -585,6 +594,11 @@ int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &
     out.stack_size = (uint32_t)std::max(8, (depth + 7) & ~7);
   }
   out.fused_rmw = fused;
+  // sentinel: a program that falls off its end fails its lanes on the device
+  // instead of fetching past the allocation
+  DInsn sentinel{};
+  sentinel.op = X_BAD;
+  p.push_back(sentinel);
   out.prog = std::move(p);
   return 0;
 }
