@@ -1,0 +1,369 @@
+// bpftime_amd: device-side helpers of the interpreter (maps, XDP helpers,
+// wave utilities).  Included by interp.hip only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "common.hpp"
+
+namespace bpftime_amd {
+
+__device__ __forceinline__ bool is_lds_addr(uint64_t a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_is_shared((const void *)a);
+#else
+  return false;
+#endif
+}
+__device__ __forceinline__ bool is_scratch_addr(uint64_t a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_is_private((const void *)a);
+#else
+  return false;
+#endif
+}
+
+typedef uint16_t u16u __attribute__((aligned(1)));
+typedef uint32_t u32u __attribute__((aligned(1)));
+typedef uint64_t u64u __attribute__((aligned(1)));
+
+// Sized load/store on a flat address (LDS, scratch or global); the size is
+// wave-uniform so the switch is a scalar branch.
+__device__ __forceinline__ uint64_t mem_load(uint64_t a, uint32_t sz) {
+  switch (sz) {
+    case 1: return *(const volatile uint8_t *)a;
+    case 2: return *(const u16u *)a;
+    case 4: return *(const u32u *)a;
+    default: return *(const u64u *)a;
+  }
+}
+__device__ __forceinline__ void mem_store(uint64_t a, uint32_t sz, uint64_t v) {
+  switch (sz) {
+    case 1: *(uint8_t *)a = (uint8_t)v; break;
+    case 2: *(u16u *)a = (uint16_t)v; break;
+    case 4: *(u32u *)a = (uint32_t)v; break;
+    default: *(u64u *)a = v; break;
+  }
+}
+
+struct Win {
+  uint64_t lo1, hi1, lo2, hi2;
+  bool checked;
+  __device__ __forceinline__ bool ok(uint64_t a, uint32_t sz) const {
+    if (!checked) return true;
+    if (is_lds_addr(a) || is_scratch_addr(a)) return true;
+    uint64_t e = a + sz;
+    return (a >= lo1 && e <= hi1 && e >= a) || (a >= lo2 && e <= hi2 && e >= a);
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Device maps (helpers 1/2/3).  Semantics follow the reference helper view:
+//   array_map.cpp:27-64, fix_hash_map.cpp:27-45 over bpftime_hash_map.hpp,
+//   per_cpu_array_map.cpp:34-80, per_cpu_hash_map.cpp:48-107.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t key_hash(uint64_t key, uint32_t ks) {
+  // bpftime_hash_map.hpp:40-47: h = h*31 + byte over size_t
+  uint64_t h = 0;
+  for (uint32_t i = 0; i < ks; i++) h = h * 31 + *(const volatile uint8_t *)(key + i);
+  return h;
+}
+
+__device__ __forceinline__ uint32_t ald32(uint64_t a) {
+  return __hip_atomic_load((uint32_t *)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint8_t ald8(uint64_t a) {
+  uint64_t w = a & ~3ull;
+  uint32_t v = ald32(w);
+  return (uint8_t)(v >> ((a & 3) * 8));
+}
+
+// Compare the program-side key (any alignment, any memory) with a slot key
+// (8-aligned, published with agent-scope stores).
+__device__ __forceinline__ bool key_eq(uint64_t slot_key, uint64_t key, uint32_t ks) {
+  uint32_t i = 0;
+  for (; i + 4 <= ks; i += 4) {
+    uint32_t kv = *(const u32u *)(key + i);
+    if (ald32(slot_key + i) != kv) return false;
+  }
+  for (; i < ks; i++) {
+    if (ald8(slot_key + i) != *(const volatile uint8_t *)(key + i)) return false;
+  }
+  return true;
+}
+
+__device__ __forceinline__ void copy_bytes_publish(uint64_t dst, uint64_t src, uint32_t n) {
+  // dst is 8-aligned device memory; src is any flat address.
+  uint32_t i = 0;
+  for (; i + 4 <= n; i += 4)
+    __hip_atomic_store((uint32_t *)(dst + i), *(const u32u *)(src + i), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  if (i < n) {
+    uint32_t w = 0;
+    for (uint32_t j = 0; i + j < n; j++) w |= (uint32_t)(*(const volatile uint8_t *)(src + i + j)) << (8 * j);
+    __hip_atomic_store((uint32_t *)(dst + i), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__device__ __forceinline__ void copy_bytes(uint64_t dst, uint64_t src, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++)
+    *(volatile uint8_t *)(dst + i) = *(const volatile uint8_t *)(src + i);
+}
+
+constexpr uint32_t ST_EMPTY = 0, ST_FILLED = 1, ST_BUSY = 2;
+
+// Find `key`; if absent and `insert`, claim a slot and publish key + init
+// value (init == 0 -> zero).  Returns slot address or 0.  *inserted tells
+// whether this lane created the element.  The probe order is the
+// reference's: start at hash % nbuckets, linear, wrap once
+// (bpftime_hash_map.hpp:127-180).  Lanes never wait on a lane of their own
+// wave: a BUSY slot is re-read on the next loop trip, by which time the
+// claiming lane (same wave, same trip) has published it.
+__device__ uint64_t hash_find(const DMap &m, uint64_t key, bool insert, uint64_t init,
+                              uint32_t init_bytes, bool *inserted) {
+  *inserted = false;
+  uint64_t nb = m.nbuckets;
+  uint64_t idx = key_hash(key, m.key_size) % nb;
+  uint64_t start = idx;
+  uint32_t spins = 0;
+  for (;;) {
+    uint64_t s = m.data + idx * (uint64_t)m.slot_size;
+    uint32_t st = ald32(s);
+    if (st == ST_EMPTY) {
+      if (!insert) return 0;
+      // element count check (bpftime_hash_map.hpp:153-156)
+      unsigned long long c = atomicAdd((unsigned long long *)m.count_addr, 1ull);
+      if (c >= m.max_entries) {
+        atomicAdd((unsigned long long *)m.count_addr, ~0ull);  // undo
+        return 0;
+      }
+      uint32_t prev = atomicCAS((uint32_t *)s, ST_EMPTY, ST_BUSY);
+      if (prev == ST_EMPTY) {
+        copy_bytes_publish(s + m.key_off, key, m.key_size);
+        if (init)
+          copy_bytes_publish(s + m.val_off, init, init_bytes);
+        else
+          for (uint32_t i = 0; i < init_bytes; i += 4)
+            __hip_atomic_store((uint32_t *)(s + m.val_off + i), 0u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __hip_atomic_store((uint32_t *)s, ST_FILLED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        *inserted = true;
+        return s;
+      }
+      atomicAdd((unsigned long long *)m.count_addr, ~0ull);  // lost the race: undo
+      st = prev;
+    }
+    if (st == ST_BUSY) {
+      if (++spins > (1u << 22)) return 0;  // bounded: never hang the GPU
+      __builtin_amdgcn_s_sleep(1);
+      continue;  // re-read the same slot on the next trip
+    }
+    if (key_eq(s + m.key_off, key, m.key_size)) return s;
+    idx = idx + 1 == nb ? 0 : idx + 1;
+    if (idx == start) return 0;
+  }
+}
+
+struct LaneEnv {
+  uint64_t vcpu;
+  // last lookup miss (map fd, key hash) for the lookup_or_try_init race rule
+  int32_t miss_fd;
+  uint64_t miss_hash;
+};
+
+__device__ uint64_t helper_lookup(const DMap *maps, uint64_t fd, uint64_t key, LaneEnv &env) {
+  if (fd >= kMaxFds) return 0;
+  const DMap m = maps[fd];
+  switch (m.type) {
+    case MT_ARRAY: {
+      uint32_t k = *(const u32u *)key;
+      if (k >= m.max_entries) return 0;
+      return m.data + (uint64_t)k * m.value_size;
+    }
+    case MT_PERCPU_ARRAY: {
+      uint32_t k = *(const u32u *)key;
+      if (k >= m.max_entries) return 0;
+      return m.data + ((uint64_t)k * m.ncpu + env.vcpu % m.ncpu) * m.value_size;
+    }
+    case MT_HASH:
+    case MT_PERCPU_HASH: {
+      bool ins;
+      uint64_t s = hash_find(m, key, false, 0, 0, &ins);
+      if (!s) {
+        env.miss_fd = (int32_t)fd;
+        env.miss_hash = key_hash(key, m.key_size);
+        return 0;
+      }
+      uint64_t v = s + m.val_off;
+      if (m.type == MT_PERCPU_HASH) v += (env.vcpu % m.ncpu) * m.value_size;
+      return v;
+    }
+  }
+  return 0;
+}
+
+__device__ uint64_t helper_update(const DMap *maps, uint64_t fd, uint64_t key, uint64_t val,
+                                  uint64_t flags, LaneEnv &env) {
+  if (fd >= kMaxFds) return (uint64_t)-1;
+  const DMap m = maps[fd];
+  uint64_t base = flags & 0xffffffffull;
+  bool flags_ok = base == 0 || base == 1 || base == 2;  // map_common_def.hpp:83-94
+  switch (m.type) {
+    case MT_ARRAY:
+    case MT_PERCPU_ARRAY: {
+      if (!flags_ok) return (uint64_t)-1;
+      uint32_t k = *(const u32u *)key;
+      if (k < m.max_entries && flags == 1) return (uint64_t)-1;  // EEXIST
+      if (k >= m.max_entries) return (uint64_t)-1;               // E2BIG
+      uint64_t dst = m.type == MT_ARRAY
+                         ? m.data + (uint64_t)k * m.value_size
+                         : m.data + ((uint64_t)k * m.ncpu + env.vcpu % m.ncpu) * m.value_size;
+      copy_bytes(dst, val, m.value_size);
+      return 0;
+    }
+    case MT_HASH: {
+      // fix_hash_map.cpp:34-39: flags ignored, returns 0 even when full.
+      bool ins;
+      uint32_t vbytes = (m.value_size + 3) & ~3u;
+      uint64_t s = hash_find(m, key, true, val, m.value_size, &ins);
+      if (s && !ins) {
+        // Existing element: overwrite, except in the lookup-miss race (this
+        // lane's previous lookup of the same key missed, so in any serial
+        // order this update would have created the element): another lane
+        // created it first, and overwriting would drop its updates.
+        bool race = env.miss_fd == (int32_t)fd && env.miss_hash == key_hash(key, m.key_size);
+        if (!race) copy_bytes(s + m.val_off, val, m.value_size);
+      }
+      (void)vbytes;
+      env.miss_fd = -1;
+      return 0;
+    }
+    case MT_PERCPU_HASH: {
+      if (!flags_ok) return (uint64_t)-1;
+      // per_cpu_hash_map.cpp:66-94: insert zeroed ncpu*vsize, then write slot
+      bool ins;
+      uint64_t s = hash_find(m, key, true, 0, m.value_size * m.ncpu, &ins);
+      if (!s) return 0;
+      bool race = !ins && env.miss_fd == (int32_t)fd && env.miss_hash == key_hash(key, m.key_size);
+      if (!race) copy_bytes(s + m.val_off + (env.vcpu % m.ncpu) * m.value_size, val, m.value_size);
+      env.miss_fd = -1;
+      return 0;
+    }
+  }
+  return (uint64_t)-1;
+}
+
+__device__ uint64_t helper_delete(const DMap *maps, uint64_t fd, uint64_t key, LaneEnv &env) {
+  if (fd >= kMaxFds) return (uint64_t)-1;
+  const DMap m = maps[fd];
+  switch (m.type) {
+    case MT_ARRAY:
+    case MT_PERCPU_ARRAY:
+      return (uint64_t)-1;  // EINVAL (array_map.cpp:58-64)
+    case MT_HASH: {
+      bool ins;
+      uint64_t s = hash_find(m, key, false, 0, 0, &ins);
+      if (s) {
+        uint32_t prev = atomicCAS((uint32_t *)s, ST_FILLED, ST_EMPTY);  // no tombstone
+        if (prev == ST_FILLED) atomicAdd((unsigned long long *)m.count_addr, ~0ull);
+      }
+      return 0;
+    }
+    case MT_PERCPU_HASH: {
+      // per_cpu_hash_map.cpp:96-107: zeroes [0, cpu*vsize) of the element
+      bool ins;
+      uint64_t s = hash_find(m, key, false, 0, 0, &ins);
+      if (s) {
+        uint64_t n = (env.vcpu % m.ncpu) * m.value_size;
+        for (uint64_t i = 0; i < n; i++) *(volatile uint8_t *)(s + m.val_off + i) = 0;
+      }
+      return 0;
+    }
+  }
+  return (uint64_t)-1;
+}
+
+// bpf_helper.cpp:713-744
+__device__ uint64_t helper_csum_diff(uint64_t from, uint64_t from_size_, uint64_t to,
+                                     uint64_t to_size_, uint64_t seed_) {
+  int from_size = (int)from_size_, to_size = (int)to_size_;
+  int csum = -22;
+  if ((from_size % 4 != 0) || (to_size % 4 != 0)) return (uint64_t)(int64_t)csum;
+  csum = (int)seed_;
+  if (to)
+    for (int i = 0; i < to_size / 2; i++) csum += (uint16_t)(*(const u16u *)(to + 2 * i));
+  if (from)
+    for (int i = 0; i < from_size / 2; i++) csum += (uint16_t)(~*(const u16u *)(from + 2 * i));
+  if (csum < 0) csum = -22;
+  return (uint64_t)(int64_t)csum;
+}
+
+// xdp_md_userspace (runtime/extension/userspace_xdp.h:6-17)
+struct XdpCtx {
+  uint64_t data, data_end;
+  uint32_t data_meta, ingress_ifindex, rx_queue_index, egress_ifindex;
+  uint64_t buffer_start, buffer_end;
+};
+
+// bpf_helper.cpp:748-764
+__device__ uint64_t helper_adjust_head(uint64_t ctx, uint64_t off_) {
+  volatile XdpCtx *x = (volatile XdpCtx *)ctx;
+  int offset = (int)off_;
+  uint64_t data = x->data + (int64_t)offset;
+  if (data > x->data_end - 14 || data > x->buffer_end) return (uint64_t)(int64_t)-22;
+  if (data < x->buffer_start) {
+    // memmove(buffer_start + (buffer_start - data), data, data_end - data)
+    uint64_t dst = x->buffer_start + (x->buffer_start - data), src = x->data;
+    uint64_t n = x->data_end - x->data;
+    if (dst > src)
+      for (uint64_t i = n; i-- > 0;) *(volatile uint8_t *)(dst + i) = *(volatile uint8_t *)(src + i);
+    else
+      for (uint64_t i = 0; i < n; i++) *(volatile uint8_t *)(dst + i) = *(volatile uint8_t *)(src + i);
+    data = x->buffer_start;
+  }
+  x->data = data;
+  return 0;
+}
+
+// bpf_helper.cpp:766-776
+__device__ uint64_t helper_adjust_tail(uint64_t ctx, uint64_t delta_) {
+  volatile XdpCtx *x = (volatile XdpCtx *)ctx;
+  int delta = (int)delta_;
+  uint64_t data = x->data_end + (int64_t)delta;
+  if (data < x->data || data < x->buffer_start || data > x->buffer_end) return (uint64_t)(int64_t)-22;
+  x->data_end = data;
+  return 0;
+}
+
+// bpf_helper.cpp:778-788 (defined in the reference, not registered by default)
+__device__ uint64_t helper_xdp_load_bytes(uint64_t ctx, uint64_t off, uint64_t buf, uint64_t len) {
+  volatile XdpCtx *x = (volatile XdpCtx *)ctx;
+  uint64_t data = x->data + (uint32_t)off;
+  if (data + (uint32_t)len > x->data_end) return (uint64_t)(int64_t)-22;
+  copy_bytes(buf, data, (uint32_t)len);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return readlane64(x, 0);
+}
+
+// One lane of the wave adds a cached counter delta (wave-uniform arguments).
+__device__ __forceinline__ void flush_delta(uint64_t a, uint32_t sz, uint64_t delta) {
+  if (a == 0 || delta == 0) return;
+  if ((threadIdx.x & 63) == 0) {
+    if (sz == 8)
+      __hip_atomic_fetch_add((uint64_t *)a, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      __hip_atomic_fetch_add((uint32_t *)a, (uint32_t)delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+}  // namespace bpftime_amd

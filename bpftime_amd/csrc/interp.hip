@@ -4,797 +4,535 @@
 //   bpftime_prog::bpftime_prog_exec (runtime/src/bpftime_prog.cpp:231-260)
 //   -> ebpf_exec (vm/vm-core/src/ebpf-vm.cpp:56-60) -> ubpf_exec
 // with one wave64 lane per unit.  Design:
-//  * the program is pre-decoded to 16-B DInsn records and fetched with scalar
-//    loads: the pc is wave-uniform, so dispatch is a scalar branch tree;
-//  * uniform branches take a ballot fast path; a split branch switches the
-//    wave to per-lane pcs and min-pc scheduling until the lanes reconverge;
+//  * the program is pre-decoded to 16-B DInsn records fetched with scalar
+//    loads (the pc is wave-uniform) and dispatched by a scalar branch tree;
+//  * two interpreter loops: a UNIFORM loop (all live lanes at one pc: no
+//    per-lane pc, every case straight-line for the whole wave) and a
+//    DIVERGENT loop (per-lane pcs, min-pc scheduling, writes predicated by
+//    the selected lanes).  A split branch moves the wave from the first to
+//    the second; the second hands back as soon as the live lanes reconverge;
+//  * case bodies are branch-free: memory ops of lanes that must not act are
+//    redirected to a per-lane dummy LDS slot, so the compiler emits no
+//    exec-mask flow blocks per case;
+//  * helper calls leave both loops and run in the outer loop, keeping the
+//    helpers' divergent code (hash probing, copies) out of the hot loops;
 //  * r0-r10 live in LDS, lane-major (conflict-free ds_read_b64);
 //  * the XDP ctx (48 B) and a stack sized by the loader's analysis live in
-//    LDS; packet bytes and map values are read in place from HBM through
-//    flat addresses;
-//  * global accesses are confined to the batch window and the map arena
-//    (a faulting program fails its lanes, never the GPU).
+//    LDS; packet bytes and map values are read in place through flat
+//    addresses; global accesses are confined to the batch window and the
+//    map arena (a faulting program fails its lanes, never the GPU);
+//  * fused ldx/add/stx counters hit by a whole wave are summed across the
+//    wave into a per-wave delta cache flushed once per launch.
 #include <hip/hip_runtime.h>
+
 #include "common.hpp"
+#include "dev_helpers.hpp"
 
 namespace bpftime_amd {
 
-__device__ __forceinline__ bool is_lds_addr(uint64_t a) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_is_shared((const void *)a);
-#else
-  return false;
-#endif
-}
-__device__ __forceinline__ bool is_scratch_addr(uint64_t a) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_is_private((const void *)a);
-#else
-  return false;
-#endif
+// Helper dispatch (helper id is wave-uniform); returns r0, sets *err.
+__device__ __forceinline__ uint64_t call_helper(uint32_t id, uint64_t a1, uint64_t a2, uint64_t a3, uint64_t a4,
+                                                uint64_t a5, const DMap *maps, uint32_t ncpu, uint64_t seed,
+                                                LaneEnv &env, uint32_t *err) {
+  switch (id) {
+    case 1: return helper_lookup(maps, a1, a2, env);
+    case 2: return helper_update(maps, a1, a2, a3, a4, env);
+    case 3: return helper_delete(maps, a1, a2, env);
+    case 5: return (uint64_t)__builtin_amdgcn_s_memrealtime() * 10ull;
+    case 7: {
+      uint64_t x = seed * 0x9E3779B97F4A7C15ull;
+      x ^= x >> 31;
+      x *= 0xBF58476D1CE4E5B9ull;
+      x ^= x >> 29;
+      return (uint32_t)x;
+    }
+    case 8: return env.vcpu % ncpu;
+    case 28: return helper_csum_diff(a1, a2, a3, a4, a5);
+    case 44: return helper_adjust_head(a1, a2);
+    case 65: return helper_adjust_tail(a1, a2);
+    case 189: return helper_xdp_load_bytes(a1, a2, a3, a4);
+  }
+  *err = E_BADOP;
+  return 0;
 }
 
-typedef uint16_t u16u __attribute__((aligned(1)));
-typedef uint32_t u32u __attribute__((aligned(1)));
-typedef uint64_t u64u __attribute__((aligned(1)));
-
-// Sized load/store on a flat address (LDS, scratch or global); the size is
-// wave-uniform so the switch is a scalar branch.
-__device__ __forceinline__ uint64_t mem_load(uint64_t a, uint32_t sz) {
-  switch (sz) {
-    case 1: return *(const volatile uint8_t *)a;
-    case 2: return *(const u16u *)a;
-    case 4: return *(const u32u *)a;
-    default: return *(const u64u *)a;
-  }
+// Copy a wave-uniform value into a fresh SGPR (an explicit s_mov, so the
+// result is not tied to the kernel-argument tuple it was loaded into).
+__device__ __forceinline__ uint64_t sreg(uint64_t v) {
+  uint64_t o;
+  asm volatile("s_mov_b64 %0, %1" : "=s"(o) : "s"(v));
+  return o;
 }
-__device__ __forceinline__ void mem_store(uint64_t a, uint32_t sz, uint64_t v) {
-  switch (sz) {
-    case 1: *(uint8_t *)a = (uint8_t)v; break;
-    case 2: *(u16u *)a = (uint16_t)v; break;
-    case 4: *(u32u *)a = (uint32_t)v; break;
-    default: *(u64u *)a = v; break;
-  }
+__device__ __forceinline__ uint32_t sreg(uint32_t v) {
+  uint32_t o;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(o) : "s"(v));
+  return o;
 }
 
-struct Win {
-  uint64_t lo1, hi1, lo2, hi2;
-  bool checked;
-  __device__ __forceinline__ bool ok(uint64_t a, uint32_t sz) const {
-    if (!checked) return true;
-    if (is_lds_addr(a) || is_scratch_addr(a)) return true;
-    uint64_t e = a + sz;
-    return (a >= lo1 && e <= hi1 && e >= a) || (a >= lo2 && e <= hi2 && e >= a);
-  }
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef const u32x4 __attribute__((address_space(4))) *prog_ptr;
+
+// loop exits
+constexpr uint32_t R_DONE = 0, R_DIVERGE = 1, R_RECONV = 2, R_CALL = 3;
+
+// Everything one interpreter loop reads or updates (inlined; SROA'd).
+struct Ctx {
+  uint64_t *R;           // this lane's register file column: R[i * kBlock]
+  prog_ptr prog;
+  Win win;
+  uint64_t dummy;        // flat address of this lane's dummy LDS slot
+  uint32_t *verdicts;
+  uint64_t *rets;
+  uint64_t unit;
+  uint32_t step_limit;
+  // mutable state
+  uint32_t pc;           // uniform loop: the wave's pc
+  uint32_t lpc;          // divergent loop: this lane's pc
+  uint32_t steps;
+  bool alive;
+  uint32_t err;
+  uint32_t call_pc, call_id;
+  uint64_t c0a, c0d, c1a, c1d;  // per-wave fused-counter delta cache
+  uint32_t c0s, c1s;
 };
 
-// ---------------------------------------------------------------------------
-// Device maps (helpers 1/2/3).  Semantics follow the reference helper view:
-//   array_map.cpp:27-64, fix_hash_map.cpp:27-45 over bpftime_hash_map.hpp,
-//   per_cpu_array_map.cpp:34-80, per_cpu_hash_map.cpp:48-107.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t key_hash(uint64_t key, uint32_t ks) {
-  // bpftime_hash_map.hpp:40-47: h = h*31 + byte over size_t
-  uint64_t h = 0;
-  for (uint32_t i = 0; i < ks; i++) h = h * 31 + *(const volatile uint8_t *)(key + i);
-  return h;
-}
+#define RG(i) c.R[(uint32_t)(i) * kBlock]
 
-__device__ __forceinline__ uint32_t ald32(uint64_t a) {
-  return __hip_atomic_load((uint32_t *)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint8_t ald8(uint64_t a) {
-  uint64_t w = a & ~3ull;
-  uint32_t v = ald32(w);
-  return (uint8_t)(v >> ((a & 3) * 8));
-}
-
-// Compare the program-side key (any alignment, any memory) with a slot key
-// (8-aligned, published with agent-scope stores).
-__device__ __forceinline__ bool key_eq(uint64_t slot_key, uint64_t key, uint32_t ks) {
-  uint32_t i = 0;
-  for (; i + 4 <= ks; i += 4) {
-    uint32_t kv = *(const u32u *)(key + i);
-    if (ald32(slot_key + i) != kv) return false;
-  }
-  for (; i < ks; i++) {
-    if (ald8(slot_key + i) != *(const volatile uint8_t *)(key + i)) return false;
-  }
-  return true;
-}
-
-__device__ __forceinline__ void copy_bytes_publish(uint64_t dst, uint64_t src, uint32_t n) {
-  // dst is 8-aligned device memory; src is any flat address.
-  uint32_t i = 0;
-  for (; i + 4 <= n; i += 4)
-    __hip_atomic_store((uint32_t *)(dst + i), *(const u32u *)(src + i), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  if (i < n) {
-    uint32_t w = 0;
-    for (uint32_t j = 0; i + j < n; j++) w |= (uint32_t)(*(const volatile uint8_t *)(src + i + j)) << (8 * j);
-    __hip_atomic_store((uint32_t *)(dst + i), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-__device__ __forceinline__ void copy_bytes(uint64_t dst, uint64_t src, uint32_t n) {
-  for (uint32_t i = 0; i < n; i++)
-    *(volatile uint8_t *)(dst + i) = *(const volatile uint8_t *)(src + i);
-}
-
-constexpr uint32_t ST_EMPTY = 0, ST_FILLED = 1, ST_BUSY = 2;
-
-// Find `key`; if absent and `insert`, claim a slot and publish key + init
-// value (init == 0 -> zero).  Returns slot address or 0.  *inserted tells
-// whether this lane created the element.  The probe order is the
-// reference's: start at hash % nbuckets, linear, wrap once
-// (bpftime_hash_map.hpp:127-180).  Lanes never wait on a lane of their own
-// wave: a BUSY slot is re-read on the next loop trip, by which time the
-// claiming lane (same wave, same trip) has published it.
-__device__ uint64_t hash_find(const DMap &m, uint64_t key, bool insert, uint64_t init,
-                              uint32_t init_bytes, bool *inserted) {
-  *inserted = false;
-  uint64_t nb = m.nbuckets;
-  uint64_t idx = key_hash(key, m.key_size) % nb;
-  uint64_t start = idx;
-  uint32_t spins = 0;
+// Runs the program until the wave exits, diverges / reconverges, or calls
+// a helper.  UNI: every live lane is at c.pc and selected.
+template <bool UNI>
+__device__ __forceinline__ uint32_t run_loop(Ctx &c) {
   for (;;) {
-    uint64_t s = m.data + idx * (uint64_t)m.slot_size;
-    uint32_t st = ald32(s);
-    if (st == ST_EMPTY) {
-      if (!insert) return 0;
-      // element count check (bpftime_hash_map.hpp:153-156)
-      unsigned long long c = atomicAdd((unsigned long long *)m.count_addr, 1ull);
-      if (c >= m.max_entries) {
-        atomicAdd((unsigned long long *)m.count_addr, ~0ull);  // undo
-        return 0;
+    uint32_t cur;
+    bool sel;
+    if (UNI) {
+      cur = c.pc;
+      sel = c.alive;
+    } else {
+      const uint32_t m = c.alive ? c.lpc : 0xffffffffu;
+      cur = __reduce_min_sync(~0ull, m);
+      if (cur == 0xffffffffu) return R_DONE;
+      if (__ballot(c.alive && c.lpc != cur) == 0) {
+        c.pc = cur;
+        return R_RECONV;
       }
-      uint32_t prev = atomicCAS((uint32_t *)s, ST_EMPTY, ST_BUSY);
-      if (prev == ST_EMPTY) {
-        copy_bytes_publish(s + m.key_off, key, m.key_size);
-        if (init)
-          copy_bytes_publish(s + m.val_off, init, init_bytes);
-        else
-          for (uint32_t i = 0; i < init_bytes; i += 4)
-            __hip_atomic_store((uint32_t *)(s + m.val_off + i), 0u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __hip_atomic_store((uint32_t *)s, ST_FILLED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        *inserted = true;
-        return s;
+      sel = c.alive && c.lpc == cur;
+    }
+    cur = __builtin_amdgcn_readfirstlane(cur);
+    if (++c.steps > c.step_limit) {
+      c.err = c.alive ? E_STEPS : c.err;
+      c.alive = false;
+      return R_DONE;
+    }
+    const u32x4 raw = c.prog[cur];
+    DInsn d;
+    __builtin_memcpy(&d, &raw, sizeof(d));
+    const uint32_t op = d.op;
+    const bool srcreg = (d.aux & A_SRCREG) != 0;
+    const bool w32 = (d.aux & A_W32) != 0;
+    const uint64_t mask = w32 ? 0xffffffffull : ~0ull;
+    uint32_t npc = cur + 1;
+
+// write a register (only selected lanes in the divergent loop)
+#define WRO(r, val, old) RG(r) = (UNI || sel) ? (uint64_t)(val) : (uint64_t)(old)
+#define OPB(rv) (srcreg ? (rv) : (uint64_t)(int64_t)d.imm)
+#define ALU(expr)                              \
+  {                                            \
+    const uint64_t a = RG(d.dst);              \
+    const uint64_t b = OPB(RG(d.src));         \
+    WRO(d.dst, (expr), a);                     \
+    break;                                     \
+  }
+#define JMP_TAKEN(cond)                        \
+  {                                            \
+    taken = sel && (cond);                     \
+    is_jmp = true;                             \
+    break;                                     \
+  }
+    bool is_jmp = false, taken = false;
+    uint64_t ja = 0, jb = 0;
+    if (op >= X_JEQ && op <= X_JSLE) {
+      ja = RG(d.dst);
+      jb = OPB(RG(d.src));
+    }
+    switch (op) {
+      case X_ADD: ALU((a + b) & mask)
+      case X_SUB: ALU((a - b) & mask)
+      case X_MUL: ALU((a * b) & mask)
+      case X_OR: ALU((a | b) & mask)
+      case X_AND: ALU((a & b) & mask)
+      case X_XOR: ALU((a ^ b) & mask)
+      case X_MOV: ALU(b & mask)
+      case X_DIV64: ALU(b ? a / b : 0)
+      case X_MOD64: ALU(b ? a % b : a)
+      case X_LSH64: ALU(a << (b & 63))
+      case X_RSH64: ALU(a >> (b & 63))
+      case X_ARSH64: ALU((uint64_t)((int64_t)a >> (b & 63)))
+      case X_NEG64: ALU((uint64_t)(-(int64_t)a))
+      case X_DIV32: ALU((uint32_t)b ? (uint64_t)((uint32_t)a / (uint32_t)b) : 0)
+      case X_MOD32: ALU((uint32_t)b ? (uint64_t)((uint32_t)a % (uint32_t)b) : (uint64_t)(uint32_t)a)
+      case X_LSH32: ALU((uint64_t)(uint32_t)((uint32_t)a << (b & 31)))
+      case X_RSH32: ALU((uint64_t)((uint32_t)a >> (b & 31)))
+      case X_ARSH32: ALU((uint64_t)(uint32_t)((int32_t)a >> (b & 31)))
+      case X_NEG32: ALU((uint64_t)(uint32_t)(-(int64_t)a))
+      case X_LE: ALU(d.imm == 16 ? (uint64_t)(uint16_t)a : d.imm == 32 ? (uint64_t)(uint32_t)a : a)
+      case X_BE:
+        ALU(d.imm == 16   ? (uint64_t)__builtin_bswap16((uint16_t)a)
+            : d.imm == 32 ? (uint64_t)__builtin_bswap32((uint32_t)a)
+            : d.imm == 64 ? __builtin_bswap64(a)
+                          : a)
+      case X_LDDW: {
+        const uint64_t v = (uint64_t)(uint32_t)d.imm | ((uint64_t)(uint32_t)d.hi << 32);
+        if (UNI) RG(d.dst) = v;
+        else WRO(d.dst, v, RG(d.dst));
+        npc = cur + 2;
+        break;
       }
-      atomicAdd((unsigned long long *)m.count_addr, ~0ull);  // lost the race: undo
-      st = prev;
+      case X_LDX: {
+        const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
+        const uint64_t a = RG(d.src) + (int64_t)d.off;
+        const bool ok = c.win.ok(a, sz);
+        const uint64_t v = mem_load(sel && ok ? a : c.dummy, sz);
+        if (UNI) RG(d.dst) = v;
+        else WRO(d.dst, v, RG(d.dst));
+        if (__ballot(sel && !ok) != 0) {
+          c.err = (sel && !ok) ? E_OOB : c.err;
+          c.alive = c.alive && !(sel && !ok);
+          if (__ballot(c.alive) == 0) return R_DONE;
+        }
+        break;
+      }
+      case X_ST:
+      case X_STX: {
+        const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
+        const uint64_t a = RG(d.dst) + (int64_t)d.off;
+        const uint64_t v = op == X_STX ? RG(d.src) : (uint64_t)(int64_t)d.imm;
+        const bool ok = c.win.ok(a, sz);
+        mem_store(sel && ok ? a : c.dummy, sz, v);
+        if (__ballot(sel && !ok) != 0) {
+          c.err = (sel && !ok) ? E_OOB : c.err;
+          c.alive = c.alive && !(sel && !ok);
+          if (__ballot(c.alive) == 0) return R_DONE;
+        }
+        break;
+      }
+      case X_RMW_ADD: {
+        // Counters hit by a whole wave (e.g. cntrs_array[0]) are summed across
+        // the wave into the per-wave delta cache; otherwise one atomic per lane.
+        const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
+        const uint64_t a = RG(d.dst) + (int64_t)d.off;
+        const uint64_t v = OPB(RG(d.src));
+        const uint64_t selm = __ballot(sel);
+        const int first = __builtin_ctzll(selm);
+        const uint64_t a0 = readlane64(a, first);
+        if (__ballot(sel && a != a0) == 0 && c.win.ok(a0, sz) && !is_lds_addr(a0) && !is_scratch_addr(a0)) {
+          const uint64_t v0 = readlane64(v, first);
+          uint64_t total;
+          if (__ballot(sel && v != v0) == 0)
+            total = v0 * (uint64_t)__builtin_popcountll(selm);
+          else
+            total = wave_sum64(sel ? v : 0);
+          if (c.c0a == a0 && c.c0s == sz) {
+            c.c0d += total;
+          } else if (c.c1a == a0 && c.c1s == sz) {
+            c.c1d += total;
+          } else if (c.c0a == 0) {
+            c.c0a = a0;
+            c.c0s = sz;
+            c.c0d = total;
+          } else if (c.c1a == 0) {
+            c.c1a = a0;
+            c.c1s = sz;
+            c.c1d = total;
+          } else {
+            flush_delta(c.c1a, c.c1s, c.c1d);
+            c.c1a = a0;
+            c.c1s = sz;
+            c.c1d = total;
+          }
+        } else {
+          const bool ok = c.win.ok(a, sz);
+          const uint64_t ea = sel && ok ? a : c.dummy;
+          if (sz == 8)
+            __hip_atomic_fetch_add((uint64_t *)ea, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else
+            __hip_atomic_fetch_add((uint32_t *)ea, (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (__ballot(sel && !ok) != 0) {
+            c.err = (sel && !ok) ? E_OOB : c.err;
+            c.alive = c.alive && !(sel && !ok);
+            if (__ballot(c.alive) == 0) return R_DONE;
+          }
+        }
+        npc = d.tgt;
+        break;
+      }
+      case X_ATOMIC: {
+        const bool w64 = ((d.aux >> A_SIZE_SHIFT) & 3) == 3;
+        const uint64_t a = RG(d.dst) + (int64_t)d.off;
+        const uint64_t v = RG(d.src);
+        const bool ok = c.win.ok(a, w64 ? 8 : 4);
+        const uint64_t ea = sel && ok ? a : c.dummy;
+        if (d.hi == 0xf1) {  // CMPXCHG: r0 = old
+          const uint64_t r0 = RG(0);
+          uint64_t res;
+          if (w64) {
+            uint64_t e = r0;
+            __hip_atomic_compare_exchange_strong((uint64_t *)ea, &e, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            res = e;
+          } else {
+            uint32_t e = (uint32_t)r0;
+            __hip_atomic_compare_exchange_strong((uint32_t *)ea, &e, (uint32_t)v, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            res = e;
+          }
+          WRO(0, res, r0);
+        } else if (d.hi == 0xe1) {  // XCHG
+          const uint64_t old = w64 ? __hip_atomic_exchange((uint64_t *)ea, v, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT)
+                                   : (uint64_t)__hip_atomic_exchange((uint32_t *)ea, (uint32_t)v, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_AGENT);
+          WRO(d.src, old, v);
+        } else {
+          uint64_t old;
+          const uint32_t aop = (uint32_t)d.hi & ~1u;
+          if (w64) {
+            uint64_t *q = (uint64_t *)ea;
+            if (aop == 0x00) old = __hip_atomic_fetch_add(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (aop == 0x40) old = __hip_atomic_fetch_or(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (aop == 0x50) old = __hip_atomic_fetch_and(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else old = __hip_atomic_fetch_xor(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            uint32_t *q = (uint32_t *)ea;
+            const uint32_t w = (uint32_t)v;
+            if (aop == 0x00) old = __hip_atomic_fetch_add(q, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (aop == 0x40) old = __hip_atomic_fetch_or(q, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (aop == 0x50) old = __hip_atomic_fetch_and(q, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else old = __hip_atomic_fetch_xor(q, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          if (d.hi & 1) WRO(d.src, old, v);
+        }
+        if (__ballot(sel && !ok) != 0) {
+          c.err = (sel && !ok) ? E_OOB : c.err;
+          c.alive = c.alive && !(sel && !ok);
+          if (__ballot(c.alive) == 0) return R_DONE;
+        }
+        break;
+      }
+      case X_JA: JMP_TAKEN(true)
+      case X_JEQ: JMP_TAKEN((ja & mask) == (jb & mask))
+      case X_JNE: JMP_TAKEN((ja & mask) != (jb & mask))
+      case X_JGT: JMP_TAKEN((ja & mask) > (jb & mask))
+      case X_JGE: JMP_TAKEN((ja & mask) >= (jb & mask))
+      case X_JLT: JMP_TAKEN((ja & mask) < (jb & mask))
+      case X_JLE: JMP_TAKEN((ja & mask) <= (jb & mask))
+      case X_JSET: JMP_TAKEN((ja & jb & mask) != 0)
+      case X_JSGT: JMP_TAKEN((w32 ? (int64_t)(int32_t)ja : (int64_t)ja) > (w32 ? (int64_t)(int32_t)jb : (int64_t)jb))
+      case X_JSGE: JMP_TAKEN((w32 ? (int64_t)(int32_t)ja : (int64_t)ja) >= (w32 ? (int64_t)(int32_t)jb : (int64_t)jb))
+      case X_JSLT: JMP_TAKEN((w32 ? (int64_t)(int32_t)ja : (int64_t)ja) < (w32 ? (int64_t)(int32_t)jb : (int64_t)jb))
+      case X_JSLE: JMP_TAKEN((w32 ? (int64_t)(int32_t)ja : (int64_t)ja) <= (w32 ? (int64_t)(int32_t)jb : (int64_t)jb))
+      case X_CALL:
+        c.call_pc = cur;
+        c.call_id = (uint32_t)d.hi;
+        return R_CALL;
+      case X_EXIT: {
+        const uint64_t r0 = RG(0);
+        const bool w = sel && c.err == E_OK;
+        if (c.verdicts) *(uint32_t *)(w ? (uint64_t)(uintptr_t)(c.verdicts + c.unit) : c.dummy) = (uint32_t)r0;
+        if (c.rets) *(uint64_t *)(w ? (uint64_t)(uintptr_t)(c.rets + c.unit) : c.dummy) = r0;
+        c.alive = c.alive && !sel;
+        if (UNI) return R_DONE;  // every live lane was selected and has exited
+        continue;                // divergent: the other lanes continue
+      }
+      default:
+        c.err = sel ? E_BADOP : c.err;
+        c.alive = c.alive && !sel;
+        if (UNI) return R_DONE;
+        continue;
     }
-    if (st == ST_BUSY) {
-      if (++spins > (1u << 22)) return 0;  // bounded: never hang the GPU
-      __builtin_amdgcn_s_sleep(1);
-      continue;  // re-read the same slot on the next trip
+#undef ALU
+#undef JMP_TAKEN
+#undef OPB
+#undef WRO
+    // ---- next pc ----
+    if (is_jmp) {
+      if (UNI) {
+        const uint64_t tm = __ballot(taken);
+        if (tm == 0) {
+          c.pc = npc;
+        } else if (tm == __ballot(sel)) {
+          c.pc = d.tgt;
+        } else {
+          c.lpc = taken ? (uint32_t)d.tgt : npc;
+          return R_DIVERGE;
+        }
+      } else {
+        c.lpc = sel ? (taken ? (uint32_t)d.tgt : npc) : c.lpc;
+      }
+    } else {
+      if (UNI)
+        c.pc = npc;
+      else
+        c.lpc = sel ? npc : c.lpc;
     }
-    if (key_eq(s + m.key_off, key, m.key_size)) return s;
-    idx = idx + 1 == nb ? 0 : idx + 1;
-    if (idx == start) return 0;
   }
 }
-
-struct LaneEnv {
-  uint64_t vcpu;
-  // last lookup miss (map fd, key hash) for the lookup_or_try_init race rule
-  int32_t miss_fd;
-  uint64_t miss_hash;
-};
-
-__device__ uint64_t helper_lookup(const DMap *maps, uint64_t fd, uint64_t key, LaneEnv &env) {
-  if (fd >= kMaxFds) return 0;
-  const DMap m = maps[fd];
-  switch (m.type) {
-    case MT_ARRAY: {
-      uint32_t k = *(const u32u *)key;
-      if (k >= m.max_entries) return 0;
-      return m.data + (uint64_t)k * m.value_size;
-    }
-    case MT_PERCPU_ARRAY: {
-      uint32_t k = *(const u32u *)key;
-      if (k >= m.max_entries) return 0;
-      return m.data + ((uint64_t)k * m.ncpu + env.vcpu % m.ncpu) * m.value_size;
-    }
-    case MT_HASH:
-    case MT_PERCPU_HASH: {
-      bool ins;
-      uint64_t s = hash_find(m, key, false, 0, 0, &ins);
-      if (!s) {
-        env.miss_fd = (int32_t)fd;
-        env.miss_hash = key_hash(key, m.key_size);
-        return 0;
-      }
-      uint64_t v = s + m.val_off;
-      if (m.type == MT_PERCPU_HASH) v += (env.vcpu % m.ncpu) * m.value_size;
-      return v;
-    }
-  }
-  return 0;
-}
-
-__device__ uint64_t helper_update(const DMap *maps, uint64_t fd, uint64_t key, uint64_t val,
-                                  uint64_t flags, LaneEnv &env) {
-  if (fd >= kMaxFds) return (uint64_t)-1;
-  const DMap m = maps[fd];
-  uint64_t base = flags & 0xffffffffull;
-  bool flags_ok = base == 0 || base == 1 || base == 2;  // map_common_def.hpp:83-94
-  switch (m.type) {
-    case MT_ARRAY:
-    case MT_PERCPU_ARRAY: {
-      if (!flags_ok) return (uint64_t)-1;
-      uint32_t k = *(const u32u *)key;
-      if (k < m.max_entries && flags == 1) return (uint64_t)-1;  // EEXIST
-      if (k >= m.max_entries) return (uint64_t)-1;               // E2BIG
-      uint64_t dst = m.type == MT_ARRAY
-                         ? m.data + (uint64_t)k * m.value_size
-                         : m.data + ((uint64_t)k * m.ncpu + env.vcpu % m.ncpu) * m.value_size;
-      copy_bytes(dst, val, m.value_size);
-      return 0;
-    }
-    case MT_HASH: {
-      // fix_hash_map.cpp:34-39: flags ignored, returns 0 even when full.
-      bool ins;
-      uint32_t vbytes = (m.value_size + 3) & ~3u;
-      uint64_t s = hash_find(m, key, true, val, m.value_size, &ins);
-      if (s && !ins) {
-        // Existing element: overwrite, except in the lookup-miss race (this
-        // lane's previous lookup of the same key missed, so in any serial
-        // order this update would have created the element): another lane
-        // created it first, and overwriting would drop its updates.
-        bool race = env.miss_fd == (int32_t)fd && env.miss_hash == key_hash(key, m.key_size);
-        if (!race) copy_bytes(s + m.val_off, val, m.value_size);
-      }
-      (void)vbytes;
-      env.miss_fd = -1;
-      return 0;
-    }
-    case MT_PERCPU_HASH: {
-      if (!flags_ok) return (uint64_t)-1;
-      // per_cpu_hash_map.cpp:66-94: insert zeroed ncpu*vsize, then write slot
-      bool ins;
-      uint64_t s = hash_find(m, key, true, 0, m.value_size * m.ncpu, &ins);
-      if (!s) return 0;
-      bool race = !ins && env.miss_fd == (int32_t)fd && env.miss_hash == key_hash(key, m.key_size);
-      if (!race) copy_bytes(s + m.val_off + (env.vcpu % m.ncpu) * m.value_size, val, m.value_size);
-      env.miss_fd = -1;
-      return 0;
-    }
-  }
-  return (uint64_t)-1;
-}
-
-__device__ uint64_t helper_delete(const DMap *maps, uint64_t fd, uint64_t key, LaneEnv &env) {
-  if (fd >= kMaxFds) return (uint64_t)-1;
-  const DMap m = maps[fd];
-  switch (m.type) {
-    case MT_ARRAY:
-    case MT_PERCPU_ARRAY:
-      return (uint64_t)-1;  // EINVAL (array_map.cpp:58-64)
-    case MT_HASH: {
-      bool ins;
-      uint64_t s = hash_find(m, key, false, 0, 0, &ins);
-      if (s) {
-        uint32_t prev = atomicCAS((uint32_t *)s, ST_FILLED, ST_EMPTY);  // no tombstone
-        if (prev == ST_FILLED) atomicAdd((unsigned long long *)m.count_addr, ~0ull);
-      }
-      return 0;
-    }
-    case MT_PERCPU_HASH: {
-      // per_cpu_hash_map.cpp:96-107: zeroes [0, cpu*vsize) of the element
-      bool ins;
-      uint64_t s = hash_find(m, key, false, 0, 0, &ins);
-      if (s) {
-        uint64_t n = (env.vcpu % m.ncpu) * m.value_size;
-        for (uint64_t i = 0; i < n; i++) *(volatile uint8_t *)(s + m.val_off + i) = 0;
-      }
-      return 0;
-    }
-  }
-  return (uint64_t)-1;
-}
-
-// bpf_helper.cpp:713-744
-__device__ uint64_t helper_csum_diff(uint64_t from, uint64_t from_size_, uint64_t to,
-                                     uint64_t to_size_, uint64_t seed_) {
-  int from_size = (int)from_size_, to_size = (int)to_size_;
-  int csum = -22;
-  if ((from_size % 4 != 0) || (to_size % 4 != 0)) return (uint64_t)(int64_t)csum;
-  csum = (int)seed_;
-  if (to)
-    for (int i = 0; i < to_size / 2; i++) csum += (uint16_t)(*(const u16u *)(to + 2 * i));
-  if (from)
-    for (int i = 0; i < from_size / 2; i++) csum += (uint16_t)(~*(const u16u *)(from + 2 * i));
-  if (csum < 0) csum = -22;
-  return (uint64_t)(int64_t)csum;
-}
-
-// xdp_md_userspace (runtime/extension/userspace_xdp.h:6-17)
-struct XdpCtx {
-  uint64_t data, data_end;
-  uint32_t data_meta, ingress_ifindex, rx_queue_index, egress_ifindex;
-  uint64_t buffer_start, buffer_end;
-};
-
-// bpf_helper.cpp:748-764
-__device__ uint64_t helper_adjust_head(uint64_t ctx, uint64_t off_) {
-  volatile XdpCtx *x = (volatile XdpCtx *)ctx;
-  int offset = (int)off_;
-  uint64_t data = x->data + (int64_t)offset;
-  if (data > x->data_end - 14 || data > x->buffer_end) return (uint64_t)(int64_t)-22;
-  if (data < x->buffer_start) {
-    // memmove(buffer_start + (buffer_start - data), data, data_end - data)
-    uint64_t dst = x->buffer_start + (x->buffer_start - data), src = x->data;
-    uint64_t n = x->data_end - x->data;
-    if (dst > src)
-      for (uint64_t i = n; i-- > 0;) *(volatile uint8_t *)(dst + i) = *(volatile uint8_t *)(src + i);
-    else
-      for (uint64_t i = 0; i < n; i++) *(volatile uint8_t *)(dst + i) = *(volatile uint8_t *)(src + i);
-    data = x->buffer_start;
-  }
-  x->data = data;
-  return 0;
-}
-
-// bpf_helper.cpp:766-776
-__device__ uint64_t helper_adjust_tail(uint64_t ctx, uint64_t delta_) {
-  volatile XdpCtx *x = (volatile XdpCtx *)ctx;
-  int delta = (int)delta_;
-  uint64_t data = x->data_end + (int64_t)delta;
-  if (data < x->data || data < x->buffer_start || data > x->buffer_end) return (uint64_t)(int64_t)-22;
-  x->data_end = data;
-  return 0;
-}
-
-// bpf_helper.cpp:778-788 (defined in the reference, not registered by default)
-__device__ uint64_t helper_xdp_load_bytes(uint64_t ctx, uint64_t off, uint64_t buf, uint64_t len) {
-  volatile XdpCtx *x = (volatile XdpCtx *)ctx;
-  uint64_t data = x->data + (uint32_t)off;
-  if (data + (uint32_t)len > x->data_end) return (uint64_t)(int64_t)-22;
-  copy_bytes(buf, data, (uint32_t)len);
-  return 0;
-}
-
-// ---------------------------------------------------------------------------
-// The interpreter
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
-  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, lane);
-  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-  return readlane64(x, 0);
-}
-
-// One lane of the wave adds a cached counter delta (wave-uniform arguments).
-__device__ __forceinline__ void flush_delta(uint64_t a, uint32_t sz, uint64_t delta) {
-  if (a == 0 || delta == 0) return;
-  if ((threadIdx.x & 63) == 0) {
-    if (sz == 8)
-      __hip_atomic_fetch_add((uint64_t *)a, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-      __hip_atomic_fetch_add((uint32_t *)a, (uint32_t)delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-#define RREG(i) Rf[(uint32_t)(i) * kBlock + tid]
+#undef RG
 
 template <uint32_t KIND, bool BIGSTACK>
-__global__ __launch_bounds__(kBlock) void k_interp(KParams p) {
-  __shared__ uint64_t Rf[11 * kBlock];
+__global__ __launch_bounds__(kBlock) void k_interp(KParams pin) {
+  // Copy every kernel argument through an SGPR barrier: without it the
+  // compiler keeps the argument block as one 16-dword tuple that it spills
+  // and reloads whole inside the dispatch loop.
+  KParams p;
+#define SRP(f) p.f = (decltype(p.f))sreg((uint64_t)(uintptr_t)pin.f)
+#define SRV(f) p.f = sreg(pin.f)
+  SRP(prog); SRP(maps); SRP(data); SRP(lens); SRP(verdicts); SRP(rets); SRP(out_data_off); SRP(out_len);
+  SRP(err_count); SRV(n); SRV(stride); SRV(first_unit); SRV(data_lo); SRV(data_hi); SRV(arena_lo);
+  SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
+  SRV(checked); SRV(head); SRV(ordered);
+#undef SRP
+#undef SRV
+  __shared__ uint64_t Rf[12 * kBlock];  // r0..r10 + a dummy slot per lane
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
   constexpr uint32_t CTXB = KIND == CTX_XDP ? 48 : 0;
   const uint32_t tid = threadIdx.x;
   uint8_t *my_ctx = dyn + tid * CTXB;
   uint8_t *my_stack = dyn + kBlock * CTXB + tid * p.stack_size;
   uint64_t big_stack[BIGSTACK ? kStackSize / 8 : 1];
-  const Win win{p.data_lo, p.data_hi, p.arena_lo, p.arena_hi, p.checked != 0};
-  // per-wave delta cache for fused counters (wave-uniform, lives in SGPRs)
-  uint64_t c0a = 0, c0d = 0, c1a = 0, c1d = 0;
-  uint32_t c0s = 0, c1s = 0;
   const uint64_t stack_top = BIGSTACK ? (uint64_t)(uintptr_t)(big_stack + kStackSize / 8)
                                       : (uint64_t)(uintptr_t)(my_stack + p.stack_size);
 
+  Ctx c;
+  c.R = &Rf[tid];
+  c.prog = (prog_ptr)p.prog;
+  c.win = Win{p.data_lo, p.data_hi, p.arena_lo, p.arena_hi, p.checked != 0};
+  c.dummy = (uint64_t)(uintptr_t)&Rf[11 * kBlock + tid];
+  c.verdicts = p.verdicts;
+  c.rets = p.rets;
+  c.step_limit = p.step_limit > 0xffffffffull ? 0xffffffffu : (uint32_t)p.step_limit;
+  c.c0a = c.c0d = c.c1a = c.c1d = 0;
+  c.c0s = c.c1s = 0;
+
   const bool ordered = p.ordered != 0;
   const uint64_t ustep = ordered ? 1 : (uint64_t)gridDim.x * kBlock;
-  // constant address space: the program is read with scalar (s_load) loads
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 __attribute__((address_space(4))) *prog =
-      (const u32x4 __attribute__((address_space(4))) *)p.prog;
   for (uint64_t u0 = ordered ? 0 : (uint64_t)blockIdx.x * kBlock; u0 < p.n; u0 += ustep) {
     const uint64_t unit = ordered ? u0 : u0 + tid;
     const bool active = ordered ? (tid == 0 && blockIdx.x == 0) : unit < p.n;
     const uint64_t slot = (uint64_t)(uintptr_t)p.data + unit * p.stride;
     uint32_t len = p.fixed_len;
     if (active && p.lens) len = p.lens[unit];
+    const uint64_t vcpu = (p.first_unit + unit) / 64;
+    int32_t miss_fd = -1;
+    uint64_t miss_hash = 0;
 
-    LaneEnv env;
-    env.vcpu = (p.first_unit + unit) / 64;
-    env.miss_fd = -1;
-    env.miss_hash = 0;
-
-    // ---- per-unit setup (r1, r2, r10) ----
-    for (uint32_t r = 0; r < 11; r++) RREG(r) = 0;
+    // ---- per-unit setup (r1, r2, r10; other registers zero) ----
+    for (uint32_t r = 0; r < 11; r++) Rf[r * kBlock + tid] = 0;
     if (KIND == CTX_XDP) {
-      XdpCtx *c = (XdpCtx *)my_ctx;
-      c->data = slot + p.head;
-      c->data_end = slot + p.head + len;
-      c->data_meta = 0;
-      c->ingress_ifindex = p.ifindex;
-      c->rx_queue_index = p.rxq;
-      c->egress_ifindex = 0;
-      c->buffer_start = slot;
-      c->buffer_end = slot + p.stride;
-      RREG(1) = (uint64_t)(uintptr_t)c;
-      RREG(2) = 48;
+      XdpCtx *x = (XdpCtx *)my_ctx;
+      x->data = slot + p.head;
+      x->data_end = slot + p.head + len;
+      x->data_meta = 0;
+      x->ingress_ifindex = p.ifindex;
+      x->rx_queue_index = p.rxq;
+      x->egress_ifindex = 0;
+      x->buffer_start = slot;
+      x->buffer_end = slot + p.stride;
+      Rf[1 * kBlock + tid] = (uint64_t)(uintptr_t)x;
+      Rf[2 * kBlock + tid] = 48;
     } else {
-      RREG(1) = slot;
-      RREG(2) = KIND == CTX_SYSCALL ? 64 : len;
+      Rf[1 * kBlock + tid] = slot;
+      Rf[2 * kBlock + tid] = KIND == CTX_SYSCALL ? 64 : len;
     }
-    RREG(10) = stack_top;
+    Rf[10 * kBlock + tid] = stack_top;
 
     bool alive = active;
     if (KIND == CTX_SYSCALL && active) {
       // exit / exit_group bypass every callback (syscall_trace_attach_impl.cpp:25)
-      int64_t nr = *(const int64_t *)(slot + 8);
+      const int64_t nr = *(const int64_t *)(slot + 8);
       if (nr == 60 || nr == 231) alive = false;
     }
-    uint32_t err = E_OK;
-    uint32_t pc = 0;      // wave-uniform pc (uniform mode)
-    uint32_t lpc = 0;     // per-lane pc (divergent mode)
+    c.unit = unit;
+    c.alive = alive;
+    c.err = E_OK;
+    c.pc = 0;
+    c.lpc = 0;
+    c.steps = 0;
+
     bool uni = true;
-    uint64_t steps = 0;
-    if (__ballot(alive) != 0)
-    for (;;) {
-      uint32_t cur;
-      bool sel;
-      if (uni) {
-        cur = pc;
-        sel = alive;
-      } else {
-        const uint32_t m = alive ? lpc : 0xffffffffu;
-        cur = __reduce_min_sync(~0ull, m);
-        if (cur == 0xffffffffu) break;
-        sel = alive && lpc == cur;
-        if (__ballot(alive && lpc != cur) == 0) uni = true;  // reconverged
+    while (__ballot(c.alive) != 0) {
+      const uint32_t r = uni ? run_loop<true>(c) : run_loop<false>(c);
+      if (r == R_DONE) break;
+      if (r == R_DIVERGE) {
+        uni = false;
+        continue;
       }
-      cur = __builtin_amdgcn_readfirstlane(cur);
-      if (++steps > p.step_limit) {
-        if (alive) err = E_STEPS;
-        alive = false;
-        break;
+      if (r == R_RECONV) {
+        uni = true;
+        continue;
       }
-      const u32x4 raw = prog[cur];
-      DInsn d;
-      __builtin_memcpy(&d, &raw, sizeof(d));
-      const uint32_t op = __builtin_amdgcn_readfirstlane(d.op);
-      uint32_t npc = cur + 1;
-      bool jmp = false;
-      bool taken = false;
-      const uint64_t mask = (d.aux & A_W32) ? 0xffffffffull : ~0ull;
-
-#define OPB() ((d.aux & A_SRCREG) ? RREG(d.src) : (uint64_t)(int64_t)d.imm)
-#define ALU(expr)                          \
-  if (sel) {                               \
-    const uint64_t a = RREG(d.dst);        \
-    const uint64_t b = OPB();              \
-    (void)a;                               \
-    (void)b;                               \
-    RREG(d.dst) = (expr);                  \
-  }                                        \
-  break;
-#define JCMP(expr)                          \
-  jmp = true;                               \
-  if (sel) {                                \
-    uint64_t a = RREG(d.dst);               \
-    uint64_t b = OPB();                     \
-    if (d.aux & A_W32) {                    \
-      a = (uint32_t)a;                      \
-      b = (uint32_t)b;                      \
-    }                                       \
-    taken = (expr);                         \
-  }                                         \
-  break;
-#define JSCMP(cmp)                                                   \
-  jmp = true;                                                        \
-  if (sel) {                                                         \
-    int64_t a = (int64_t)RREG(d.dst);                                \
-    int64_t b = (int64_t)OPB();                                      \
-    if (d.aux & A_W32) {                                             \
-      a = (int32_t)a;                                                \
-      b = (int32_t)b;                                                \
-    }                                                                \
-    taken = a cmp b;                                                 \
-  }                                                                  \
-  break;
-
-      switch (op) {
-        case X_ADD: ALU((a + b) & mask)
-        case X_SUB: ALU((a - b) & mask)
-        case X_MUL: ALU((a * b) & mask)
-        case X_OR: ALU((a | b) & mask)
-        case X_AND: ALU((a & b) & mask)
-        case X_XOR: ALU((a ^ b) & mask)
-        case X_MOV: ALU(b & mask)
-        case X_DIV64: ALU(b ? a / b : 0)
-        case X_MOD64: ALU(b ? a % b : a)
-        case X_LSH64: ALU(a << (b & 63))
-        case X_RSH64: ALU(a >> (b & 63))
-        case X_ARSH64: ALU((uint64_t)((int64_t)a >> (b & 63)))
-        case X_NEG64: ALU((uint64_t)(-(int64_t)a))
-        case X_DIV32: ALU((uint32_t)b ? (uint64_t)((uint32_t)a / (uint32_t)b) : 0)
-        case X_MOD32: ALU((uint32_t)b ? (uint64_t)((uint32_t)a % (uint32_t)b) : (uint64_t)(uint32_t)a)
-        case X_LSH32: ALU((uint64_t)(uint32_t)((uint32_t)a << (b & 31)))
-        case X_RSH32: ALU((uint64_t)((uint32_t)a >> (b & 31)))
-        case X_ARSH32: ALU((uint64_t)(uint32_t)((int32_t)a >> (b & 31)))
-        case X_NEG32: ALU((uint64_t)(uint32_t)(-(int64_t)a))
-        case X_LE:
-          ALU(d.imm == 16 ? (uint64_t)(uint16_t)a : d.imm == 32 ? (uint64_t)(uint32_t)a : a)
-        case X_BE:
-          ALU(d.imm == 16   ? (uint64_t)__builtin_bswap16((uint16_t)a)
-              : d.imm == 32 ? (uint64_t)__builtin_bswap32((uint32_t)a)
-              : d.imm == 64 ? __builtin_bswap64(a)
-                            : a)
-        case X_LDDW:
-          if (sel) RREG(d.dst) = (uint64_t)(uint32_t)d.imm | ((uint64_t)(uint32_t)d.hi << 32);
-          npc = cur + 2;
-          break;
-        case X_LDX: {
-          const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
-          if (sel) {
-            const uint64_t a = RREG(d.src) + (int64_t)d.off;
-            if (win.ok(a, sz)) {
-              RREG(d.dst) = mem_load(a, sz);
-            } else {
-              err = E_OOB;
-              alive = false;
-            }
-          }
-          break;
+      // ---- R_CALL: helper call (bpf_helper.cpp helpers; csrc/dev_helpers.hpp) ----
+      const bool csel = uni ? c.alive : (c.alive && c.lpc == c.call_pc);
+      if (csel) {
+        LaneEnv env;
+        env.vcpu = vcpu;
+        env.miss_fd = miss_fd;
+        env.miss_hash = miss_hash;
+        uint32_t cerr = E_OK;
+        uint64_t *R = &Rf[tid];
+        const uint64_t rv = call_helper(c.call_id, R[1 * kBlock], R[2 * kBlock], R[3 * kBlock], R[4 * kBlock],
+                                        R[5 * kBlock], p.maps, p.ncpu,
+                                        (p.first_unit + unit) ^ ((uint64_t)c.steps << 40), env, &cerr);
+        R[0] = rv;
+        miss_fd = env.miss_fd;
+        miss_hash = env.miss_hash;
+        if (cerr != E_OK) {
+          c.err = cerr;
+          c.alive = false;
         }
-        case X_ST:
-        case X_STX: {
-          const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
-          if (sel) {
-            const uint64_t a = RREG(d.dst) + (int64_t)d.off;
-            const uint64_t v = op == X_STX ? RREG(d.src) : (uint64_t)(int64_t)d.imm;
-            if (win.ok(a, sz)) {
-              mem_store(a, sz, v);
-            } else {
-              err = E_OOB;
-              alive = false;
-            }
-          }
-          break;
-        }
-        case X_RMW_ADD: {
-          // fused ldx/add/stx (loaded register proven dead by the loader)
-          // Counters hit by a whole wave (e.g. cntrs_array[0]) are summed across
-          // the wave and kept in a per-wave scalar delta cache flushed with one
-          // atomic at the end of the launch; otherwise one atomic per lane.
-          const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
-          uint64_t a = 0, v = 0;
-          if (sel) {
-            a = RREG(d.dst) + (int64_t)d.off;
-            v = OPB();
-          }
-          const uint64_t selm = __ballot(sel);
-          const int first = __builtin_ctzll(selm);
-          const uint64_t a0 = readlane64(a, first);
-          if (__ballot(sel && a != a0) == 0 && win.ok(a0, sz) && !is_lds_addr(a0) && !is_scratch_addr(a0)) {
-            const uint64_t v0 = readlane64(v, first);
-            uint64_t total;
-            if (__ballot(sel && v != v0) == 0)
-              total = v0 * (uint64_t)__builtin_popcountll(selm);
-            else
-              total = wave_sum64(sel ? v : 0);
-            if (c0a == a0 && c0s == sz) {
-              c0d += total;
-            } else if (c1a == a0 && c1s == sz) {
-              c1d += total;
-            } else if (c0a == 0) {
-              c0a = a0; c0s = sz; c0d = total;
-            } else if (c1a == 0) {
-              c1a = a0; c1s = sz; c1d = total;
-            } else {
-              flush_delta(c1a, c1s, c1d);
-              c1a = a0; c1s = sz; c1d = total;
-            }
-          } else if (sel) {
-            if (win.ok(a, sz)) {
-              if (sz == 8)
-                __hip_atomic_fetch_add((uint64_t *)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              else if (sz == 4)
-                __hip_atomic_fetch_add((uint32_t *)a, (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              else
-                mem_store(a, sz, mem_load(a, sz) + v);  // 1/2-byte: not fused by the loader
-            } else {
-              err = E_OOB;
-              alive = false;
-            }
-          }
-          npc = d.tgt;
-          break;
-        }
-        case X_ATOMIC: {
-          const bool w64 = ((d.aux >> A_SIZE_SHIFT) & 3) == 3;
-          if (sel) {
-            const uint64_t a = RREG(d.dst) + (int64_t)d.off;
-            const uint64_t v = RREG(d.src);
-            if (!win.ok(a, w64 ? 8 : 4)) {
-              err = E_OOB;
-              alive = false;
-            } else if (d.hi == 0xf1) {  // CMPXCHG: r0 = old
-              if (w64) {
-                uint64_t e = RREG(0);
-                __hip_atomic_compare_exchange_strong((uint64_t *)a, &e, v, __ATOMIC_RELAXED,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                RREG(0) = e;
-              } else {
-                uint32_t e = (uint32_t)RREG(0);
-                __hip_atomic_compare_exchange_strong((uint32_t *)a, &e, (uint32_t)v, __ATOMIC_RELAXED,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                RREG(0) = e;
-              }
-            } else if (d.hi == 0xe1) {  // XCHG
-              RREG(d.src) = w64 ? __hip_atomic_exchange((uint64_t *)a, v, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT)
-                                : (uint64_t)__hip_atomic_exchange((uint32_t *)a, (uint32_t)v,
-                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-              uint64_t old = 0;
-              const uint32_t aop = d.hi & ~1;
-              if (w64) {
-                uint64_t *q = (uint64_t *)a;
-                if (aop == 0x00) old = __hip_atomic_fetch_add(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else if (aop == 0x40) old = __hip_atomic_fetch_or(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else if (aop == 0x50) old = __hip_atomic_fetch_and(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else old = __hip_atomic_fetch_xor(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              } else {
-                uint32_t *q = (uint32_t *)a;
-                const uint32_t w = (uint32_t)v;
-                if (aop == 0x00) old = __hip_atomic_fetch_add(q, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else if (aop == 0x40) old = __hip_atomic_fetch_or(q, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else if (aop == 0x50) old = __hip_atomic_fetch_and(q, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else old = __hip_atomic_fetch_xor(q, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              }
-              if (d.hi & 1) RREG(d.src) = old;
-            }
-          }
-          break;
-        }
-        case X_JA:
-          jmp = true;
-          taken = sel;
-          break;
-        case X_JEQ: JCMP(a == b)
-        case X_JGT: JCMP(a > b)
-        case X_JGE: JCMP(a >= b)
-        case X_JSET: JCMP((a & b) != 0)
-        case X_JNE: JCMP(a != b)
-        case X_JLT: JCMP(a < b)
-        case X_JLE: JCMP(a <= b)
-        case X_JSGT: JSCMP(>)
-        case X_JSGE: JSCMP(>=)
-        case X_JSLT: JSCMP(<)
-        case X_JSLE: JSCMP(<=)
-        case X_CALL: {
-          if (sel) {
-            const uint64_t a1 = RREG(1), a2 = RREG(2), a3 = RREG(3), a4 = RREG(4), a5 = RREG(5);
-            uint64_t r = 0;
-            switch (d.hi) {
-              case 1: r = helper_lookup(p.maps, a1, a2, env); break;
-              case 2: r = helper_update(p.maps, a1, a2, a3, a4, env); break;
-              case 3: r = helper_delete(p.maps, a1, a2, env); break;
-              case 5: r = (uint64_t)__builtin_amdgcn_s_memrealtime() * 10ull; break;
-              case 7: {
-                uint64_t x = (p.first_unit + unit) * 0x9E3779B97F4A7C15ull + steps;
-                x ^= x >> 31; x *= 0xBF58476D1CE4E5B9ull; x ^= x >> 29;
-                r = (uint32_t)x;
-                break;
-              }
-              case 8: r = env.vcpu % p.ncpu; break;
-              case 28: r = helper_csum_diff(a1, a2, a3, a4, a5); break;
-              case 44: r = helper_adjust_head(a1, a2); break;
-              case 65: r = helper_adjust_tail(a1, a2); break;
-              case 189: r = helper_xdp_load_bytes(a1, a2, a3, a4); break;
-              default: err = E_BADOP; alive = false; break;
-            }
-            RREG(0) = r;
-          }
-          break;
-        }
-        case X_EXIT:
-          if (sel) {
-            alive = false;
-            if (err == E_OK) {
-              const uint64_t r0 = RREG(0);
-              if (p.verdicts) p.verdicts[unit] = (uint32_t)r0;
-              if (p.rets) p.rets[unit] = r0;
-            }
-          }
-          npc = 0xffffffffu;
-          break;
-        default:
-          if (sel) {
-            err = E_BADOP;
-            alive = false;
-          }
-          break;
       }
-#undef ALU
-#undef JCMP
-#undef JSCMP
-#undef OPB
-
-      // ---- next pc ----
-      if (op == X_EXIT) {
-        if (uni) break;  // every alive lane was selected and has exited
-        continue;        // divergent: remaining lanes continue
-      }
-      if (jmp) {
-        const uint64_t tm = __ballot(taken);
-        const uint64_t sm = __ballot(sel);
-        if (uni) {
-          if (tm == 0) {
-            pc = npc;
-          } else if (tm == sm) {
-            pc = d.tgt;
-          } else {
-            uni = false;
-            if (sel) lpc = taken ? (uint32_t)d.tgt : npc;
-          }
-        } else {
-          if (sel) lpc = taken ? (uint32_t)d.tgt : npc;
-        }
-      } else {
-        if (uni)
-          pc = npc;
-        else if (sel)
-          lpc = npc;
-      }
-      if (!uni && __ballot(alive) == 0) break;
-      if (uni && op >= X_LDX && op <= X_RMW_ADD && __ballot(alive) == 0) break;
-      if (uni && (op == X_CALL || op == X_BAD || op >= X_NOP) && __ballot(alive) == 0) break;
+      if (uni)
+        c.pc = c.call_pc + 1;
+      else
+        c.lpc = csel ? c.call_pc + 1 : c.lpc;
     }
 
     if (active) {
-      if (err != E_OK) {
+      if (c.err != E_OK) {
         // bpftime_prog.cpp:250-257: a failed exec reports 0
         if (p.verdicts) p.verdicts[unit] = 0;
         if (p.rets) p.rets[unit] = 0;
         atomicAdd(p.err_count, 1u);
       } else if (KIND == CTX_SYSCALL) {
-        int64_t nr = *(const int64_t *)(slot + 8);
+        const int64_t nr = *(const int64_t *)(slot + 8);
         if (nr == 60 || nr == 231) {
           if (p.verdicts) p.verdicts[unit] = 0;
           if (p.rets) p.rets[unit] = 0;
         }
       }
       if (KIND == CTX_XDP) {
-        const XdpCtx *c = (const XdpCtx *)my_ctx;
-        if (p.out_data_off) p.out_data_off[unit] = (int32_t)(c->data - slot);
-        if (p.out_len) p.out_len[unit] = (uint32_t)(c->data_end - c->data);
+        const XdpCtx *x = (const XdpCtx *)my_ctx;
+        if (p.out_data_off) p.out_data_off[unit] = (int32_t)(x->data - slot);
+        if (p.out_len) p.out_len[unit] = (uint32_t)(x->data_end - x->data);
       }
     }
   }
-  flush_delta(c0a, c0s, c0d);
-  flush_delta(c1a, c1s, c1d);
+  flush_delta(c.c0a, c.c0s, c.c0d);
+  flush_delta(c.c1a, c.c1s, c.c1d);
 }
-#undef RREG
 
 // ---------------------------------------------------------------------------
 // Host-side launch wrappers
 // ---------------------------------------------------------------------------
-extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind, bool big_stack,
-                                                uint32_t grid, uint32_t ordered, hipStream_t stream) {
+static size_t dyn_lds_bytes(uint32_t kind, bool big_stack, uint32_t stack_size) {
+  return kBlock * ((kind == CTX_XDP ? 48 : 0) + (big_stack ? 0 : stack_size));
+}
+
+extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind, bool big_stack, uint32_t grid,
+                                                uint32_t ordered, hipStream_t stream) {
   KParams q = *p;
   q.ordered = ordered;
-  const size_t ctxb = kind == CTX_XDP ? 48 : 0;
-  const size_t dyn = kBlock * (ctxb + (big_stack ? 0 : p->stack_size));
+  const size_t dyn = dyn_lds_bytes(kind, big_stack, p->stack_size);
   dim3 g(grid), b(kBlock);
 #define L(K, B) hipLaunchKernelGGL((k_interp<K, B>), g, b, dyn, stream, q)
   if (kind == CTX_XDP) {

@@ -596,8 +596,10 @@ int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &
   out.fused_rmw = fused;
   // sentinel: a program that falls off its end fails its lanes on the device
   // instead of fetching past the allocation
+  // (two of them: the device prefetches pc + 1)
   DInsn sentinel{};
   sentinel.op = X_BAD;
+  p.push_back(sentinel);
   p.push_back(sentinel);
   out.prog = std::move(p);
   return 0;
