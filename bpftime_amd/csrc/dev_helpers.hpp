@@ -67,8 +67,16 @@ __device__ __forceinline__ uint64_t key_hash(uint64_t key, uint32_t ks) {
   return h;
 }
 
+// Hash-table words are shared between workgroups on different XCDs while a
+// batch runs: every access is a GLOBAL (address_space(1)) agent-scope atomic
+// (sc1), never a flat access (MI355X_MICROARCH.md, inter-workgroup visibility).
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+#define G32(a) ((gu32 *)(uintptr_t)(a))
+#define G64(a) ((gu64 *)(uintptr_t)(a))
+
 __device__ __forceinline__ uint32_t ald32(uint64_t a) {
-  return __hip_atomic_load((uint32_t *)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(G32(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint8_t ald8(uint64_t a) {
   uint64_t w = a & ~3ull;
@@ -76,16 +84,27 @@ __device__ __forceinline__ uint8_t ald8(uint64_t a) {
   return (uint8_t)(v >> ((a & 3) * 8));
 }
 
+// Coherent read: an atomic is performed at the coherence point, so it sees
+// every store another XCD has drained, even when this XCD's L2 still holds
+// an older copy of the line (an sc1 load is served by the local L2).
+__device__ __forceinline__ uint32_t acoh32(uint64_t a) {
+  return __hip_atomic_fetch_or(G32(a), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Compare the program-side key (any alignment, any memory) with a slot key
-// (8-aligned, published with agent-scope stores).
-__device__ __forceinline__ bool key_eq(uint64_t slot_key, uint64_t key, uint32_t ks) {
+// (8-aligned, published with agent-scope stores).  `coh` selects coherent
+// reads: needed when the slot's FILLED state was learned from an atomic
+// rather than from a load of the same (line-contained) slot.
+__device__ __forceinline__ bool key_eq(uint64_t slot_key, uint64_t key, uint32_t ks, bool coh) {
   uint32_t i = 0;
   for (; i + 4 <= ks; i += 4) {
     uint32_t kv = *(const u32u *)(key + i);
-    if (ald32(slot_key + i) != kv) return false;
+    if ((coh ? acoh32(slot_key + i) : ald32(slot_key + i)) != kv) return false;
   }
   for (; i < ks; i++) {
-    if (ald8(slot_key + i) != *(const volatile uint8_t *)(key + i)) return false;
+    uint64_t w = (slot_key + i) & ~3ull;
+    uint32_t v = coh ? acoh32(w) : ald32(w);
+    if ((uint8_t)(v >> (((slot_key + i) & 3) * 8)) != *(const volatile uint8_t *)(key + i)) return false;
   }
   return true;
 }
@@ -94,12 +113,12 @@ __device__ __forceinline__ void copy_bytes_publish(uint64_t dst, uint64_t src, u
   // dst is 8-aligned device memory; src is any flat address.
   uint32_t i = 0;
   for (; i + 4 <= n; i += 4)
-    __hip_atomic_store((uint32_t *)(dst + i), *(const u32u *)(src + i), __ATOMIC_RELAXED,
+    __hip_atomic_store(G32(dst + i), *(const u32u *)(src + i), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   if (i < n) {
     uint32_t w = 0;
     for (uint32_t j = 0; i + j < n; j++) w |= (uint32_t)(*(const volatile uint8_t *)(src + i + j)) << (8 * j);
-    __hip_atomic_store((uint32_t *)(dst + i), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(G32(dst + i), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -126,38 +145,53 @@ __device__ uint64_t hash_find(const DMap &m, uint64_t key, bool insert, uint64_t
   uint32_t spins = 0;
   for (;;) {
     uint64_t s = m.data + idx * (uint64_t)m.slot_size;
+    // A slot never straddles a 128-B line (maps.cpp slot sizing), so a
+    // FILLED state read by a load comes with the key bytes of that same
+    // line snapshot.  Anything else is confirmed at the coherence point: a
+    // stale EMPTY from this XCD's L2 would end the probe with a false miss.
     uint32_t st = ald32(s);
+    bool coh = false;
+    if (st != ST_FILLED) {
+      st = acoh32(s);
+      coh = true;
+    }
     if (st == ST_EMPTY) {
       if (!insert) return 0;
-      // element count check (bpftime_hash_map.hpp:153-156)
-      unsigned long long c = atomicAdd((unsigned long long *)m.count_addr, 1ull);
-      if (c >= m.max_entries) {
-        atomicAdd((unsigned long long *)m.count_addr, ~0ull);  // undo
-        return 0;
-      }
-      uint32_t prev = atomicCAS((uint32_t *)s, ST_EMPTY, ST_BUSY);
+      uint32_t prev = ST_EMPTY;
+      __hip_atomic_compare_exchange_strong(G32(s), &prev, ST_BUSY, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
       if (prev == ST_EMPTY) {
+        // Element count check (bpftime_hash_map.hpp:153-156), made only by
+        // the lane that owns the slot: reserving before the claim lets
+        // thousands of concurrent losers over-count a table that is not full.
+        unsigned long long c = __hip_atomic_fetch_add(G64(m.count_addr), 1ull, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+        if (c >= m.max_entries) {
+          __hip_atomic_fetch_add(G64(m.count_addr), ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(G32(s), ST_EMPTY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          return 0;
+        }
         copy_bytes_publish(s + m.key_off, key, m.key_size);
         if (init)
           copy_bytes_publish(s + m.val_off, init, init_bytes);
         else
           for (uint32_t i = 0; i < init_bytes; i += 4)
-            __hip_atomic_store((uint32_t *)(s + m.val_off + i), 0u, __ATOMIC_RELAXED,
+            __hip_atomic_store(G32(s + m.val_off + i), 0u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __hip_atomic_store((uint32_t *)s, ST_FILLED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // key/value stores drained first
+        __hip_atomic_store(G32(s), ST_FILLED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         *inserted = true;
         return s;
       }
-      atomicAdd((unsigned long long *)m.count_addr, ~0ull);  // lost the race: undo
-      st = prev;
+      st = prev;  // lost the claim: BUSY or FILLED, learned at the coherence point
     }
     if (st == ST_BUSY) {
       if (++spins > (1u << 22)) return 0;  // bounded: never hang the GPU
       __builtin_amdgcn_s_sleep(1);
       continue;  // re-read the same slot on the next trip
     }
-    if (key_eq(s + m.key_off, key, m.key_size)) return s;
+    if (key_eq(s + m.key_off, key, m.key_size, coh)) return s;
     idx = idx + 1 == nb ? 0 : idx + 1;
     if (idx == start) return 0;
   }
@@ -263,8 +297,10 @@ __device__ uint64_t helper_delete(const DMap *maps, uint64_t fd, uint64_t key, L
       bool ins;
       uint64_t s = hash_find(m, key, false, 0, 0, &ins);
       if (s) {
-        uint32_t prev = atomicCAS((uint32_t *)s, ST_FILLED, ST_EMPTY);  // no tombstone
-        if (prev == ST_FILLED) atomicAdd((unsigned long long *)m.count_addr, ~0ull);
+        uint32_t prev = ST_FILLED;  // no tombstone (bpftime_hash_map.hpp:182-199)
+        if (__hip_atomic_compare_exchange_strong(G32(s), &prev, ST_EMPTY, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+          __hip_atomic_fetch_add(G64(m.count_addr), ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return 0;
     }

@@ -222,6 +222,16 @@ static DInsn decode_one(const std::vector<RawInsn> &in, uint32_t i) {
 }
 
 // ---- analysis --------------------------------------------------------------
+// Argument count of each device helper (linux/bpf.h prototypes).
+static int helper_arity(uint32_t id) {
+  switch (id) {
+    case 5: case 7: case 8: return 0;          // ktime_get_ns, get_prandom_u32, get_smp_processor_id
+    case 1: case 3: case 44: case 65: return 2;  // map_lookup/delete_elem, xdp_adjust_head/tail
+    case 2: case 189: return 4;                // map_update_elem, xdp_load_bytes
+    default: return 5;                         // csum_diff and anything else
+  }
+}
+
 typedef uint16_t RegSet;  // bit per register r0..r10
 
 static void use_def(const DInsn &d, RegSet &use, RegSet &def) {
@@ -265,7 +275,9 @@ static void use_def(const DInsn &d, RegSet &use, RegSet &def) {
       if (d.aux & A_SRCREG) U(d.src);
       break;
     case X_CALL:
-      for (int r = 1; r <= 5; r++) U(r);
+      // a helper reads only its declared arguments; r1-r5 survive the call
+      // (ubpf semantics, restated by oracle/interp.c: helpers get copies)
+      for (int r = 1; r <= helper_arity((uint32_t)d.hi); r++) U(r);
       D(0);
       break;
     case X_EXIT: U(0); break;

@@ -200,7 +200,16 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
       d.key_off = 8;
       d.val_off = 8 + ((m.key_size + 7) & ~7u);
       uint64_t vbytes = (uint64_t)m.value_size * (m.type == MT_PERCPU_HASH ? d.ncpu : 1);
-      d.slot_size = (uint32_t)(d.val_off + ((vbytes + 7) & ~7ull));
+      // Slots never straddle a 128-B cache line: a power of two up to one
+      // line, whole lines beyond.  A lane that loads a FILLED state then
+      // reads the key from the same line snapshot (dev_helpers.hpp hash_find).
+      uint64_t raw = d.val_off + ((vbytes + 7) & ~7ull);
+      uint64_t ss = 16;
+      if (raw > 128)
+        ss = (raw + 127) & ~127ull;
+      else
+        while (ss < raw) ss <<= 1;
+      d.slot_size = (uint32_t)ss;
       m.bytes = d.nbuckets * d.slot_size;
       break;
     }
@@ -209,7 +218,7 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
       set_error("unsupported map type " + std::to_string(m.type));
       return -1;
   }
-  uint64_t extra = (m.type == MT_HASH || m.type == MT_PERCPU_HASH) ? 64 : 0;
+  uint64_t extra = (m.type == MT_HASH || m.type == MT_PERCPU_HASH) ? 128 : 0;
   uint64_t base = r.arena_alloc(m.bytes + extra + 8);
   if (!base) {
     errno = ENOMEM;
@@ -217,7 +226,7 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
     return -1;
   }
   d.data = base;
-  d.count_addr = extra ? base + ((m.bytes + 63) & ~63ull) : 0;
+  d.count_addr = extra ? base + ((m.bytes + 127) & ~127ull) : 0;
   if (hipMemset((void *)base, 0, m.bytes + extra + 8) != hipSuccess) return -1;
   r.maps[fd] = m;
   r.kind[fd] = HKind::MAP;

@@ -1,0 +1,198 @@
+"""Device maps: the reference map unit-test assertions against the device
+registry (syscall-side API), and the hash / per-CPU configs of BASELINE.json
+(flow-hash = configs[2], syscall-agg = configs[4]) against the oracle."""
+import errno
+import random
+import struct
+
+import numpy as np
+import pytest
+
+from bpftime_amd import gen, isa, programs
+from bpftime_amd.isa import Asm
+
+from _helpers import make_maps
+
+pytestmark = pytest.mark.gpu
+
+I32 = lambda v: struct.pack("<i", v)  # noqa: E731
+I64 = lambda v: struct.pack("<q", v)  # noqa: E731
+
+
+def test_device_hash_map_kat(fresh_runtime):
+    dev = fresh_runtime
+    m = dev.Map(isa.BPF_MAP_TYPE_HASH, 4, 8, 10)
+    assert m.geometry()[0] == 11  # next_prime(10) buckets
+    assert m.update(I32(1234), I64(5678)) == 0 and m.update(I32(4321), I64(8765)) == 0
+    assert m.lookup(I32(1234)) == I64(5678) and m.lookup(I32(4321)) == I64(8765)
+    assert m.lookup(I32(9999)) is None
+    assert m.update(I32(1234), I64(1)) == 0 and m.lookup(I32(1234)) == I64(1)
+    assert m.count() == 2
+    assert m.delete(I32(1234)) == 0 and m.lookup(I32(1234)) is None and m.count() == 1
+    for i in range(10):
+        m.update(I32(100 + i), I64(i))
+    assert m.count() == 10
+    assert m.update(I32(999), I64(1)) == 0 and m.lookup(I32(999)) is None  # full, returns 0
+
+
+def test_device_array_map_kat(fresh_runtime):
+    dev = fresh_runtime
+    m = dev.Map(isa.BPF_MAP_TYPE_ARRAY, 4, 8, 2)
+    assert m.update(I32(1), I64(1234), isa.BPF_ANY) == 0
+    assert m.update(I32(1), I64(0), isa.BPF_NOEXIST) < 0
+    assert m.lookup(I32(1)) == I64(1234) and m.lookup(I32(0)) == I64(0)
+    assert m.update(I32(2), I64(0), isa.BPF_EXIST) < 0 and m.lookup(I32(2)) is None
+    assert m.next_key(None) == I32(0) and m.next_key(I32(0)) == I32(1) and m.next_key(I32(1)) is None
+    assert m.delete(I32(1)) < 0
+
+
+def test_hash_next_key_matches_oracle_layout(fresh_oracle, fresh_runtime):
+    """Same hash (h*31+b) and linear probing as bpftime_hash_map: inserting
+    the same keys in the same order gives the same bucket order."""
+    po, dev = fresh_oracle, fresh_runtime
+    (om,), (dm,) = make_maps([(isa.BPF_MAP_TYPE_HASH, 4, 4, 97)], po, dev)
+    keys = random.Random(5).sample(range(1 << 31), 60)
+    for k in keys:
+        om.update(I32(k), I32(k + 1))
+        dm.update(I32(k), I32(k + 1))
+    walk_o, k = [], om.next_key(None)
+    while k is not None:
+        walk_o.append(k)
+        k = om.next_key(k)
+    walk_d, k = [], dm.next_key(None)
+    while k is not None:
+        walk_d.append(k)
+        k = dm.next_key(k)
+    assert walk_d == walk_o
+
+
+def _duplicate_keys(m):
+    nb, ss, ko, vo, nc = m.geometry()
+    raw = m.snapshot().reshape(nb, ss)
+    filled = raw[raw[:, :4].view(np.uint32)[:, 0] == 1]
+    keys = [bytes(r[ko:ko + m.key_size]) for r in filled]
+    return len(keys) - len(set(keys))
+
+
+def _flow_setup(po, dev, nflows_max=65536):
+    return make_maps([(isa.BPF_MAP_TYPE_HASH, 16, 16, nflows_max)], po, dev)
+
+
+@pytest.mark.parametrize("n,nflows", [(4096, 300), (50000, 4000)])
+def test_flow_hash_parity(fresh_oracle, fresh_runtime, n, nflows):
+    po, dev = fresh_oracle, fresh_runtime
+    (om,), (dm,) = _flow_setup(po, dev)
+    code = programs.flow_hash(dm.fd)
+    slots, lens = gen.flow_packets(n, nflows=nflows, stride=2048)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    ov = ovm.run_xdp(slots.copy(), lens=lens)
+    vm = dev.VM()
+    vm.load(code)
+    d = dev.DeviceBuffer.from_array(slots)
+    dl = dev.DeviceBuffer.from_array(lens)
+    dv = dev.DeviceBuffer(4 * n)
+    assert vm.exec_batch(dev.CTX_XDP, d, n, 2048, lens=dl, verdicts=dv) == 0
+    np.testing.assert_array_equal(dv.download(np.uint32), ov)
+    # map contents as key -> value sets (bucket order may differ under races)
+    o_items = om.items()
+    d_items = dm.hash_items()
+    assert d_items == o_items
+    # size-independent property: totals = exact histogram of the input
+    tot_pkts = sum(struct.unpack("<QQ", v)[0] for v in d_items.values())
+    tot_bytes = sum(struct.unpack("<QQ", v)[1] for v in d_items.values())
+    ip = (slots[:, 12] == 0x08) & (slots[:, 13] == 0)
+    assert tot_pkts == int(ip.sum()) and tot_bytes == int(lens[ip].sum())
+
+
+def test_syscall_agg_parity(fresh_oracle, fresh_runtime):
+    po, dev = fresh_oracle, fresh_runtime
+    (om,), (dm,) = make_maps([(isa.BPF_MAP_TYPE_HASH, 4, 32, 8192)], po, dev)
+    code = programs.syscall_agg(dm.fd)
+    n = 60000
+    recs = gen.syscall_records(n)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    orets, ran = ovm.run_syscall(recs)
+    vm = dev.VM()
+    vm.load(code)
+    assert vm.info()["fused_rmw"] == 2
+    d = dev.DeviceBuffer.from_array(recs)
+    dr = dev.DeviceBuffer(8 * n)
+    assert vm.exec_batch(dev.CTX_SYSCALL, d, n, 64, rets=dr) == 0
+    np.testing.assert_array_equal(dr.download(np.uint64), orets)
+    assert _duplicate_keys(dm) == 0
+    assert dm.hash_items() == om.items()
+    ids = recs.view(np.uint64).reshape(n, 8)[:, 1]
+    live = (ids != 60) & (ids != 231)
+    counts = {struct.unpack("<I", k)[0]: struct.unpack("<QQ", v[:16]) for k, v in dm.hash_items().items()}
+    assert sum(c for c, _ in counts.values()) == int(live.sum())
+    assert 60 not in counts and 231 not in counts
+
+
+def test_percpu_array_counter(fresh_oracle, fresh_runtime):
+    """bpf_get_smp_processor_id + PERCPU_ARRAY: virtual CPU of unit i is
+    (i // 64) % ncpu on both sides."""
+    po, dev = fresh_oracle, fresh_runtime
+    ncpu = 8
+    po.set_ncpu(ncpu)
+    dev.set_ncpu(ncpu)
+    (om,), (dm,) = make_maps([(isa.BPF_MAP_TYPE_PERCPU_ARRAY, 4, 8, 4)], po, dev)
+    a = Asm()
+    a.ldx(8, 6, 1, 0)                      # r6 = unit word
+    a.alu64("and", 6, 3).stx(4, 10, -4, "r6")
+    a.ld_map_fd(1, dm.fd).mov64(2, "r10").add64(2, -4).call(1)
+    a.jmp("jeq", 0, 0, "out")
+    a.ldx(8, 1, 0, 0).add64(1, 1).stx(8, 0, 0, "r1")
+    a.call(isa.BPF_FUNC_get_smp_processor_id)
+    a.label("out").exit()
+    code = a.assemble()
+    n = 5000
+    units = gen.sm64(8, np.arange(n, dtype=np.uint64)).view(np.uint8).reshape(n, 8)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    o = np.zeros(n, dtype=np.uint64)
+    for w0 in range(0, n, 64):
+        po.set_cpu((w0 // 64) % ncpu)
+        o[w0:w0 + 64] = ovm.run_raw(units[w0:w0 + 64].copy(), 8)
+    vm = dev.VM()
+    vm.load(code)
+    d = dev.DeviceBuffer.from_array(units)
+    dr = dev.DeviceBuffer(8 * n)
+    assert vm.exec_batch(dev.CTX_RAW, d, n, 8, fixed_len=8, rets=dr) == 0
+    np.testing.assert_array_equal(dr.download(np.uint64), o)
+    for k in range(4):
+        assert dm.lookup(I32(k)) == om.lookup(I32(k)), k
+
+
+def test_percpu_hash_update_lookup(fresh_oracle, fresh_runtime):
+    po, dev = fresh_oracle, fresh_runtime
+    ncpu = 4
+    po.set_ncpu(ncpu)
+    dev.set_ncpu(ncpu)
+    (om,), (dm,) = make_maps([(isa.BPF_MAP_TYPE_PERCPU_HASH, 4, 8, 1024)], po, dev)
+    # each unit writes value = unit word into key (word & 15) on its cpu slot
+    # (last writer wins: run ORDERED for the reference's sequential result)
+    a = Asm()
+    a.ldx(8, 6, 1, 0).mov64(7, "r6").alu64("and", 7, 15).stx(4, 10, -4, "r7")
+    a.stx(8, 10, -16, "r6")
+    a.ld_map_fd(1, dm.fd).mov64(2, "r10").add64(2, -4).mov64(3, "r10").add64(3, -16).mov64(4, 0).call(2)
+    a.ld_map_fd(1, dm.fd).mov64(2, "r10").add64(2, -4).call(1)
+    a.jmp("jeq", 0, 0, "out").ldx(8, 0, 0, 0).label("out").exit()
+    code = a.assemble()
+    n = 64 * ncpu
+    units = np.zeros((n, 8), dtype=np.uint8)
+    units.view(np.uint64)[:, 0] = np.arange(n, dtype=np.uint64) * 7 + 3
+    ovm = po.OracleVM()
+    ovm.load(code)
+    o = np.zeros(n, dtype=np.uint64)
+    for w0 in range(0, n, 64):
+        po.set_cpu((w0 // 64) % ncpu)
+        o[w0:w0 + 64] = ovm.run_raw(units[w0:w0 + 64].copy(), 8)
+    vm = dev.VM()
+    vm.load(code)
+    d = dev.DeviceBuffer.from_array(units)
+    dr = dev.DeviceBuffer(8 * n)
+    assert vm.exec_batch(dev.CTX_RAW, d, n, 8, fixed_len=8, rets=dr, flags=dev.BATCH_SYNC | dev.BATCH_ORDERED) == 0
+    np.testing.assert_array_equal(dr.download(np.uint64), o)
+    assert {k: v for k, v in dm.hash_items().items()} == om.items()
