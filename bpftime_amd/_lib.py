@@ -95,6 +95,11 @@ SIGNATURES = [
     ("bpftime_amd_memcpy_dtoh", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     ("bpftime_amd_memset", C.c_int, [C.c_void_p, C.c_int, C.c_uint64]),
     ("bpftime_amd_sync", C.c_int, []),
+    ("bpftime_amd_memcpy_htod_async", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    ("bpftime_amd_memcpy_dtoh_async", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    ("bpftime_amd_stream_create", C.c_void_p, []),
+    ("bpftime_amd_stream_destroy", None, [C.c_void_p]),
+    ("bpftime_amd_stream_sync", C.c_int, [C.c_void_p]),
     ("bpftime_amd_host_alloc", C.c_void_p, [C.c_uint64]),
     ("bpftime_amd_host_free", None, [C.c_void_p]),
     ("bpftime_amd_event_create", C.c_void_p, []),

@@ -45,7 +45,11 @@ class Mi355xVm {
   bool loaded = false;
   LoadOut prog;
   DInsn *d_prog = nullptr;
+  // failed-unit counters, one per in-flight batch: concurrent batches on
+  // different streams must not share (and re-zero) one counter
+  static constexpr uint32_t kErrSlots = 64;
   uint32_t *d_err = nullptr;
+  uint32_t err_slot = 0;
   // staging for ebpf_exec
   uint8_t *d_stage = nullptr;
   size_t stage_size = 0;
@@ -106,7 +110,7 @@ class Mi355xVm {
       error = "device upload failed";
       return -1;
     }
-    if (!d_err && hipMalloc((void **)&d_err, 4) != hipSuccess) {
+    if (!d_err && hipMalloc((void **)&d_err, 4 * kErrSlots) != hipSuccess) {
       error = "device alloc failed";
       return -1;
     }
@@ -140,7 +144,8 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   p.rets = b->rets;
   p.out_data_off = b->data_off_out;
   p.out_len = b->len_out;
-  p.err_count = d_err;
+  uint32_t *err = d_err + (err_slot++ % kErrSlots);
+  p.err_count = err;
   p.n = b->count;
   p.stride = b->stride;
   p.first_unit = b->first_unit;
@@ -156,7 +161,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   p.rxq = b->rx_queue_index;
   p.head = b->head;
   p.checked = (b->flags & EBPF_BATCH_UNCHECKED) ? 0 : 1;
-  if (hipMemsetAsync(d_err, 0, 4, s) != hipSuccess) {
+  if (hipMemsetAsync(err, 0, 4, s) != hipSuccess) {
     error = "hipMemsetAsync failed";
     return -1;
   }
@@ -185,7 +190,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   }
   if (b->flags & EBPF_BATCH_SYNC) {
     uint32_t failed = 0;
-    if (hipMemcpyAsync(&failed, d_err, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (hipMemcpyAsync(&failed, err, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
       error = "batch sync failed";
       return -1;
@@ -443,6 +448,23 @@ int bpftime_amd_memcpy_htod(void *dst, const void *src, uint64_t bytes) {
 }
 int bpftime_amd_memcpy_dtoh(void *dst, const void *src, uint64_t bytes) {
   return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+int bpftime_amd_memcpy_htod_async(void *dst, const void *src, uint64_t bytes, void *stream) {
+  return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream) == hipSuccess ? 0 : -1;
+}
+int bpftime_amd_memcpy_dtoh_async(void *dst, const void *src, uint64_t bytes, void *stream) {
+  return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream) == hipSuccess ? 0 : -1;
+}
+void *bpftime_amd_stream_create(void) {
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  return (void *)s;
+}
+void bpftime_amd_stream_destroy(void *stream) {
+  if (stream) hipStreamDestroy((hipStream_t)stream);
+}
+int bpftime_amd_stream_sync(void *stream) {
+  return hipStreamSynchronize((hipStream_t)stream) == hipSuccess ? 0 : -1;
 }
 int bpftime_amd_memset(void *dst, int v, uint64_t bytes) { return hipMemset(dst, v, bytes) == hipSuccess ? 0 : -1; }
 int bpftime_amd_sync(void) { return hipDeviceSynchronize() == hipSuccess ? 0 : -1; }

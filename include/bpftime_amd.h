@@ -113,6 +113,12 @@ void *bpftime_amd_dev_alloc(uint64_t bytes);
 void bpftime_amd_dev_free(void *p);
 int bpftime_amd_memcpy_htod(void *dst, const void *src, uint64_t bytes);
 int bpftime_amd_memcpy_dtoh(void *dst, const void *src, uint64_t bytes);
+/* async copies on a stream (host side must be pinned for overlap) */
+int bpftime_amd_memcpy_htod_async(void *dst, const void *src, uint64_t bytes, void *stream);
+int bpftime_amd_memcpy_dtoh_async(void *dst, const void *src, uint64_t bytes, void *stream);
+void *bpftime_amd_stream_create(void); /* non-blocking hipStream_t */
+void bpftime_amd_stream_destroy(void *stream);
+int bpftime_amd_stream_sync(void *stream);
 int bpftime_amd_memset(void *dst, int v, uint64_t bytes);
 int bpftime_amd_sync(void);
 void *bpftime_amd_host_alloc(uint64_t bytes); /* pinned */
