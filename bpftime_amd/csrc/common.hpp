@@ -86,8 +86,10 @@ constexpr uint32_t CTX_XDP = 1;      // r1 = xdp_md_userspace (48 B, LDS)
 constexpr uint32_t CTX_SYSCALL = 2;  // r1 = 64-B trace_event_raw_sys_enter record
 
 // Kernel launch parameters (passed by value).
+struct FInsn;
 struct KParams {
   const DInsn *prog;
+  const FInsn *fast;      // threaded-code form for the asm fast path
   const DMap *maps;
   uint8_t *data;          // base of unit slots (device)
   const uint32_t *lens;   // per-unit lengths or nullptr

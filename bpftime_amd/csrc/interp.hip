@@ -27,6 +27,8 @@
 
 #include "common.hpp"
 #include "dev_helpers.hpp"
+#include "fast_asm.inc"
+#include "fast_ops.hpp"
 
 namespace bpftime_amd {
 
@@ -73,7 +75,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef const u32x4 __attribute__((address_space(4))) *prog_ptr;
 
 // loop exits
-constexpr uint32_t R_DONE = 0, R_DIVERGE = 1, R_RECONV = 2, R_CALL = 3;
+constexpr uint32_t R_DONE = 0, R_DIVERGE = 1, R_RECONV = 2, R_CALL = 3, R_STEP = 4;
 
 // Everything one interpreter loop reads or updates (inlined; SROA'd).
 struct Ctx {
@@ -99,8 +101,9 @@ struct Ctx {
 #define RG(i) c.R[(uint32_t)(i) * kBlock]
 
 // Runs the program until the wave exits, diverges / reconverges, or calls
-// a helper.  UNI: every live lane is at c.pc and selected.
-template <bool UNI>
+// a helper.  UNI: every live lane is at c.pc and selected.  ONE: return
+// R_STEP after one instruction (the slow step behind the asm fast path).
+template <bool UNI, bool ONE = false>
 __device__ __forceinline__ uint32_t run_loop(Ctx &c) {
   for (;;) {
     uint32_t cur;
@@ -375,9 +378,37 @@ __device__ __forceinline__ uint32_t run_loop(Ctx &c) {
       else
         c.lpc = sel ? npc : c.lpc;
     }
+    if (ONE) return R_STEP;
   }
 }
 #undef RG
+
+// Threaded-code fast path (gen_fast.py): runs the uniform loop in asm from
+// c.pc until an instruction it does not handle; returns 1 if the step limit
+// was crossed at a taken jump, else 0 (c.pc = the instruction to run in C++).
+struct FastEnv {
+  const FInsn *fast;
+  uint64_t dlo, dhi, alo, ahi;
+  uint32_t shi, phi;
+  uint32_t rb;  // LDS byte address of this lane's R[0]
+};
+
+__device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f) {
+  // every "s" operand must be provably uniform: readfirstlane what the
+  // compiler cannot prove (the values are uniform by construction)
+  uint32_t pc = __builtin_amdgcn_readfirstlane(c.pc), steps = __builtin_amdgcn_readfirstlane(c.steps), why;
+  const uint64_t alive = __ballot(c.alive);
+  const uint32_t limit = __builtin_amdgcn_readfirstlane(c.step_limit);
+  asm volatile(BPFTIME_AMD_FAST_ASM
+               : [pc] "+s"(pc), [steps] "+s"(steps), [why] "=s"(why)
+               : [prog] "s"(f.fast), [dlo] "s"(f.dlo), [dhi] "s"(f.dhi), [alo] "s"(f.alo), [ahi] "s"(f.ahi),
+                 [shi] "s"(f.shi), [phi] "s"(f.phi), [limit] "s"(limit), [rb] "v"(f.rb),
+                 [alive] "s"(alive)
+               : BPFTIME_AMD_FAST_CLOBBERS);
+  c.pc = pc;
+  c.steps = steps;
+  return why;
+}
 
 template <uint32_t KIND, bool BIGSTACK>
 __global__ __launch_bounds__(kBlock) void k_interp(KParams pin) {
@@ -387,7 +418,7 @@ __global__ __launch_bounds__(kBlock) void k_interp(KParams pin) {
   KParams p;
 #define SRP(f) p.f = (decltype(p.f))sreg((uint64_t)(uintptr_t)pin.f)
 #define SRV(f) p.f = sreg(pin.f)
-  SRP(prog); SRP(maps); SRP(data); SRP(lens); SRP(verdicts); SRP(rets); SRP(out_data_off); SRP(out_len);
+  SRP(prog); SRP(fast); SRP(maps); SRP(data); SRP(lens); SRP(verdicts); SRP(rets); SRP(out_data_off); SRP(out_len);
   SRP(err_count); SRV(n); SRV(stride); SRV(first_unit); SRV(data_lo); SRV(data_hi); SRV(arena_lo);
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
   SRV(checked); SRV(head); SRV(ordered);
@@ -413,6 +444,19 @@ __global__ __launch_bounds__(kBlock) void k_interp(KParams pin) {
   c.step_limit = p.step_limit > 0xffffffffull ? 0xffffffffu : (uint32_t)p.step_limit;
   c.c0a = c.c0d = c.c1a = c.c1d = 0;
   c.c0s = c.c1s = 0;
+
+  // fast-path operands, computed once into SGPRs (sreg: no per-entry rebuild)
+  FastEnv fe;
+  fe.fast = (const FInsn *)sreg((uint64_t)(uintptr_t)p.fast);
+  fe.dlo = sreg((uint64_t)(p.checked ? p.data_lo : 0));
+  fe.dhi = sreg((uint64_t)(p.checked ? p.data_hi : ~(uint64_t)0));
+  fe.alo = p.arena_lo;
+  fe.ahi = p.arena_hi;
+  fe.shi = sreg((uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)(uintptr_t)&Rf[0] >> 32)));
+  fe.phi = BIGSTACK ? sreg((uint32_t)__builtin_amdgcn_readfirstlane(
+                          (uint32_t)((uint64_t)(uintptr_t)&big_stack[0] >> 32)))
+                    : fe.shi;
+  fe.rb = (uint32_t)(uintptr_t)&Rf[tid];
 
   const bool ordered = p.ordered != 0;
   const uint64_t ustep = ordered ? 1 : (uint64_t)gridDim.x * kBlock;
@@ -461,7 +505,18 @@ __global__ __launch_bounds__(kBlock) void k_interp(KParams pin) {
 
     bool uni = true;
     while (__ballot(c.alive) != 0) {
-      const uint32_t r = uni ? run_loop<true>(c) : run_loop<false>(c);
+      uint32_t r;
+      if (uni) {
+        if (run_fast(c, fe)) {
+          c.err = c.alive ? E_STEPS : c.err;
+          c.alive = false;
+          break;
+        }
+        r = run_loop<true, true>(c);
+      } else {
+        r = run_loop<false>(c);
+      }
+      if (r == R_STEP) continue;
       if (r == R_DONE) break;
       if (r == R_DIVERGE) {
         uni = false;

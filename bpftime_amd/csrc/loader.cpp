@@ -618,3 +618,74 @@ int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &
 }
 
 }  // namespace bpftime_amd
+
+namespace bpftime_amd {
+
+static uint32_t fast_id(const DInsn &d) {
+  const bool r = (d.aux & A_SRCREG) != 0;
+  const bool w32 = (d.aux & A_W32) != 0;
+  const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
+  auto alu = [&](uint32_t r64, uint32_t i64, uint32_t r32, uint32_t i32) {
+    return w32 ? (r ? r32 : i32) : (r ? r64 : i64);
+  };
+  auto by_size = [&](uint32_t s1, uint32_t s2, uint32_t s4, uint32_t s8) {
+    return sz == 1 ? s1 : sz == 2 ? s2 : sz == 4 ? s4 : s8;
+  };
+#define ALU4(OP) alu(F_A64_##OP##_R, F_A64_##OP##_I, F_A32_##OP##_R, F_A32_##OP##_I)
+#define JCC(CC) alu(F_J64_##CC##_R, F_J64_##CC##_I, F_J32_##CC##_R, F_J32_##CC##_I)
+  switch (d.op) {
+    case X_ADD: return ALU4(ADD);
+    case X_SUB: return ALU4(SUB);
+    case X_MUL: return ALU4(MUL);
+    case X_OR: return ALU4(OR);
+    case X_AND: return ALU4(AND);
+    case X_XOR: return ALU4(XOR);
+    case X_MOV: return ALU4(MOV);
+    case X_LSH64: return r ? F_A64_LSH_R : F_A64_LSH_I;
+    case X_RSH64: return r ? F_A64_RSH_R : F_A64_RSH_I;
+    case X_ARSH64: return r ? F_A64_ARSH_R : F_A64_ARSH_I;
+    case X_LSH32: return r ? F_A32_LSH_R : F_A32_LSH_I;
+    case X_RSH32: return r ? F_A32_RSH_R : F_A32_RSH_I;
+    case X_ARSH32: return r ? F_A32_ARSH_R : F_A32_ARSH_I;
+    case X_NEG64: return F_A64_NEG;
+    case X_NEG32: return F_A32_NEG;
+    case X_LE: return d.imm == 16 ? F_LE16 : d.imm == 32 ? F_LE32 : d.imm == 64 ? F_NOP : F_SLOW;
+    case X_BE: return d.imm == 16 ? F_BE16 : d.imm == 32 ? F_BE32 : d.imm == 64 ? F_BE64 : F_SLOW;
+    case X_LDX: return by_size(F_LDX1, F_LDX2, F_LDX4, F_LDX8);
+    case X_STX: return by_size(F_STX1, F_STX2, F_STX4, F_STX8);
+    case X_ST: return by_size(F_ST1, F_ST2, F_ST4, F_ST8);
+    case X_LDDW: return F_LDDW;
+    case X_JA: return F_JA;
+    case X_JEQ: return JCC(EQ);
+    case X_JGT: return JCC(GT);
+    case X_JGE: return JCC(GE);
+    case X_JSET: return JCC(SET);
+    case X_JNE: return JCC(NE);
+    case X_JSGT: return JCC(SGT);
+    case X_JSGE: return JCC(SGE);
+    case X_JLT: return JCC(LT);
+    case X_JLE: return JCC(LE);
+    case X_JSLT: return JCC(SLT);
+    case X_JSLE: return JCC(SLE);
+    default: return F_SLOW;  // div/mod, atomics, fused counters, call, exit
+  }
+#undef ALU4
+#undef JCC
+}
+
+void build_fast(const std::vector<DInsn> &prog, std::vector<FInsn> &fast) {
+  fast.assign(prog.size(), FInsn{});
+  for (size_t i = 0; i < prog.size(); i++) {
+    const DInsn &d = prog[i];
+    FInsn &f = fast[i];
+    f.hoff = 4 + 4 * fast_id(d);
+    f.dst_off = (uint32_t)d.dst * kBlock * 8;
+    f.src_off = (uint32_t)d.src * kBlock * 8;
+    f.imm = d.op == X_LDDW ? (int64_t)((uint64_t)(uint32_t)d.imm | ((uint64_t)(uint32_t)d.hi << 32))
+                           : (int64_t)d.imm;
+    f.target = (uint32_t)d.tgt * (uint32_t)sizeof(FInsn);
+    f.off = (int64_t)d.off;
+  }
+}
+
+}  // namespace bpftime_amd

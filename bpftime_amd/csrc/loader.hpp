@@ -5,6 +5,7 @@
 #include <string>
 #include <vector>
 #include "common.hpp"
+#include "fast_ops.hpp"
 
 namespace bpftime_amd {
 
@@ -28,6 +29,7 @@ struct LddwHelpers {
 
 struct LoadOut {
   std::vector<DInsn> prog;
+  std::vector<FInsn> fast;   // threaded-code form of `prog` (gen_fast.py)
   uint32_t stack_size = 8;   // per-lane bytes (LDS)
   bool big_stack = false;    // 512-B scratch stack
   uint32_t fused_rmw = 0;
@@ -35,6 +37,10 @@ struct LoadOut {
 
 // Helper ids the device implements (interp.hip helper switch).
 bool device_helper_supported(uint32_t id);
+
+// Threaded-code records for the asm fast path: one per DInsn; instructions
+// without a fast handler dispatch to F_SLOW (the C++ interpreter).
+void build_fast(const std::vector<DInsn> &prog, std::vector<FInsn> &fast);
 
 // Runs the compat_ubpf.cpp:61-200 patching (call remap check, lddw pseudo
 // sources), ubpf-style validation, pre-decoding and the dataflow analyses

@@ -45,6 +45,7 @@ class Mi355xVm {
   bool loaded = false;
   LoadOut prog;
   DInsn *d_prog = nullptr;
+  FInsn *d_fast = nullptr;
   // failed-unit counters, one per in-flight batch: concurrent batches on
   // different streams must not share (and re-zero) one counter
   static constexpr uint32_t kErrSlots = 64;
@@ -69,6 +70,8 @@ class Mi355xVm {
   void unload() {
     if (d_prog) hipFree(d_prog);
     d_prog = nullptr;
+    if (d_fast) hipFree(d_fast);
+    d_fast = nullptr;
     loaded = false;
     prog = LoadOut();
   }
@@ -104,9 +107,13 @@ class Mi355xVm {
       error = "no HIP device: " + rt().last_error;
       return -1;
     }
+    build_fast(out.prog, out.fast);
     size_t bytes = out.prog.size() * sizeof(DInsn);
+    size_t fbytes = out.fast.size() * sizeof(FInsn);
     if (hipMalloc((void **)&d_prog, bytes) != hipSuccess ||
-        hipMemcpy(d_prog, out.prog.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(d_prog, out.prog.data(), bytes, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMalloc((void **)&d_fast, fbytes) != hipSuccess ||
+        hipMemcpy(d_fast, out.fast.data(), fbytes, hipMemcpyHostToDevice) != hipSuccess) {
       error = "device upload failed";
       return -1;
     }
@@ -137,6 +144,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   Runtime &r = rt();
   KParams p{};
   p.prog = d_prog;
+  p.fast = d_fast;
   p.maps = r.d_maptab;
   p.data = (uint8_t *)b->data;
   p.lens = b->lens;
