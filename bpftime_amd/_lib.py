@@ -109,6 +109,10 @@ SIGNATURES = [
     ("bpftime_amd_last_error", C.c_char_p, []),
     ("bpftime_amd_gen_xdp", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64,
                                        C.c_uint64, C.c_void_p]),
+    ("bpftime_amd_gen_flow", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                                        C.c_void_p, C.c_uint32, C.c_void_p]),
+    ("bpftime_amd_gen_syscall", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint32,
+                                           C.c_void_p]),
 ]
 
 # symbols outside include/*.h that the Python layer also uses

@@ -27,7 +27,100 @@ __global__ void k_gen_xdp(uint8_t *base, uint64_t n, uint64_t stride, uint64_t s
   }
 }
 
+// Bounded Zipf id by inverse CDF (gen.py zipf_ids): the first index whose
+// cdf entry exceeds u (numpy searchsorted side="right"), clamped.
+__device__ __forceinline__ uint32_t zipf_pick(const double *cdf, uint32_t support, uint64_t seed, uint64_t g) {
+  const double u = (double)(sm64(seed, g) >> 11) * (1.0 / 9007199254740992.0);
+  uint32_t lo = 0, hi = support;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (cdf[mid] <= u) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < support ? lo : support - 1;
+}
+
+// config 3 frames (gen.py flow_packets): slot noise, then Ethernet/IPv4
+// header fields of the unit's Zipf flow; one thread per 8-B word, the
+// thread holding word 1 of a slot also writes its length.
+__global__ void k_gen_flow(uint8_t *base, uint32_t *lens, uint64_t n, uint64_t stride, uint64_t seed,
+                           uint64_t first, const double *cdf, uint32_t nflows) {
+  const uint64_t W = stride / 8;
+  const uint64_t total = n * W;
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total;
+       w += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t unit = w / W, j = w % W, g = first + unit;
+    uint64_t v = sm64(seed ^ 0x4444, g * W + j);
+    if (j >= 1 && j <= 4) {
+      const uint64_t r = sm64(seed ^ 0x1111, g);
+      const bool is_ip = ((r >> 8) % 100) < 95;
+      const uint64_t flow = zipf_pick(cdf, nflows, seed, g);
+      const uint64_t fk = sm64(seed ^ 0x2222, flow), fk2 = sm64(seed ^ 0x3333, flow);
+      uint8_t *b = (uint8_t *)&v;
+      const uint64_t o = j * 8;  // byte offset of this word in the slot
+      auto put = [&](uint64_t at, uint8_t x) {
+        if (at >= o && at < o + 8) b[at - o] = x;
+      };
+      put(12, is_ip ? 0x08 : 0x86);
+      put(13, is_ip ? 0x00 : 0xDD);
+      put(14, 0x45);
+      put(23, ((fk2 >> 40) & 1) ? 6 : 17);
+      for (int k = 0; k < 4; k++) {
+        put(26 + k, (uint8_t)(fk >> (8 * k)));
+        put(30 + k, (uint8_t)(fk >> (32 + 8 * k)));
+        put(34 + k, (uint8_t)(fk2 >> (8 * k)));
+      }
+      if (j == 1 && lens) {
+        const uint64_t sel = r % 12;
+        lens[unit] = sel < 7 ? 64 : sel < 11 ? 570 : 1500;
+      }
+    }
+    *(uint64_t *)(base + unit * stride + j * 8) = v;
+  }
+}
+
+// config 5 records (gen.py syscall_records): 64-B trace_event_raw_sys_enter,
+// id Zipf over [0, support) with 1 % exit(60) / exit_group(231).
+__global__ void k_gen_syscall(uint8_t *base, uint64_t n, uint64_t seed, uint64_t first, const double *cdf,
+                              uint32_t support) {
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n * 8;
+       w += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t unit = w / 8, j = w % 8, g = first + unit;
+    uint64_t v = 0;
+    if (j == 1) {
+      const uint64_t r = sm64(seed ^ 0x5555, g);
+      v = (r % 100) == 0 ? (((r >> 9) & 1) ? 60 : 231) : zipf_pick(cdf, support, seed, g);
+    } else if (j >= 2) {
+      v = sm64(seed ^ (0x6000 + (j - 2)), g) & 0xFFFFFFFFFFull;
+    }
+    *(uint64_t *)(base + unit * 64 + j * 8) = v;
+  }
+}
+
 }  // namespace bpftime_amd
+
+static uint32_t gen_blocks(uint64_t total) {
+  uint64_t blocks = (total + 255) / 256;
+  return (uint32_t)(blocks > 16384 ? 16384 : blocks);
+}
+
+extern "C" int bpftime_amd_gen_flow(void *dev, uint32_t *lens, uint64_t n, uint64_t stride, uint64_t seed,
+                                    uint64_t first, const double *cdf, uint32_t nflows, void *stream) {
+  if (stride % 8 || stride < 64 || !cdf || !nflows) return -1;
+  if (!n) return 0;
+  hipLaunchKernelGGL(bpftime_amd::k_gen_flow, dim3(gen_blocks(n * (stride / 8))), dim3(256), 0,
+                     (hipStream_t)stream, (uint8_t *)dev, lens, n, stride, seed, first, cdf, nflows);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int bpftime_amd_gen_syscall(void *dev, uint64_t n, uint64_t seed, uint64_t first, const double *cdf,
+                                       uint32_t support, void *stream) {
+  if (!cdf || !support) return -1;
+  if (!n) return 0;
+  hipLaunchKernelGGL(bpftime_amd::k_gen_syscall, dim3(gen_blocks(n * 8)), dim3(256), 0, (hipStream_t)stream,
+                     (uint8_t *)dev, n, seed, first, cdf, support);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 extern "C" int bpftime_amd_gen_xdp(void *dev, uint64_t n, uint64_t stride, uint32_t len, uint64_t seed,
                                    uint64_t first, void *stream) {

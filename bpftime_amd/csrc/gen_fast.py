@@ -11,33 +11,62 @@ a table of `s_branch` instructions; dispatch is
     s_add_u32/s_addc_u32 T, TB, W0
     s_setpc_b64 T                 ; -> table entry -> handler
 
-instead of a compare tree.  The handlers cover ALU64/ALU32 (reg and imm),
-byte swaps, loads/stores of every size with the batch/arena/LDS window check,
-lddw, ja and every conditional jump whose outcome is wave-uniform.  Anything
-else (helper calls, exit, fused counters, atomics, div/mod, a split branch,
-an access failing the window check) leaves the block at that pc, and the C++
-interpreter executes that one instruction (interp.hip, run_loop<true, true>).
+instead of a compare tree.  exec = the wave's live lanes inside the block, so
+compare results and stores need no per-lane predication.
 
-exec = the wave's live lanes inside the block, so compare results and
-stores need no per-lane predication.
+Registers.  r0..r10 live in VGPRs v[60:81] (r_i = v[60+2i : 61+2i]) while the
+block runs; an instruction's register fields are VGPR indices used with
+`s_set_gpr_idx_on` (register numbers are wave-uniform).  The C++ side keeps
+its LDS copy (lane-major, 2 KiB per register): a fresh unit initialises the
+VGPRs from operands, a re-entry loads them from LDS, and every exit other
+than `exit` stores them back.
 
-Register file: r0..r10 stay in LDS, lane-major (8 B per lane, 2 KiB per
-register), so the C++ path and the asm path share one representation.
+Unit staging.  On a fresh unit the first 64 bytes of the unit's slot are
+loaded into v[84:99] with four global_load_dwordx4.  A load or store whose
+offset from the slot is wave-uniform and inside the window is served from
+those VGPRs (dword index via s_set_gpr_idx_on, bytes via v_alignbit /
+v_bfi); stores mark 16-byte chunks dirty and dirty chunks are written back
+(global_store_dwordx4) before any exit and before any other access that
+overlaps the window (which also ends staging for the unit).  A packet's
+header reads and rewrites then cost two coalesced HBM transactions instead
+of a chain of dependent byte loads and stores.
+
+The handlers cover ALU64/ALU32 (reg and imm), byte swaps, loads/stores of
+every size with the batch/arena/LDS window check, lddw, ja, every
+conditional jump whose outcome is wave-uniform, array-map lookups with a
+wave-uniform fd, wave-uniform fused counters and exit.  Anything else (other
+helpers, atomics, div/mod, a split branch, an access failing the window
+check) leaves the block at that pc, and the C++ interpreter executes that
+one instruction (interp.hip, run_loop<true, true>).
 
 Fixed registers (declared as clobbers; the compiler keeps nothing live in
-them across the block):
-  s[40:47] W   current FInsn: w0 handler offset, w1 dst*2048, w[2:3] imm64,
-               w4 src*2048, w5 jump target (byte offset from PROG), w[6:7] off64
+them across the block).  The handlers are written against the numbering
+below; main() relocates every VGPR to the top of a 128-register budget
+(v40-v42 -> v72-v74, v44-v55 -> v76-v87, v60-v81 -> v88-v109,
+v84-v101 -> v110-v127):
+  s[40:47] W   current FInsn: w0 handler offset, w1 dst*2, w[2:3] imm64,
+               w4 src*2, w5 jump target (byte offset from PROG), w[6:7] off64
   s[48:49] IP  address of the current FInsn     s[50:51] TB  table base - 4
-  s[52:53] T   scratch / dispatch target        s[54:55], s[56:57], s[76:77] masks
-  s[58:59] saved exec                            s[60:61] PROG (FInsn base)
-  s[62:63]/s[64:65] batch window lo/hi           s[66:67]/s[68:69] map arena lo/hi
-  s70 LDS aperture (address bits 63:32)          s71 scratch aperture
-  s72 steps  s73 step limit  s74 exit reason  s75 scratch
-  v40 lane's R[0] LDS address  v41/v42 register addresses
+  s[52:53] T   scratch / dispatch target        s[54:55], s[56:57], s[60:61] masks
+  s[58:59] saved exec                            s[62:63] A0 (wave-uniform address)
+  s[64:65] V0 (wave-uniform value)               s[66:67] TOT (wave total)
+  s68 exit reason   s69/s70/s71 scratch          s[72:75] DMap words 0-3
+  s[76:77] DMap data pointer                     s[78:79] PROG (FInsn base)
+  s[80:81] S (staged bytes, 64-bit)              s[82:83] O (uniform window offset)
+  s84 dirty 16-B chunk mask                      s85 scratch
+  v40 lane's R[0] LDS address  v41/v42 scratch
   v[44:45] X  v[46:47] Y  v[48:49] Z (address)  v[50:51] E (address end)
+  v[52:53] slot address (staging base)           v[54:55] O (per-lane offset)
+  v[60:81] r0..r10                               v[84:99] staged bytes
+Loop-invariant inputs (window bounds, apertures, step limit, map table,
+output addresses) and the per-wave counter cache are asm operands, so they
+stay in the registers the compiler already holds them in.
+
+Exit reasons (s68 -> why): 0 run the instruction at pc in C++, 1 step limit
+crossed at a taken jump, 2 every live lane executed exit (r0 stored).
 """
 import os
+import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -46,6 +75,9 @@ JCC = ["EQ", "GT", "GE", "SET", "NE", "SGT", "SGE", "LT", "LE", "SLT", "SLE"]
 CMP64 = {"EQ": "eq_u64", "GT": "gt_u64", "GE": "ge_u64", "NE": "ne_u64", "SGT": "gt_i64",
          "SGE": "ge_i64", "LT": "lt_u64", "LE": "le_u64", "SLT": "lt_i64", "SLE": "le_i64"}
 CMP32 = {k: v.replace("64", "32") for k, v in CMP64.items()}
+R0 = 60        # first VGPR of the eBPF register file
+STG = 84       # first VGPR of the staged bytes
+NREG = 11
 
 
 def handler_ids():
@@ -58,7 +90,7 @@ def handler_ids():
     ids += ["LE16", "LE32", "BE16", "BE32", "BE64", "NOP"]
     for sz in (1, 2, 4, 8):
         ids += [f"LDX{sz}", f"STX{sz}", f"ST{sz}"]
-    ids += ["LDDW", "JA"]
+    ids += ["LDDW", "JA", "CALL_LOOKUP", "EXIT", "RMW4_R", "RMW4_I", "RMW8_R", "RMW8_I"]
     for w in ("64", "32"):
         for cc in JCC:
             for k in ("R", "I"):
@@ -73,15 +105,20 @@ def L(name):
 class Gen:
     def __init__(self):
         self.out = []
+        self.uid = 0
 
     def e(self, *lines):
         self.out.extend(lines)
 
-    # ---- building blocks ----
+    def label(self, stem):
+        self.uid += 1
+        return L(f"{stem}{self.uid}")
+
+    # ---- dispatch ----
     def dispatch(self):
         """IP points at the next FInsn: fetch it and jump to its handler."""
         self.e("s_load_dwordx8 s[40:47], s[48:49], 0x0",
-               "s_add_u32 s72, s72, 1",
+               "s_add_u32 %[steps], %[steps], 1",
                "s_waitcnt lgkmcnt(0)",
                "s_add_u32 s52, s50, s40",
                "s_addc_u32 s53, s51, 0",
@@ -92,52 +129,135 @@ class Gen:
         self.dispatch()
 
     def jump_taken(self):
-        self.e("s_add_u32 s48, s60, s45", "s_addc_u32 s49, s61, 0",
-               "s_cmp_gt_u32 s72, s73", f"s_cbranch_scc1 {L('steps')}")
+        self.e("s_add_u32 s48, s78, s45", "s_addc_u32 s49, s79, 0",
+               "s_cmp_gt_u32 %[steps], %[limit]", f"s_cbranch_scc1 {L('steps')}")
         self.dispatch()
 
-    def read_dst(self):  # X = R[dst], v41 = &R[dst]
-        self.e("v_add_u32 v41, s41, v40", "ds_read_b64 v[44:45], v41")
+    # ---- register file (VGPRs, indexed by a wave-uniform SGPR) ----
+    def rd(self, sidx, v):
+        """v[v:v+1] = r[sidx / 2]"""
+        self.e(f"s_set_gpr_idx_on {sidx}, gpr_idx(SRC0)",
+               f"v_mov_b32 v{v}, v{R0}", f"v_mov_b32 v{v + 1}, v{R0 + 1}",
+               "s_set_gpr_idx_off")
 
-    def read_src(self):  # Y = R[src]
-        self.e("v_add_u32 v42, s44, v40", "ds_read_b64 v[46:47], v42")
+    def wr(self, sidx, v):
+        """r[sidx / 2] = v[v:v+1]"""
+        self.e(f"s_set_gpr_idx_on {sidx}, gpr_idx(DST)",
+               f"v_mov_b32 v{R0}, v{v}", f"v_mov_b32 v{R0 + 1}, v{v + 1}",
+               "s_set_gpr_idx_off")
+
+    def rd_fixed(self, r, v):
+        self.e(f"v_mov_b32 v{v}, v{R0 + 2 * r}", f"v_mov_b32 v{v + 1}, v{R0 + 2 * r + 1}")
 
     def imm_y(self):     # Y = imm (sign-extended by the loader)
         self.e("v_mov_b32 v46, s42", "v_mov_b32 v47, s43")
 
-    def write_dst(self):
-        self.e("ds_write_b64 v41, v[44:45]")
-
+    # ---- memory ----
     def check(self, sz):
         """Every live lane's [Z, Z+sz) inside the batch window, the map arena,
         or the LDS / scratch aperture; else leave for the C++ path (which
         fails the offending lanes)."""
         self.e(f"v_lshl_add_u64 v[50:51], v[48:49], 0, {sz}",
-               "v_cmp_le_u64 s[54:55], s[62:63], v[48:49]",
-               "v_cmp_ge_u64 s[56:57], s[64:65], v[50:51]",
+               "v_cmp_le_u64 s[54:55], %[dlo], v[48:49]",
+               "v_cmp_ge_u64 s[56:57], %[dhi], v[50:51]",
                "s_and_b64 s[54:55], s[54:55], s[56:57]",
-               "v_cmp_le_u64 s[56:57], s[66:67], v[48:49]",
-               "v_cmp_ge_u64 s[76:77], s[68:69], v[50:51]",
-               "s_and_b64 s[56:57], s[56:57], s[76:77]",
+               "v_cmp_le_u64 s[56:57], %[alo], v[48:49]",
+               "v_cmp_ge_u64 s[60:61], %[ahi], v[50:51]",
+               "s_and_b64 s[56:57], s[56:57], s[60:61]",
                "s_or_b64 s[54:55], s[54:55], s[56:57]",
-               "v_cmp_eq_u32 s[56:57], s70, v49",
+               "v_cmp_eq_u32 s[56:57], %[shi], v49",
                "s_or_b64 s[54:55], s[54:55], s[56:57]",
-               "v_cmp_eq_u32 s[56:57], s71, v49",
+               "v_cmp_eq_u32 s[56:57], %[phi], v49",
                "s_or_b64 s[54:55], s[54:55], s[56:57]",
                "s_andn2_b64 s[54:55], exec, s[54:55]",
                f"s_cbranch_scc1 {L('slow')}")
 
+    def flush(self):
+        """Write dirty staged chunks back to the slots (exec = live lanes)."""
+        for c in range(4):
+            skip = self.label("fl")
+            self.e(f"s_bitcmp1_b32 s84, {c}", f"s_cbranch_scc0 {skip}",
+                   f"global_store_dwordx4 v[52:53], v[{STG + 4 * c}:{STG + 4 * c + 3}], off offset:{16 * c}",
+                   f"{skip}:")
+        self.e("s_mov_b32 s84, 0")
+
+    def staged_or(self, sz, on_staged, on_global):
+        """Z is the access address.  If staging is on and every live lane
+        accesses [Z, Z+sz) at the same offset O inside its staged window,
+        continue at `on_staged` with s82 = O.  Otherwise, if any lane's access
+        overlaps its window, write back dirty chunks and end staging; then
+        continue at `on_global`."""
+        conflict = self.label("cf")
+        self.e("s_cmp_eq_u64 s[80:81], 0", f"s_cbranch_scc1 {on_global}",
+               "v_sub_co_u32 v54, vcc, v48, v52", "v_subb_co_u32 v55, vcc, v49, v53, vcc",
+               "v_readfirstlane_b32 s82, v54", "v_readfirstlane_b32 s83, v55",
+               "v_cmp_ne_u64 s[54:55], s[82:83], v[54:55]",
+               "s_cmp_lg_u64 s[54:55], 0", f"s_cbranch_scc1 {conflict}",
+               f"s_add_u32 s69, s82, {sz}", "s_addc_u32 s70, s83, 0",
+               "s_cmp_lg_u32 s70, 0", f"s_cbranch_scc1 {conflict}",
+               "s_cmp_gt_u32 s69, s80", f"s_cbranch_scc0 {on_staged}",
+               f"{conflict}:",
+               # overlap per lane: O < S, or the access starts below the
+               # window and reaches into it (-sz <= O < 0 as a signed value)
+               "v_cmp_gt_u64 s[54:55], s[80:81], v[54:55]",
+               f"v_cmp_le_i64 s[56:57], -{sz}, v[54:55]",
+               "v_cmp_gt_i64 s[60:61], 0, v[54:55]",
+               "s_and_b64 s[56:57], s[56:57], s[60:61]",
+               "s_or_b64 s[54:55], s[54:55], s[56:57]",
+               "s_and_b64 s[54:55], s[54:55], exec",
+               "s_cmp_eq_u64 s[54:55], 0", f"s_cbranch_scc1 {on_global}")
+        self.flush()
+        self.e("s_waitcnt vmcnt(0)", "s_mov_b64 s[80:81], 0", f"s_branch {on_global}")
+
+    def staged_load(self, sz):
+        """X = sz bytes at window offset s82 (zero-extended)."""
+        self.e("s_waitcnt vmcnt(0)",                       # staging loads landed
+               "s_lshr_b32 s70, s82, 2", "s_and_b32 s71, s82, 3", "s_lshl_b32 s71, s71, 3",
+               "s_set_gpr_idx_on s70, gpr_idx(SRC0)",
+               f"v_mov_b32 v44, v{STG}", f"v_mov_b32 v45, v{STG + 1}", f"v_mov_b32 v46, v{STG + 2}",
+               "s_set_gpr_idx_off",
+               "v_alignbit_b32 v44, v45, v44, s71")
+        if sz == 8:
+            self.e("v_alignbit_b32 v45, v46, v45, s71")
+        elif sz == 4:
+            self.e("v_mov_b32 v45, 0")
+        else:
+            self.e(f"v_and_b32 v44, {'0xff' if sz == 1 else '0xffff'}, v44", "v_mov_b32 v45, 0")
+
+    def staged_store(self, sz, on_unaligned):
+        """Window offset s82 = X (low sz bytes).  Needs the access inside one
+        dword (sz <= 2) or dword-aligned (sz 4, 8); else `on_unaligned`."""
+        self.e("s_and_b32 s71, s82, 3")
+        if sz >= 4:
+            self.e("s_cmp_lg_u32 s71, 0", f"s_cbranch_scc1 {on_unaligned}")
+        else:
+            self.e(f"s_add_u32 s69, s71, {sz}", "s_cmp_gt_u32 s69, 4", f"s_cbranch_scc1 {on_unaligned}")
+        self.e("s_waitcnt vmcnt(0)", "s_lshr_b32 s70, s82, 2")
+        if sz == 8:
+            self.e("s_set_gpr_idx_on s70, gpr_idx(DST)", f"v_mov_b32 v{STG}, v44", f"v_mov_b32 v{STG + 1}, v45",
+                   "s_set_gpr_idx_off")
+        elif sz == 4:
+            self.e("s_set_gpr_idx_on s70, gpr_idx(DST)", f"v_mov_b32 v{STG}, v44", "s_set_gpr_idx_off")
+        else:
+            self.e("s_lshl_b32 s71, s71, 3",
+                   f"s_bfm_b32 s69, {8 * sz}, s71",
+                   "v_lshlrev_b32 v44, s71, v44",
+                   "s_set_gpr_idx_on s70, gpr_idx(SRC0)", f"v_mov_b32 v46, v{STG}", "s_set_gpr_idx_off",
+                   "v_bfi_b32 v46, s69, v44, v46",
+                   "s_set_gpr_idx_on s70, gpr_idx(DST)", f"v_mov_b32 v{STG}, v46", "s_set_gpr_idx_off")
+        # dirty chunks: the 16-B chunks of the first and the last byte
+        self.e("s_lshr_b32 s69, s82, 4", "s_lshl_b32 s69, 1, s69", "s_or_b32 s84, s84, s69",
+               f"s_add_u32 s69, s82, {sz - 1}", "s_lshr_b32 s69, s69, 4", "s_lshl_b32 s69, 1, s69",
+               "s_or_b32 s84, s84, s69")
+
     # ---- handlers ----
     def alu(self, w, op, k):
         if op != "MOV":
-            self.read_dst()
-        else:
-            self.e("v_add_u32 v41, s41, v40")
+            self.rd("s41", 44)
         if k == "R":
-            self.read_src()
+            self.rd("s44", 46)
         else:
             self.imm_y()
-        self.e("s_waitcnt lgkmcnt(0)")
         if w == "64":
             body = {
                 "ADD": ["v_lshl_add_u64 v[44:45], v[44:45], 0, v[46:47]"],
@@ -167,59 +287,70 @@ class Gen:
                 "ARSH": ["v_ashrrev_i32 v44, v46, v44"],
             }[op] + ["v_mov_b32 v45, 0"]                          # ALU32 zero-extends
         self.e(*body)
-        self.write_dst()
+        self.wr("s41", 44)
         self.next_seq()
 
     def neg(self, w):
-        self.read_dst()
-        self.e("s_waitcnt lgkmcnt(0)")
+        self.rd("s41", 44)
         if w == "64":
             self.e("v_sub_co_u32 v44, vcc, 0, v44", "v_subb_co_u32 v45, vcc, 0, v45, vcc")
         else:
             self.e("v_sub_u32 v44, 0, v44", "v_mov_b32 v45, 0")
-        self.write_dst()
+        self.wr("s41", 44)
         self.next_seq()
 
     def endian(self, name):
-        self.read_dst()
-        self.e("s_waitcnt lgkmcnt(0)")
+        self.rd("s41", 44)
         body = {
             "LE16": ["v_and_b32 v44, 0xffff, v44", "v_mov_b32 v45, 0"],
             "LE32": ["v_mov_b32 v45, 0"],
-            "BE16": ["s_mov_b32 s75, 0x0c0c0001", "v_perm_b32 v44, 0, v44, s75", "v_mov_b32 v45, 0"],
-            "BE32": ["s_mov_b32 s75, 0x00010203", "v_perm_b32 v44, 0, v44, s75", "v_mov_b32 v45, 0"],
-            "BE64": ["s_mov_b32 s75, 0x00010203", "v_perm_b32 v48, 0, v45, s75",
-                     "v_perm_b32 v45, 0, v44, s75", "v_mov_b32 v44, v48"],
+            "BE16": ["s_mov_b32 s69, 0x0c0c0001", "v_perm_b32 v44, 0, v44, s69", "v_mov_b32 v45, 0"],
+            "BE32": ["s_mov_b32 s69, 0x00010203", "v_perm_b32 v44, 0, v44, s69", "v_mov_b32 v45, 0"],
+            "BE64": ["s_mov_b32 s69, 0x00010203", "v_perm_b32 v48, 0, v45, s69",
+                     "v_perm_b32 v45, 0, v44, s69", "v_mov_b32 v44, v48"],
         }[name]
         self.e(*body)
-        self.write_dst()
+        self.wr("s41", 44)
         self.next_seq()
 
     def ldx(self, sz):
-        self.read_src_as_addr()
+        stg, glb = self.label("ls"), self.label("lg")
+        self.rd("s44", 48)
+        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[46:47]")
+        self.staged_or(sz, stg, glb)
+        self.e(f"{stg}:")
+        self.staged_load(sz)
+        self.wr("s41", 44)
+        self.next_seq()
+        self.e(f"{glb}:")
         self.check(sz)
         ld = {1: "flat_load_ubyte v44, v[48:49]", 2: "flat_load_ushort v44, v[48:49]",
               4: "flat_load_dword v44, v[48:49]", 8: "flat_load_dwordx2 v[44:45], v[48:49]"}[sz]
         self.e(ld)
         if sz < 8:
             self.e("v_mov_b32 v45, 0")
-        self.e("v_add_u32 v41, s41, v40", "s_waitcnt vmcnt(0) lgkmcnt(0)")
-        self.write_dst()
+        self.e("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        self.wr("s41", 44)
         self.next_seq()
 
-    def read_src_as_addr(self):
-        # Z = R[src] + off
-        self.e("v_add_u32 v42, s44, v40", "ds_read_b64 v[48:49], v42", "s_waitcnt lgkmcnt(0)",
-               "v_lshl_add_u64 v[48:49], v[48:49], 0, s[46:47]")
-
     def store(self, sz, from_reg):
-        # Z = R[dst] + off ; value = R[src] or imm
-        self.e("v_add_u32 v41, s41, v40", "ds_read_b64 v[48:49], v41")
+        stg, glb, unal = self.label("ss"), self.label("sg"), self.label("su")
+        # Z = R[dst] + off ; X = value
+        self.rd("s41", 48)
         if from_reg:
-            self.e("v_add_u32 v42, s44, v40", "ds_read_b64 v[44:45], v42")
+            self.rd("s44", 44)
         else:
             self.e("v_mov_b32 v44, s42", "v_mov_b32 v45, s43")
-        self.e("s_waitcnt lgkmcnt(0)", "v_lshl_add_u64 v[48:49], v[48:49], 0, s[46:47]")
+        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[46:47]")
+        self.staged_or(sz, stg, glb)
+        self.e(f"{stg}:")
+        self.staged_store(sz, unal)
+        self.next_seq()
+        # a staged store straddling dwords: write back, end staging, store to memory
+        self.e(f"{unal}:")
+        self.flush()
+        self.e("s_waitcnt vmcnt(0)", "s_mov_b64 s[80:81], 0")
+        self.e(f"{glb}:")
         self.check(sz)
         st = {1: "flat_store_byte v[48:49], v44", 2: "flat_store_short v[48:49], v44",
               4: "flat_store_dword v[48:49], v44", 8: "flat_store_dwordx2 v[48:49], v[44:45]"}[sz]
@@ -227,15 +358,14 @@ class Gen:
         self.next_seq()
 
     def lddw(self):
-        self.e("v_add_u32 v41, s41, v40", "v_mov_b32 v44, s42", "v_mov_b32 v45, s43")
-        self.write_dst()
+        self.e("v_mov_b32 v44, s42", "v_mov_b32 v45, s43")
+        self.wr("s41", 44)
         self.next_seq(2)
 
     def jcc(self, w, cc, k):
-        self.read_dst()
+        self.rd("s41", 44)
         if k == "R":
-            self.read_src()
-        self.e("s_waitcnt lgkmcnt(0)")
+            self.rd("s44", 46)
         y64 = "v[46:47]" if k == "R" else "s[42:43]"
         y32 = "v46" if k == "R" else "s42"
         if cc == "SET":
@@ -253,23 +383,140 @@ class Gen:
         else:
             self.e(f"v_cmp_{CMP32[cc]} s[54:55], v44, {y32}")
         # v_cmp writes 0 for inactive lanes: none taken / all taken / split
-        nt = L(f"nt_{w}_{cc}_{k}")
+        nt = self.label("nt")
         self.e("s_cmp_eq_u64 s[54:55], 0", f"s_cbranch_scc1 {nt}",
                "s_cmp_eq_u64 s[54:55], exec", f"s_cbranch_scc0 {L('slow')}")
         self.jump_taken()
         self.e(f"{nt}:")
         self.next_seq()
 
+    def uniform64(self, vpair, spair):
+        """spair = lane-0 value of vpair; leave unless every live lane agrees."""
+        lo, hi = vpair
+        slo, shi_ = spair
+        self.e(f"v_readfirstlane_b32 s{slo}, v{lo}", f"v_readfirstlane_b32 s{shi_}, v{hi}",
+               f"v_cmp_ne_u64 s[54:55], s[{slo}:{shi_}], v[{lo}:{hi}]",
+               "s_cmp_lg_u64 s[54:55], 0", f"s_cbranch_scc1 {L('slow')}")
+
+    def call_lookup(self):
+        """bpf_map_lookup_elem on an ARRAY map with a wave-uniform map fd
+        (array_map.cpp:27-40): r0 = key < max_entries ? &data[key * vsz] : 0.
+        Any other map type leaves for the C++ helper."""
+        stg, glb, got = self.label("ks"), self.label("kg"), self.label("kd")
+        self.rd_fixed(1, 44)                      # r1 = fd
+        self.rd_fixed(2, 48)                      # r2 = key pointer
+        self.uniform64((44, 45), (62, 63))
+        self.e("s_cmp_lg_u32 s63, 0", f"s_cbranch_scc1 {L('slow')}",
+               "s_cmpk_ge_u32 s62, 0x400", f"s_cbranch_scc1 {L('slow')}",  # fd >= kMaxFds
+               "s_lshl_b32 s85, s62, 6",
+               "s_load_dwordx4 s[72:75], %[maps], s85",                      # type, ksz, vsz, max
+               "s_add_u32 s85, s85, 16",
+               "s_load_dwordx2 s[76:77], %[maps], s85",                     # data
+               "s_waitcnt lgkmcnt(0)",
+               "s_cmp_lg_u32 s72, 2", f"s_cbranch_scc1 {L('slow')}")        # not BPF_MAP_TYPE_ARRAY
+        self.staged_or(4, stg, glb)
+        self.e(f"{stg}:")
+        self.staged_load(4)
+        self.e("v_mov_b32 v46, v44", f"s_branch {got}")
+        self.e(f"{glb}:")
+        self.check(4)
+        self.e("flat_load_dword v46, v[48:49]", "s_waitcnt vmcnt(0) lgkmcnt(0)")
+        self.e(f"{got}:",
+               "v_cmp_gt_u32 s[54:55], s75, v46",                            # key < max_entries
+               "v_mov_b32 v47, s74",
+               "v_mad_u64_u32 v[50:51], s[56:57], v46, v47, s[76:77]",
+               f"v_cndmask_b32 v{R0}, 0, v50, s[54:55]",
+               f"v_cndmask_b32 v{R0 + 1}, 0, v51, s[54:55]")
+        self.next_seq()
+
+    def rmw(self, sz, k):
+        """Fused counter (loader: ldx/add/stx, register dead after).  A wave
+        whose live lanes all add the same value to the same global address
+        adds popcount * value into the per-wave delta cache (two entries,
+        flushed by the C++ side); anything else leaves for C++ atomics."""
+        stg, glb = self.label("rs"), self.label("rg")
+        self.rd("s41", 48)
+        if k == "R":
+            self.rd("s44", 46)
+        else:
+            self.imm_y()
+        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[46:47]")
+        self.staged_or(sz, stg, glb)
+        self.e(f"{stg}:", f"s_branch {L('slow')}")   # a counter inside the unit's own bytes
+        self.e(f"{glb}:")
+        self.check(sz)
+        self.uniform64((48, 49), (62, 63))
+        self.e("s_cmp_eq_u32 s63, %[shi]", f"s_cbranch_scc1 {L('slow')}",   # LDS / scratch targets
+               "s_cmp_eq_u32 s63, %[phi]", f"s_cbranch_scc1 {L('slow')}")
+        self.uniform64((46, 47), (64, 65))
+        t1, t2, t3, done = (self.label(x) for x in ("t1", "t2", "t3", "done"))
+        self.e("s_bcnt1_i32_b64 s69, exec",
+               "s_mul_i32 s66, s64, s69", "s_mul_hi_u32 s67, s64, s69",
+               "s_mul_i32 s70, s65, s69", "s_add_u32 s67, s67, s70",
+               "s_cmp_eq_u64 %[c0a], s[62:63]", f"s_cbranch_scc0 {t1}",
+               f"s_cmp_eq_u32 %[c0s], {sz}", f"s_cbranch_scc0 {t1}",
+               "s_add_u32 %[c0dl], %[c0dl], s66", "s_addc_u32 %[c0dh], %[c0dh], s67", f"s_branch {done}",
+               f"{t1}:",
+               "s_cmp_eq_u64 %[c1a], s[62:63]", f"s_cbranch_scc0 {t2}",
+               f"s_cmp_eq_u32 %[c1s], {sz}", f"s_cbranch_scc0 {t2}",
+               "s_add_u32 %[c1dl], %[c1dl], s66", "s_addc_u32 %[c1dh], %[c1dh], s67", f"s_branch {done}",
+               f"{t2}:",
+               "s_cmp_eq_u64 %[c0a], 0", f"s_cbranch_scc0 {t3}",
+               "s_mov_b64 %[c0a], s[62:63]", "s_mov_b32 %[c0dl], s66", "s_mov_b32 %[c0dh], s67",
+               f"s_mov_b32 %[c0s], {sz}", f"s_branch {done}",
+               f"{t3}:",
+               "s_cmp_eq_u64 %[c1a], 0", f"s_cbranch_scc0 {L('slow')}",      # both taken: C++ evicts
+               "s_mov_b64 %[c1a], s[62:63]", "s_mov_b32 %[c1dl], s66", "s_mov_b32 %[c1dh], s67",
+               f"s_mov_b32 %[c1s], {sz}",
+               f"{done}:",
+               "s_add_u32 s48, s78, s45", "s_addc_u32 s49, s79, 0")           # continue after the stx
+        self.dispatch()
+
+    def exit_(self):
+        """Every live lane exits: write back the unit's dirty bytes, store r0
+        as verdict (u32) and ret (u64)."""
+        nv, nr = self.label("nv"), self.label("nr")
+        self.flush()
+        self.e("s_bitcmp1_b32 %[oflags], 0", f"s_cbranch_scc0 {nv}",
+               f"global_store_dword %[vaddr], v{R0}, off",
+               f"{nv}:",
+               "s_bitcmp1_b32 %[oflags], 1", f"s_cbranch_scc0 {nr}",
+               f"global_store_dwordx2 %[raddr], v[{R0}:{R0 + 1}], off",
+               f"{nr}:",
+               "s_mov_b32 s68, 2", f"s_branch {L('done')}")
+
     def build(self):
         ids = handler_ids()
         e = self.e
-        # ---- entry: inputs into fixed registers ----
-        e("s_mov_b64 s[60:61], %[prog]", "s_mov_b64 s[62:63], %[dlo]", "s_mov_b64 s[64:65], %[dhi]",
-          "s_mov_b64 s[66:67], %[alo]", "s_mov_b64 s[68:69], %[ahi]", "s_mov_b32 s70, %[shi]",
-          "s_mov_b32 s71, %[phi]", "s_mov_b32 s72, %[steps]", "s_mov_b32 s73, %[limit]",
+        fresh, loaded = self.label("fresh"), self.label("loaded")
+        # ---- entry ----
+        e("s_mov_b64 s[78:79], %[prog]",
           "v_mov_b32 v40, %[rb]",
-          "s_lshl_b32 s52, %[pc], 5", "s_add_u32 s48, s60, s52", "s_addc_u32 s49, s61, 0",
+          "s_lshl_b32 s52, %[pc], 5", "s_add_u32 s48, s78, s52", "s_addc_u32 s49, s79, 0",
           "s_mov_b64 s[58:59], exec", "s_mov_b64 exec, %[alive]",
+          "s_mov_b32 s80, 0", "s_mov_b32 s81, 0", "s_mov_b32 s84, 0",
+          "s_bitcmp1_b32 %[entry], 0", f"s_cbranch_scc1 {fresh}")
+        # re-entry: registers from the C++ side's LDS copy, no staging
+        for r in range(NREG):
+            e(f"ds_read_b64 v[{R0 + 2 * r}:{R0 + 2 * r + 1}], v40 offset:{r * 2048}")
+        e("s_waitcnt lgkmcnt(0)", f"s_branch {loaded}")
+        # fresh unit: r1, r2, r10 from operands, the rest zero; stage the slot
+        e(f"{fresh}:")
+        for r in range(NREG):
+            if r == 1:
+                e(f"v_mov_b32 v{R0 + 2}, %[r1lo]", f"v_mov_b32 v{R0 + 3}, %[r1hi]")
+            elif r == 2:
+                e(f"v_mov_b32 v{R0 + 4}, %[r2lo]", f"v_mov_b32 v{R0 + 5}, 0")
+            elif r == 10:
+                e(f"v_mov_b32 v{R0 + 20}, %[r10lo]", f"v_mov_b32 v{R0 + 21}, %[r10hi]")
+            else:
+                e(f"v_mov_b32 v{R0 + 2 * r}, 0", f"v_mov_b32 v{R0 + 2 * r + 1}, 0")
+        e("v_mov_b32 v52, %[slotlo]", "v_mov_b32 v53, %[slothi]",
+          "s_bitcmp1_b32 %[entry], 1", f"s_cbranch_scc0 {loaded}",
+          "s_mov_b32 s80, 64")
+        for c in range(4):
+            e(f"global_load_dwordx4 v[{STG + 4 * c}:{STG + 4 * c + 3}], v[52:53], off offset:{16 * c}")
+        e(f"{loaded}:",
           "s_getpc_b64 s[50:51]",          # = address of the s_branch below
           f"s_branch {L('start')}")
         for name in ids:                   # table: entry i at TB + 4 + 4*i
@@ -300,43 +547,73 @@ class Gen:
                 self.lddw()
             elif name == "JA":
                 self.jump_taken()
+            elif name == "CALL_LOOKUP":
+                self.call_lookup()
+            elif name == "EXIT":
+                self.exit_()
+            elif name.startswith("RMW"):
+                self.rmw(int(name[3]), name[5])
             elif name[0] == "J":
                 w, cc, k = name[1:3], name.split("_")[1], name.split("_")[2]
                 self.jcc(w, cc, k)
             else:
                 raise ValueError(name)
-        # ---- exits: the instruction was not executed; one step was counted
-        e(f"{L('steps')}:", "s_mov_b32 s74, 1", f"s_branch {L('exit')}")
-        e(f"{L('slow')}:", "s_mov_b32 s74, 0", "s_sub_u32 s72, s72, 1")
-        e(f"{L('exit')}:",
+        # ---- exits: the instruction at pc was not executed (one step was
+        # counted at its dispatch); write back staging, spill registers
+        e(f"{L('steps')}:", "s_mov_b32 s68, 1", f"s_branch {L('spill')}")
+        e(f"{L('slow')}:", "s_mov_b32 s68, 0", "s_sub_u32 %[steps], %[steps], 1")
+        e(f"{L('spill')}:")
+        self.flush()
+        for r in range(NREG):
+            e(f"ds_write_b64 v40, v[{R0 + 2 * r}:{R0 + 2 * r + 1}] offset:{r * 2048}")
+        e(f"{L('done')}:",
           "s_waitcnt vmcnt(0) lgkmcnt(0)",
           "s_mov_b64 exec, s[58:59]",
-          "s_sub_u32 s52, s48, s60", "s_lshr_b32 s52, s52, 5",
-          "s_mov_b32 %[pc], s52", "s_mov_b32 %[steps], s72", "s_mov_b32 %[why], s74")
+          "s_sub_u32 s52, s48, s78", "s_lshr_b32 s52, s52, 5",
+          "s_mov_b32 %[pc], s52", "s_mov_b32 %[why], s68")
         return ids
+
+
+def vmap(n):
+    """Handlers are written against v40..v101; the block is placed at the top
+    of a 128-VGPR budget (v72..v127) so that the compiler's own values stay
+    below it and the kernel keeps 4 waves per SIMD."""
+    return n + 32 if n < 60 else n + 28 if n < 84 else n + 26
+
+
+def relocate(line):
+    line = re.sub(r"v\[(\d+):(\d+)\]", lambda m: f"v[{vmap(int(m.group(1)))}:{vmap(int(m.group(2)))}]", line)
+    return re.sub(r"\bv(\d+)\b", lambda m: f"v{vmap(int(m.group(1)))}", line)
 
 
 def main():
     g = Gen()
     ids = g.build()
-    clob = [f"s{i}" for i in range(40, 78)] + [f"v{i}" for i in range(40, 52)]
+    g.out = [relocate(x) for x in g.out]
+    # v126/v127 (v100/v101 before relocation) are read, never written, by
+    # staged loads near the window end
+    clob = [f"s{i}" for i in range(40, 86)] + [f"v{vmap(i)}" for i in range(40, 102) if not 42 < i < 44 and not 55 < i < 60 and not 81 < i < 84]
     with open(os.path.join(HERE, "fast_asm.inc"), "w") as f:
         f.write("// Generated by gen_fast.py; do not edit.\n")
         f.write("#define BPFTIME_AMD_FAST_ASM \\\n")
         for line in g.out:
             f.write('  "%s\\n" \\\n' % line)
         f.write('  ""\n')
-        f.write("#define BPFTIME_AMD_FAST_CLOBBERS %s\n" % ", ".join('"%s"' % c for c in clob + ["vcc", "scc", "memory"]))
+        f.write("#define BPFTIME_AMD_FAST_CLOBBERS %s\n" %
+                ", ".join('"%s"' % c for c in clob + ["vcc", "scc", "m0", "memory"]))
     with open(os.path.join(HERE, "fast_ops.hpp"), "w") as f:
         f.write("// Generated by gen_fast.py; do not edit.\n#pragma once\n#include <stdint.h>\n\n")
         f.write("namespace bpftime_amd {\n\n// handler ids of the threaded fast path (FInsn::hoff = 4 + 4 * id)\nenum FOp : uint32_t {\n")
         for i, name in enumerate(ids):
             f.write(f"  F_{name} = {i},\n")
         f.write(f"  F_COUNT = {len(ids)}\n}};\n\n")
-        f.write("// 32-byte threaded instruction (gen_fast.py register map, word for word)\n"
-                "struct FInsn {\n  uint32_t hoff;\n  uint32_t dst_off;\n  int64_t imm;\n  uint32_t src_off;\n"
+        f.write("// 32-byte threaded instruction (gen_fast.py register map, word for word);\n"
+                "// dst_x2 / src_x2 are eBPF register numbers times two (VGPR pair index)\n"
+                "struct FInsn {\n  uint32_t hoff;\n  uint32_t dst_x2;\n  int64_t imm;\n  uint32_t src_x2;\n"
                 "  uint32_t target;\n  int64_t off;\n};\n"
-                "static_assert(sizeof(FInsn) == 32, \"FInsn must be 32 bytes\");\n\n}  // namespace bpftime_amd\n")
+                "static_assert(sizeof(FInsn) == 32, \"FInsn must be 32 bytes\");\n\n"
+                "constexpr uint32_t kFastStageBytes = 64;  // staged bytes per unit\n\n"
+                "}  // namespace bpftime_amd\n")
 
 
 if __name__ == "__main__":

@@ -388,30 +388,59 @@ __device__ __forceinline__ uint32_t run_loop(Ctx &c) {
 // was crossed at a taken jump, else 0 (c.pc = the instruction to run in C++).
 struct FastEnv {
   const FInsn *fast;
+  const DMap *maps;
   uint64_t dlo, dhi, alo, ahi;
   uint32_t shi, phi;
-  uint32_t rb;  // LDS byte address of this lane's R[0]
+  uint32_t oflags;  // bit 0: verdicts, bit 1: rets
+  uint32_t rb;      // LDS byte address of this lane's R[0]
 };
 
-__device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f) {
+constexpr uint32_t FAST_SLOW = 0, FAST_STEPS = 1, FAST_EXIT = 2;
+
+// Per-unit inputs of a fresh entry (gen_fast.py: registers from operands,
+// optional staging of the slot's first kFastStageBytes bytes).
+struct FastUnit {
+  uint64_t r1, r10, slot;
+  uint32_t r2;
+  uint32_t entry;  // bit 0: fresh unit, bit 1: stage the slot
+};
+
+__device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const FastUnit &u) {
   // every "s" operand must be provably uniform: readfirstlane what the
   // compiler cannot prove (the values are uniform by construction)
   uint32_t pc = __builtin_amdgcn_readfirstlane(c.pc), steps = __builtin_amdgcn_readfirstlane(c.steps), why;
   const uint64_t alive = __ballot(c.alive);
   const uint32_t limit = __builtin_amdgcn_readfirstlane(c.step_limit);
+  const uint32_t entry = __builtin_amdgcn_readfirstlane(u.entry);
+  uint64_t c0a = c.c0a, c1a = c.c1a;
+  uint32_t c0dl = (uint32_t)c.c0d, c0dh = (uint32_t)(c.c0d >> 32), c1dl = (uint32_t)c.c1d,
+           c1dh = (uint32_t)(c.c1d >> 32), c0s = c.c0s, c1s = c.c1s;
+  const uint64_t vaddr = c.verdicts ? (uint64_t)(uintptr_t)(c.verdicts + c.unit) : 0;
+  const uint64_t raddr = c.rets ? (uint64_t)(uintptr_t)(c.rets + c.unit) : 0;
   asm volatile(BPFTIME_AMD_FAST_ASM
-               : [pc] "+s"(pc), [steps] "+s"(steps), [why] "=s"(why)
-               : [prog] "s"(f.fast), [dlo] "s"(f.dlo), [dhi] "s"(f.dhi), [alo] "s"(f.alo), [ahi] "s"(f.ahi),
-                 [shi] "s"(f.shi), [phi] "s"(f.phi), [limit] "s"(limit), [rb] "v"(f.rb),
-                 [alive] "s"(alive)
+               : [pc] "+s"(pc), [steps] "+s"(steps), [why] "=s"(why), [c0a] "+s"(c0a), [c1a] "+s"(c1a),
+                 [c0dl] "+s"(c0dl), [c0dh] "+s"(c0dh), [c1dl] "+s"(c1dl), [c1dh] "+s"(c1dh), [c0s] "+s"(c0s),
+                 [c1s] "+s"(c1s)
+               : [prog] "s"(f.fast), [maps] "s"(f.maps), [dlo] "s"(f.dlo), [dhi] "s"(f.dhi), [alo] "s"(f.alo),
+                 [ahi] "s"(f.ahi), [shi] "s"(f.shi), [phi] "s"(f.phi), [limit] "s"(limit), [rb] "v"(f.rb),
+                 [alive] "s"(alive), [oflags] "s"(f.oflags), [vaddr] "v"(vaddr), [raddr] "v"(raddr),
+                 [entry] "s"(entry), [r1lo] "v"((uint32_t)u.r1), [r1hi] "v"((uint32_t)(u.r1 >> 32)),
+                 [r2lo] "v"(u.r2), [r10lo] "v"((uint32_t)u.r10), [r10hi] "v"((uint32_t)(u.r10 >> 32)),
+                 [slotlo] "v"((uint32_t)u.slot), [slothi] "v"((uint32_t)(u.slot >> 32))
                : BPFTIME_AMD_FAST_CLOBBERS);
   c.pc = pc;
   c.steps = steps;
+  c.c0a = c0a;
+  c.c1a = c1a;
+  c.c0d = (uint64_t)c0dl | ((uint64_t)c0dh << 32);
+  c.c1d = (uint64_t)c1dl | ((uint64_t)c1dh << 32);
+  c.c0s = c0s;
+  c.c1s = c1s;
   return why;
 }
 
 template <uint32_t KIND, bool BIGSTACK>
-__global__ __launch_bounds__(kBlock) void k_interp(KParams pin) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_interp(KParams pin) {
   // Copy every kernel argument through an SGPR barrier: without it the
   // compiler keeps the argument block as one 16-dword tuple that it spills
   // and reloads whole inside the dispatch loop.
@@ -448,6 +477,8 @@ __global__ __launch_bounds__(kBlock) void k_interp(KParams pin) {
   // fast-path operands, computed once into SGPRs (sreg: no per-entry rebuild)
   FastEnv fe;
   fe.fast = (const FInsn *)sreg((uint64_t)(uintptr_t)p.fast);
+  fe.maps = p.maps;
+  fe.oflags = sreg((uint32_t)__builtin_amdgcn_readfirstlane((p.verdicts ? 1u : 0u) | (p.rets ? 2u : 0u)));
   fe.dlo = sreg((uint64_t)(p.checked ? p.data_lo : 0));
   fe.dhi = sreg((uint64_t)(p.checked ? p.data_hi : ~(uint64_t)0));
   fe.alo = p.arena_lo;
@@ -457,6 +488,11 @@ __global__ __launch_bounds__(kBlock) void k_interp(KParams pin) {
                           (uint32_t)((uint64_t)(uintptr_t)&big_stack[0] >> 32)))
                     : fe.shi;
   fe.rb = (uint32_t)(uintptr_t)&Rf[tid];
+
+  // stage each unit's first 64 B in VGPRs when slots are 16-B aligned and
+  // at least that long (gen_fast.py, unit staging)
+  const bool stage_ok = p.stride >= kFastStageBytes && (p.stride & 15) == 0 &&
+                        ((uint64_t)(uintptr_t)p.data & 15) == 0;
 
   const bool ordered = p.ordered != 0;
   const uint64_t ustep = ordered ? 1 : (uint64_t)gridDim.x * kBlock;
@@ -470,8 +506,12 @@ __global__ __launch_bounds__(kBlock) void k_interp(KParams pin) {
     int32_t miss_fd = -1;
     uint64_t miss_hash = 0;
 
-    // ---- per-unit setup (r1, r2, r10; other registers zero) ----
-    for (uint32_t r = 0; r < 11; r++) Rf[r * kBlock + tid] = 0;
+    // ---- per-unit setup: r1, r2, r10 (other registers zero) are set by the
+    // fast path's fresh entry, which every unit starts with ----
+    FastUnit fu;
+    fu.slot = slot;
+    fu.r10 = stack_top;
+    fu.entry = 1u | (stage_ok ? 2u : 0u);
     if (KIND == CTX_XDP) {
       XdpCtx *x = (XdpCtx *)my_ctx;
       x->data = slot + p.head;
@@ -482,13 +522,12 @@ __global__ __launch_bounds__(kBlock) void k_interp(KParams pin) {
       x->egress_ifindex = 0;
       x->buffer_start = slot;
       x->buffer_end = slot + p.stride;
-      Rf[1 * kBlock + tid] = (uint64_t)(uintptr_t)x;
-      Rf[2 * kBlock + tid] = 48;
+      fu.r1 = (uint64_t)(uintptr_t)x;
+      fu.r2 = 48;
     } else {
-      Rf[1 * kBlock + tid] = slot;
-      Rf[2 * kBlock + tid] = KIND == CTX_SYSCALL ? 64 : len;
+      fu.r1 = slot;
+      fu.r2 = KIND == CTX_SYSCALL ? 64 : len;
     }
-    Rf[10 * kBlock + tid] = stack_top;
 
     bool alive = active;
     if (KIND == CTX_SYSCALL && active) {
@@ -507,7 +546,13 @@ __global__ __launch_bounds__(kBlock) void k_interp(KParams pin) {
     while (__ballot(c.alive) != 0) {
       uint32_t r;
       if (uni) {
-        if (run_fast(c, fe)) {
+        const uint32_t why = run_fast(c, fe, fu);
+        fu.entry = 0;
+        if (why == FAST_EXIT) {  // every live lane ran exit; r0 already stored
+          c.alive = false;
+          break;
+        }
+        if (why == FAST_STEPS) {
           c.err = c.alive ? E_STEPS : c.err;
           c.alive = false;
           break;

@@ -667,7 +667,11 @@ static uint32_t fast_id(const DInsn &d) {
     case X_JLE: return JCC(LE);
     case X_JSLT: return JCC(SLT);
     case X_JSLE: return JCC(SLE);
-    default: return F_SLOW;  // div/mod, atomics, fused counters, call, exit
+    case X_CALL: return d.hi == 1 ? F_CALL_LOOKUP : F_SLOW;  // map_lookup_elem; other helpers in C++
+    case X_EXIT: return F_EXIT;
+    case X_RMW_ADD:
+      return sz == 8 ? (r ? F_RMW8_R : F_RMW8_I) : sz == 4 ? (r ? F_RMW4_R : F_RMW4_I) : F_SLOW;
+    default: return F_SLOW;  // div/mod, atomics
   }
 #undef ALU4
 #undef JCC
@@ -679,8 +683,8 @@ void build_fast(const std::vector<DInsn> &prog, std::vector<FInsn> &fast) {
     const DInsn &d = prog[i];
     FInsn &f = fast[i];
     f.hoff = 4 + 4 * fast_id(d);
-    f.dst_off = (uint32_t)d.dst * kBlock * 8;
-    f.src_off = (uint32_t)d.src * kBlock * 8;
+    f.dst_x2 = (uint32_t)d.dst * 2;
+    f.src_x2 = (uint32_t)d.src * 2;
     f.imm = d.op == X_LDDW ? (int64_t)((uint64_t)(uint32_t)d.imm | ((uint64_t)(uint32_t)d.hi << 32))
                            : (int64_t)d.imm;
     f.target = (uint32_t)d.tgt * (uint32_t)sizeof(FInsn);

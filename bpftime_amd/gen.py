@@ -40,11 +40,17 @@ def _uniform(seed: int, k: np.ndarray) -> np.ndarray:
     return (sm64(seed, k) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
 
 
-def zipf_ids(seed: int, first: int, n: int, support: int, s: float) -> np.ndarray:
-    """Bounded Zipf(s) ids in [0, support) by inverse CDF of a uniform stream."""
+def zipf_cdf(support: int, s: float) -> np.ndarray:
+    """CDF table of the bounded Zipf(s) law (also uploaded for csrc/gen.hip)."""
     w = 1.0 / np.arange(1, support + 1, dtype=np.float64) ** s
     cdf = np.cumsum(w)
     cdf /= cdf[-1]
+    return cdf
+
+
+def zipf_ids(seed: int, first: int, n: int, support: int, s: float) -> np.ndarray:
+    """Bounded Zipf(s) ids in [0, support) by inverse CDF of a uniform stream."""
+    cdf = zipf_cdf(support, s)
     u = _uniform(seed, np.arange(first, first + n, dtype=np.uint64))
     return np.minimum(np.searchsorted(cdf, u, side="right"), support - 1).astype(np.int64)
 

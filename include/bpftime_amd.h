@@ -138,6 +138,13 @@ const char *bpftime_amd_last_error(void);
  * 12..13 = 0x08 0x00); unit i uses words of stream index first+i. */
 int bpftime_amd_gen_xdp(void *dev, uint64_t n, uint64_t stride, uint32_t len, uint64_t seed,
                         uint64_t first, void *stream);
+/* config 3 frames (gen.py flow_packets): `cdf` = device copy of the Zipf
+ * CDF (nflows doubles, computed on the host); per-unit lengths to `lens`. */
+int bpftime_amd_gen_flow(void *dev, uint32_t *lens, uint64_t n, uint64_t stride, uint64_t seed,
+                         uint64_t first, const double *cdf, uint32_t nflows, void *stream);
+/* config 5 records (gen.py syscall_records), 64 B each. */
+int bpftime_amd_gen_syscall(void *dev, uint64_t n, uint64_t seed, uint64_t first, const double *cdf,
+                            uint32_t support, void *stream);
 
 #ifdef __cplusplus
 }

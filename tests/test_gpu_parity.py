@@ -318,3 +318,24 @@ def test_load_errors_match_oracle(fresh_oracle, fresh_runtime):
         o_rc, o_msg = po.OracleVM().try_load(c)
         d_rc, d_msg = dev.VM().try_load(c)
         assert (o_rc < 0) == (d_rc < 0) and o_msg == d_msg, (o_msg, d_msg)
+
+
+@pytest.mark.parametrize("first", [0, 12345])
+def test_device_generators_match_numpy(fresh_runtime, first):
+    """csrc/gen.hip regenerates gen.py's config-3/5 inputs word for word, so
+    full-size device-resident runs use the same inputs as the parity tests."""
+    dev = fresh_runtime
+    L = dev.lib()
+    n = 3000
+    cdf = gen.zipf_cdf(65536, 1.1)
+    dc = dev.DeviceBuffer.from_array(cdf)
+    fb, fl = dev.DeviceBuffer(n * 2048), dev.DeviceBuffer(4 * n)
+    assert L.bpftime_amd_gen_flow(fb.ptr, fl.ptr, n, 2048, gen.SEED_CFG3, first, dc.ptr, 65536, None) == 0
+    slots, lens = gen.flow_packets(n, first=first)
+    np.testing.assert_array_equal(fb.download(np.uint8).reshape(n, 2048), slots)
+    np.testing.assert_array_equal(fl.download(np.uint32), lens)
+    cdf5 = gen.zipf_cdf(335, 1.2)
+    dc5 = dev.DeviceBuffer.from_array(cdf5)
+    sb = dev.DeviceBuffer(n * 64)
+    assert L.bpftime_amd_gen_syscall(sb.ptr, n, gen.SEED_CFG5, first, dc5.ptr, 335, None) == 0
+    np.testing.assert_array_equal(sb.download(np.uint8).reshape(n, 64), gen.syscall_records(n, first=first))
