@@ -90,7 +90,11 @@ def handler_ids():
     ids += ["LE16", "LE32", "BE16", "BE32", "BE64", "NOP"]
     for sz in (1, 2, 4, 8):
         ids += [f"LDX{sz}", f"STX{sz}", f"ST{sz}"]
-    ids += ["LDDW", "JA", "CALL_LOOKUP", "EXIT", "RMW4_R", "RMW4_I", "RMW8_R", "RMW8_I"]
+    for sz in (1, 2, 4, 8):
+        for kind in ("PKT", "SLOT", "STK"):
+            ids += [f"LDX{sz}_{kind}", f"STX{sz}_{kind}", f"ST{sz}_{kind}"]
+    ids += ["LDX_CTXDATA", "LDX_CTXEND"]
+    ids += ["LDDW", "JA", "CALL_LOOKUP", "CALL_LOOKUP_STK", "EXIT", "RMW4_R", "RMW4_I", "RMW8_R", "RMW8_I"]
     for w in ("64", "32"):
         for cc in JCC:
             for k in ("R", "I"):
@@ -357,6 +361,59 @@ class Gen:
         self.e(st)
         self.next_seq()
 
+    # ---- loads / stores through a statically typed base (loader pointer kinds;
+    # w5 = the access's byte offset from data (PKT), the slot (SLOT) or the
+    # initial stack top (STK)).  No per-lane window check is needed: the
+    # staged window and the lane's LDS stack are the lane's own memory.
+    def staged_static(self, sz, pkt, generic):
+        """s82 = window offset of a packet / slot access; the generic handler
+        takes over when staging is off or the access leaves the window."""
+        if pkt:
+            self.e("s_add_u32 s82, s45, %[head]")
+        else:
+            self.e("s_mov_b32 s82, s45")
+        self.e("s_cmp_eq_u32 s80, 0", f"s_cbranch_scc1 {generic}",
+               f"s_add_u32 s69, s82, {sz}", "s_cmp_gt_u32 s69, s80", f"s_cbranch_scc1 {generic}")
+
+    def ldx_static(self, sz, kind):
+        if kind == "STK":
+            ds = {1: "ds_read_u8", 2: "ds_read_u16", 4: "ds_read_b32", 8: "ds_read_b64"}[sz]
+            self.e("v_add_u32 v41, s45, %[stklo]",
+                   f"{ds} {'v[44:45]' if sz == 8 else 'v44'}, v41")
+            if sz < 8:
+                self.e("v_mov_b32 v45, 0")
+            self.e("s_waitcnt lgkmcnt(0)")
+        else:
+            self.staged_static(sz, kind == "PKT", L(f"h_LDX{sz}"))
+            self.staged_load(sz)
+        self.wr("s41", 44)
+        self.next_seq()
+
+    def store_static(self, sz, kind, from_reg):
+        if from_reg:
+            self.rd("s44", 44)
+        else:
+            self.e("v_mov_b32 v44, s42", "v_mov_b32 v45, s43")
+        if kind == "STK":
+            ds = {1: "ds_write_b8", 2: "ds_write_b16", 4: "ds_write_b32", 8: "ds_write_b64"}[sz]
+            self.e("v_add_u32 v41, s45, %[stklo]",
+                   f"{ds} v41, {'v[44:45]' if sz == 8 else 'v44'}")
+        else:
+            generic = L(f"h_{'STX' if from_reg else 'ST'}{sz}")
+            self.staged_static(sz, kind == "PKT", generic)
+            self.staged_store(sz, generic)
+        self.next_seq()
+
+    def ctx_field(self, end):
+        """ctx->data = slot + head; ctx->data_end = slot + head + len."""
+        if end:
+            self.e("v_add_u32 v46, %[head], %[ulen]")
+        else:
+            self.e("v_mov_b32 v46, %[head]")
+        self.e("v_add_co_u32 v44, vcc, v52, v46", "v_addc_co_u32 v45, vcc, v53, 0, vcc")
+        self.wr("s41", 44)
+        self.next_seq()
+
     def lddw(self):
         self.e("v_mov_b32 v44, s42", "v_mov_b32 v45, s43")
         self.wr("s41", 44)
@@ -398,10 +455,11 @@ class Gen:
                f"v_cmp_ne_u64 s[54:55], s[{slo}:{shi_}], v[{lo}:{hi}]",
                "s_cmp_lg_u64 s[54:55], 0", f"s_cbranch_scc1 {L('slow')}")
 
-    def call_lookup(self):
+    def call_lookup(self, stack_key=False):
         """bpf_map_lookup_elem on an ARRAY map with a wave-uniform map fd
         (array_map.cpp:27-40): r0 = key < max_entries ? &data[key * vsz] : 0.
-        Any other map type leaves for the C++ helper."""
+        Any other map type leaves for the C++ helper.  stack_key: the loader
+        proved r2 = stack top + w5 (4-aligned), so the key is one ds_read."""
         stg, glb, got = self.label("ks"), self.label("kg"), self.label("kd")
         self.rd_fixed(1, 44)                      # r1 = fd
         self.rd_fixed(2, 48)                      # r2 = key pointer
@@ -414,6 +472,9 @@ class Gen:
                "s_load_dwordx2 s[76:77], %[maps], s85",                     # data
                "s_waitcnt lgkmcnt(0)",
                "s_cmp_lg_u32 s72, 2", f"s_cbranch_scc1 {L('slow')}")        # not BPF_MAP_TYPE_ARRAY
+        if stack_key:
+            self.e("v_add_u32 v41, s45, %[stklo]", "ds_read_b32 v46, v41", "s_waitcnt lgkmcnt(0)",
+                   f"s_branch {got}")
         self.staged_or(4, stg, glb)
         self.e(f"{stg}:")
         self.staged_load(4)
@@ -495,6 +556,7 @@ class Gen:
           "s_lshl_b32 s52, %[pc], 5", "s_add_u32 s48, s78, s52", "s_addc_u32 s49, s79, 0",
           "s_mov_b64 s[58:59], exec", "s_mov_b64 exec, %[alive]",
           "s_mov_b32 s80, 0", "s_mov_b32 s81, 0", "s_mov_b32 s84, 0",
+          "v_mov_b32 v52, %[slotlo]", "v_mov_b32 v53, %[slothi]",
           "s_bitcmp1_b32 %[entry], 0", f"s_cbranch_scc1 {fresh}")
         # re-entry: registers from the C++ side's LDS copy, no staging
         for r in range(NREG):
@@ -511,8 +573,7 @@ class Gen:
                 e(f"v_mov_b32 v{R0 + 20}, %[r10lo]", f"v_mov_b32 v{R0 + 21}, %[r10hi]")
             else:
                 e(f"v_mov_b32 v{R0 + 2 * r}, 0", f"v_mov_b32 v{R0 + 2 * r + 1}, 0")
-        e("v_mov_b32 v52, %[slotlo]", "v_mov_b32 v53, %[slothi]",
-          "s_bitcmp1_b32 %[entry], 1", f"s_cbranch_scc0 {loaded}",
+        e("s_bitcmp1_b32 %[entry], 1", f"s_cbranch_scc0 {loaded}",
           "s_mov_b32 s80, 64")
         for c in range(4):
             e(f"global_load_dwordx4 v[{STG + 4 * c}:{STG + 4 * c + 3}], v[52:53], off offset:{16 * c}")
@@ -537,6 +598,16 @@ class Gen:
                 self.endian(name)
             elif name == "NOP":
                 self.next_seq()
+            elif name in ("LDX_CTXDATA", "LDX_CTXEND"):
+                self.ctx_field(name == "LDX_CTXEND")
+            elif "_" in name and name.split("_")[1] in ("PKT", "SLOT", "STK"):
+                op, kind = name.split("_")
+                if op.startswith("LDX"):
+                    self.ldx_static(int(op[3:]), kind)
+                elif op.startswith("STX"):
+                    self.store_static(int(op[3:]), kind, True)
+                else:
+                    self.store_static(int(op[2:]), kind, False)
             elif name.startswith("LDX"):
                 self.ldx(int(name[3:]))
             elif name.startswith("STX"):
@@ -549,6 +620,8 @@ class Gen:
                 self.jump_taken()
             elif name == "CALL_LOOKUP":
                 self.call_lookup()
+            elif name == "CALL_LOOKUP_STK":
+                self.call_lookup(stack_key=True)
             elif name == "EXIT":
                 self.exit_()
             elif name.startswith("RMW"):

@@ -392,6 +392,7 @@ struct FastEnv {
   uint64_t dlo, dhi, alo, ahi;
   uint32_t shi, phi;
   uint32_t oflags;  // bit 0: verdicts, bit 1: rets
+  uint32_t head;    // batch head: ctx->data = slot + head
   uint32_t rb;      // LDS byte address of this lane's R[0]
 };
 
@@ -402,6 +403,7 @@ constexpr uint32_t FAST_SLOW = 0, FAST_STEPS = 1, FAST_EXIT = 2;
 struct FastUnit {
   uint64_t r1, r10, slot;
   uint32_t r2;
+  uint32_t len;    // unit length (ctx->data_end - ctx->data)
   uint32_t entry;  // bit 0: fresh unit, bit 1: stage the slot
 };
 
@@ -426,7 +428,8 @@ __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const Fas
                  [alive] "s"(alive), [oflags] "s"(f.oflags), [vaddr] "v"(vaddr), [raddr] "v"(raddr),
                  [entry] "s"(entry), [r1lo] "v"((uint32_t)u.r1), [r1hi] "v"((uint32_t)(u.r1 >> 32)),
                  [r2lo] "v"(u.r2), [r10lo] "v"((uint32_t)u.r10), [r10hi] "v"((uint32_t)(u.r10 >> 32)),
-                 [slotlo] "v"((uint32_t)u.slot), [slothi] "v"((uint32_t)(u.slot >> 32))
+                 [slotlo] "v"((uint32_t)u.slot), [slothi] "v"((uint32_t)(u.slot >> 32)),
+                 [head] "s"(f.head), [ulen] "v"(u.len), [stklo] "v"((uint32_t)u.r10)
                : BPFTIME_AMD_FAST_CLOBBERS);
   c.pc = pc;
   c.steps = steps;
@@ -478,6 +481,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   FastEnv fe;
   fe.fast = (const FInsn *)sreg((uint64_t)(uintptr_t)p.fast);
   fe.maps = p.maps;
+  fe.head = p.head;
   fe.oflags = sreg((uint32_t)__builtin_amdgcn_readfirstlane((p.verdicts ? 1u : 0u) | (p.rets ? 2u : 0u)));
   fe.dlo = sreg((uint64_t)(p.checked ? p.data_lo : 0));
   fe.dhi = sreg((uint64_t)(p.checked ? p.data_hi : ~(uint64_t)0));
@@ -511,6 +515,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     FastUnit fu;
     fu.slot = slot;
     fu.r10 = stack_top;
+    fu.len = len;
     fu.entry = 1u | (stage_ok ? 2u : 0u);
     if (KIND == CTX_XDP) {
       XdpCtx *x = (XdpCtx *)my_ctx;

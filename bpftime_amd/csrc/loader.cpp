@@ -677,7 +677,121 @@ static uint32_t fast_id(const DInsn &d) {
 #undef JCC
 }
 
-void build_fast(const std::vector<DInsn> &prog, std::vector<FInsn> &fast) {
+// ---------------------------------------------------------------------------
+// Pointer kinds for the fast path (a small slice of what the kernel verifier
+// tracks): which registers hold the unit's slot, its packet data, its XDP
+// ctx or its stack, at a constant offset.  A load/store whose base has such
+// a kind gets a handler that needs no per-lane window check: packet / slot
+// bytes come from the staged VGPRs, ctx fields are computed from the unit's
+// slot / length, stack bytes are plain LDS accesses.
+// ---------------------------------------------------------------------------
+enum PKind : uint8_t { P_UNDEF = 0, P_CTX, P_PKT, P_SLOT, P_STK, P_OTHER };
+struct PVal {
+  uint8_t kind;
+  int32_t k;
+  bool operator==(const PVal &o) const { return kind == o.kind && k == o.k; }
+};
+static PVal pjoin(PVal a, PVal b) {
+  if (a.kind == P_UNDEF) return b;
+  if (b.kind == P_UNDEF) return a;
+  return a == b ? a : PVal{P_OTHER, 0};
+}
+
+// in[i][r]: kind of register r before instruction i; returns false when the
+// program may rewrite its ctx (then no ctx / packet kinds are trusted).
+static bool pointer_kinds(const std::vector<DInsn> &p, bool xdp, bool pkt_ok,
+                          std::vector<std::vector<PVal>> &in) {
+  const uint32_t n = (uint32_t)p.size();
+  in.assign(n, std::vector<PVal>(11, PVal{P_UNDEF, 0}));
+  std::vector<bool> queued(n, false);
+  std::vector<uint32_t> work;
+  for (int r = 0; r < 11; r++) in[0][r] = PVal{P_OTHER, 0};
+  in[0][1] = xdp ? PVal{P_CTX, 0} : PVal{P_SLOT, 0};
+  in[0][10] = PVal{P_STK, 0};
+  work.push_back(0);
+  queued[0] = true;
+  bool ctx_written = false;
+  auto ptr = [](uint8_t k) { return k == P_CTX || k == P_PKT || k == P_SLOT || k == P_STK; };
+  while (!work.empty()) {
+    const uint32_t i = work.back();
+    work.pop_back();
+    queued[i] = false;
+    std::vector<PVal> st = in[i];
+    const DInsn &d = p[i];
+    const bool w32 = (d.aux & A_W32) != 0, sreg = (d.aux & A_SRCREG) != 0;
+    switch (d.op) {
+      case X_MOV:
+        st[d.dst] = (sreg && !w32) ? st[d.src] : PVal{P_OTHER, 0};
+        break;
+      case X_ADD:
+      case X_SUB:
+        if (ptr(st[d.dst].kind) && !sreg && !w32) {
+          const int64_t k = (int64_t)st[d.dst].k + (d.op == X_ADD ? (int64_t)d.imm : -(int64_t)d.imm);
+          st[d.dst] = (k > -(1 << 20) && k < (1 << 20)) ? PVal{st[d.dst].kind, (int32_t)k} : PVal{P_OTHER, 0};
+        } else {
+          st[d.dst] = PVal{P_OTHER, 0};
+        }
+        break;
+      case X_LDX: {
+        const PVal b = st[d.src];
+        const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
+        PVal v{P_OTHER, 0};
+        if (b.kind == P_CTX && sz == 8) {
+          const int64_t at = (int64_t)b.k + d.off;
+          if (at == 0 && pkt_ok) v = PVal{P_PKT, 0};        // ctx->data
+          else if (at == 32) v = PVal{P_SLOT, 0};           // ctx->buffer_start
+        }
+        st[d.dst] = v;
+        break;
+      }
+      case X_ST:
+      case X_STX:
+      case X_RMW_ADD:
+        if (st[d.dst].kind == P_CTX) ctx_written = true;
+        break;
+      case X_ATOMIC:
+        if (st[d.dst].kind == P_CTX) ctx_written = true;
+        if (d.hi == 0xf1) st[0] = PVal{P_OTHER, 0};
+        else if (d.hi & 1) st[d.src] = PVal{P_OTHER, 0};
+        break;
+      case X_CALL:
+        st[0] = PVal{P_OTHER, 0};  // r1-r5 survive (ubpf)
+        break;
+      case X_EXIT: case X_JA: case X_JEQ: case X_JGT: case X_JGE: case X_JSET: case X_JNE:
+      case X_JSGT: case X_JSGE: case X_JLT: case X_JLE: case X_JSLT: case X_JSLE:
+        break;
+      default: {
+        RegSet u, df;
+        use_def(d, u, df);
+        for (int r = 0; r < 11; r++)
+          if (df & (1u << r)) st[r] = PVal{P_OTHER, 0};
+        break;
+      }
+    }
+    uint32_t sx[2];
+    int ns;
+    successors(p, i, sx, ns);
+    for (int j = 0; j < ns; j++) {
+      const uint32_t t = sx[j];
+      bool changed = false;
+      for (int r = 0; r < 11; r++) {
+        const PVal nv = pjoin(in[t][r], st[r]);
+        if (!(nv == in[t][r])) {
+          in[t][r] = nv;
+          changed = true;
+        }
+      }
+      if (changed && !queued[t]) {
+        queued[t] = true;
+        work.push_back(t);
+      }
+    }
+  }
+  return !ctx_written;
+}
+
+void build_fast(const std::vector<DInsn> &prog, bool xdp, bool big_stack, uint32_t stack_size,
+                std::vector<FInsn> &fast, uint32_t *specialized) {
   fast.assign(prog.size(), FInsn{});
   for (size_t i = 0; i < prog.size(); i++) {
     const DInsn &d = prog[i];
@@ -690,6 +804,63 @@ void build_fast(const std::vector<DInsn> &prog, std::vector<FInsn> &fast) {
     f.target = (uint32_t)d.tgt * (uint32_t)sizeof(FInsn);
     f.off = (int64_t)d.off;
   }
+  // helpers that move ctx->data / data_end invalidate packet pointers
+  bool pkt_ok = true;
+  for (const DInsn &d : prog)
+    if (d.op == X_CALL && (d.hi == 44 || d.hi == 65)) pkt_ok = false;
+  std::vector<std::vector<PVal>> in;
+  if (!pointer_kinds(prog, xdp, pkt_ok, in)) return;  // ctx rewritten: generic handlers only
+  uint32_t nspec = 0;
+  for (size_t i = 0; i < prog.size(); i++) {
+    const DInsn &d = prog[i];
+    if (d.op != X_LDX && d.op != X_STX && d.op != X_ST && d.op != X_CALL) continue;
+    const std::vector<PVal> &st = in[i];
+    if (st[0].kind == P_UNDEF && st[1].kind == P_UNDEF) continue;  // unreachable
+    const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
+    const uint32_t si = sz == 1 ? 0 : sz == 2 ? 1 : sz == 4 ? 2 : 3;
+    FInsn &f = fast[i];
+    if (d.op == X_CALL) {
+      // array lookup with its key on the stack: key read straight from LDS
+      const PVal key = st[2];
+      const int64_t at = (int64_t)key.k;
+      if (d.hi == 1 && key.kind == P_STK && !big_stack && at >= -(int64_t)stack_size && at + 4 <= 0 &&
+          at % 4 == 0) {
+        f.hoff = 4 + 4 * F_CALL_LOOKUP_STK;
+        f.target = (uint32_t)(int32_t)at;
+        nspec++;
+      }
+      continue;
+    }
+    const PVal b = st[d.op == X_LDX ? d.src : d.dst];
+    const int64_t at = (int64_t)b.k + d.off;
+    static const uint32_t ldp[4] = {F_LDX1_PKT, F_LDX2_PKT, F_LDX4_PKT, F_LDX8_PKT};
+    static const uint32_t stxp[4] = {F_STX1_PKT, F_STX2_PKT, F_STX4_PKT, F_STX8_PKT};
+    static const uint32_t stp[4] = {F_ST1_PKT, F_ST2_PKT, F_ST4_PKT, F_ST8_PKT};
+    static const uint32_t lds[4] = {F_LDX1_SLOT, F_LDX2_SLOT, F_LDX4_SLOT, F_LDX8_SLOT};
+    static const uint32_t stxs[4] = {F_STX1_SLOT, F_STX2_SLOT, F_STX4_SLOT, F_STX8_SLOT};
+    static const uint32_t sts[4] = {F_ST1_SLOT, F_ST2_SLOT, F_ST4_SLOT, F_ST8_SLOT};
+    static const uint32_t ldk[4] = {F_LDX1_STK, F_LDX2_STK, F_LDX4_STK, F_LDX8_STK};
+    static const uint32_t stxk[4] = {F_STX1_STK, F_STX2_STK, F_STX4_STK, F_STX8_STK};
+    static const uint32_t stk[4] = {F_ST1_STK, F_ST2_STK, F_ST4_STK, F_ST8_STK};
+    const uint32_t *tab = nullptr;
+    if ((b.kind == P_PKT || b.kind == P_SLOT) && at >= 0 && at + sz <= kFastStageBytes) {
+      // packet bytes: data = slot + head; the handler adds the batch head
+      if (b.kind == P_PKT) tab = d.op == X_LDX ? ldp : d.op == X_STX ? stxp : stp;
+      else tab = d.op == X_LDX ? lds : d.op == X_STX ? stxs : sts;
+    } else if (b.kind == P_STK && !big_stack && at >= -(int64_t)stack_size && at + sz <= 0 && at % sz == 0) {
+      tab = d.op == X_LDX ? ldk : d.op == X_STX ? stxk : stk;
+    } else if (pkt_ok && b.kind == P_CTX && d.op == X_LDX && sz == 8 && (at == 0 || at == 8)) {
+      // ctx->data = slot + head, ctx->data_end = data + len (interp.hip setup)
+      f.hoff = 4 + 4 * (at == 0 ? F_LDX_CTXDATA : F_LDX_CTXEND);
+      nspec++;
+      continue;
+    }
+    if (!tab) continue;
+    f.hoff = 4 + 4 * tab[si];
+    f.target = (uint32_t)(int32_t)at;  // static byte offset (signed for the stack)
+    nspec++;
+  }
+  if (specialized) *specialized = nspec;
 }
 
 }  // namespace bpftime_amd

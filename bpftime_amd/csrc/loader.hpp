@@ -39,8 +39,12 @@ struct LoadOut {
 bool device_helper_supported(uint32_t id);
 
 // Threaded-code records for the asm fast path: one per DInsn; instructions
-// without a fast handler dispatch to F_SLOW (the C++ interpreter).
-void build_fast(const std::vector<DInsn> &prog, std::vector<FInsn> &fast);
+// without a fast handler dispatch to F_SLOW (the C++ interpreter).  `xdp`
+// selects the entry convention (r1 = XDP ctx, else r1 = the unit's slot);
+// loads/stores whose base pointer kind is known statically get
+// specialized handlers (count in *specialized).
+void build_fast(const std::vector<DInsn> &prog, bool xdp, bool big_stack, uint32_t stack_size,
+                std::vector<FInsn> &fast, uint32_t *specialized);
 
 // Runs the compat_ubpf.cpp:61-200 patching (call remap check, lddw pseudo
 // sources), ubpf-style validation, pre-decoding and the dataflow analyses

@@ -45,7 +45,8 @@ class Mi355xVm {
   bool loaded = false;
   LoadOut prog;
   DInsn *d_prog = nullptr;
-  FInsn *d_fast = nullptr;
+  FInsn *d_fast = nullptr;      // [XDP form | raw/syscall form], prog.prog.size() each
+  uint32_t spec_xdp = 0, spec_raw = 0;  // accesses with statically typed bases
   // failed-unit counters, one per in-flight batch: concurrent batches on
   // different streams must not share (and re-zero) one counter
   static constexpr uint32_t kErrSlots = 64;
@@ -107,7 +108,12 @@ class Mi355xVm {
       error = "no HIP device: " + rt().last_error;
       return -1;
     }
-    build_fast(out.prog, out.fast);
+    // two threaded-code forms: XDP entry (r1 = ctx) and raw/syscall entry
+    // (r1 = the unit's slot) differ in the loader's pointer kinds
+    std::vector<FInsn> fraw;
+    build_fast(out.prog, true, out.big_stack, out.stack_size, out.fast, &spec_xdp);
+    build_fast(out.prog, false, out.big_stack, out.stack_size, fraw, &spec_raw);
+    out.fast.insert(out.fast.end(), fraw.begin(), fraw.end());
     size_t bytes = out.prog.size() * sizeof(DInsn);
     size_t fbytes = out.fast.size() * sizeof(FInsn);
     if (hipMalloc((void **)&d_prog, bytes) != hipSuccess ||
@@ -144,7 +150,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   Runtime &r = rt();
   KParams p{};
   p.prog = d_prog;
-  p.fast = d_fast;
+  p.fast = d_fast + (b->ctx_kind == CTX_XDP ? 0 : prog.prog.size());
   p.maps = r.d_maptab;
   p.data = (uint8_t *)b->data;
   p.lens = b->lens;
@@ -429,6 +435,12 @@ int bpftime_amd_vm_info(const struct ebpf_vm *vm, uint32_t *stack_size, int *big
   if (big_stack) *big_stack = vm->impl->prog.big_stack;
   if (fused_rmw) *fused_rmw = vm->impl->prog.fused_rmw;
   if (n_insns) *n_insns = (uint32_t)vm->impl->prog.prog.size();
+  return 0;
+}
+
+int bpftime_amd_vm_fast_info(const struct ebpf_vm *vm, uint32_t ctx_kind, uint32_t *specialized) {
+  if (!vm || !vm->impl->loaded) return -1;
+  if (specialized) *specialized = ctx_kind == CTX_XDP ? vm->impl->spec_xdp : vm->impl->spec_raw;
   return 0;
 }
 

@@ -212,6 +212,12 @@ class VM:
         return {"stack_size": ss.value, "big_stack": bool(big.value), "fused_rmw": fused.value,
                 "n_insns": n.value}
 
+    def fast_specialized(self, kind: int) -> int:
+        n = C.c_uint32()
+        if lib().bpftime_amd_vm_fast_info(C.c_void_p(self.h), kind, C.byref(n)):
+            raise EbpfError("vm_fast_info failed")
+        return n.value
+
     def set_step_limit(self, n: int) -> None:
         lib().bpftime_amd_set_step_limit(C.c_void_p(self.h), n)
 

@@ -101,6 +101,9 @@ int bpftime_amd_register_default_helpers(struct ebpf_vm *vm);
 int bpftime_amd_vm_info(const struct ebpf_vm *vm, uint32_t *stack_size, int *big_stack,
                         uint32_t *fused_rmw, uint32_t *n_insns);
 void bpftime_amd_set_step_limit(struct ebpf_vm *vm, uint64_t limit);
+/* loads/stores (and array-lookup keys) the loader typed statically for the
+ * fast path under the given ctx kind (packet, slot, ctx or stack bases) */
+int bpftime_amd_vm_fast_info(const struct ebpf_vm *vm, uint32_t ctx_kind, uint32_t *specialized);
 
 /* ---- host merge of per-GPU map shards ---- */
 /* acc += shard - init over u64 words (array counters, additive rule) */

@@ -43,6 +43,8 @@ def test_xdp_counter_parity(fresh_oracle, fresh_runtime, n):
     ov, os_, dv, ds, failed, vm = run_xdp_both(po, dev, code, slots)
     assert failed == 0
     assert vm.info()["fused_rmw"] == 1
+    # stack store + lookup key, ctx data/data_end, 6 packet loads, 6 stores
+    assert vm.fast_specialized(dev.CTX_XDP) == 16
     np.testing.assert_array_equal(dv, ov)
     np.testing.assert_array_equal(ds, os_)
     assert (dv == isa.XDP_TX).all()
@@ -339,3 +341,66 @@ def test_device_generators_match_numpy(fresh_runtime, first):
     sb = dev.DeviceBuffer(n * 64)
     assert L.bpftime_amd_gen_syscall(sb.ptr, n, gen.SEED_CFG5, first, dc5.ptr, 335, None) == 0
     np.testing.assert_array_equal(sb.download(np.uint8).reshape(n, 64), gen.syscall_records(n, first=first))
+
+
+def _staged_mix():
+    """Packet / stack / ctx accesses of every size at aligned, unaligned,
+    dword-straddling and window-edge offsets, reads after writes, and one
+    store the staged path cannot take (straddling) — the fast path's typed
+    handlers against the oracle."""
+    a = Asm()
+    a.mov64(6, "r1").ldx(8, 2, 6, 0).ldx(8, 3, 6, 8)
+    a.mov64(4, "r2").add64(4, 64).jmp("jgt", 4, "r3", "short")
+    a.mov64(0, 0)
+    for sz, off in [(1, 63), (2, 1), (4, 2), (8, 5), (8, 56), (2, 62), (1, 0), (4, 60)]:
+        a.ldx(sz, 5, 2, off).alu64("xor", 0, "r5").alu64("lsh", 0, 3).alu64("add", 0, "r5")
+    a.stx(1, 2, 7, "r0").stx(2, 2, 3, "r0").stx(4, 2, 8, "r0").stx(8, 2, 16, "r0")
+    a.st(4, 2, 40, 0x1234567).st(2, 2, 62, -2).st(1, 2, 33, 7).st(8, 2, 48, -5)
+    a.ldx(4, 5, 2, 8).alu64("add", 0, "r5").ldx(2, 5, 2, 3).alu64("add", 0, "r5")
+    a.ldx(8, 5, 2, 14).alu64("xor", 0, "r5")
+    a.stx(8, 10, -8, "r0").stx(4, 10, -12, "r5").st(1, 10, -13, 9).st(2, 10, -16, 300)
+    a.ldx(4, 5, 10, -8).alu64("add", 0, "r5").ldx(1, 5, 10, -13).alu64("add", 0, "r5")
+    a.ldx(2, 5, 10, -16).alu64("add", 0, "r5").ldx(8, 5, 10, -16).alu64("xor", 0, "r5")
+    a.ldx(4, 5, 6, 20).alu64("add", 0, "r5")          # ifindex: generic ctx load
+    a.alu64("and", 0, 0xffff).exit()
+    a.label("short").mov64(0, 1).exit()
+    return a.assemble()
+
+
+@pytest.mark.parametrize("stride,n", [(64, 5000), (128, 3001), (2048, 700)])
+def test_staged_typed_accesses(fresh_oracle, fresh_runtime, stride, n):
+    po, dev = fresh_oracle, fresh_runtime
+    code = _staged_mix()
+    slots = gen.xdp_packets(n, stride=stride, seed=77)
+    lens = np.full(n, stride, dtype=np.uint32)
+    lens[::7] = 40                                     # short units take the other path
+    ov, os_, dv, ds, failed, vm = run_xdp_both(po, dev, code, slots, lens=lens, fixed_len=0)
+    assert failed == 0
+    assert vm.fast_specialized(dev.CTX_XDP) == 29
+    np.testing.assert_array_equal(dv, ov)
+    np.testing.assert_array_equal(ds, os_)
+
+
+def test_staged_raw_slot_accesses(fresh_oracle, fresh_runtime):
+    """RAW units (r1 = the slot itself): slot-typed accesses read the staged
+    copy and see earlier stores."""
+    po, dev = fresh_oracle, fresh_runtime
+    a = Asm().mov64(0, 0)
+    for sz, off in [(8, 0), (4, 12), (2, 30), (1, 63)]:
+        a.ldx(sz, 3, 1, off).alu64("add", 0, "r3")
+    a.stx(4, 1, 12, "r0").ldx(4, 3, 1, 12).alu64("xor", 0, "r3").stx(8, 1, 40, "r0").exit()
+    code = a.assemble()
+    n = 4000
+    units = gen.xdp_packets(n, stride=64, seed=5)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    ou = units.copy()
+    orets = ovm.run_raw(ou, 64)
+    vm = dev.VM()
+    vm.load(code)
+    assert vm.fast_specialized(dev.CTX_RAW) == 7
+    d = dev.DeviceBuffer.from_array(units)
+    dr = dev.DeviceBuffer(8 * n)
+    assert vm.exec_batch(dev.CTX_RAW, d, n, 64, fixed_len=64, rets=dr) == 0
+    np.testing.assert_array_equal(dr.download(np.uint64), orets)
+    np.testing.assert_array_equal(d.download().reshape(n, 64), ou)
