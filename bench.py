@@ -27,17 +27,28 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--log2n", type=int, default=24, help="packets per GPU = 2^log2n")
+    ap.add_argument("--log2n", type=int, default=None, help="units per GPU = 2^log2n (xdp-counter: 24)")
+    ap.add_argument("--workload", default="xdp-counter", choices=["xdp-counter", "flow-hash", "syscall-agg"],
+                    help="xdp-counter is the headline (BASELINE metric); the others are configs[2]/[4] "
+                         "(bench_workloads.py)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--unchecked", action="store_true", help="skip the global-window check")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe-inclusive) leg")
     ap.add_argument("--e2e-chunk-log2", type=int, default=20, help="packets per H2D chunk = 2^k")
-    return ap.parse_args()
+    args = ap.parse_args()
+    args.log2n_set = args.log2n is not None
+    if args.log2n is None:
+        args.log2n = 24
+    return args
 
 
 def main():
     args = parse()
+    if args.workload != "xdp-counter":
+        from bench_workloads import run
+        run(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -41,9 +41,8 @@ one instruction (interp.hip, run_loop<true, true>).
 
 Fixed registers (declared as clobbers; the compiler keeps nothing live in
 them across the block).  The handlers are written against the numbering
-below; main() relocates every VGPR to the top of a 128-register budget
-(v40-v42 -> v72-v74, v44-v55 -> v76-v87, v60-v81 -> v88-v109,
-v84-v101 -> v110-v127):
+below; main() relocates every VGPR by +26 to the top of a 128-register
+budget (v40..v101 -> v66..v127):
   s[40:47] W   current FInsn: w0 handler offset, w1 dst*2, w[2:3] imm64,
                w4 src*2, w5 jump target (byte offset from PROG), w[6:7] off64
   s[48:49] IP  address of the current FInsn     s[50:51] TB  table base - 4
@@ -54,10 +53,11 @@ v84-v101 -> v110-v127):
   s[76:77] DMap data pointer                     s[78:79] PROG (FInsn base)
   s[80:81] S (staged bytes, 64-bit)              s[82:83] O (uniform window offset)
   s84 dirty 16-B chunk mask                      s85 scratch
-  v40 lane's R[0] LDS address  v41/v42 scratch
+  v40 lane's R[0] LDS address  v41, v[42:43] scratch
   v[44:45] X  v[46:47] Y  v[48:49] Z (address)  v[50:51] E (address end)
   v[52:53] slot address (staging base)           v[54:55] O (per-lane offset)
-  v[60:81] r0..r10                               v[84:99] staged bytes
+  v56..v59 scratch (hash probing)                v[60:81] r0..r10
+  v[84:99] staged bytes
 Loop-invariant inputs (window bounds, apertures, step limit, map table,
 output addresses) and the per-wave counter cache are asm operands, so they
 stay in the registers the compiler already holds them in.
@@ -94,6 +94,9 @@ def handler_ids():
         for kind in ("PKT", "SLOT", "STK"):
             ids += [f"LDX{sz}_{kind}", f"STX{sz}_{kind}", f"ST{sz}_{kind}"]
     ids += ["LDX_CTXDATA", "LDX_CTXEND"]
+    for sz in (4, 8):
+        for op in ("ADD", "OR", "AND", "XOR"):
+            ids += [f"ATOM{sz}_{op}", f"ATOM{sz}_{op}_F"]
     ids += ["LDDW", "JA", "CALL_LOOKUP", "CALL_LOOKUP_STK", "EXIT", "RMW4_R", "RMW4_I", "RMW8_R", "RMW8_I"]
     for w in ("64", "32"):
         for cc in JCC:
@@ -173,6 +176,25 @@ class Gen:
                "s_or_b64 s[54:55], s[54:55], s[56:57]",
                "v_cmp_eq_u32 s[56:57], %[phi], v49",
                "s_or_b64 s[54:55], s[54:55], s[56:57]",
+               "s_andn2_b64 s[54:55], exec, s[54:55]",
+               f"s_cbranch_scc1 {L('slow')}")
+
+    def check_global(self, sz):
+        """Every live lane's [Z, Z+sz) inside the batch window or the map
+        arena and not in the LDS / scratch apertures (global atomics need a
+        global address even when window checks are off); else leave."""
+        self.e(f"v_lshl_add_u64 v[50:51], v[48:49], 0, {sz}",
+               "v_cmp_le_u64 s[54:55], %[dlo], v[48:49]",
+               "v_cmp_ge_u64 s[56:57], %[dhi], v[50:51]",
+               "s_and_b64 s[54:55], s[54:55], s[56:57]",
+               "v_cmp_le_u64 s[56:57], %[alo], v[48:49]",
+               "v_cmp_ge_u64 s[60:61], %[ahi], v[50:51]",
+               "s_and_b64 s[56:57], s[56:57], s[60:61]",
+               "s_or_b64 s[54:55], s[54:55], s[56:57]",
+               "v_cmp_ne_u32 s[56:57], %[shi], v49",
+               "s_and_b64 s[54:55], s[54:55], s[56:57]",
+               "v_cmp_ne_u32 s[56:57], %[phi], v49",
+               "s_and_b64 s[54:55], s[54:55], s[56:57]",
                "s_andn2_b64 s[54:55], exec, s[54:55]",
                f"s_cbranch_scc1 {L('slow')}")
 
@@ -456,10 +478,14 @@ class Gen:
                "s_cmp_lg_u64 s[54:55], 0", f"s_cbranch_scc1 {L('slow')}")
 
     def call_lookup(self, stack_key=False):
-        """bpf_map_lookup_elem on an ARRAY map with a wave-uniform map fd
-        (array_map.cpp:27-40): r0 = key < max_entries ? &data[key * vsz] : 0.
-        Any other map type leaves for the C++ helper.  stack_key: the loader
-        proved r2 = stack top + w5 (4-aligned), so the key is one ds_read."""
+        """bpf_map_lookup_elem with a wave-uniform map fd.
+        ARRAY (array_map.cpp:27-40): r0 = key < max_entries ? &data[key * vsz] : 0.
+        HASH with its key on the stack (stack_key: the loader proved r2 =
+        stack top + w5, 4-aligned): the bpftime_hash_map probe
+        (bpftime_hash_map.hpp:40-47, 127-151) per lane; a wave whose lanes
+        all hit stays here, any miss or in-flight insert leaves for the C++
+        helper (which also records the miss for lookup_or_try_init).
+        Other map types leave for C++."""
         stg, glb, got = self.label("ks"), self.label("kg"), self.label("kd")
         self.rd_fixed(1, 44)                      # r1 = fd
         self.rd_fixed(2, 48)                      # r2 = key pointer
@@ -470,24 +496,105 @@ class Gen:
                "s_load_dwordx4 s[72:75], %[maps], s85",                      # type, ksz, vsz, max
                "s_add_u32 s85, s85, 16",
                "s_load_dwordx2 s[76:77], %[maps], s85",                     # data
-               "s_waitcnt lgkmcnt(0)",
-               "s_cmp_lg_u32 s72, 2", f"s_cbranch_scc1 {L('slow')}")        # not BPF_MAP_TYPE_ARRAY
+               "s_waitcnt lgkmcnt(0)")
+        if stack_key:
+            hsh = self.label("hash")
+            self.e("s_cmp_eq_u32 s72, 1", f"s_cbranch_scc1 {hsh}")          # BPF_MAP_TYPE_HASH
+        self.e("s_cmp_lg_u32 s72, 2", f"s_cbranch_scc1 {L('slow')}")        # not BPF_MAP_TYPE_ARRAY
         if stack_key:
             self.e("v_add_u32 v41, s45, %[stklo]", "ds_read_b32 v46, v41", "s_waitcnt lgkmcnt(0)",
                    f"s_branch {got}")
-        self.staged_or(4, stg, glb)
-        self.e(f"{stg}:")
-        self.staged_load(4)
-        self.e("v_mov_b32 v46, v44", f"s_branch {got}")
-        self.e(f"{glb}:")
-        self.check(4)
-        self.e("flat_load_dword v46, v[48:49]", "s_waitcnt vmcnt(0) lgkmcnt(0)")
+        else:
+            self.staged_or(4, stg, glb)
+            self.e(f"{stg}:")
+            self.staged_load(4)
+            self.e("v_mov_b32 v46, v44", f"s_branch {got}")
+            self.e(f"{glb}:")
+            self.check(4)
+            self.e("flat_load_dword v46, v[48:49]", "s_waitcnt vmcnt(0) lgkmcnt(0)")
         self.e(f"{got}:",
                "v_cmp_gt_u32 s[54:55], s75, v46",                            # key < max_entries
                "v_mov_b32 v47, s74",
                "v_mad_u64_u32 v[50:51], s[56:57], v46, v47, s[76:77]",
                f"v_cndmask_b32 v{R0}, 0, v50, s[54:55]",
                f"v_cndmask_b32 v{R0 + 1}, 0, v51, s[54:55]")
+        self.next_seq()
+        if stack_key:
+            self.e(f"{hsh}:")
+            self.hash_lookup()
+
+    def hash_mod_step(self):
+        """v[50:51] = x (f64, integer < 2^48) -> v56 = x mod nb, with v[58:59]
+        = nb and v[54:55] ~ 1/nb (f64).  q = trunc(x / nb) is off by at most
+        one, x - q*nb is exact in one fma, then one correction each way."""
+        self.e("v_mul_f64 v[42:43], v[50:51], v[54:55]",
+               "v_trunc_f64 v[42:43], v[42:43]",
+               "v_fma_f64 v[50:51], -v[42:43], v[58:59], v[50:51]",
+               "v_cmp_gt_f64 vcc, 0, v[50:51]",
+               "v_add_f64 v[42:43], v[50:51], v[58:59]",
+               "v_cndmask_b32 v50, v50, v42, vcc", "v_cndmask_b32 v51, v51, v43, vcc",
+               "v_cmp_le_f64 vcc, v[58:59], v[50:51]",
+               "v_add_f64 v[42:43], v[50:51], -v[58:59]",
+               "v_cndmask_b32 v50, v50, v42, vcc", "v_cndmask_b32 v51, v51, v43, vcc",
+               "v_cvt_u32_f64 v56, v[50:51]")
+
+    def hash_lookup(self):
+        done, bail = self.label("hdone"), self.label("hbail")
+        # DMap words 4-11: data, nbuckets, slot_size, key_off, val_off, ncpu
+        self.e("s_lshl_b32 s85, s62, 6", "s_add_u32 s85, s85, 16",
+               "s_load_dwordx8 s[64:71], %[maps], s85",
+               "s_waitcnt lgkmcnt(0)",
+               "s_cmp_lg_u32 s67, 0", f"s_cbranch_scc1 {L('slow')}",       # nbuckets >= 2^32
+               "v_add_u32 v41, s45, %[stklo]",
+               "ds_read_b32 v44, v41", "ds_read_b32 v45, v41 offset:4",
+               "ds_read_b32 v46, v41 offset:8", "ds_read_b32 v47, v41 offset:12",
+               "s_mov_b64 s[60:61], exec",
+               "s_waitcnt lgkmcnt(0)")
+        for kd in (1, 2, 3, 4):
+            nxt = self.label("kdn")
+            self.e(f"s_cmp_lg_u32 s73, {4 * kd}", f"s_cbranch_scc1 {nxt}")
+            # h = sum over key bytes of h * 31 + byte (size_t arithmetic)
+            self.e("v_mov_b32 v48, 0", "v_mov_b32 v49, 0")
+            for i in range(4 * kd):
+                self.e("v_lshlrev_b64 v[50:51], 5, v[48:49]",
+                       "v_sub_co_u32 v48, vcc, v50, v48", "v_subb_co_u32 v49, vcc, v51, v49, vcc",
+                       f"v_bfe_u32 v50, v{44 + i // 4}, {8 * (i % 4)}, 8",
+                       "v_add_co_u32 v48, vcc, v48, v50", "v_addc_co_u32 v49, vcc, 0, v49, vcc")
+            # idx = h % nbuckets: h = ((hi * 2^16 + lo >> 16) * 2^16 + lo & 0xffff)
+            self.e("v_cvt_f64_u32 v[58:59], s66", "v_rcp_f64 v[54:55], v[58:59]",
+                   "v_cvt_f64_u32 v[50:51], v49")
+            self.hash_mod_step()
+            for part in ("v_lshrrev_b32 v57, 16, v48", "v_and_b32 v57, 0xffff, v48"):
+                self.e("v_cvt_f64_u32 v[50:51], v56", "v_ldexp_f64 v[50:51], v[50:51], 16",
+                       part, "v_cvt_f64_u32 v[42:43], v57", "v_add_f64 v[50:51], v[50:51], v[42:43]")
+                self.hash_mod_step()
+            # linear probing from idx until every lane hits; stop at anything else
+            loop = self.label("probe")
+            self.e("v_mov_b32 v57, v56", "v_mov_b32 v43, s68", "s_mov_b32 s85, 0",
+                   f"{loop}:",
+                   "v_mad_u64_u32 v[54:55], s[56:57], v56, v43, s[64:65]",
+                   "global_load_dword v58, v[54:55], off sc1",
+                   "global_load_dwordx4 v[48:51], v[54:55], off offset:8 sc1",
+                   "s_waitcnt vmcnt(0)",
+                   "v_cmp_ne_u32 s[56:57], 1, v58",                          # not FILLED
+                   "s_cmp_lg_u64 s[56:57], 0", f"s_cbranch_scc1 {bail}",
+                   "v_cmp_eq_u32 s[56:57], v48, v44")
+            for j in range(1, kd):
+                self.e(f"v_cmp_eq_u32 vcc, v{48 + j}, v{44 + j}", "s_and_b64 s[56:57], s[56:57], vcc")
+            self.e("s_and_saveexec_b64 s[62:63], s[56:57]",                   # exec = hits
+                   f"v_add_co_u32 v{R0}, vcc, s70, v54", f"v_addc_co_u32 v{R0 + 1}, vcc, 0, v55, vcc",
+                   "s_andn2_b64 exec, s[62:63], s[56:57]",                    # exec = other keys
+                   f"s_cbranch_execz {done}",
+                   "v_add_u32 v56, 1, v56",
+                   "v_cmp_eq_u32 vcc, s66, v56", "v_cndmask_b32 v56, v56, 0, vcc",
+                   "v_cmp_eq_u32 vcc, v57, v56",                              # wrapped: a miss
+                   f"s_cbranch_vccnz {bail}",
+                   "s_add_u32 s85, s85, 1", "s_cmp_gt_u32 s85, 63", f"s_cbranch_scc1 {bail}",
+                   f"s_branch {loop}",
+                   f"{nxt}:")
+        self.e(f"s_branch {L('slow')}",
+               f"{bail}:", "s_mov_b64 exec, s[60:61]", f"s_branch {L('slow')}",
+               f"{done}:", "s_mov_b64 exec, s[60:61]")
         self.next_seq()
 
     def rmw(self, sz, k):
@@ -506,11 +613,15 @@ class Gen:
         self.e(f"{stg}:", f"s_branch {L('slow')}")   # a counter inside the unit's own bytes
         self.e(f"{glb}:")
         self.check(sz)
-        self.uniform64((48, 49), (62, 63))
-        self.e("s_cmp_eq_u32 s63, %[shi]", f"s_cbranch_scc1 {L('slow')}",   # LDS / scratch targets
-               "s_cmp_eq_u32 s63, %[phi]", f"s_cbranch_scc1 {L('slow')}")
-        self.uniform64((46, 47), (64, 65))
-        t1, t2, t3, done = (self.label(x) for x in ("t1", "t2", "t3", "done"))
+        t1, t2, t3, done, lane = (self.label(x) for x in ("t1", "t2", "t3", "done", "lane"))
+        self.e("v_readfirstlane_b32 s62, v48", "v_readfirstlane_b32 s63, v49",
+               "v_cmp_ne_u64 s[54:55], s[62:63], v[48:49]",
+               "s_cmp_lg_u64 s[54:55], 0", f"s_cbranch_scc1 {lane}",
+               "s_cmp_eq_u32 s63, %[shi]", f"s_cbranch_scc1 {L('slow')}",   # LDS / scratch targets
+               "s_cmp_eq_u32 s63, %[phi]", f"s_cbranch_scc1 {L('slow')}",
+               "v_readfirstlane_b32 s64, v46", "v_readfirstlane_b32 s65, v47",
+               "v_cmp_ne_u64 s[54:55], s[64:65], v[46:47]",
+               "s_cmp_lg_u64 s[54:55], 0", f"s_cbranch_scc1 {lane}")
         self.e("s_bcnt1_i32_b64 s69, exec",
                "s_mul_i32 s66, s64, s69", "s_mul_hi_u32 s67, s64, s69",
                "s_mul_i32 s70, s65, s69", "s_add_u32 s67, s67, s70",
@@ -529,9 +640,37 @@ class Gen:
                "s_cmp_eq_u64 %[c1a], 0", f"s_cbranch_scc0 {L('slow')}",      # both taken: C++ evicts
                "s_mov_b64 %[c1a], s[62:63]", "s_mov_b32 %[c1dl], s66", "s_mov_b32 %[c1dh], s67",
                f"s_mov_b32 %[c1s], {sz}",
+               f"s_branch {done}",
+               # lanes disagree on address or value: one atomic add per lane
+               f"{lane}:")
+        self.check_global(sz)
+        self.e("global_atomic_add_x2 v[48:49], v[46:47], off" if sz == 8 else "global_atomic_add v[48:49], v46, off",
                f"{done}:",
                "s_add_u32 s48, s78, s45", "s_addc_u32 s49, s79, 0")           # continue after the stx
         self.dispatch()
+
+    def atomic(self, sz, op, fetch):
+        """BPF_ATOMIC add/or/and/xor (+ BPF_FETCH) on global memory: one
+        device-scope atomic per lane (array_map values, hash values).  LDS or
+        scratch targets and the unit's own staged bytes leave for C++."""
+        glb = self.label("ag")
+        self.rd("s41", 48)
+        self.rd("s44", 44)
+        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[46:47]")
+        self.staged_or(sz, L("slow"), glb)
+        self.e(f"{glb}:")
+        self.check_global(sz)
+        mn = op.lower() + ("_x2" if sz == 8 else "")
+        val = "v[44:45]" if sz == 8 else "v44"
+        if fetch:
+            self.e(f"global_atomic_{mn} {'v[46:47]' if sz == 8 else 'v46'}, v[48:49], {val}, off sc0",
+                   "s_waitcnt vmcnt(0)")
+            if sz == 4:
+                self.e("v_mov_b32 v47, 0")
+            self.wr("s44", 46)
+        else:
+            self.e(f"global_atomic_{mn} v[48:49], {val}, off")
+        self.next_seq()
 
     def exit_(self):
         """Every live lane exits: write back the unit's dirty bytes, store r0
@@ -589,6 +728,9 @@ class Gen:
             e(f"{L('h_' + name)}:")
             if name == "SLOW":
                 e(f"s_branch {L('slow')}")
+            elif name.startswith("ATOM"):
+                parts = name.split("_")
+                self.atomic(int(parts[0][4:]), parts[1], len(parts) == 3)
             elif name in ("A64_NEG", "A32_NEG"):
                 self.neg(name[1:3])
             elif name[0] == "A":
@@ -649,9 +791,11 @@ class Gen:
 
 def vmap(n):
     """Handlers are written against v40..v101; the block is placed at the top
-    of a 128-VGPR budget (v72..v127) so that the compiler's own values stay
-    below it and the kernel keeps 4 waves per SIMD."""
-    return n + 32 if n < 60 else n + 28 if n < 84 else n + 26
+    of a 128-VGPR budget (v66..v127, an even shift so register pairs stay
+    aligned) so that the compiler's own values stay below it and the kernel
+    keeps 4 waves per SIMD."""
+    assert 40 <= n <= 101, n
+    return n + 26
 
 
 def relocate(line):
@@ -665,7 +809,7 @@ def main():
     g.out = [relocate(x) for x in g.out]
     # v126/v127 (v100/v101 before relocation) are read, never written, by
     # staged loads near the window end
-    clob = [f"s{i}" for i in range(40, 86)] + [f"v{vmap(i)}" for i in range(40, 102) if not 42 < i < 44 and not 55 < i < 60 and not 81 < i < 84]
+    clob = [f"s{i}" for i in range(40, 86)] + [f"v{vmap(i)}" for i in range(40, 102)]
     with open(os.path.join(HERE, "fast_asm.inc"), "w") as f:
         f.write("// Generated by gen_fast.py; do not edit.\n")
         f.write("#define BPFTIME_AMD_FAST_ASM \\\n")

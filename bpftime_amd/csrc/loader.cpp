@@ -669,6 +669,17 @@ static uint32_t fast_id(const DInsn &d) {
     case X_JSLE: return JCC(SLE);
     case X_CALL: return d.hi == 1 ? F_CALL_LOOKUP : F_SLOW;  // map_lookup_elem; other helpers in C++
     case X_EXIT: return F_EXIT;
+    case X_ATOMIC: {
+      const uint32_t aop = (uint32_t)d.hi & ~1u, fetch = (uint32_t)d.hi & 1u;
+      if (sz != 4 && sz != 8) return F_SLOW;
+      static const uint32_t t4[4][2] = {{F_ATOM4_ADD, F_ATOM4_ADD_F}, {F_ATOM4_OR, F_ATOM4_OR_F},
+                                        {F_ATOM4_AND, F_ATOM4_AND_F}, {F_ATOM4_XOR, F_ATOM4_XOR_F}};
+      static const uint32_t t8[4][2] = {{F_ATOM8_ADD, F_ATOM8_ADD_F}, {F_ATOM8_OR, F_ATOM8_OR_F},
+                                        {F_ATOM8_AND, F_ATOM8_AND_F}, {F_ATOM8_XOR, F_ATOM8_XOR_F}};
+      const int k = aop == 0x00 ? 0 : aop == 0x40 ? 1 : aop == 0x50 ? 2 : aop == 0xa0 ? 3 : -1;
+      if (k < 0) return F_SLOW;  // xchg / cmpxchg
+      return sz == 8 ? t8[k][fetch] : t4[k][fetch];
+    }
     case X_RMW_ADD:
       return sz == 8 ? (r ? F_RMW8_R : F_RMW8_I) : sz == 4 ? (r ? F_RMW4_R : F_RMW4_I) : F_SLOW;
     default: return F_SLOW;  // div/mod, atomics

@@ -404,3 +404,64 @@ def test_staged_raw_slot_accesses(fresh_oracle, fresh_runtime):
     assert vm.exec_batch(dev.CTX_RAW, d, n, 64, fixed_len=64, rets=dr) == 0
     np.testing.assert_array_equal(dr.download(np.uint64), orets)
     np.testing.assert_array_equal(d.download().reshape(n, 64), ou)
+
+
+def test_atomics_shared_map_and_own_bytes(fresh_oracle, fresh_runtime):
+    """Device-scope atomics from every lane onto shared array-map values
+    (commutative, so any interleaving gives the oracle's totals), fetch
+    forms with the fetched value discarded, and an atomic on the unit's own
+    staged bytes (the C++ path, after write-back)."""
+    po, dev = fresh_oracle, fresh_runtime
+    (om,), (dm,) = make_maps([(isa.BPF_MAP_TYPE_ARRAY, 4, 16, 4)], po, dev)
+    a = Asm()
+    a.ldx(8, 6, 1, 0).mov64(7, "r6").alu64("and", 7, 3).stx(4, 10, -4, "r7")
+    a.mov64(9, "r1").ld_map_fd(1, dm.fd).mov64(2, "r10").add64(2, -4).call(1)
+    a.jmp("jeq", 0, 0, "out")
+    a.atomic(8, isa.ATOMIC_ADD, 0, 0, "r6")
+    a.mov64(8, "r6").atomic(8, isa.ATOMIC_ADD | isa.ATOMIC_FETCH, 0, 0, "r8")
+    a.mov64(8, "r6").atomic(4, isa.ATOMIC_XOR, 0, 8, "r8")
+    a.mov64(8, "r6").atomic(4, isa.ATOMIC_OR | isa.ATOMIC_FETCH, 0, 12, "r8")
+    a.stx(8, 9, 16, "r6").atomic(8, isa.ATOMIC_ADD, 9, 16, "r7")   # own staged bytes
+    a.label("out").mov64(0, "r7").exit()
+    code = a.assemble()
+    n = 20000
+    units = gen.xdp_packets(n, stride=64, seed=31)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    ou = units.copy()
+    orets = ovm.run_raw(ou, 64)
+    vm = dev.VM()
+    vm.load(code)
+    d = dev.DeviceBuffer.from_array(units)
+    dr = dev.DeviceBuffer(8 * n)
+    assert vm.exec_batch(dev.CTX_RAW, d, n, 64, fixed_len=64, rets=dr) == 0
+    np.testing.assert_array_equal(dr.download(np.uint64), orets)
+    np.testing.assert_array_equal(d.download().reshape(n, 64), ou)
+    for k in range(4):
+        assert dm.lookup(struct.pack("<I", k)) == om.lookup(struct.pack("<I", k)), k
+
+
+def test_fused_counter_per_lane_addresses(fresh_oracle, fresh_runtime):
+    """ldx/add/stx fused counters whose address differs per lane (hash of
+    the unit): one atomic per lane in the fast path."""
+    po, dev = fresh_oracle, fresh_runtime
+    (om,), (dm,) = make_maps([(isa.BPF_MAP_TYPE_ARRAY, 4, 8, 64)], po, dev)
+    a = Asm()
+    a.ldx(4, 6, 1, 4).alu64("and", 6, 63).stx(4, 10, -4, "r6")
+    a.ld_map_fd(1, dm.fd).mov64(2, "r10").add64(2, -4).call(1)
+    a.jmp("jeq", 0, 0, "out")
+    a.ldx(8, 1, 0, 0).add64(1, "r6").stx(8, 0, 0, "r1")
+    a.label("out").mov64(0, 2).exit()
+    code = a.assemble()
+    n = 30000
+    units = gen.xdp_packets(n, stride=64, seed=32)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    ovm.run_raw(units.copy(), 64)
+    vm = dev.VM()
+    vm.load(code)
+    assert vm.info()["fused_rmw"] == 1
+    d = dev.DeviceBuffer.from_array(units)
+    assert vm.exec_batch(dev.CTX_RAW, d, n, 64, fixed_len=64) == 0
+    for k in range(64):
+        assert dm.lookup(struct.pack("<I", k)) == om.lookup(struct.pack("<I", k)), k

@@ -24,12 +24,18 @@ HOT = "k_interp"
 
 
 def pmc_means(path):
-    """{kernel: {counter: mean per dispatch}} over dispatches of each kernel."""
+    """{kernel: {counter: mean per dispatch}} over the dispatches of each
+    kernel with its largest grid (the timed batch, not warm-up or e2e chunks)."""
     per = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))
     if not os.path.exists(path):
         return {}
     with open(path) as f:
-        for row in csv.DictReader(f):
+        rows = list(csv.DictReader(f))
+    big = defaultdict(int)
+    for row in rows:
+        big[row["Kernel_Name"]] = max(big[row["Kernel_Name"]], int(row["Grid_Size"]))
+    for row in rows:
+        if int(row["Grid_Size"]) == big[row["Kernel_Name"]]:
             per[row["Kernel_Name"]][row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
     return {k: {c: statistics.mean(d.values()) for c, d in cs.items()} for k, cs in per.items()}
 
