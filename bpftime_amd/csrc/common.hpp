@@ -90,6 +90,7 @@ struct FInsn;
 struct KParams {
   const DInsn *prog;
   const FInsn *fast;      // threaded-code form for the asm fast path
+  uint32_t fast_div;      // lane groups (divergence) may be scheduled in asm
   const DMap *maps;
   uint8_t *data;          // base of unit slots (device)
   const uint32_t *lens;   // per-unit lengths or nullptr

@@ -53,6 +53,8 @@ budget (v40..v101 -> v66..v127):
   s[76:77] DMap data pointer                     s[78:79] PROG (FInsn base)
   s[80:81] S (staged bytes, 64-bit)              s[82:83] O (uniform window offset)
   s84 dirty 16-B chunk mask                      s85 scratch
+  s86/s87, s[88:89]/s[90:91], s92  pending lane groups (divergence): FInsn
+               address bits 31:0, lane masks, count
   v40 lane's R[0] LDS address  v41, v[42:43] scratch
   v[44:45] X  v[46:47] Y  v[48:49] Z (address)  v[50:51] E (address end)
   v[52:53] slot address (staging base)           v[54:55] O (per-lane offset)
@@ -63,7 +65,9 @@ output addresses) and the per-wave counter cache are asm operands, so they
 stay in the registers the compiler already holds them in.
 
 Exit reasons (s68 -> why): 0 run the instruction at pc in C++, 1 step limit
-crossed at a taken jump, 2 every live lane executed exit (r0 stored).
+crossed at a taken jump, 2 every live lane executed exit (r0 stored), 3 the
+wave is split into lane groups: lpc holds each lane's pc for the C++
+divergent loop.  aliveout = the lanes that have not exited.
 """
 import os
 import re
@@ -198,14 +202,28 @@ class Gen:
                "s_andn2_b64 s[54:55], exec, s[54:55]",
                f"s_cbranch_scc1 {L('slow')}")
 
-    def flush(self):
-        """Write dirty staged chunks back to the slots (exec = live lanes)."""
+    def flush(self, clear=True):
+        """Write dirty staged chunks back to the slots of the exec lanes."""
         for c in range(4):
             skip = self.label("fl")
             self.e(f"s_bitcmp1_b32 s84, {c}", f"s_cbranch_scc0 {skip}",
                    f"global_store_dwordx4 v[52:53], v[{STG + 4 * c}:{STG + 4 * c + 3}], off offset:{16 * c}",
                    f"{skip}:")
-        self.e("s_mov_b32 s84, 0")
+        if clear:
+            self.e("s_mov_b32 s84, 0")
+
+    def union_exec(self):
+        """exec |= the masks of the pending lane groups (divergence)."""
+        self.e("s_cmp_ge_u32 s92, 1", "s_cselect_b64 s[56:57], s[88:89], 0", "s_or_b64 exec, exec, s[56:57]",
+               "s_cmp_ge_u32 s92, 2", "s_cselect_b64 s[56:57], s[90:91], 0", "s_or_b64 exec, exec, s[56:57]")
+
+    def flush_all(self):
+        """Write back the dirty chunks of every live lane, pending groups
+        included (staging is about to end for the whole wave)."""
+        self.e("s_mov_b64 s[60:61], exec")
+        self.union_exec()
+        self.flush()
+        self.e("s_mov_b64 exec, s[60:61]")
 
     def staged_or(self, sz, on_staged, on_global):
         """Z is the access address.  If staging is on and every live lane
@@ -232,7 +250,7 @@ class Gen:
                "s_or_b64 s[54:55], s[54:55], s[56:57]",
                "s_and_b64 s[54:55], s[54:55], exec",
                "s_cmp_eq_u64 s[54:55], 0", f"s_cbranch_scc1 {on_global}")
-        self.flush()
+        self.flush_all()
         self.e("s_waitcnt vmcnt(0)", "s_mov_b64 s[80:81], 0", f"s_branch {on_global}")
 
     def staged_load(self, sz):
@@ -374,7 +392,7 @@ class Gen:
         self.next_seq()
         # a staged store straddling dwords: write back, end staging, store to memory
         self.e(f"{unal}:")
-        self.flush()
+        self.flush_all()
         self.e("s_waitcnt vmcnt(0)", "s_mov_b64 s[80:81], 0")
         self.e(f"{glb}:")
         self.check(sz)
@@ -464,7 +482,7 @@ class Gen:
         # v_cmp writes 0 for inactive lanes: none taken / all taken / split
         nt = self.label("nt")
         self.e("s_cmp_eq_u64 s[54:55], 0", f"s_cbranch_scc1 {nt}",
-               "s_cmp_eq_u64 s[54:55], exec", f"s_cbranch_scc0 {L('slow')}")
+               "s_cmp_eq_u64 s[54:55], exec", f"s_cbranch_scc0 {L('split')}")
         self.jump_taken()
         self.e(f"{nt}:")
         self.next_seq()
@@ -673,17 +691,124 @@ class Gen:
         self.next_seq()
 
     def exit_(self):
-        """Every live lane exits: write back the unit's dirty bytes, store r0
-        as verdict (u32) and ret (u64)."""
-        nv, nr = self.label("nv"), self.label("nr")
-        self.flush()
+        """The running lanes exit: write back their dirty bytes, store r0 as
+        verdict (u32) and ret (u64); then the next pending lane group runs,
+        or the block ends (every live lane has exited)."""
+        nv, nr, last = self.label("nv"), self.label("nr"), self.label("last")
+        self.flush(clear=False)
         self.e("s_bitcmp1_b32 %[oflags], 0", f"s_cbranch_scc0 {nv}",
                f"global_store_dword %[vaddr], v{R0}, off",
                f"{nv}:",
                "s_bitcmp1_b32 %[oflags], 1", f"s_cbranch_scc0 {nr}",
                f"global_store_dwordx2 %[raddr], v[{R0}:{R0 + 1}], off",
                f"{nr}:",
-               "s_mov_b32 s68, 2", f"s_branch {L('done')}")
+               "s_cmp_eq_u32 s92, 0", f"s_cbranch_scc1 {last}",
+               "s_mov_b32 s48, s86", "s_mov_b64 exec, s[88:89]")
+        self.pop0()
+        self.dispatch()
+        self.e(f"{last}:", "s_mov_b32 s84, 0", "s_mov_b64 exec, 0", "s_mov_b32 s68, 2", f"s_branch {L('done')}")
+
+    # ---- divergence: min-pc scheduling of lane groups ----
+    # A split branch leaves the wave as the running group (IP, exec) plus up
+    # to two pending groups (s86/s87 = FInsn address bits 31:0, s[88:89] /
+    # s[90:91] = lane masks, s92 = count), sorted by address.  The running
+    # group always has the lowest pc; while any group is pending, dispatch
+    # goes through the divergent table, whose entries compare IP with the
+    # first pending pc: equal -> the groups merge (reconvergence), greater ->
+    # the running group is parked and the pending one runs.  A third pending
+    # group, or any instruction the asm does not run, hands every group's pc
+    # to the C++ divergent loop (exit reason 3).
+    def set_table(self, divergent):
+        n4 = 4 * len(handler_ids())
+        if divergent:
+            self.e(f"s_add_u32 s50, s50, {n4}", "s_addc_u32 s51, s51, 0")
+        else:
+            self.e(f"s_sub_u32 s50, s50, {n4}", "s_subb_u32 s51, s51, 0")
+
+    def pop0(self):
+        keep = self.label("keep")
+        self.e("s_mov_b32 s86, s87", "s_mov_b64 s[88:89], s[90:91]", "s_mov_b32 s87, -1",
+               "s_sub_u32 s92, s92, 1", "s_cmp_eq_u32 s92, 0", f"s_cbranch_scc0 {keep}")
+        self.set_table(False)
+        self.e(f"{keep}:")
+
+    def push(self):
+        """Park group (s69 = FInsn address bits 31:0, s[62:63] = lanes)."""
+        nonempty, ne0, after0, two, done = (self.label(x) for x in ("pne", "pn0", "pa0", "p2", "pd"))
+        self.e("s_cmp_eq_u32 s92, 0", f"s_cbranch_scc0 {nonempty}",
+               "s_mov_b32 s86, s69", "s_mov_b64 s[88:89], s[62:63]", "s_mov_b32 s92, 1")
+        self.set_table(True)
+        self.e(f"s_branch {done}",
+               f"{nonempty}:",
+               "s_cmp_eq_u32 s69, s86", f"s_cbranch_scc0 {ne0}",
+               "s_or_b64 s[88:89], s[88:89], s[62:63]", f"s_branch {done}",
+               f"{ne0}:",
+               "s_cmp_eq_u32 s92, 1", f"s_cbranch_scc0 {two}",
+               "s_cmp_lt_u32 s69, s86", f"s_cbranch_scc0 {after0}",
+               "s_mov_b32 s87, s86", "s_mov_b64 s[90:91], s[88:89]",
+               "s_mov_b32 s86, s69", "s_mov_b64 s[88:89], s[62:63]", "s_mov_b32 s92, 2", f"s_branch {done}",
+               f"{after0}:",
+               "s_mov_b32 s87, s69", "s_mov_b64 s[90:91], s[62:63]", "s_mov_b32 s92, 2", f"s_branch {done}",
+               f"{two}:",
+               "s_cmp_eq_u32 s69, s87", f"s_cbranch_scc0 {L('overflow')}",
+               "s_or_b64 s[90:91], s[90:91], s[62:63]",
+               f"{done}:")
+
+    def materialize(self, extra):
+        """Every group's pc (FInsn index) into the lpc output of its lanes,
+        exec = all of them; exit reason 3."""
+        self.e("s_sub_u32 s52, s48, s78", "s_lshr_b32 s52, s52, 5", "v_mov_b32 %[lpc], s52",
+               "s_mov_b64 s[60:61], exec")
+        if extra:
+            self.e("s_mov_b64 exec, s[62:63]", "s_sub_u32 s52, s69, s78", "s_lshr_b32 s52, s52, 5",
+                   "v_mov_b32 %[lpc], s52", "s_or_b64 s[60:61], s[60:61], exec")
+        for i, (pc, m) in enumerate((("s86", "s[88:89]"), ("s87", "s[90:91]"))):
+            skip = self.label("mz")
+            self.e(f"s_cmp_ge_u32 s92, {i + 1}", f"s_cbranch_scc0 {skip}",
+                   f"s_mov_b64 exec, {m}", f"s_sub_u32 s52, {pc}, s78", "s_lshr_b32 s52, s52, 5",
+                   "v_mov_b32 %[lpc], s52", "s_or_b64 s[60:61], s[60:61], exec", f"{skip}:")
+        self.e("s_mov_b64 exec, s[60:61]", "s_mov_b32 s68, 3", f"s_branch {L('spill')}")
+
+    def divergence_routines(self):
+        n4 = 4 * len(handler_ids())
+        back, spush, ahead = self.label("sback"), self.label("spush"), self.label("dahead")
+        # split branch: s[54:55] = taken lanes, W = the branch
+        self.e(f"{L('split')}:",
+               "s_bitcmp1_b32 %[entry], 2", f"s_cbranch_scc0 {L('slow')}",
+               "s_andn2_b64 s[56:57], exec, s[54:55]",
+               "s_add_u32 s52, s78, s45",
+               "s_add_u32 s48, s48, 32", "s_addc_u32 s49, s49, 0",
+               "s_cmp_lt_u32 s52, s48", f"s_cbranch_scc1 {back}",
+               # forward: not-taken lanes run on, taken lanes wait at the target
+               "s_mov_b32 s69, s52", "s_mov_b64 s[62:63], s[54:55]", "s_mov_b64 exec, s[56:57]",
+               f"s_branch {spush}",
+               # backward (loop): taken lanes run on, the others wait after the branch
+               f"{back}:",
+               "s_mov_b32 s69, s48", "s_mov_b64 s[62:63], s[56:57]", "s_mov_b64 exec, s[54:55]",
+               "s_mov_b32 s48, s52",
+               "s_cmp_gt_u32 %[steps], %[limit]", f"s_cbranch_scc1 {L('steps')}",
+               f"{spush}:")
+        self.push()
+        self.dispatch()
+        # divergent dispatch check (s[52:53] = divergent table entry)
+        self.e(f"{L('dcheck')}:",
+               "s_cmp_ge_u32 s48, s86", f"s_cbranch_scc1 {L('dswitch')}",
+               f"s_sub_u32 s52, s52, {n4}", "s_subb_u32 s53, s53, 0",
+               "s_setpc_b64 s[52:53]",
+               f"{L('dswitch')}:",
+               "s_sub_u32 %[steps], %[steps], 1",            # the fetched insn did not run
+               "s_cmp_eq_u32 s48, s86", f"s_cbranch_scc0 {ahead}",
+               "s_or_b64 exec, exec, s[88:89]")                # reconvergence
+        self.pop0()
+        self.dispatch()
+        self.e(f"{ahead}:",
+               "s_mov_b32 s69, s48", "s_mov_b64 s[62:63], exec",
+               "s_mov_b32 s48, s86", "s_mov_b64 exec, s[88:89]")
+        self.pop0()
+        self.push()
+        self.dispatch()
+        self.e(f"{L('overflow')}:")
+        self.materialize(extra=True)
 
     def build(self):
         ids = handler_ids()
@@ -694,7 +819,8 @@ class Gen:
           "v_mov_b32 v40, %[rb]",
           "s_lshl_b32 s52, %[pc], 5", "s_add_u32 s48, s78, s52", "s_addc_u32 s49, s79, 0",
           "s_mov_b64 s[58:59], exec", "s_mov_b64 exec, %[alive]",
-          "s_mov_b32 s80, 0", "s_mov_b32 s81, 0", "s_mov_b32 s84, 0",
+          "s_mov_b32 s80, 0", "s_mov_b32 s81, 0", "s_mov_b32 s84, 0", "s_mov_b32 s92, 0",
+          "s_mov_b32 s86, -1", "s_mov_b32 s87, -1",
           "v_mov_b32 v52, %[slotlo]", "v_mov_b32 v53, %[slothi]",
           "s_bitcmp1_b32 %[entry], 0", f"s_cbranch_scc1 {fresh}")
         # re-entry: registers from the C++ side's LDS copy, no staging
@@ -721,6 +847,8 @@ class Gen:
           f"s_branch {L('start')}")
         for name in ids:                   # table: entry i at TB + 4 + 4*i
             e(f"s_branch {L('h_' + name)}")
+        for name in ids:                   # divergent table: TB + 4N + 4 + 4*i
+            e(f"s_branch {L('dcheck')}")
         e(f"{L('start')}:")
         self.dispatch()
         # ---- handlers ----
@@ -773,16 +901,22 @@ class Gen:
                 self.jcc(w, cc, k)
             else:
                 raise ValueError(name)
+        self.divergence_routines()
         # ---- exits: the instruction at pc was not executed (one step was
         # counted at its dispatch); write back staging, spill registers
-        e(f"{L('steps')}:", "s_mov_b32 s68, 1", f"s_branch {L('spill')}")
-        e(f"{L('slow')}:", "s_mov_b32 s68, 0", "s_sub_u32 %[steps], %[steps], 1")
+        e(f"{L('steps')}:", "s_mov_b32 s68, 1")
+        self.union_exec()
+        e(f"s_branch {L('spill')}")
+        e(f"{L('slow')}:", "s_mov_b32 s68, 0", "s_sub_u32 %[steps], %[steps], 1",
+          "s_cmp_eq_u32 s92, 0", f"s_cbranch_scc1 {L('spill')}")
+        self.materialize(extra=False)
         e(f"{L('spill')}:")
         self.flush()
         for r in range(NREG):
             e(f"ds_write_b64 v40, v[{R0 + 2 * r}:{R0 + 2 * r + 1}] offset:{r * 2048}")
         e(f"{L('done')}:",
           "s_waitcnt vmcnt(0) lgkmcnt(0)",
+          "s_mov_b64 %[aliveout], exec",
           "s_mov_b64 exec, s[58:59]",
           "s_sub_u32 s52, s48, s78", "s_lshr_b32 s52, s52, 5",
           "s_mov_b32 %[pc], s52", "s_mov_b32 %[why], s68")
@@ -809,7 +943,7 @@ def main():
     g.out = [relocate(x) for x in g.out]
     # v126/v127 (v100/v101 before relocation) are read, never written, by
     # staged loads near the window end
-    clob = [f"s{i}" for i in range(40, 86)] + [f"v{vmap(i)}" for i in range(40, 102)]
+    clob = [f"s{i}" for i in range(40, 93)] + [f"v{vmap(i)}" for i in range(40, 102)]
     with open(os.path.join(HERE, "fast_asm.inc"), "w") as f:
         f.write("// Generated by gen_fast.py; do not edit.\n")
         f.write("#define BPFTIME_AMD_FAST_ASM \\\n")

@@ -396,7 +396,7 @@ struct FastEnv {
   uint32_t rb;      // LDS byte address of this lane's R[0]
 };
 
-constexpr uint32_t FAST_SLOW = 0, FAST_STEPS = 1, FAST_EXIT = 2;
+constexpr uint32_t FAST_SLOW = 0, FAST_STEPS = 1, FAST_EXIT = 2, FAST_SPLIT = 3;
 
 // Per-unit inputs of a fresh entry (gen_fast.py: registers from operands,
 // optional staging of the slot's first kFastStageBytes bytes).
@@ -404,13 +404,15 @@ struct FastUnit {
   uint64_t r1, r10, slot;
   uint32_t r2;
   uint32_t len;    // unit length (ctx->data_end - ctx->data)
-  uint32_t entry;  // bit 0: fresh unit, bit 1: stage the slot
+  uint32_t entry;  // bit 0: fresh unit, bit 1: stage the slot, bit 2: lane groups in asm
 };
 
 __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const FastUnit &u) {
   // every "s" operand must be provably uniform: readfirstlane what the
   // compiler cannot prove (the values are uniform by construction)
   uint32_t pc = __builtin_amdgcn_readfirstlane(c.pc), steps = __builtin_amdgcn_readfirstlane(c.steps), why;
+  uint64_t alive_out;
+  uint32_t lpc;
   const uint64_t alive = __ballot(c.alive);
   const uint32_t limit = __builtin_amdgcn_readfirstlane(c.step_limit);
   const uint32_t entry = __builtin_amdgcn_readfirstlane(u.entry);
@@ -420,7 +422,8 @@ __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const Fas
   const uint64_t vaddr = c.verdicts ? (uint64_t)(uintptr_t)(c.verdicts + c.unit) : 0;
   const uint64_t raddr = c.rets ? (uint64_t)(uintptr_t)(c.rets + c.unit) : 0;
   asm volatile(BPFTIME_AMD_FAST_ASM
-               : [pc] "+s"(pc), [steps] "+s"(steps), [why] "=s"(why), [c0a] "+s"(c0a), [c1a] "+s"(c1a),
+               : [pc] "+s"(pc), [steps] "+s"(steps), [why] "=s"(why), [aliveout] "=s"(alive_out),
+                 [lpc] "=v"(lpc), [c0a] "+s"(c0a), [c1a] "+s"(c1a),
                  [c0dl] "+s"(c0dl), [c0dh] "+s"(c0dh), [c1dl] "+s"(c1dl), [c1dh] "+s"(c1dh), [c0s] "+s"(c0s),
                  [c1s] "+s"(c1s)
                : [prog] "s"(f.fast), [maps] "s"(f.maps), [dlo] "s"(f.dlo), [dhi] "s"(f.dhi), [alo] "s"(f.alo),
@@ -439,6 +442,9 @@ __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const Fas
   c.c1d = (uint64_t)c1dl | ((uint64_t)c1dh << 32);
   c.c0s = c0s;
   c.c1s = c1s;
+  // lanes that ran exit inside the block are done (verdict stored)
+  c.alive = c.alive && ((alive_out >> __lane_id()) & 1);
+  if (why == FAST_SPLIT) c.lpc = lpc;
   return why;
 }
 
@@ -453,7 +459,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   SRP(prog); SRP(fast); SRP(maps); SRP(data); SRP(lens); SRP(verdicts); SRP(rets); SRP(out_data_off); SRP(out_len);
   SRP(err_count); SRV(n); SRV(stride); SRV(first_unit); SRV(data_lo); SRV(data_hi); SRV(arena_lo);
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
-  SRV(checked); SRV(head); SRV(ordered);
+  SRV(checked); SRV(head); SRV(ordered); SRV(fast_div);
 #undef SRP
 #undef SRV
   __shared__ uint64_t Rf[12 * kBlock];  // r0..r10 + a dummy slot per lane
@@ -516,7 +522,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     fu.slot = slot;
     fu.r10 = stack_top;
     fu.len = len;
-    fu.entry = 1u | (stage_ok ? 2u : 0u);
+    fu.entry = 1u | (stage_ok ? 2u : 0u) | (p.fast_div ? 4u : 0u);
     if (KIND == CTX_XDP) {
       XdpCtx *x = (XdpCtx *)my_ctx;
       x->data = slot + p.head;
@@ -552,10 +558,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       uint32_t r;
       if (uni) {
         const uint32_t why = run_fast(c, fe, fu);
-        fu.entry = 0;
+        fu.entry &= 4u;
         if (why == FAST_EXIT) {  // every live lane ran exit; r0 already stored
           c.alive = false;
           break;
+        }
+        if (why == FAST_SPLIT) {  // lane groups at different pcs: C++ divergent loop
+          uni = false;
+          continue;
         }
         if (why == FAST_STEPS) {
           c.err = c.alive ? E_STEPS : c.err;

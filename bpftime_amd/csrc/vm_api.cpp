@@ -151,6 +151,13 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   KParams p{};
   p.prog = d_prog;
   p.fast = d_fast + (b->ctx_kind == CTX_XDP ? 0 : prog.prog.size());
+  {
+    // the asm keeps pending lane groups by FInsn address bits 31:0: only
+    // when the array does not straddle a 4 GiB boundary
+    const uint64_t lo = (uint64_t)(uintptr_t)p.fast, hi = lo + prog.prog.size() * sizeof(FInsn);
+    p.fast_div = (lo >> 32) == ((hi - 1) >> 32) ? 1 : 0;
+    if (getenv("BPFTIME_AMD_NO_ASM_DIVERGENCE")) p.fast_div = 0;
+  }
   p.maps = r.d_maptab;
   p.data = (uint8_t *)b->data;
   p.lens = b->lens;

@@ -239,7 +239,12 @@ def _random_program(rng, nins=60):
     return a.assemble()
 
 
-def test_random_programs(fresh_oracle, fresh_runtime):
+@pytest.mark.parametrize("asm_groups", [True, False])
+def test_random_programs(fresh_oracle, fresh_runtime, monkeypatch, asm_groups):
+    """Random forward-branch programs: lane groups scheduled inside the asm
+    fast path, and (BPFTIME_AMD_NO_ASM_DIVERGENCE) by the C++ loop alone."""
+    if not asm_groups:
+        monkeypatch.setenv("BPFTIME_AMD_NO_ASM_DIVERGENCE", "1")
     po, dev = fresh_oracle, fresh_runtime
     rng = np.random.default_rng(1234)
     units = _operands(2048, 77).view(np.uint8).reshape(2048, 16)
