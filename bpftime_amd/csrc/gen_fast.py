@@ -202,6 +202,45 @@ class Gen:
                "s_andn2_b64 s[54:55], exec, s[54:55]",
                f"s_cbranch_scc1 {L('slow')}")
 
+    def comb_add(self, sz):
+        """Per-lane add of Y (v46, v[46:47] for 8 B) at the global address Z
+        through the workgroup's LDS combining table (interp.hip: %[combn]
+        entries of {tag = address | size bit, delta}, flushed by the block at
+        its end): Zipf-hot counters cost an LDS add instead of a same-address
+        device atomic per lane (those serialize at the memory side).  Entry =
+        a multiplicative hash of the address, second try in the neighbour;
+        lanes finding both taken by other addresses, and misaligned
+        addresses, add to memory directly."""
+        done, direct = self.label("cd"), self.label("cx")
+        self.e("s_mov_b64 s[60:61], exec", "s_mov_b64 s[54:55], 0",
+               "s_cmp_eq_u32 %[combn], 0", f"s_cbranch_scc1 {direct}",
+               f"v_and_b32 v41, {sz - 1}, v48", "v_cmp_eq_u32 vcc, 0, v41",            # aligned lanes
+               "s_and_b64 exec, exec, vcc", f"s_cbranch_execz {direct}",
+               "v_mov_b32 v54, v48", "v_mov_b32 v55, v49")
+        if sz == 4:
+            self.e("v_or_b32 v54, 1, v54", "v_mov_b32 v47, 0")
+        self.e("v_lshrrev_b32 v41, 3, v48", "s_mov_b32 s69, 0x9e3779b1", "v_mul_lo_u32 v41, v41, s69",
+               "v_lshrrev_b32 v41, 24, v41", "v_lshlrev_b32 v41, 4, v41", "v_add_u32 v41, %[comb], v41",
+               "v_mov_b32 v42, 0", "v_mov_b32 v43, 0")
+        for attempt in range(2):
+            if attempt:
+                self.e("v_xor_b32 v41, 16, v41")              # the neighbouring entry
+            self.e("ds_cmpst_rtn_b64 v[50:51], v41, v[42:43], v[54:55]",      # claim if empty
+                   "s_waitcnt lgkmcnt(0)",
+                   "v_cmp_eq_u64 s[56:57], 0, v[50:51]",
+                   "v_cmp_eq_u64 vcc, v[54:55], v[50:51]",
+                   "s_or_b64 s[56:57], s[56:57], vcc",                        # entry is ours
+                   "s_or_b64 s[54:55], s[54:55], s[56:57]",
+                   "s_mov_b64 s[62:63], exec",
+                   "s_and_b64 exec, exec, s[56:57]")
+            skip = self.label("cs")
+            self.e(f"s_cbranch_execz {skip}", "ds_add_u64 v41, v[46:47] offset:8", f"{skip}:",
+                   "s_andn2_b64 exec, s[62:63], s[56:57]", f"s_cbranch_execz {direct}")
+        self.e(f"{direct}:",
+               "s_andn2_b64 exec, s[60:61], s[54:55]", f"s_cbranch_execz {done}")
+        self.e("global_atomic_add_x2 v[48:49], v[46:47], off" if sz == 8 else "global_atomic_add v[48:49], v46, off",
+               f"{done}:", "s_mov_b64 exec, s[60:61]")
+
     def flush(self, clear=True):
         """Write dirty staged chunks back to the slots of the exec lanes."""
         for c in range(4):
@@ -662,8 +701,8 @@ class Gen:
                # lanes disagree on address or value: one atomic add per lane
                f"{lane}:")
         self.check_global(sz)
-        self.e("global_atomic_add_x2 v[48:49], v[46:47], off" if sz == 8 else "global_atomic_add v[48:49], v46, off",
-               f"{done}:",
+        self.comb_add(sz)
+        self.e(f"{done}:",
                "s_add_u32 s48, s78, s45", "s_addc_u32 s49, s79, 0")           # continue after the stx
         self.dispatch()
 
@@ -686,6 +725,9 @@ class Gen:
             if sz == 4:
                 self.e("v_mov_b32 v47, 0")
             self.wr("s44", 46)
+        elif op == "ADD":
+            self.e("v_mov_b32 v46, v44", "v_mov_b32 v47, v45")
+            self.comb_add(sz)
         else:
             self.e(f"global_atomic_{mn} v[48:49], {val}, off")
         self.next_seq()

@@ -393,6 +393,8 @@ struct FastEnv {
   uint32_t shi, phi;
   uint32_t oflags;  // bit 0: verdicts, bit 1: rets
   uint32_t head;    // batch head: ctx->data = slot + head
+  uint32_t comb;    // LDS address of the block's combining table
+  uint32_t combn;   // its entries (0: add straight to memory)
   uint32_t rb;      // LDS byte address of this lane's R[0]
 };
 
@@ -432,7 +434,7 @@ __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const Fas
                  [entry] "s"(entry), [r1lo] "v"((uint32_t)u.r1), [r1hi] "v"((uint32_t)(u.r1 >> 32)),
                  [r2lo] "v"(u.r2), [r10lo] "v"((uint32_t)u.r10), [r10hi] "v"((uint32_t)(u.r10 >> 32)),
                  [slotlo] "v"((uint32_t)u.slot), [slothi] "v"((uint32_t)(u.slot >> 32)),
-                 [head] "s"(f.head), [ulen] "v"(u.len), [stklo] "v"((uint32_t)u.r10)
+                 [head] "s"(f.head), [ulen] "v"(u.len), [stklo] "v"((uint32_t)u.r10), [comb] "s"(f.comb), [combn] "s"(f.combn)
                : BPFTIME_AMD_FAST_CLOBBERS);
   c.pc = pc;
   c.steps = steps;
@@ -459,7 +461,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   SRP(prog); SRP(fast); SRP(maps); SRP(data); SRP(lens); SRP(verdicts); SRP(rets); SRP(out_data_off); SRP(out_len);
   SRP(err_count); SRV(n); SRV(stride); SRV(first_unit); SRV(data_lo); SRV(data_hi); SRV(arena_lo);
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
-  SRV(checked); SRV(head); SRV(ordered); SRV(fast_div);
+  SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries);
 #undef SRP
 #undef SRV
   __shared__ uint64_t Rf[12 * kBlock];  // r0..r10 + a dummy slot per lane
@@ -468,6 +470,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   const uint32_t tid = threadIdx.x;
   uint8_t *my_ctx = dyn + tid * CTXB;
   uint8_t *my_stack = dyn + kBlock * CTXB + tid * p.stack_size;
+  // combining table for per-lane counter adds (gen_fast.py comb_add), after
+  // the ctx and stack areas: {tag = address | (4-byte ? 1 : 0), delta},
+  // flushed when the block ends; sized 0 for programs that never need it
+  uint64_t *comb = (uint64_t *)(dyn + kBlock * (CTXB + (BIGSTACK ? 0 : p.stack_size)));
+  for (uint32_t i = tid; i < 2 * p.comb_entries; i += kBlock) comb[i] = 0;
+  __syncthreads();
   uint64_t big_stack[BIGSTACK ? kStackSize / 8 : 1];
   const uint64_t stack_top = BIGSTACK ? (uint64_t)(uintptr_t)(big_stack + kStackSize / 8)
                                       : (uint64_t)(uintptr_t)(my_stack + p.stack_size);
@@ -487,6 +495,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   FastEnv fe;
   fe.fast = (const FInsn *)sreg((uint64_t)(uintptr_t)p.fast);
   fe.maps = p.maps;
+  fe.comb = sreg((uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)comb));
+  fe.combn = p.comb_entries;
   fe.head = p.head;
   fe.oflags = sreg((uint32_t)__builtin_amdgcn_readfirstlane((p.verdicts ? 1u : 0u) | (p.rets ? 2u : 0u)));
   fe.dlo = sreg((uint64_t)(p.checked ? p.data_lo : 0));
@@ -634,20 +644,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   }
   flush_delta(c.c0a, c.c0s, c.c0d);
   flush_delta(c.c1a, c.c1s, c.c1d);
+  __syncthreads();
+  for (uint32_t e = tid; e < p.comb_entries; e += kBlock) {
+    const uint64_t tag = comb[2 * e], delta = comb[2 * e + 1];
+    if (tag & 1)
+      __hip_atomic_fetch_add((uint32_t *)(uintptr_t)(tag & ~1ull), (uint32_t)delta, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    else if (tag)
+      __hip_atomic_fetch_add((uint64_t *)(uintptr_t)tag, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // ---------------------------------------------------------------------------
 // Host-side launch wrappers
 // ---------------------------------------------------------------------------
-static size_t dyn_lds_bytes(uint32_t kind, bool big_stack, uint32_t stack_size) {
-  return kBlock * ((kind == CTX_XDP ? 48 : 0) + (big_stack ? 0 : stack_size));
+static size_t dyn_lds_bytes(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries) {
+  return kBlock * ((kind == CTX_XDP ? 48 : 0) + (big_stack ? 0 : stack_size)) + 16 * (size_t)comb_entries;
 }
 
 extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind, bool big_stack, uint32_t grid,
                                                 uint32_t ordered, hipStream_t stream) {
   KParams q = *p;
   q.ordered = ordered;
-  const size_t dyn = dyn_lds_bytes(kind, big_stack, p->stack_size);
+  const size_t dyn = dyn_lds_bytes(kind, big_stack, p->stack_size, p->comb_entries);
   dim3 g(grid), b(kBlock);
 #define L(K, B) hipLaunchKernelGGL((k_interp<K, B>), g, b, dyn, stream, q)
   if (kind == CTX_XDP) {

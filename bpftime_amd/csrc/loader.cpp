@@ -696,7 +696,9 @@ static uint32_t fast_id(const DInsn &d) {
 // bytes come from the staged VGPRs, ctx fields are computed from the unit's
 // slot / length, stack bytes are plain LDS accesses.
 // ---------------------------------------------------------------------------
-enum PKind : uint8_t { P_UNDEF = 0, P_CTX, P_PKT, P_SLOT, P_STK, P_OTHER };
+// P_CONST: a wave-uniform constant (lddw immediates and map-value
+// addresses, plus constant offsets): counters behind it need no combining.
+enum PKind : uint8_t { P_UNDEF = 0, P_CTX, P_PKT, P_SLOT, P_STK, P_CONST, P_OTHER };
 struct PVal {
   uint8_t kind;
   int32_t k;
@@ -722,7 +724,7 @@ static bool pointer_kinds(const std::vector<DInsn> &p, bool xdp, bool pkt_ok,
   work.push_back(0);
   queued[0] = true;
   bool ctx_written = false;
-  auto ptr = [](uint8_t k) { return k == P_CTX || k == P_PKT || k == P_SLOT || k == P_STK; };
+  auto ptr = [](uint8_t k) { return k == P_CTX || k == P_PKT || k == P_SLOT || k == P_STK || k == P_CONST; };
   while (!work.empty()) {
     const uint32_t i = work.back();
     work.pop_back();
@@ -768,6 +770,9 @@ static bool pointer_kinds(const std::vector<DInsn> &p, bool xdp, bool pkt_ok,
       case X_CALL:
         st[0] = PVal{P_OTHER, 0};  // r1-r5 survive (ubpf)
         break;
+      case X_LDDW:
+        st[d.dst] = PVal{P_CONST, 0};
+        break;
       case X_EXIT: case X_JA: case X_JEQ: case X_JGT: case X_JGE: case X_JSET: case X_JNE:
       case X_JSGT: case X_JSGE: case X_JLT: case X_JLE: case X_JSLT: case X_JSLE:
         break;
@@ -802,7 +807,8 @@ static bool pointer_kinds(const std::vector<DInsn> &p, bool xdp, bool pkt_ok,
 }
 
 void build_fast(const std::vector<DInsn> &prog, bool xdp, bool big_stack, uint32_t stack_size,
-                std::vector<FInsn> &fast, uint32_t *specialized) {
+                std::vector<FInsn> &fast, uint32_t *specialized, bool *needs_comb) {
+  if (needs_comb) *needs_comb = true;
   fast.assign(prog.size(), FInsn{});
   for (size_t i = 0; i < prog.size(); i++) {
     const DInsn &d = prog[i];
@@ -821,6 +827,15 @@ void build_fast(const std::vector<DInsn> &prog, bool xdp, bool big_stack, uint32
     if (d.op == X_CALL && (d.hi == 44 || d.hi == 65)) pkt_ok = false;
   std::vector<std::vector<PVal>> in;
   if (!pointer_kinds(prog, xdp, pkt_ok, in)) return;  // ctx rewritten: generic handlers only
+  // per-lane counter adds (fused counters, atomic adds without fetch) whose
+  // target is not a wave-uniform constant use the LDS combining table
+  bool comb = false;
+  for (size_t i = 0; i < prog.size(); i++) {
+    const DInsn &d = prog[i];
+    const bool add = d.op == X_RMW_ADD || (d.op == X_ATOMIC && d.hi == 0x00);
+    if (add && in[i][d.dst].kind != P_CONST && in[i][d.dst].kind != P_UNDEF) comb = true;
+  }
+  if (needs_comb) *needs_comb = comb;
   uint32_t nspec = 0;
   for (size_t i = 0; i < prog.size(); i++) {
     const DInsn &d = prog[i];

@@ -33,6 +33,7 @@ struct LoadOut {
   uint32_t stack_size = 8;   // per-lane bytes (LDS)
   bool big_stack = false;    // 512-B scratch stack
   uint32_t fused_rmw = 0;
+  uint32_t comb_entries = 0;  // per-block LDS combining entries (0 = none needed)
 };
 
 // Helper ids the device implements (interp.hip helper switch).
@@ -44,7 +45,7 @@ bool device_helper_supported(uint32_t id);
 // loads/stores whose base pointer kind is known statically get
 // specialized handlers (count in *specialized).
 void build_fast(const std::vector<DInsn> &prog, bool xdp, bool big_stack, uint32_t stack_size,
-                std::vector<FInsn> &fast, uint32_t *specialized);
+                std::vector<FInsn> &fast, uint32_t *specialized, bool *needs_comb);
 
 // Runs the compat_ubpf.cpp:61-200 patching (call remap check, lddw pseudo
 // sources), ubpf-style validation, pre-decoding and the dataflow analyses

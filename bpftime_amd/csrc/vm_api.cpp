@@ -111,8 +111,10 @@ class Mi355xVm {
     // two threaded-code forms: XDP entry (r1 = ctx) and raw/syscall entry
     // (r1 = the unit's slot) differ in the loader's pointer kinds
     std::vector<FInsn> fraw;
-    build_fast(out.prog, true, out.big_stack, out.stack_size, out.fast, &spec_xdp);
-    build_fast(out.prog, false, out.big_stack, out.stack_size, fraw, &spec_raw);
+    bool comb_x = true, comb_r = true;
+    build_fast(out.prog, true, out.big_stack, out.stack_size, out.fast, &spec_xdp, &comb_x);
+    build_fast(out.prog, false, out.big_stack, out.stack_size, fraw, &spec_raw, &comb_r);
+    out.comb_entries = (comb_x || comb_r) ? kComb : 0;
     out.fast.insert(out.fast.end(), fraw.begin(), fraw.end());
     size_t bytes = out.prog.size() * sizeof(DInsn);
     size_t fbytes = out.fast.size() * sizeof(FInsn);
@@ -177,6 +179,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   p.step_limit = step_limit;
   p.fixed_len = b->fixed_len;
   p.stack_size = prog.stack_size;
+  p.comb_entries = prog.comb_entries;
   p.ncpu = r.ncpu;
   p.ifindex = b->ingress_ifindex;
   p.rxq = b->rx_queue_index;
@@ -197,7 +200,8 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       hipGetDeviceProperties(&prop, dev);
       cus = prop.multiProcessorCount;
     }
-    const size_t dyn = kBlock * ((b->ctx_kind == CTX_XDP ? 48 : 0) + (prog.big_stack ? 0 : prog.stack_size));
+    const size_t dyn = kBlock * ((b->ctx_kind == CTX_XDP ? 48 : 0) + (prog.big_stack ? 0 : prog.stack_size)) +
+                       16 * (size_t)prog.comb_entries;
     int occ = bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn);
     if (occ < 1) occ = 1;
     uint64_t want = (b->count + kBlock - 1) / kBlock;
