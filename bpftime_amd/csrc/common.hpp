@@ -115,6 +115,8 @@ struct KParams {
   uint32_t checked;       // 1 = confine global accesses to the two windows
   uint32_t head;          // XDP: initial data offset inside each slot
   uint32_t ordered;       // 1 = a single lane runs the units in index order
+  uint32_t stage;         // bytes of each unit staged in VGPRs by the fast path (0 = none)
+  uint32_t needs_ctx;     // XDP: the program reads its ctx generically (build it in LDS)
 };
 
 // Error codes recorded per unit (err_count counts units with any error)

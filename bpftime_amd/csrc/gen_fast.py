@@ -7,54 +7,77 @@ inline-asm block.  Each eBPF instruction is pre-decoded by the loader into a
 32-byte FInsn whose first word is the byte offset of its handler's entry in
 a table of `s_branch` instructions; dispatch is
 
-    s_load_dwordx8 W, IP          ; fetch (scalar cache)
+    s_load_dwordx8 W, PROG, IP    ; fetch (scalar cache, IP = byte offset)
     s_add_u32/s_addc_u32 T, TB, W0
     s_setpc_b64 T                 ; -> table entry -> handler
 
 instead of a compare tree.  exec = the wave's live lanes inside the block, so
 compare results and stores need no per-lane predication.
 
+Cost model (MI355X_MICROARCH.md): a CU has ONE scalar unit shared by its four
+SIMD-32s, each of which retires a wave64 VALU instruction every 2 cycles, so
+at 16 waves per CU the SALU is the first pipe to saturate.  The handlers are
+written to minimise SALU instructions per eBPF instruction: one SALU to
+advance IP, two to form the handler address, no per-instruction step count
+(steps are counted at taken jumps, the only way to loop), and register
+operands read and written in place under GPR-index mode.
+
 Registers.  r0..r10 live in VGPRs v[60:81] (r_i = v[60+2i : 61+2i]) while the
 block runs; an instruction's register fields are VGPR indices used with
-`s_set_gpr_idx_on` (register numbers are wave-uniform).  The C++ side keeps
-its LDS copy (lane-major, 2 KiB per register): a fresh unit initialises the
-VGPRs from operands, a re-entry loads them from LDS, and every exit other
-than `exit` stores them back.
+`s_set_gpr_idx_on` (register numbers are wave-uniform).  Where the eBPF
+operation is `dst op= y` the VALU instruction itself runs in index mode
+(SRC0/SRC1 and DST indexed by dst*2), so the register is neither copied out
+nor back.  The C++ side keeps its LDS copy (lane-major, 2 KiB per register):
+a fresh unit initialises the VGPRs from operands, a re-entry loads them from
+LDS, and every exit other than `exit` stores them back.
 
-Unit staging.  On a fresh unit the first 64 bytes of the unit's slot are
-loaded into v[84:99] with four global_load_dwordx4.  A load or store whose
-offset from the slot is wave-uniform and inside the window is served from
-those VGPRs (dword index via s_set_gpr_idx_on, bytes via v_alignbit /
-v_bfi); stores mark 16-byte chunks dirty and dirty chunks are written back
-(global_store_dwordx4) before any exit and before any other access that
-overlaps the window (which also ends staging for the unit).  A packet's
-header reads and rewrites then cost two coalesced HBM transactions instead
-of a chain of dependent byte loads and stores.
+Unit staging.  On a fresh unit the first %[stage] bytes (16..64, sized per
+launch from the program's statically typed packet/slot accesses) of the
+unit's slot are loaded into v[84:99] with global_load_dwordx4.  The loader's
+pointer-kind analysis gives every packet / slot access at a constant offset a
+*staged* handler (resolved per launch, when the batch head is known): its
+dword index, bit shift, byte mask and dirty-chunk bits are precomputed in the
+FInsn, so the access is one or two index-mode moves.  Generic loads/stores
+whose address falls inside the window at a wave-uniform offset are served
+from the same VGPRs (v_alignbit / v_bfi).  Dirty 16-byte chunks are written
+back (global_store_dwordx4) before any exit and before any other access that
+overlaps the window (which also ends staging for the unit).
+
+Map-bound handlers.  lddw of a map fd is bound at load time (as the kernel
+binds BPF_PSEUDO_MAP_FD): an ARRAY lookup with a constant map and a stack key
+is a bounds compare and one multiply-add; loads/stores/counters through a
+non-null map-value pointer need no window check; a fused counter on a
+constant map-value address needs no address uniformity test.
 
 The handlers cover ALU64/ALU32 (reg and imm), byte swaps, loads/stores of
 every size with the batch/arena/LDS window check, lddw, ja, every
-conditional jump whose outcome is wave-uniform, array-map lookups with a
-wave-uniform fd, wave-uniform fused counters and exit.  Anything else (other
-helpers, atomics, div/mod, a split branch, an access failing the window
-check) leaves the block at that pc, and the C++ interpreter executes that
-one instruction (interp.hip, run_loop<true, true>).
+conditional jump (uniform outcome, or split into lane groups), array / hash
+lookups, atomics add/or/and/xor (+fetch), fused counters and exit.  Anything
+else (other helpers, div/mod, cmpxchg/xchg, an access failing the window
+check) leaves the block at that pc, and the C++ interpreter executes that one
+instruction (interp.hip, run_loop<true, true>).
 
 Fixed registers (declared as clobbers; the compiler keeps nothing live in
 them across the block).  The handlers are written against the numbering
 below; main() relocates every VGPR by +26 to the top of a 128-register
 budget (v40..v101 -> v66..v127):
-  s[40:47] W   current FInsn: w0 handler offset, w1 dst*2, w[2:3] imm64,
-               w4 src*2, w5 jump target (byte offset from PROG), w[6:7] off64
-  s[48:49] IP  address of the current FInsn     s[50:51] TB  table base - 4
-  s[52:53] T   scratch / dispatch target        s[54:55], s[56:57], s[60:61] masks
-  s[58:59] saved exec                            s[62:63] A0 (wave-uniform address)
-  s[64:65] V0 (wave-uniform value)               s[66:67] TOT (wave total)
-  s68 exit reason   s69/s70/s71 scratch          s[72:75] DMap words 0-3
+  s[40:47] W   current FInsn: w0 handler offset, w1 0, w[2:3] imm64 or off64
+               (staged: w2 dword index, w3 bit shift), w4 dst*2 (staged
+               stores: dirty-chunk bits; lookups: max_entries), w5 src*2
+               (staged imm stores: the imm; lookups: value size), w6 jump
+               target IP / static offset / continuation IP, w7 imm32 (ST, RMW)
+               or byte mask (staged stores)
+  s48 IP (byte offset of the current FInsn from PROG)   s49 scratch
+  s[50:51] TB  table base - 4                    s[52:53] T scratch / target
+  s[54:55], s[56:57], s[60:61] masks             s[58:59] saved exec
+  s[62:63] A0 (wave-uniform address)             s[64:65] V0 (uniform value)
+  s[66:67] TOT (wave total)                      s68 exit reason
+  s69/s70/s71 scratch                            s[72:75] DMap words 0-3
   s[76:77] DMap data pointer                     s[78:79] PROG (FInsn base)
-  s[80:81] S (staged bytes, 64-bit)              s[82:83] O (uniform window offset)
+  s80 S (staged bytes; 0 = staging off)  s81 0   s[82:83] O (uniform offset)
   s84 dirty 16-B chunk mask                      s85 scratch
-  s86/s87, s[88:89]/s[90:91], s92  pending lane groups (divergence): FInsn
-               address bits 31:0, lane masks, count
+  s86/s87, s[88:89]/s[90:91], s92  pending lane groups (divergence): IPs,
+               lane masks, count
   v40 lane's R[0] LDS address  v41, v[42:43] scratch
   v[44:45] X  v[46:47] Y  v[48:49] Z (address)  v[50:51] E (address end)
   v[52:53] slot address (staging base)           v[54:55] O (per-lane offset)
@@ -82,6 +105,11 @@ CMP32 = {k: v.replace("64", "32") for k, v in CMP64.items()}
 R0 = 60        # first VGPR of the eBPF register file
 STG = 84       # first VGPR of the staged bytes
 NREG = 11
+INSN = 32      # FInsn bytes
+
+# staged (link-resolved) packet / slot accesses
+STAGED_LD = ["LDXS1", "LDXS2", "LDXS4", "LDXS2X", "LDXS4X", "LDXS8A", "LDXS8U"]
+STAGED_ST = ["STXS1", "STXS2", "STXS4", "STXS8", "STS1", "STS2", "STS4", "STS8"]
 
 
 def handler_ids():
@@ -95,13 +123,19 @@ def handler_ids():
     for sz in (1, 2, 4, 8):
         ids += [f"LDX{sz}", f"STX{sz}", f"ST{sz}"]
     for sz in (1, 2, 4, 8):
-        for kind in ("PKT", "SLOT", "STK"):
-            ids += [f"LDX{sz}_{kind}", f"STX{sz}_{kind}", f"ST{sz}_{kind}"]
+        ids += [f"LDX{sz}_STK", f"STX{sz}_STK", f"ST{sz}_STK"]
+    for sz in (1, 2, 4, 8):
+        ids += [f"LDX{sz}_MV", f"STX{sz}_MV"]
+    ids += STAGED_LD + STAGED_ST
     ids += ["LDX_CTXDATA", "LDX_CTXEND"]
     for sz in (4, 8):
         for op in ("ADD", "OR", "AND", "XOR"):
             ids += [f"ATOM{sz}_{op}", f"ATOM{sz}_{op}_F"]
-    ids += ["LDDW", "JA", "CALL_LOOKUP", "CALL_LOOKUP_STK", "EXIT", "RMW4_R", "RMW4_I", "RMW8_R", "RMW8_I"]
+        ids += [f"ATOMMV{sz}_ADD"]
+    ids += ["LDDW", "JA", "CALL_LOOKUP", "CALL_LOOKUP_STK", "CALL_LOOKUP_AK", "EXIT"]
+    for sz in (4, 8):
+        for k in ("R", "I"):
+            ids += [f"RMW{sz}_{k}", f"RMWMV{sz}_{k}", f"RMWK{sz}_{k}"]
     for w in ("64", "32"):
         for cc in JCC:
             for k in ("R", "I"):
@@ -127,41 +161,59 @@ class Gen:
 
     # ---- dispatch ----
     def dispatch(self):
-        """IP points at the next FInsn: fetch it and jump to its handler."""
-        self.e("s_load_dwordx8 s[40:47], s[48:49], 0x0",
-               "s_add_u32 %[steps], %[steps], 1",
+        """IP is the byte offset of the next FInsn: fetch it and jump to its
+        handler through the table."""
+        self.e("s_load_dwordx8 s[40:47], s[78:79], s48",
                "s_waitcnt lgkmcnt(0)",
                "s_add_u32 s52, s50, s40",
                "s_addc_u32 s53, s51, 0",
                "s_setpc_b64 s[52:53]")
 
     def next_seq(self, slots=1):
-        self.e(f"s_add_u32 s48, s48, {32 * slots}", "s_addc_u32 s49, s49, 0")
+        self.e(f"s_add_u32 s48, s48, {INSN * slots}")
         self.dispatch()
 
     def jump_taken(self):
-        self.e("s_add_u32 s48, s78, s45", "s_addc_u32 s49, s79, 0",
+        """IP = target; a taken jump is the only way back, so the step limit
+        is enforced here."""
+        self.e("s_mov_b32 s48, s46",
+               "s_add_u32 %[steps], %[steps], 1",
                "s_cmp_gt_u32 %[steps], %[limit]", f"s_cbranch_scc1 {L('steps')}")
         self.dispatch()
 
     # ---- register file (VGPRs, indexed by a wave-uniform SGPR) ----
+    def idx(self, sreg, modes):
+        self.e(f"s_set_gpr_idx_on {sreg}, gpr_idx({modes})")
+
+    def idx_off(self):
+        self.e("s_set_gpr_idx_off")
+
     def rd(self, sidx, v):
         """v[v:v+1] = r[sidx / 2]"""
-        self.e(f"s_set_gpr_idx_on {sidx}, gpr_idx(SRC0)",
-               f"v_mov_b32 v{v}, v{R0}", f"v_mov_b32 v{v + 1}, v{R0 + 1}",
-               "s_set_gpr_idx_off")
+        self.idx(sidx, "SRC0")
+        self.e(f"v_mov_b32 v{v}, v{R0}", f"v_mov_b32 v{v + 1}, v{R0 + 1}")
+        self.idx_off()
 
-    def wr(self, sidx, v):
-        """r[sidx / 2] = v[v:v+1]"""
-        self.e(f"s_set_gpr_idx_on {sidx}, gpr_idx(DST)",
-               f"v_mov_b32 v{R0}, v{v}", f"v_mov_b32 v{R0 + 1}, v{v + 1}",
-               "s_set_gpr_idx_off")
+    def rd_lo(self, sidx, v):
+        """v[v] = low half of r[sidx / 2]"""
+        self.idx(sidx, "SRC0")
+        self.e(f"v_mov_b32 v{v}, v{R0}")
+        self.idx_off()
+
+    def wr(self, sidx, v, hi=None):
+        """r[sidx / 2] = v[v:v+1] (hi: another source for the upper half)"""
+        self.idx(sidx, "DST")
+        self.e(f"v_mov_b32 v{R0}, v{v}", f"v_mov_b32 v{R0 + 1}, {hi if hi is not None else 'v%d' % (v + 1)}")
+        self.idx_off()
 
     def rd_fixed(self, r, v):
         self.e(f"v_mov_b32 v{v}, v{R0 + 2 * r}", f"v_mov_b32 v{v + 1}, v{R0 + 2 * r + 1}")
 
-    def imm_y(self):     # Y = imm (sign-extended by the loader)
+    def imm_y(self):     # Y = imm64 (sign-extended by the loader)
         self.e("v_mov_b32 v46, s42", "v_mov_b32 v47, s43")
+
+    def imm32_x(self):   # X = imm32 (w7) sign-extended to 64 bits
+        self.e("v_mov_b32 v44, s47", "v_ashrrev_i32 v45, 31, v44")
 
     # ---- memory ----
     def check(self, sz):
@@ -271,7 +323,7 @@ class Gen:
         overlaps its window, write back dirty chunks and end staging; then
         continue at `on_global`."""
         conflict = self.label("cf")
-        self.e("s_cmp_eq_u64 s[80:81], 0", f"s_cbranch_scc1 {on_global}",
+        self.e("s_cmp_eq_u32 s80, 0", f"s_cbranch_scc1 {on_global}",
                "v_sub_co_u32 v54, vcc, v48, v52", "v_subb_co_u32 v55, vcc, v49, v53, vcc",
                "v_readfirstlane_b32 s82, v54", "v_readfirstlane_b32 s83, v55",
                "v_cmp_ne_u64 s[54:55], s[82:83], v[54:55]",
@@ -290,16 +342,16 @@ class Gen:
                "s_and_b64 s[54:55], s[54:55], exec",
                "s_cmp_eq_u64 s[54:55], 0", f"s_cbranch_scc1 {on_global}")
         self.flush_all()
-        self.e("s_waitcnt vmcnt(0)", "s_mov_b64 s[80:81], 0", f"s_branch {on_global}")
+        self.e("s_waitcnt vmcnt(0)", "s_mov_b32 s80, 0", f"s_branch {on_global}")
 
     def staged_load(self, sz):
         """X = sz bytes at window offset s82 (zero-extended)."""
         self.e("s_waitcnt vmcnt(0)",                       # staging loads landed
-               "s_lshr_b32 s70, s82, 2", "s_and_b32 s71, s82, 3", "s_lshl_b32 s71, s71, 3",
-               "s_set_gpr_idx_on s70, gpr_idx(SRC0)",
-               f"v_mov_b32 v44, v{STG}", f"v_mov_b32 v45, v{STG + 1}", f"v_mov_b32 v46, v{STG + 2}",
-               "s_set_gpr_idx_off",
-               "v_alignbit_b32 v44, v45, v44, s71")
+               "s_lshr_b32 s70, s82, 2", "s_and_b32 s71, s82, 3", "s_lshl_b32 s71, s71, 3")
+        self.idx("s70", "SRC0")
+        self.e(f"v_mov_b32 v44, v{STG}", f"v_mov_b32 v45, v{STG + 1}", f"v_mov_b32 v46, v{STG + 2}")
+        self.idx_off()
+        self.e("v_alignbit_b32 v44, v45, v44, s71")
         if sz == 8:
             self.e("v_alignbit_b32 v45, v46, v45, s71")
         elif sz == 4:
@@ -317,73 +369,121 @@ class Gen:
             self.e(f"s_add_u32 s69, s71, {sz}", "s_cmp_gt_u32 s69, 4", f"s_cbranch_scc1 {on_unaligned}")
         self.e("s_waitcnt vmcnt(0)", "s_lshr_b32 s70, s82, 2")
         if sz == 8:
-            self.e("s_set_gpr_idx_on s70, gpr_idx(DST)", f"v_mov_b32 v{STG}, v44", f"v_mov_b32 v{STG + 1}, v45",
-                   "s_set_gpr_idx_off")
+            self.idx("s70", "DST")
+            self.e(f"v_mov_b32 v{STG}, v44", f"v_mov_b32 v{STG + 1}, v45")
+            self.idx_off()
         elif sz == 4:
-            self.e("s_set_gpr_idx_on s70, gpr_idx(DST)", f"v_mov_b32 v{STG}, v44", "s_set_gpr_idx_off")
+            self.idx("s70", "DST")
+            self.e(f"v_mov_b32 v{STG}, v44")
+            self.idx_off()
         else:
             self.e("s_lshl_b32 s71, s71, 3",
                    f"s_bfm_b32 s69, {8 * sz}, s71",
-                   "v_lshlrev_b32 v44, s71, v44",
-                   "s_set_gpr_idx_on s70, gpr_idx(SRC0)", f"v_mov_b32 v46, v{STG}", "s_set_gpr_idx_off",
-                   "v_bfi_b32 v46, s69, v44, v46",
-                   "s_set_gpr_idx_on s70, gpr_idx(DST)", f"v_mov_b32 v{STG}, v46", "s_set_gpr_idx_off")
+                   "v_lshlrev_b32 v44, s71, v44")
+            self.idx("s70", "SRC0")
+            self.e(f"v_mov_b32 v46, v{STG}")
+            self.idx_off()
+            self.e("v_bfi_b32 v46, s69, v44, v46")
+            self.idx("s70", "DST")
+            self.e(f"v_mov_b32 v{STG}, v46")
+            self.idx_off()
         # dirty chunks: the 16-B chunks of the first and the last byte
         self.e("s_lshr_b32 s69, s82, 4", "s_lshl_b32 s69, 1, s69", "s_or_b32 s84, s84, s69",
                f"s_add_u32 s69, s82, {sz - 1}", "s_lshr_b32 s69, s69, 4", "s_lshl_b32 s69, 1, s69",
                "s_or_b32 s84, s84, s69")
 
     # ---- handlers ----
+    # dst op= y with the VALU instruction itself in index mode: (y-is-register
+    # body, y-is-imm body).  VOP2 encodings (_e32): one SGPR operand at most,
+    # and src1 must be a VGPR, so the imm forms put the SGPR in src0 and index
+    # src1; the carry chains take the imm's high half from a VGPR.
+    INPLACE64 = {
+        "ADD": (["v_add_co_u32_e32 v60, vcc, v60, v46", "v_addc_co_u32_e32 v61, vcc, v61, v47, vcc"],
+                ["v_add_co_u32_e32 v60, vcc, s42, v60", "v_addc_co_u32_e32 v61, vcc, v47, v61, vcc"]),
+        "SUB": (["v_sub_co_u32_e32 v60, vcc, v60, v46", "v_subb_co_u32_e32 v61, vcc, v61, v47, vcc"],
+                ["v_subrev_co_u32_e32 v60, vcc, s42, v60", "v_subbrev_co_u32_e32 v61, vcc, v47, v61, vcc"]),
+        "OR": (["v_or_b32_e32 v60, v60, v46", "v_or_b32_e32 v61, v61, v47"],
+               ["v_or_b32_e32 v60, s42, v60", "v_or_b32_e32 v61, s43, v61"]),
+        "AND": (["v_and_b32_e32 v60, v60, v46", "v_and_b32_e32 v61, v61, v47"],
+                ["v_and_b32_e32 v60, s42, v60", "v_and_b32_e32 v61, s43, v61"]),
+        "XOR": (["v_xor_b32_e32 v60, v60, v46", "v_xor_b32_e32 v61, v61, v47"],
+                ["v_xor_b32_e32 v60, s42, v60", "v_xor_b32_e32 v61, s43, v61"]),
+        "MOV": (["v_mov_b32_e32 v60, v46", "v_mov_b32_e32 v61, v47"],
+                ["v_mov_b32_e32 v60, s42", "v_mov_b32_e32 v61, s43"]),
+    }
+    INPLACE32 = {
+        "ADD": ("v_add_u32_e32 v60, v60, v46", "v_add_u32_e32 v60, s42, v60"),
+        "SUB": ("v_sub_u32_e32 v60, v60, v46", "v_subrev_u32_e32 v60, s42, v60"),
+        "OR": ("v_or_b32_e32 v60, v60, v46", "v_or_b32_e32 v60, s42, v60"),
+        "AND": ("v_and_b32_e32 v60, v60, v46", "v_and_b32_e32 v60, s42, v60"),
+        "XOR": ("v_xor_b32_e32 v60, v60, v46", "v_xor_b32_e32 v60, s42, v60"),
+        "MOV": ("v_mov_b32_e32 v60, v46", "v_mov_b32_e32 v60, s42"),
+        # shift amount in src0, the shifted register in src1 (& 31 in hardware)
+        "LSH": ("v_lshlrev_b32_e32 v60, v46, v60", "v_lshlrev_b32_e32 v60, s42, v60"),
+        "RSH": ("v_lshrrev_b32_e32 v60, v46, v60", "v_lshrrev_b32_e32 v60, s42, v60"),
+        "ARSH": ("v_ashrrev_i32_e32 v60, v46, v60", "v_ashrrev_i32_e32 v60, s42, v60"),
+    }
+
     def alu(self, w, op, k):
-        if op != "MOV":
-            self.rd("s41", 44)
+        if w == "64" and op in self.INPLACE64:
+            body = self.INPLACE64[op][0 if k == "R" else 1]
+            if k == "R":
+                self.rd("s45", 46)
+            elif op in ("ADD", "SUB"):
+                self.e("v_mov_b32 v47, s43")
+            mode = "DST" if op == "MOV" else ("SRC0,DST" if k == "R" else "SRC1,DST")
+            self.idx("s44", mode)
+            self.e(*body)
+            self.idx_off()
+            self.next_seq()
+            return
+        if w == "32" and op in self.INPLACE32:
+            body = self.INPLACE32[op][0 if k == "R" else 1]
+            if k == "R":
+                self.rd_lo("s45", 46)
+            if op == "MOV":
+                mode = "DST"
+            elif k == "R" and op not in ("LSH", "RSH", "ARSH"):
+                mode = "SRC0,DST"
+            else:
+                mode = "SRC1,DST"
+            self.idx("s44", mode)
+            self.e(body, "v_mov_b32_e32 v61, 0")      # ALU32 zero-extends
+            self.idx_off()
+            self.next_seq()
+            return
+        # MUL and 64-bit shifts: X = r[dst], Y = src / imm, X op= Y, r[dst] = X
+        self.rd("s44", 44)
         if k == "R":
-            self.rd("s44", 46)
+            self.rd("s45", 46)
         else:
             self.imm_y()
         if w == "64":
             body = {
-                "ADD": ["v_lshl_add_u64 v[44:45], v[44:45], 0, v[46:47]"],
-                "SUB": ["v_sub_co_u32 v44, vcc, v44, v46", "v_subb_co_u32 v45, vcc, v45, v47, vcc"],
                 "MUL": ["v_mul_lo_u32 v48, v44, v47", "v_mul_lo_u32 v49, v45, v46",
                         "v_mul_hi_u32 v50, v44, v46", "v_mul_lo_u32 v44, v44, v46",
                         "v_add3_u32 v45, v48, v49, v50"],
-                "OR": ["v_or_b32 v44, v44, v46", "v_or_b32 v45, v45, v47"],
-                "AND": ["v_and_b32 v44, v44, v46", "v_and_b32 v45, v45, v47"],
-                "XOR": ["v_xor_b32 v44, v44, v46", "v_xor_b32 v45, v45, v47"],
-                "MOV": ["v_mov_b32 v44, v46", "v_mov_b32 v45, v47"],
                 "LSH": ["v_lshlrev_b64 v[44:45], v46, v[44:45]"],   # shift count & 63 in hardware
                 "RSH": ["v_lshrrev_b64 v[44:45], v46, v[44:45]"],
                 "ARSH": ["v_ashrrev_i64 v[44:45], v46, v[44:45]"],
             }[op]
         else:
-            body = {
-                "ADD": ["v_add_u32 v44, v44, v46"],
-                "SUB": ["v_sub_u32 v44, v44, v46"],
-                "MUL": ["v_mul_lo_u32 v44, v44, v46"],
-                "OR": ["v_or_b32 v44, v44, v46"],
-                "AND": ["v_and_b32 v44, v44, v46"],
-                "XOR": ["v_xor_b32 v44, v44, v46"],
-                "MOV": ["v_mov_b32 v44, v46"],
-                "LSH": ["v_lshlrev_b32 v44, v46, v44"],             # & 31 in hardware
-                "RSH": ["v_lshrrev_b32 v44, v46, v44"],
-                "ARSH": ["v_ashrrev_i32 v44, v46, v44"],
-            }[op] + ["v_mov_b32 v45, 0"]                          # ALU32 zero-extends
+            body = {"MUL": ["v_mul_lo_u32 v44, v44, v46"]}[op] + ["v_mov_b32 v45, 0"]
         self.e(*body)
-        self.wr("s41", 44)
+        self.wr("s44", 44)
         self.next_seq()
 
     def neg(self, w):
-        self.rd("s41", 44)
+        self.idx("s44", "SRC1,DST")
         if w == "64":
-            self.e("v_sub_co_u32 v44, vcc, 0, v44", "v_subb_co_u32 v45, vcc, 0, v45, vcc")
+            self.e("v_sub_co_u32_e32 v60, vcc, 0, v60", "v_subb_co_u32_e32 v61, vcc, 0, v61, vcc")
         else:
-            self.e("v_sub_u32 v44, 0, v44", "v_mov_b32 v45, 0")
-        self.wr("s41", 44)
+            self.e("v_sub_u32_e32 v60, 0, v60", "v_mov_b32_e32 v61, 0")
+        self.idx_off()
         self.next_seq()
 
     def endian(self, name):
-        self.rd("s41", 44)
+        self.rd("s44", 44)
         body = {
             "LE16": ["v_and_b32 v44, 0xffff, v44", "v_mov_b32 v45, 0"],
             "LE32": ["v_mov_b32 v45, 0"],
@@ -393,38 +493,43 @@ class Gen:
                      "v_perm_b32 v45, 0, v44, s69", "v_mov_b32 v44, v48"],
         }[name]
         self.e(*body)
-        self.wr("s41", 44)
+        self.wr("s44", 44)
         self.next_seq()
 
+    LD = {1: "flat_load_ubyte v44, v[48:49]", 2: "flat_load_ushort v44, v[48:49]",
+          4: "flat_load_dword v44, v[48:49]", 8: "flat_load_dwordx2 v[44:45], v[48:49]"}
+    ST = {1: "flat_store_byte v[48:49], v44", 2: "flat_store_short v[48:49], v44",
+          4: "flat_store_dword v[48:49], v44", 8: "flat_store_dwordx2 v[48:49], v[44:45]"}
+
     def ldx(self, sz):
-        stg, glb = self.label("ls"), self.label("lg")
-        self.rd("s44", 48)
-        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[46:47]")
+        stg = self.label("ls")
+        glb = L(f"ldx{sz}_glb")
+        self.rd("s45", 48)
+        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[42:43]")
         self.staged_or(sz, stg, glb)
         self.e(f"{stg}:")
         self.staged_load(sz)
-        self.wr("s41", 44)
+        self.wr("s44", 44)
         self.next_seq()
-        self.e(f"{glb}:")
+        self.e(f"{glb}:")                 # also the staged handlers' way out (staging off)
         self.check(sz)
-        ld = {1: "flat_load_ubyte v44, v[48:49]", 2: "flat_load_ushort v44, v[48:49]",
-              4: "flat_load_dword v44, v[48:49]", 8: "flat_load_dwordx2 v[44:45], v[48:49]"}[sz]
-        self.e(ld)
+        self.e(self.LD[sz])
         if sz < 8:
             self.e("v_mov_b32 v45, 0")
         self.e("s_waitcnt vmcnt(0) lgkmcnt(0)")
-        self.wr("s41", 44)
+        self.wr("s44", 44)
         self.next_seq()
 
     def store(self, sz, from_reg):
-        stg, glb, unal = self.label("ss"), self.label("sg"), self.label("su")
+        stg, unal = self.label("ss"), self.label("su")
+        glb = L(("stx" if from_reg else "st") + f"{sz}_glb")
         # Z = R[dst] + off ; X = value
-        self.rd("s41", 48)
+        self.rd("s44", 48)
         if from_reg:
-            self.rd("s44", 44)
+            self.rd("s45", 44)
         else:
-            self.e("v_mov_b32 v44, s42", "v_mov_b32 v45, s43")
-        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[46:47]")
+            self.imm32_x()
+        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[42:43]")
         self.staged_or(sz, stg, glb)
         self.e(f"{stg}:")
         self.staged_store(sz, unal)
@@ -432,76 +537,144 @@ class Gen:
         # a staged store straddling dwords: write back, end staging, store to memory
         self.e(f"{unal}:")
         self.flush_all()
-        self.e("s_waitcnt vmcnt(0)", "s_mov_b64 s[80:81], 0")
+        self.e("s_waitcnt vmcnt(0)", "s_mov_b32 s80, 0")
         self.e(f"{glb}:")
         self.check(sz)
-        st = {1: "flat_store_byte v[48:49], v44", 2: "flat_store_short v[48:49], v44",
-              4: "flat_store_dword v[48:49], v44", 8: "flat_store_dwordx2 v[48:49], v[44:45]"}[sz]
-        self.e(st)
+        self.e(self.ST[sz])
         self.next_seq()
 
-    # ---- loads / stores through a statically typed base (loader pointer kinds;
-    # w5 = the access's byte offset from data (PKT), the slot (SLOT) or the
-    # initial stack top (STK)).  No per-lane window check is needed: the
-    # staged window and the lane's LDS stack are the lane's own memory.
-    def staged_static(self, sz, pkt, generic):
-        """s82 = window offset of a packet / slot access; the generic handler
-        takes over when staging is off or the access leaves the window."""
-        if pkt:
-            self.e("s_add_u32 s82, s45, %[head]")
-        else:
-            self.e("s_mov_b32 s82, s45")
-        self.e("s_cmp_eq_u32 s80, 0", f"s_cbranch_scc1 {generic}",
-               f"s_add_u32 s69, s82, {sz}", "s_cmp_gt_u32 s69, s80", f"s_cbranch_scc1 {generic}")
-
-    def ldx_static(self, sz, kind):
-        if kind == "STK":
-            ds = {1: "ds_read_u8", 2: "ds_read_u16", 4: "ds_read_b32", 8: "ds_read_b64"}[sz]
-            self.e("v_add_u32 v41, s45, %[stklo]",
-                   f"{ds} {'v[44:45]' if sz == 8 else 'v44'}, v41")
-            if sz < 8:
-                self.e("v_mov_b32 v45, 0")
-            self.e("s_waitcnt lgkmcnt(0)")
-        else:
-            self.staged_static(sz, kind == "PKT", L(f"h_LDX{sz}"))
-            self.staged_load(sz)
-        self.wr("s41", 44)
+    # ---- map values (loader: a non-null lookup result, access inside the
+    # value): no window check, never inside the staged window
+    def ldx_mv(self, sz):
+        ld = {1: "global_load_ubyte v44, v[48:49], off", 2: "global_load_ushort v44, v[48:49], off",
+              4: "global_load_dword v44, v[48:49], off", 8: "global_load_dwordx2 v[44:45], v[48:49], off"}[sz]
+        self.rd("s45", 48)
+        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[42:43]", ld)
+        if sz < 8:
+            self.e("v_mov_b32 v45, 0")
+        self.e("s_waitcnt vmcnt(0)")
+        self.wr("s44", 44)
         self.next_seq()
 
-    def store_static(self, sz, kind, from_reg):
+    def stx_mv(self, sz):
+        st = {1: "global_store_byte v[48:49], v44, off", 2: "global_store_short v[48:49], v44, off",
+              4: "global_store_dword v[48:49], v44, off", 8: "global_store_dwordx2 v[48:49], v[44:45], off"}[sz]
+        self.rd("s44", 48)
+        self.rd("s45", 44)
+        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[42:43]", st)
+        self.next_seq()
+
+    # ---- stack (loader: r10 + constant, in the lane's LDS stack) ----
+    def ldx_stk(self, sz):
+        ds = {1: "ds_read_u8", 2: "ds_read_u16", 4: "ds_read_b32", 8: "ds_read_b64"}[sz]
+        self.e("v_add_u32 v41, s46, %[stklo]",
+               f"{ds} {'v[44:45]' if sz == 8 else 'v44'}, v41",
+               "s_waitcnt lgkmcnt(0)")
+        self.wr("s44", 44, hi=None if sz == 8 else "0")
+        self.next_seq()
+
+    def store_stk(self, sz, from_reg):
         if from_reg:
-            self.rd("s44", 44)
+            (self.rd if sz == 8 else self.rd_lo)("s45", 44)
         else:
-            self.e("v_mov_b32 v44, s42", "v_mov_b32 v45, s43")
-        if kind == "STK":
-            ds = {1: "ds_write_b8", 2: "ds_write_b16", 4: "ds_write_b32", 8: "ds_write_b64"}[sz]
-            self.e("v_add_u32 v41, s45, %[stklo]",
-                   f"{ds} v41, {'v[44:45]' if sz == 8 else 'v44'}")
-        else:
-            generic = L(f"h_{'STX' if from_reg else 'ST'}{sz}")
-            self.staged_static(sz, kind == "PKT", generic)
-            self.staged_store(sz, generic)
+            self.imm32_x()
+        ds = {1: "ds_write_b8", 2: "ds_write_b16", 4: "ds_write_b32", 8: "ds_write_b64"}[sz]
+        self.e("v_add_u32 v41, s46, %[stklo]",
+               f"{ds} v41, {'v[44:45]' if sz == 8 else 'v44'}")
         self.next_seq()
+
+    # ---- staged packet / slot accesses (link-resolved: inside the window) ----
+    def fallback_addr(self):
+        """Z = slot + static slot offset (w6), for the generic handlers."""
+        self.e("v_add_co_u32_e32 v48, vcc, s46, v52", "v_addc_co_u32_e32 v49, vcc, 0, v53, vcc")
+
+    def ldxs(self, name):
+        fb = self.label("lfb")
+        sz = int(name[4])
+        self.e("s_cmp_eq_u32 s80, 0", f"s_cbranch_scc1 {fb}", "s_waitcnt vmcnt(0)")
+        self.idx("s42", "SRC0")
+        n = {"LDXS1": 1, "LDXS2": 1, "LDXS4": 1, "LDXS2X": 2, "LDXS4X": 2, "LDXS8A": 2, "LDXS8U": 3}[name]
+        for j in range(n):
+            self.e(f"v_mov_b32 v{44 + j}, v{STG + j}")
+        self.idx_off()
+        body = {
+            "LDXS1": ["v_bfe_u32 v44, v44, s43, 8"],
+            "LDXS2": ["v_bfe_u32 v44, v44, s43, 16"],
+            "LDXS4": [],
+            "LDXS2X": ["v_alignbit_b32 v44, v45, v44, s43", "v_and_b32 v44, 0xffff, v44"],
+            "LDXS4X": ["v_alignbit_b32 v44, v45, v44, s43"],
+            "LDXS8A": [],
+            "LDXS8U": ["v_alignbit_b32 v44, v45, v44, s43", "v_alignbit_b32 v45, v46, v45, s43"],
+        }[name]
+        self.e(*body)
+        self.wr("s44", 44, hi=None if sz == 8 else "0")
+        self.next_seq()
+        self.e(f"{fb}:")
+        self.fallback_addr()
+        self.e(f"s_branch {L('ldx%d_glb' % sz)}")
+
+    def stxs(self, name):
+        imm = name.startswith("STS")
+        sz = int(name[-1])
+        fb = self.label("sfb")
+        self.e("s_cmp_eq_u32 s80, 0", f"s_cbranch_scc1 {fb}", "s_waitcnt vmcnt(0)")
+        if not imm:
+            (self.rd if sz == 8 else self.rd_lo)("s45", 44)
+        elif sz == 8:
+            self.e("v_mov_b32 v44, s45", "v_ashrrev_i32 v45, 31, v44")
+        elif sz == 4:
+            self.e("v_mov_b32 v44, s45")
+        else:
+            self.e("s_lshl_b32 s69, s45, s43", "v_mov_b32 v44, s69")
+        if sz <= 2:
+            if not imm:
+                self.e("v_lshlrev_b32 v44, s43, v44")
+            self.idx("s42", "SRC0")
+            self.e(f"v_mov_b32 v46, v{STG}")
+            self.idx_off()
+            self.e("v_bfi_b32 v46, s47, v44, v46")
+            self.idx("s42", "DST")
+            self.e(f"v_mov_b32 v{STG}, v46")
+            self.idx_off()
+        else:
+            self.idx("s42", "DST")
+            self.e(f"v_mov_b32 v{STG}, v44")
+            if sz == 8:
+                self.e(f"v_mov_b32 v{STG + 1}, v45")
+            self.idx_off()
+        self.e("s_or_b32 s84, s84, s44")
+        self.next_seq()
+        self.e(f"{fb}:")
+        self.fallback_addr()
+        if imm:
+            self.e("v_mov_b32 v44, s45", "v_ashrrev_i32 v45, 31, v44")
+        else:
+            self.rd("s45", 44)
+        self.e(f"s_branch {L(('st' if imm else 'stx') + '%d_glb' % sz)}")
 
     def ctx_field(self, end):
         """ctx->data = slot + head; ctx->data_end = slot + head + len."""
         if end:
             self.e("v_add_u32 v46, %[head], %[ulen]")
+        self.idx("s44", "DST")
+        if end:
+            self.e("v_add_co_u32_e32 v60, vcc, v46, v52")
         else:
-            self.e("v_mov_b32 v46, %[head]")
-        self.e("v_add_co_u32 v44, vcc, v52, v46", "v_addc_co_u32 v45, vcc, v53, 0, vcc")
-        self.wr("s41", 44)
+            self.e("v_add_co_u32_e32 v60, vcc, %[head], v52")
+        self.e("v_addc_co_u32_e32 v61, vcc, 0, v53, vcc")
+        self.idx_off()
         self.next_seq()
 
     def lddw(self):
-        self.e("v_mov_b32 v44, s42", "v_mov_b32 v45, s43")
-        self.wr("s41", 44)
+        self.idx("s44", "DST")
+        self.e("v_mov_b32_e32 v60, s42", "v_mov_b32_e32 v61, s43")
+        self.idx_off()
         self.next_seq(2)
 
     def jcc(self, w, cc, k):
-        self.rd("s41", 44)
+        (self.rd if w == "64" else self.rd_lo)("s44", 44)
         if k == "R":
-            self.rd("s44", 46)
+            (self.rd if w == "64" else self.rd_lo)("s45", 46)
         y64 = "v[46:47]" if k == "R" else "s[42:43]"
         y32 = "v46" if k == "R" else "s42"
         if cc == "SET":
@@ -513,15 +686,15 @@ class Gen:
                 self.e("v_or_b32 v44, v44, v45")
             else:
                 self.e(f"v_and_b32 v44, {'v46' if k == 'R' else 's42'}, v44")
-            self.e("v_cmp_ne_u32 s[54:55], 0, v44")
+            self.e("v_cmp_ne_u32_e64 vcc, 0, v44")
         elif w == "64":
-            self.e(f"v_cmp_{CMP64[cc]} s[54:55], v[44:45], {y64}")
+            self.e(f"v_cmp_{CMP64[cc]}_e64 vcc, v[44:45], {y64}")
         else:
-            self.e(f"v_cmp_{CMP32[cc]} s[54:55], v44, {y32}")
+            self.e(f"v_cmp_{CMP32[cc]}_e64 vcc, v44, {y32}")
         # v_cmp writes 0 for inactive lanes: none taken / all taken / split
         nt = self.label("nt")
-        self.e("s_cmp_eq_u64 s[54:55], 0", f"s_cbranch_scc1 {nt}",
-               "s_cmp_eq_u64 s[54:55], exec", f"s_cbranch_scc0 {L('split')}")
+        self.e(f"s_cbranch_vccz {nt}",
+               "s_cmp_eq_u64 vcc, exec", f"s_cbranch_scc0 {L('split')}")
         self.jump_taken()
         self.e(f"{nt}:")
         self.next_seq()
@@ -538,7 +711,7 @@ class Gen:
         """bpf_map_lookup_elem with a wave-uniform map fd.
         ARRAY (array_map.cpp:27-40): r0 = key < max_entries ? &data[key * vsz] : 0.
         HASH with its key on the stack (stack_key: the loader proved r2 =
-        stack top + w5, 4-aligned): the bpftime_hash_map probe
+        stack top + w6, 4-aligned): the bpftime_hash_map probe
         (bpftime_hash_map.hpp:40-47, 127-151) per lane; a wave whose lanes
         all hit stays here, any miss or in-flight insert leaves for the C++
         helper (which also records the miss for lookup_or_try_init).
@@ -559,7 +732,7 @@ class Gen:
             self.e("s_cmp_eq_u32 s72, 1", f"s_cbranch_scc1 {hsh}")          # BPF_MAP_TYPE_HASH
         self.e("s_cmp_lg_u32 s72, 2", f"s_cbranch_scc1 {L('slow')}")        # not BPF_MAP_TYPE_ARRAY
         if stack_key:
-            self.e("v_add_u32 v41, s45, %[stklo]", "ds_read_b32 v46, v41", "s_waitcnt lgkmcnt(0)",
+            self.e("v_add_u32 v41, s46, %[stklo]", "ds_read_b32 v46, v41", "s_waitcnt lgkmcnt(0)",
                    f"s_branch {got}")
         else:
             self.staged_or(4, stg, glb)
@@ -579,6 +752,18 @@ class Gen:
         if stack_key:
             self.e(f"{hsh}:")
             self.hash_lookup()
+
+    def call_lookup_ak(self):
+        """ARRAY lookup, map bound at load (w[2:3] = value base, w4 =
+        max_entries, w5 = value size), key at stack offset w6:
+        r0 = key < max_entries ? base + key * vsz : 0 (array_map.cpp:27-40)."""
+        self.e("v_add_u32 v41, s46, %[stklo]", "ds_read_b32 v46, v41", "s_waitcnt lgkmcnt(0)",
+               "v_cmp_gt_u32 s[54:55], s44, v46",
+               "v_mov_b32 v47, s45",
+               "v_mad_u64_u32 v[50:51], s[56:57], v46, v47, s[42:43]",
+               f"v_cndmask_b32 v{R0}, 0, v50, s[54:55]",
+               f"v_cndmask_b32 v{R0 + 1}, 0, v51, s[54:55]")
+        self.next_seq()
 
     def hash_mod_step(self):
         """v[50:51] = x (f64, integer < 2^48) -> v56 = x mod nb, with v[58:59]
@@ -602,7 +787,7 @@ class Gen:
                "s_load_dwordx8 s[64:71], %[maps], s85",
                "s_waitcnt lgkmcnt(0)",
                "s_cmp_lg_u32 s67, 0", f"s_cbranch_scc1 {L('slow')}",       # nbuckets >= 2^32
-               "v_add_u32 v41, s45, %[stklo]",
+               "v_add_u32 v41, s46, %[stklo]",
                "ds_read_b32 v44, v41", "ds_read_b32 v45, v41 offset:4",
                "ds_read_b32 v46, v41 offset:8", "ds_read_b32 v47, v41 offset:12",
                "s_mov_b64 s[60:61], exec",
@@ -654,31 +839,12 @@ class Gen:
                f"{done}:", "s_mov_b64 exec, s[60:61]")
         self.next_seq()
 
-    def rmw(self, sz, k):
-        """Fused counter (loader: ldx/add/stx, register dead after).  A wave
-        whose live lanes all add the same value to the same global address
-        adds popcount * value into the per-wave delta cache (two entries,
-        flushed by the C++ side); anything else leaves for C++ atomics."""
-        stg, glb = self.label("rs"), self.label("rg")
-        self.rd("s41", 48)
-        if k == "R":
-            self.rd("s44", 46)
-        else:
-            self.imm_y()
-        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[46:47]")
-        self.staged_or(sz, stg, glb)
-        self.e(f"{stg}:", f"s_branch {L('slow')}")   # a counter inside the unit's own bytes
-        self.e(f"{glb}:")
-        self.check(sz)
-        t1, t2, t3, done, lane = (self.label(x) for x in ("t1", "t2", "t3", "done", "lane"))
-        self.e("v_readfirstlane_b32 s62, v48", "v_readfirstlane_b32 s63, v49",
-               "v_cmp_ne_u64 s[54:55], s[62:63], v[48:49]",
-               "s_cmp_lg_u64 s[54:55], 0", f"s_cbranch_scc1 {lane}",
-               "s_cmp_eq_u32 s63, %[shi]", f"s_cbranch_scc1 {L('slow')}",   # LDS / scratch targets
-               "s_cmp_eq_u32 s63, %[phi]", f"s_cbranch_scc1 {L('slow')}",
-               "v_readfirstlane_b32 s64, v46", "v_readfirstlane_b32 s65, v47",
-               "v_cmp_ne_u64 s[54:55], s[64:65], v[46:47]",
-               "s_cmp_lg_u64 s[54:55], 0", f"s_cbranch_scc1 {lane}")
+    def counter_cache(self, sz, done):
+        """A0 = s[62:63] (uniform address), V0 = s[64:65] (uniform value):
+        add popcount(exec) * V0 into the per-wave delta cache (two entries,
+        flushed by the C++ side); both entries taken by other addresses ->
+        leave (C++ evicts one)."""
+        t1, t2, t3 = (self.label(x) for x in ("t1", "t2", "t3"))
         self.e("s_bcnt1_i32_b64 s69, exec",
                "s_mul_i32 s66, s64, s69", "s_mul_hi_u32 s67, s64, s69",
                "s_mul_i32 s70, s65, s69", "s_add_u32 s67, s67, s70",
@@ -697,26 +863,81 @@ class Gen:
                "s_cmp_eq_u64 %[c1a], 0", f"s_cbranch_scc0 {L('slow')}",      # both taken: C++ evicts
                "s_mov_b64 %[c1a], s[62:63]", "s_mov_b32 %[c1dl], s66", "s_mov_b32 %[c1dh], s67",
                f"s_mov_b32 %[c1s], {sz}",
-               f"s_branch {done}",
-               # lanes disagree on address or value: one atomic add per lane
-               f"{lane}:")
-        self.check_global(sz)
+               f"s_branch {done}")
+
+    def rmw_value(self, k):
+        if k == "R":
+            self.rd("s45", 46)
+        else:
+            self.e("v_mov_b32 v46, s47", "v_ashrrev_i32 v47, 31, v46")
+
+    def rmw(self, sz, k, mv=False):
+        """Fused counter (loader: ldx/add/stx, register dead after).  A wave
+        whose live lanes all add the same value to the same global address
+        adds popcount * value into the per-wave delta cache; otherwise each
+        lane adds through the LDS combining table.  mv: the base is a
+        non-null map-value pointer (no staging / window checks)."""
+        stg, glb = self.label("rs"), self.label("rg")
+        self.rd("s44", 48)
+        self.rmw_value(k)
+        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[42:43]")
+        if not mv:
+            self.staged_or(sz, stg, glb)
+            self.e(f"{stg}:", f"s_branch {L('slow')}")   # a counter inside the unit's own bytes
+            self.e(f"{glb}:")
+            self.check(sz)
+        done, lane = self.label("done"), self.label("lane")
+        self.e("v_readfirstlane_b32 s62, v48", "v_readfirstlane_b32 s63, v49",
+               "v_cmp_ne_u64 s[54:55], s[62:63], v[48:49]",
+               "s_cmp_lg_u64 s[54:55], 0", f"s_cbranch_scc1 {lane}")
+        if not mv:
+            self.e("s_cmp_eq_u32 s63, %[shi]", f"s_cbranch_scc1 {L('slow')}",   # LDS / scratch targets
+                   "s_cmp_eq_u32 s63, %[phi]", f"s_cbranch_scc1 {L('slow')}")
+        self.e("v_readfirstlane_b32 s64, v46", "v_readfirstlane_b32 s65, v47",
+               "v_cmp_ne_u64 s[54:55], s[64:65], v[46:47]",
+               "s_cmp_lg_u64 s[54:55], 0", f"s_cbranch_scc1 {lane}")
+        self.counter_cache(sz, done)
+        # lanes disagree on address or value: one add per lane
+        self.e(f"{lane}:")
+        if not mv:
+            self.check_global(sz)
         self.comb_add(sz)
-        self.e(f"{done}:",
-               "s_add_u32 s48, s78, s45", "s_addc_u32 s49, s79, 0")           # continue after the stx
+        self.e(f"{done}:", "s_mov_b32 s48, s46")           # continue after the stx
         self.dispatch()
 
-    def atomic(self, sz, op, fetch):
+    def rmwk(self, sz, k):
+        """Fused counter on a constant map-value address (lddw map_val +
+        offset, bound at load: w[2:3] = the address)."""
+        done, lane = self.label("done"), self.label("lane")
+        if k == "I":
+            self.e("s_mov_b32 s64, s47", "s_ashr_i32 s65, s47, 31")
+        else:
+            self.rd("s45", 46)
+            self.e("v_readfirstlane_b32 s64, v46", "v_readfirstlane_b32 s65, v47",
+                   "v_cmp_ne_u64 s[54:55], s[64:65], v[46:47]",
+                   "s_cmp_lg_u64 s[54:55], 0", f"s_cbranch_scc1 {lane}")
+        self.e("s_mov_b64 s[62:63], s[42:43]")
+        self.counter_cache(sz, done)
+        self.e(f"{lane}:")
+        if k == "R":
+            self.e("v_mov_b32 v48, s42", "v_mov_b32 v49, s43")
+            self.comb_add(sz)
+        self.e(f"{done}:", "s_mov_b32 s48, s46")
+        self.dispatch()
+
+    def atomic(self, sz, op, fetch, mv=False):
         """BPF_ATOMIC add/or/and/xor (+ BPF_FETCH) on global memory: one
         device-scope atomic per lane (array_map values, hash values).  LDS or
-        scratch targets and the unit's own staged bytes leave for C++."""
+        scratch targets and the unit's own staged bytes leave for C++.  mv:
+        the base is a non-null map-value pointer."""
         glb = self.label("ag")
-        self.rd("s41", 48)
-        self.rd("s44", 44)
-        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[46:47]")
-        self.staged_or(sz, L("slow"), glb)
-        self.e(f"{glb}:")
-        self.check_global(sz)
+        self.rd("s44", 48)
+        self.rd("s45", 44)
+        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[42:43]")
+        if not mv:
+            self.staged_or(sz, L("slow"), glb)
+            self.e(f"{glb}:")
+            self.check_global(sz)
         mn = op.lower() + ("_x2" if sz == 8 else "")
         val = "v[44:45]" if sz == 8 else "v44"
         if fetch:
@@ -724,7 +945,7 @@ class Gen:
                    "s_waitcnt vmcnt(0)")
             if sz == 4:
                 self.e("v_mov_b32 v47, 0")
-            self.wr("s44", 46)
+            self.wr("s45", 46)
         elif op == "ADD":
             self.e("v_mov_b32 v46, v44", "v_mov_b32 v47, v45")
             self.comb_add(sz)
@@ -752,14 +973,14 @@ class Gen:
 
     # ---- divergence: min-pc scheduling of lane groups ----
     # A split branch leaves the wave as the running group (IP, exec) plus up
-    # to two pending groups (s86/s87 = FInsn address bits 31:0, s[88:89] /
-    # s[90:91] = lane masks, s92 = count), sorted by address.  The running
-    # group always has the lowest pc; while any group is pending, dispatch
-    # goes through the divergent table, whose entries compare IP with the
-    # first pending pc: equal -> the groups merge (reconvergence), greater ->
-    # the running group is parked and the pending one runs.  A third pending
-    # group, or any instruction the asm does not run, hands every group's pc
-    # to the C++ divergent loop (exit reason 3).
+    # to two pending groups (s86/s87 = IPs, s[88:89] / s[90:91] = lane masks,
+    # s92 = count), sorted by IP.  The running group always has the lowest
+    # pc; while any group is pending, dispatch goes through the divergent
+    # table, whose entries compare IP with the first pending IP: equal -> the
+    # groups merge (reconvergence), greater -> the running group is parked
+    # and the pending one runs.  A third pending group, or any instruction
+    # the asm does not run, hands every group's pc to the C++ divergent loop
+    # (exit reason 3).
     def set_table(self, divergent):
         n4 = 4 * len(handler_ids())
         if divergent:
@@ -775,7 +996,7 @@ class Gen:
         self.e(f"{keep}:")
 
     def push(self):
-        """Park group (s69 = FInsn address bits 31:0, s[62:63] = lanes)."""
+        """Park group (s69 = IP, s[62:63] = lanes)."""
         nonempty, ne0, after0, two, done = (self.label(x) for x in ("pne", "pn0", "pa0", "p2", "pd"))
         self.e("s_cmp_eq_u32 s92, 0", f"s_cbranch_scc0 {nonempty}",
                "s_mov_b32 s86, s69", "s_mov_b64 s[88:89], s[62:63]", "s_mov_b32 s92, 1")
@@ -799,35 +1020,35 @@ class Gen:
     def materialize(self, extra):
         """Every group's pc (FInsn index) into the lpc output of its lanes,
         exec = all of them; exit reason 3."""
-        self.e("s_sub_u32 s52, s48, s78", "s_lshr_b32 s52, s52, 5", "v_mov_b32 %[lpc], s52",
+        self.e("s_lshr_b32 s52, s48, 5", "v_mov_b32 %[lpc], s52",
                "s_mov_b64 s[60:61], exec")
         if extra:
-            self.e("s_mov_b64 exec, s[62:63]", "s_sub_u32 s52, s69, s78", "s_lshr_b32 s52, s52, 5",
+            self.e("s_mov_b64 exec, s[62:63]", "s_lshr_b32 s52, s69, 5",
                    "v_mov_b32 %[lpc], s52", "s_or_b64 s[60:61], s[60:61], exec")
         for i, (pc, m) in enumerate((("s86", "s[88:89]"), ("s87", "s[90:91]"))):
             skip = self.label("mz")
             self.e(f"s_cmp_ge_u32 s92, {i + 1}", f"s_cbranch_scc0 {skip}",
-                   f"s_mov_b64 exec, {m}", f"s_sub_u32 s52, {pc}, s78", "s_lshr_b32 s52, s52, 5",
+                   f"s_mov_b64 exec, {m}", f"s_lshr_b32 s52, {pc}, 5",
                    "v_mov_b32 %[lpc], s52", "s_or_b64 s[60:61], s[60:61], exec", f"{skip}:")
         self.e("s_mov_b64 exec, s[60:61]", "s_mov_b32 s68, 3", f"s_branch {L('spill')}")
 
     def divergence_routines(self):
         n4 = 4 * len(handler_ids())
         back, spush, ahead = self.label("sback"), self.label("spush"), self.label("dahead")
-        # split branch: s[54:55] = taken lanes, W = the branch
+        # split branch: vcc = taken lanes, W = the branch
         self.e(f"{L('split')}:",
                "s_bitcmp1_b32 %[entry], 2", f"s_cbranch_scc0 {L('slow')}",
-               "s_andn2_b64 s[56:57], exec, s[54:55]",
-               "s_add_u32 s52, s78, s45",
-               "s_add_u32 s48, s48, 32", "s_addc_u32 s49, s49, 0",
-               "s_cmp_lt_u32 s52, s48", f"s_cbranch_scc1 {back}",
+               "s_andn2_b64 s[56:57], exec, vcc",
+               f"s_add_u32 s48, s48, {INSN}",
+               "s_cmp_lt_u32 s46, s48", f"s_cbranch_scc1 {back}",
                # forward: not-taken lanes run on, taken lanes wait at the target
-               "s_mov_b32 s69, s52", "s_mov_b64 s[62:63], s[54:55]", "s_mov_b64 exec, s[56:57]",
+               "s_mov_b32 s69, s46", "s_mov_b64 s[62:63], vcc", "s_mov_b64 exec, s[56:57]",
                f"s_branch {spush}",
                # backward (loop): taken lanes run on, the others wait after the branch
                f"{back}:",
-               "s_mov_b32 s69, s48", "s_mov_b64 s[62:63], s[56:57]", "s_mov_b64 exec, s[54:55]",
-               "s_mov_b32 s48, s52",
+               "s_mov_b32 s69, s48", "s_mov_b64 s[62:63], s[56:57]", "s_mov_b64 exec, vcc",
+               "s_mov_b32 s48, s46",
+               "s_add_u32 %[steps], %[steps], 1",
                "s_cmp_gt_u32 %[steps], %[limit]", f"s_cbranch_scc1 {L('steps')}",
                f"{spush}:")
         self.push()
@@ -838,7 +1059,6 @@ class Gen:
                f"s_sub_u32 s52, s52, {n4}", "s_subb_u32 s53, s53, 0",
                "s_setpc_b64 s[52:53]",
                f"{L('dswitch')}:",
-               "s_sub_u32 %[steps], %[steps], 1",            # the fetched insn did not run
                "s_cmp_eq_u32 s48, s86", f"s_cbranch_scc0 {ahead}",
                "s_or_b64 exec, exec, s[88:89]")                # reconvergence
         self.pop0()
@@ -859,7 +1079,7 @@ class Gen:
         # ---- entry ----
         e("s_mov_b64 s[78:79], %[prog]",
           "v_mov_b32 v40, %[rb]",
-          "s_lshl_b32 s52, %[pc], 5", "s_add_u32 s48, s78, s52", "s_addc_u32 s49, s79, 0",
+          "s_lshl_b32 s48, %[pc], 5",
           "s_mov_b64 s[58:59], exec", "s_mov_b64 exec, %[alive]",
           "s_mov_b32 s80, 0", "s_mov_b32 s81, 0", "s_mov_b32 s84, 0", "s_mov_b32 s92, 0",
           "s_mov_b32 s86, -1", "s_mov_b32 s87, -1",
@@ -881,9 +1101,11 @@ class Gen:
             else:
                 e(f"v_mov_b32 v{R0 + 2 * r}, 0", f"v_mov_b32 v{R0 + 2 * r + 1}, 0")
         e("s_bitcmp1_b32 %[entry], 1", f"s_cbranch_scc0 {loaded}",
-          "s_mov_b32 s80, 64")
-        for c in range(4):
-            e(f"global_load_dwordx4 v[{STG + 4 * c}:{STG + 4 * c + 3}], v[52:53], off offset:{16 * c}")
+          "s_mov_b32 s80, %[stage]",
+          f"global_load_dwordx4 v[{STG}:{STG + 3}], v[52:53], off")
+        for c in range(1, 4):
+            e(f"s_cmp_lt_u32 %[stage], {16 * (c + 1)}", f"s_cbranch_scc1 {loaded}",
+              f"global_load_dwordx4 v[{STG + 4 * c}:{STG + 4 * c + 3}], v[52:53], off offset:{16 * c}")
         e(f"{loaded}:",
           "s_getpc_b64 s[50:51]",          # = address of the s_branch below
           f"s_branch {L('start')}")
@@ -898,6 +1120,8 @@ class Gen:
             e(f"{L('h_' + name)}:")
             if name == "SLOW":
                 e(f"s_branch {L('slow')}")
+            elif name.startswith("ATOMMV"):
+                self.atomic(int(name[6]), "ADD", False, mv=True)
             elif name.startswith("ATOM"):
                 parts = name.split("_")
                 self.atomic(int(parts[0][4:]), parts[1], len(parts) == 3)
@@ -912,14 +1136,24 @@ class Gen:
                 self.next_seq()
             elif name in ("LDX_CTXDATA", "LDX_CTXEND"):
                 self.ctx_field(name == "LDX_CTXEND")
-            elif "_" in name and name.split("_")[1] in ("PKT", "SLOT", "STK"):
-                op, kind = name.split("_")
+            elif name in STAGED_LD:
+                self.ldxs(name)
+            elif name in STAGED_ST:
+                self.stxs(name)
+            elif name.endswith("_STK") and not name.startswith("CALL"):
+                op = name.split("_")[0]
                 if op.startswith("LDX"):
-                    self.ldx_static(int(op[3:]), kind)
+                    self.ldx_stk(int(op[3:]))
                 elif op.startswith("STX"):
-                    self.store_static(int(op[3:]), kind, True)
+                    self.store_stk(int(op[3:]), True)
                 else:
-                    self.store_static(int(op[2:]), kind, False)
+                    self.store_stk(int(op[2:]), False)
+            elif name.endswith("_MV"):
+                op = name.split("_")[0]
+                if op.startswith("LDX"):
+                    self.ldx_mv(int(op[3:]))
+                else:
+                    self.stx_mv(int(op[3:]))
             elif name.startswith("LDX"):
                 self.ldx(int(name[3:]))
             elif name.startswith("STX"):
@@ -934,8 +1168,14 @@ class Gen:
                 self.call_lookup()
             elif name == "CALL_LOOKUP_STK":
                 self.call_lookup(stack_key=True)
+            elif name == "CALL_LOOKUP_AK":
+                self.call_lookup_ak()
             elif name == "EXIT":
                 self.exit_()
+            elif name.startswith("RMWMV"):
+                self.rmw(int(name[5]), name[7], mv=True)
+            elif name.startswith("RMWK"):
+                self.rmwk(int(name[4]), name[6])
             elif name.startswith("RMW"):
                 self.rmw(int(name[3]), name[5])
             elif name[0] == "J":
@@ -944,12 +1184,12 @@ class Gen:
             else:
                 raise ValueError(name)
         self.divergence_routines()
-        # ---- exits: the instruction at pc was not executed (one step was
-        # counted at its dispatch); write back staging, spill registers
+        # ---- exits: the instruction at pc was not executed; write back
+        # staging, spill registers
         e(f"{L('steps')}:", "s_mov_b32 s68, 1")
         self.union_exec()
         e(f"s_branch {L('spill')}")
-        e(f"{L('slow')}:", "s_mov_b32 s68, 0", "s_sub_u32 %[steps], %[steps], 1",
+        e(f"{L('slow')}:", "s_mov_b32 s68, 0",
           "s_cmp_eq_u32 s92, 0", f"s_cbranch_scc1 {L('spill')}")
         self.materialize(extra=False)
         e(f"{L('spill')}:")
@@ -960,7 +1200,7 @@ class Gen:
           "s_waitcnt vmcnt(0) lgkmcnt(0)",
           "s_mov_b64 %[aliveout], exec",
           "s_mov_b64 exec, s[58:59]",
-          "s_sub_u32 s52, s48, s78", "s_lshr_b32 s52, s52, 5",
+          "s_lshr_b32 s52, s48, 5",
           "s_mov_b32 %[pc], s52", "s_mov_b32 %[why], s68")
         return ids
 
@@ -1000,12 +1240,14 @@ def main():
         for i, name in enumerate(ids):
             f.write(f"  F_{name} = {i},\n")
         f.write(f"  F_COUNT = {len(ids)}\n}};\n\n")
-        f.write("// 32-byte threaded instruction (gen_fast.py register map, word for word);\n"
-                "// dst_x2 / src_x2 are eBPF register numbers times two (VGPR pair index)\n"
-                "struct FInsn {\n  uint32_t hoff;\n  uint32_t dst_x2;\n  int64_t imm;\n  uint32_t src_x2;\n"
-                "  uint32_t target;\n  int64_t off;\n};\n"
+        f.write("// 32-byte threaded instruction (gen_fast.py register map, word for word):\n"
+                "//   dst_x2 / src_x2 are eBPF register numbers times two (VGPR pair index);\n"
+                "//   the staged / map-bound handlers reuse the fields as documented there\n"
+                "struct FInsn {\n  uint32_t hoff;\n  uint32_t w1;\n  int64_t imm;\n  uint32_t dst_x2;\n"
+                "  uint32_t src_x2;\n  uint32_t target;\n  int32_t aux;\n};\n"
                 "static_assert(sizeof(FInsn) == 32, \"FInsn must be 32 bytes\");\n\n"
-                "constexpr uint32_t kFastStageBytes = 64;  // staged bytes per unit\n\n"
+                f"constexpr uint32_t kFastInsnBytes = {INSN};\n"
+                "constexpr uint32_t kFastStageBytes = 64;  // max staged bytes per unit\n\n"
                 "}  // namespace bpftime_amd\n")
 
 

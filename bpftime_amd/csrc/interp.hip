@@ -396,6 +396,7 @@ struct FastEnv {
   uint32_t comb;    // LDS address of the block's combining table
   uint32_t combn;   // its entries (0: add straight to memory)
   uint32_t rb;      // LDS byte address of this lane's R[0]
+  uint32_t stage;   // staged bytes per unit (0: no staging)
 };
 
 constexpr uint32_t FAST_SLOW = 0, FAST_STEPS = 1, FAST_EXIT = 2, FAST_SPLIT = 3;
@@ -434,7 +435,8 @@ __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const Fas
                  [entry] "s"(entry), [r1lo] "v"((uint32_t)u.r1), [r1hi] "v"((uint32_t)(u.r1 >> 32)),
                  [r2lo] "v"(u.r2), [r10lo] "v"((uint32_t)u.r10), [r10hi] "v"((uint32_t)(u.r10 >> 32)),
                  [slotlo] "v"((uint32_t)u.slot), [slothi] "v"((uint32_t)(u.slot >> 32)),
-                 [head] "s"(f.head), [ulen] "v"(u.len), [stklo] "v"((uint32_t)u.r10), [comb] "s"(f.comb), [combn] "s"(f.combn)
+                 [head] "s"(f.head), [ulen] "v"(u.len), [stklo] "v"((uint32_t)u.r10), [comb] "s"(f.comb), [combn] "s"(f.combn),
+                 [stage] "s"(f.stage)
                : BPFTIME_AMD_FAST_CLOBBERS);
   c.pc = pc;
   c.steps = steps;
@@ -461,7 +463,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   SRP(prog); SRP(fast); SRP(maps); SRP(data); SRP(lens); SRP(verdicts); SRP(rets); SRP(out_data_off); SRP(out_len);
   SRP(err_count); SRV(n); SRV(stride); SRV(first_unit); SRV(data_lo); SRV(data_hi); SRV(arena_lo);
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
-  SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries);
+  SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
 #undef SRP
 #undef SRV
   __shared__ uint64_t Rf[12 * kBlock];  // r0..r10 + a dummy slot per lane
@@ -508,11 +510,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                           (uint32_t)((uint64_t)(uintptr_t)&big_stack[0] >> 32)))
                     : fe.shi;
   fe.rb = (uint32_t)(uintptr_t)&Rf[tid];
-
-  // stage each unit's first 64 B in VGPRs when slots are 16-B aligned and
-  // at least that long (gen_fast.py, unit staging)
-  const bool stage_ok = p.stride >= kFastStageBytes && (p.stride & 15) == 0 &&
-                        ((uint64_t)(uintptr_t)p.data & 15) == 0;
+  // the host sized the staged window (gen_fast.py, unit staging) from the
+  // program's static packet / slot accesses, 16-B aligned slots only
+  fe.stage = p.stage;
 
   const bool ordered = p.ordered != 0;
   const uint64_t ustep = ordered ? 1 : (uint64_t)gridDim.x * kBlock;
@@ -532,9 +532,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     fu.slot = slot;
     fu.r10 = stack_top;
     fu.len = len;
-    fu.entry = 1u | (stage_ok ? 2u : 0u) | (p.fast_div ? 4u : 0u);
+    fu.entry = 1u | (p.stage ? 2u : 0u) | (p.fast_div ? 4u : 0u);
     if (KIND == CTX_XDP) {
+      // the ctx only exists in LDS when the program reads it generically
+      // (loader: ctx uses other than the specialised data / data_end loads)
       XdpCtx *x = (XdpCtx *)my_ctx;
+      if (p.needs_ctx) {
       x->data = slot + p.head;
       x->data_end = slot + p.head + len;
       x->data_meta = 0;
@@ -543,6 +546,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       x->egress_ifindex = 0;
       x->buffer_start = slot;
       x->buffer_end = slot + p.stride;
+      }
       fu.r1 = (uint64_t)(uintptr_t)x;
       fu.r2 = 48;
     } else {
@@ -637,8 +641,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       }
       if (KIND == CTX_XDP) {
         const XdpCtx *x = (const XdpCtx *)my_ctx;
-        if (p.out_data_off) p.out_data_off[unit] = (int32_t)(x->data - slot);
-        if (p.out_len) p.out_len[unit] = (uint32_t)(x->data_end - x->data);
+        if (p.out_data_off) p.out_data_off[unit] = p.needs_ctx ? (int32_t)(x->data - slot) : (int32_t)p.head;
+        if (p.out_len) p.out_len[unit] = p.needs_ctx ? (uint32_t)(x->data_end - x->data) : len;
       }
     }
   }

@@ -9,6 +9,7 @@
 // read-modify-writes into one atomic add, sizing the per-lane stack -- are
 // described in DESIGN.md §3.
 #include "loader.hpp"
+#include "runtime.hpp"
 
 #include <errno.h>
 #include <stdarg.h>
@@ -444,6 +445,7 @@ int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &
     return -1;
   }
   std::vector<RawInsn> in(code, code + n);
+  out.lddw_src.assign(n, 0);
   // compat_ubpf.cpp:72-190
   for (size_t i = 0; i < n; i++) {
     RawInsn &cur = in[i];
@@ -504,6 +506,7 @@ int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &
       }
       cur.imm = (int32_t)(uint32_t)(imm & 0xffffffffu);
       nx.imm = (int32_t)(uint32_t)(imm >> 32);
+      out.lddw_src[i] = cur.src;
       cur.src = 0;
       i++;
     }
@@ -688,43 +691,73 @@ static uint32_t fast_id(const DInsn &d) {
 #undef JCC
 }
 
+
 // ---------------------------------------------------------------------------
 // Pointer kinds for the fast path (a small slice of what the kernel verifier
 // tracks): which registers hold the unit's slot, its packet data, its XDP
-// ctx or its stack, at a constant offset.  A load/store whose base has such
-// a kind gets a handler that needs no per-lane window check: packet / slot
-// bytes come from the staged VGPRs, ctx fields are computed from the unit's
-// slot / length, stack bytes are plain LDS accesses.
+// ctx, its stack, a map or a map value, at a constant offset.  A load/store
+// whose base has such a kind gets a handler that needs no per-lane window
+// check: packet / slot bytes come from the staged VGPRs (link_fast), ctx
+// fields are computed from the unit's slot / length, stack bytes are plain
+// LDS accesses, map values are plain global accesses.
 // ---------------------------------------------------------------------------
-// P_CONST: a wave-uniform constant (lddw immediates and map-value
-// addresses, plus constant offsets): counters behind it need no combining.
-enum PKind : uint8_t { P_UNDEF = 0, P_CTX, P_PKT, P_SLOT, P_STK, P_CONST, P_OTHER };
+// P_CONST: an lddw immediate (id = its pc) plus a constant offset k: a
+// wave-uniform constant, counters behind it need no combining.  P_MAPFD: lddw
+// of a map fd (id = the fd, as map_ptr_by_fd yields it).  P_MVNULL: the
+// result of map_lookup_elem before its null check; P_MAPVAL after it (id =
+// fd, k = offset into the value).  Map fds are bound at load time, as the
+// kernel binds BPF_PSEUDO_MAP_FD.
+enum PKind : uint8_t { P_UNDEF = 0, P_CTX, P_PKT, P_SLOT, P_STK, P_CONST, P_MAPFD, P_MVNULL, P_MAPVAL, P_OTHER };
 struct PVal {
   uint8_t kind;
   int32_t k;
-  bool operator==(const PVal &o) const { return kind == o.kind && k == o.k; }
+  int32_t id;
+  bool operator==(const PVal &o) const { return kind == o.kind && k == o.k && id == o.id; }
 };
+static const PVal kOther{P_OTHER, 0, 0};
 static PVal pjoin(PVal a, PVal b) {
   if (a.kind == P_UNDEF) return b;
   if (b.kind == P_UNDEF) return a;
-  return a == b ? a : PVal{P_OTHER, 0};
+  return a == b ? a : kOther;
 }
+
+static const MapRec *map_rec(int64_t fd) {
+  Runtime &r = rt();
+  if (fd < 0 || fd >= (int64_t)kMaxFds || r.kind[fd] != HKind::MAP) return nullptr;
+  return &r.maps[fd];
+}
+
+// [a, a+sz) inside the storage of an array map (map_val addresses)
+static bool in_array_storage(uint64_t a, uint32_t sz) {
+  Runtime &r = rt();
+  for (uint32_t fd = 0; fd < kMaxFds; fd++) {
+    if (r.kind[fd] != HKind::MAP) continue;
+    const MapRec &m = r.maps[fd];
+    if (m.type != MT_ARRAY && m.type != MT_PERCPU_ARRAY) continue;
+    if (a >= m.d.data && a + sz <= m.d.data + m.bytes) return true;
+  }
+  return false;
+}
+
+static bool is_cond_jump(uint8_t op) { return op >= X_JEQ && op <= X_JSLE; }
 
 // in[i][r]: kind of register r before instruction i; returns false when the
 // program may rewrite its ctx (then no ctx / packet kinds are trusted).
-static bool pointer_kinds(const std::vector<DInsn> &p, bool xdp, bool pkt_ok,
-                          std::vector<std::vector<PVal>> &in) {
+static bool pointer_kinds(const std::vector<DInsn> &p, const std::vector<uint8_t> &lddw_src, bool xdp,
+                          bool pkt_ok, std::vector<std::vector<PVal>> &in) {
   const uint32_t n = (uint32_t)p.size();
-  in.assign(n, std::vector<PVal>(11, PVal{P_UNDEF, 0}));
+  in.assign(n, std::vector<PVal>(11, PVal{P_UNDEF, 0, 0}));
   std::vector<bool> queued(n, false);
   std::vector<uint32_t> work;
-  for (int r = 0; r < 11; r++) in[0][r] = PVal{P_OTHER, 0};
-  in[0][1] = xdp ? PVal{P_CTX, 0} : PVal{P_SLOT, 0};
-  in[0][10] = PVal{P_STK, 0};
+  for (int r = 0; r < 11; r++) in[0][r] = kOther;
+  in[0][1] = xdp ? PVal{P_CTX, 0, 0} : PVal{P_SLOT, 0, 0};
+  in[0][10] = PVal{P_STK, 0, 0};
   work.push_back(0);
   queued[0] = true;
   bool ctx_written = false;
-  auto ptr = [](uint8_t k) { return k == P_CTX || k == P_PKT || k == P_SLOT || k == P_STK || k == P_CONST; };
+  auto ptr = [](uint8_t k) {
+    return k == P_CTX || k == P_PKT || k == P_SLOT || k == P_STK || k == P_CONST || k == P_MAPVAL;
+  };
   while (!work.empty()) {
     const uint32_t i = work.back();
     work.pop_back();
@@ -734,25 +767,25 @@ static bool pointer_kinds(const std::vector<DInsn> &p, bool xdp, bool pkt_ok,
     const bool w32 = (d.aux & A_W32) != 0, sreg = (d.aux & A_SRCREG) != 0;
     switch (d.op) {
       case X_MOV:
-        st[d.dst] = (sreg && !w32) ? st[d.src] : PVal{P_OTHER, 0};
+        st[d.dst] = (sreg && !w32) ? st[d.src] : kOther;
         break;
       case X_ADD:
       case X_SUB:
         if (ptr(st[d.dst].kind) && !sreg && !w32) {
           const int64_t k = (int64_t)st[d.dst].k + (d.op == X_ADD ? (int64_t)d.imm : -(int64_t)d.imm);
-          st[d.dst] = (k > -(1 << 20) && k < (1 << 20)) ? PVal{st[d.dst].kind, (int32_t)k} : PVal{P_OTHER, 0};
+          st[d.dst] = (k > -(1 << 20) && k < (1 << 20)) ? PVal{st[d.dst].kind, (int32_t)k, st[d.dst].id} : kOther;
         } else {
-          st[d.dst] = PVal{P_OTHER, 0};
+          st[d.dst] = kOther;
         }
         break;
       case X_LDX: {
         const PVal b = st[d.src];
         const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
-        PVal v{P_OTHER, 0};
+        PVal v = kOther;
         if (b.kind == P_CTX && sz == 8) {
           const int64_t at = (int64_t)b.k + d.off;
-          if (at == 0 && pkt_ok) v = PVal{P_PKT, 0};        // ctx->data
-          else if (at == 32) v = PVal{P_SLOT, 0};           // ctx->buffer_start
+          if (at == 0 && pkt_ok) v = PVal{P_PKT, 0, 0};        // ctx->data
+          else if (at == 32) v = PVal{P_SLOT, 0, 0};           // ctx->buffer_start
         }
         st[d.dst] = v;
         break;
@@ -764,15 +797,21 @@ static bool pointer_kinds(const std::vector<DInsn> &p, bool xdp, bool pkt_ok,
         break;
       case X_ATOMIC:
         if (st[d.dst].kind == P_CTX) ctx_written = true;
-        if (d.hi == 0xf1) st[0] = PVal{P_OTHER, 0};
-        else if (d.hi & 1) st[d.src] = PVal{P_OTHER, 0};
+        if (d.hi == 0xf1) st[0] = kOther;
+        else if (d.hi & 1) st[d.src] = kOther;
         break;
-      case X_CALL:
-        st[0] = PVal{P_OTHER, 0};  // r1-r5 survive (ubpf)
+      case X_CALL: {
+        // r1-r5 survive (ubpf); a lookup on a bound map yields a nullable value pointer
+        const PVal m = st[1];
+        st[0] = (d.hi == 1 && m.kind == P_MAPFD && map_rec(m.id)) ? PVal{P_MVNULL, 0, m.id} : kOther;
         break;
-      case X_LDDW:
-        st[d.dst] = PVal{P_CONST, 0};
+      }
+      case X_LDDW: {
+        const uint64_t v = (uint64_t)(uint32_t)d.imm | ((uint64_t)(uint32_t)d.hi << 32);
+        const bool fd = i < lddw_src.size() && lddw_src[i] == 1 && v < kMaxFds;
+        st[d.dst] = fd ? PVal{P_MAPFD, 0, (int32_t)v} : PVal{P_CONST, 0, (int32_t)i};
         break;
+      }
       case X_EXIT: case X_JA: case X_JEQ: case X_JGT: case X_JGE: case X_JSET: case X_JNE:
       case X_JSGT: case X_JSGE: case X_JLT: case X_JLE: case X_JSLT: case X_JSLE:
         break;
@@ -780,18 +819,31 @@ static bool pointer_kinds(const std::vector<DInsn> &p, bool xdp, bool pkt_ok,
         RegSet u, df;
         use_def(d, u, df);
         for (int r = 0; r < 11; r++)
-          if (df & (1u << r)) st[r] = PVal{P_OTHER, 0};
+          if (df & (1u << r)) st[r] = kOther;
         break;
       }
     }
     uint32_t sx[2];
     int ns;
     successors(p, i, sx, ns);
+    // null check of a lookup result: `if (r == 0)` / `if (r != 0)` refines r
+    // to a map-value pointer on the non-null edge
+    const bool nullchk = (d.op == X_JEQ || d.op == X_JNE) && !sreg && !w32 && d.imm == 0 &&
+                         st[d.dst].kind == P_MVNULL && d.tgt != i + 1;
     for (int j = 0; j < ns; j++) {
       const uint32_t t = sx[j];
+      std::vector<PVal> edge;
+      const std::vector<PVal> *src = &st;
+      if (nullchk) {
+        edge = st;
+        const bool taken = t == d.tgt;
+        const bool nonnull = d.op == X_JEQ ? !taken : taken;
+        edge[d.dst] = nonnull ? PVal{P_MAPVAL, 0, st[d.dst].id} : kOther;
+        src = &edge;
+      }
       bool changed = false;
       for (int r = 0; r < 11; r++) {
-        const PVal nv = pjoin(in[t][r], st[r]);
+        const PVal nv = pjoin(in[t][r], (*src)[r]);
         if (!(nv == in[t][r])) {
           in[t][r] = nv;
           changed = true;
@@ -806,27 +858,33 @@ static bool pointer_kinds(const std::vector<DInsn> &p, bool xdp, bool pkt_ok,
   return !ctx_written;
 }
 
-void build_fast(const std::vector<DInsn> &prog, bool xdp, bool big_stack, uint32_t stack_size,
-                std::vector<FInsn> &fast, uint32_t *specialized, bool *needs_comb) {
-  if (needs_comb) *needs_comb = true;
-  fast.assign(prog.size(), FInsn{});
+void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
+  const std::vector<DInsn> &prog = lo.prog;
+  out.fast.assign(prog.size(), FInsn{});
+  out.stat.assign(prog.size(), FStatic{});
+  out.specialized = 0;
+  out.needs_comb = true;
+  out.needs_ctx = xdp;
   for (size_t i = 0; i < prog.size(); i++) {
     const DInsn &d = prog[i];
-    FInsn &f = fast[i];
+    FInsn &f = out.fast[i];
+    const bool mem = d.op == X_LDX || d.op == X_ST || d.op == X_STX || d.op == X_ATOMIC || d.op == X_RMW_ADD;
     f.hoff = 4 + 4 * fast_id(d);
+    f.w1 = 0;
     f.dst_x2 = (uint32_t)d.dst * 2;
     f.src_x2 = (uint32_t)d.src * 2;
     f.imm = d.op == X_LDDW ? (int64_t)((uint64_t)(uint32_t)d.imm | ((uint64_t)(uint32_t)d.hi << 32))
+            : mem          ? (int64_t)d.off
                            : (int64_t)d.imm;
-    f.target = (uint32_t)d.tgt * (uint32_t)sizeof(FInsn);
-    f.off = (int64_t)d.off;
+    f.target = (uint32_t)d.tgt * kFastInsnBytes;
+    f.aux = d.imm;
   }
   // helpers that move ctx->data / data_end invalidate packet pointers
   bool pkt_ok = true;
   for (const DInsn &d : prog)
     if (d.op == X_CALL && (d.hi == 44 || d.hi == 65)) pkt_ok = false;
   std::vector<std::vector<PVal>> in;
-  if (!pointer_kinds(prog, xdp, pkt_ok, in)) return;  // ctx rewritten: generic handlers only
+  if (!pointer_kinds(prog, lo.lddw_src, xdp, pkt_ok, in)) return;  // ctx rewritten: generic handlers only
   // per-lane counter adds (fused counters, atomic adds without fetch) whose
   // target is not a wave-uniform constant use the LDS combining table
   bool comb = false;
@@ -835,58 +893,170 @@ void build_fast(const std::vector<DInsn> &prog, bool xdp, bool big_stack, uint32
     const bool add = d.op == X_RMW_ADD || (d.op == X_ATOMIC && d.hi == 0x00);
     if (add && in[i][d.dst].kind != P_CONST && in[i][d.dst].kind != P_UNDEF) comb = true;
   }
-  if (needs_comb) *needs_comb = comb;
+  out.needs_comb = comb;
   uint32_t nspec = 0;
+  bool ctx_escapes = false;
+  const bool big_stack = lo.big_stack;
+  const int64_t stack_size = lo.stack_size;
   for (size_t i = 0; i < prog.size(); i++) {
     const DInsn &d = prog[i];
-    if (d.op != X_LDX && d.op != X_STX && d.op != X_ST && d.op != X_CALL) continue;
     const std::vector<PVal> &st = in[i];
     if (st[0].kind == P_UNDEF && st[1].kind == P_UNDEF) continue;  // unreachable
     const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
     const uint32_t si = sz == 1 ? 0 : sz == 2 ? 1 : sz == 4 ? 2 : 3;
-    FInsn &f = fast[i];
+    const bool sreg = (d.aux & A_SRCREG) != 0;
+    FInsn &f = out.fast[i];
+    if (xdp) {
+      // the LDS ctx is needed unless the ctx pointer is only copied, offset
+      // by constants, compared, or read through the specialised data /
+      // data_end loads
+      RegSet u, df;
+      use_def(d, u, df);
+      for (int r = 0; r < 11; r++) {
+        if (!(u & (1u << r)) || st[r].kind != P_CTX) continue;
+        bool ok = false;
+        if (d.op == X_MOV) ok = sreg && r == d.src;
+        else if (d.op == X_ADD || d.op == X_SUB) ok = r == d.dst && !sreg && !(d.aux & A_W32);
+        else if (d.op == X_LDX) {
+          const int64_t at = (int64_t)st[r].k + d.off;
+          ok = r == d.src && pkt_ok && sz == 8 && (at == 0 || at == 8);
+        } else if (is_cond_jump(d.op) || d.op == X_EXIT) {
+          ok = true;
+        }
+        if (!ok) ctx_escapes = true;
+      }
+    }
     if (d.op == X_CALL) {
-      // array lookup with its key on the stack: key read straight from LDS
+      if (d.hi != 1) continue;
+      // lookup with its key on the stack: key read straight from LDS; an
+      // ARRAY map bound at load needs no map-table read at all
       const PVal key = st[2];
       const int64_t at = (int64_t)key.k;
-      if (d.hi == 1 && key.kind == P_STK && !big_stack && at >= -(int64_t)stack_size && at + 4 <= 0 &&
-          at % 4 == 0) {
-        f.hoff = 4 + 4 * F_CALL_LOOKUP_STK;
+      if (key.kind == P_STK && !big_stack && at >= -stack_size && at + 4 <= 0 && at % 4 == 0) {
+        const MapRec *m = st[1].kind == P_MAPFD ? map_rec(st[1].id) : nullptr;
+        if (m && m->type == MT_ARRAY) {
+          f.hoff = 4 + 4 * F_CALL_LOOKUP_AK;
+          f.imm = (int64_t)m->d.data;
+          f.dst_x2 = m->max_entries;
+          f.src_x2 = m->value_size;
+        } else {
+          f.hoff = 4 + 4 * F_CALL_LOOKUP_STK;
+        }
         f.target = (uint32_t)(int32_t)at;
         nspec++;
       }
       continue;
     }
+    if (d.op == X_RMW_ADD || (d.op == X_ATOMIC && d.hi == 0x00)) {
+      if (sz != 4 && sz != 8) continue;
+      const PVal b = st[d.dst];
+      const int64_t at = (int64_t)b.k + d.off;
+      const MapRec *m = b.kind == P_MAPVAL ? map_rec(b.id) : nullptr;
+      const bool in_value = m && at >= 0 && at + sz <= m->value_size;
+      if (d.op == X_ATOMIC) {
+        if (in_value) {
+          f.hoff = 4 + 4 * (sz == 8 ? F_ATOMMV8_ADD : F_ATOMMV4_ADD);
+          nspec++;
+        }
+        continue;
+      }
+      if (b.kind == P_CONST && lo.lddw_src[b.id] == 2) {
+        const DInsn &l = prog[b.id];
+        const uint64_t a = ((uint64_t)(uint32_t)l.imm | ((uint64_t)(uint32_t)l.hi << 32)) + (uint64_t)at;
+        if (a % sz == 0 && in_array_storage(a, sz)) {
+          f.hoff = 4 + 4 * (sz == 8 ? (sreg ? F_RMWK8_R : F_RMWK8_I) : (sreg ? F_RMWK4_R : F_RMWK4_I));
+          f.imm = (int64_t)a;
+          nspec++;
+        }
+      } else if (in_value) {
+        f.hoff = 4 + 4 * (sz == 8 ? (sreg ? F_RMWMV8_R : F_RMWMV8_I) : (sreg ? F_RMWMV4_R : F_RMWMV4_I));
+        nspec++;
+      }
+      continue;
+    }
+    if (d.op != X_LDX && d.op != X_STX && d.op != X_ST) continue;
     const PVal b = st[d.op == X_LDX ? d.src : d.dst];
     const int64_t at = (int64_t)b.k + d.off;
-    static const uint32_t ldp[4] = {F_LDX1_PKT, F_LDX2_PKT, F_LDX4_PKT, F_LDX8_PKT};
-    static const uint32_t stxp[4] = {F_STX1_PKT, F_STX2_PKT, F_STX4_PKT, F_STX8_PKT};
-    static const uint32_t stp[4] = {F_ST1_PKT, F_ST2_PKT, F_ST4_PKT, F_ST8_PKT};
-    static const uint32_t lds[4] = {F_LDX1_SLOT, F_LDX2_SLOT, F_LDX4_SLOT, F_LDX8_SLOT};
-    static const uint32_t stxs[4] = {F_STX1_SLOT, F_STX2_SLOT, F_STX4_SLOT, F_STX8_SLOT};
-    static const uint32_t sts[4] = {F_ST1_SLOT, F_ST2_SLOT, F_ST4_SLOT, F_ST8_SLOT};
     static const uint32_t ldk[4] = {F_LDX1_STK, F_LDX2_STK, F_LDX4_STK, F_LDX8_STK};
     static const uint32_t stxk[4] = {F_STX1_STK, F_STX2_STK, F_STX4_STK, F_STX8_STK};
     static const uint32_t stk[4] = {F_ST1_STK, F_ST2_STK, F_ST4_STK, F_ST8_STK};
-    const uint32_t *tab = nullptr;
+    static const uint32_t ldm[4] = {F_LDX1_MV, F_LDX2_MV, F_LDX4_MV, F_LDX8_MV};
+    static const uint32_t stxm[4] = {F_STX1_MV, F_STX2_MV, F_STX4_MV, F_STX8_MV};
     if ((b.kind == P_PKT || b.kind == P_SLOT) && at >= 0 && at + sz <= kFastStageBytes) {
-      // packet bytes: data = slot + head; the handler adds the batch head
-      if (b.kind == P_PKT) tab = d.op == X_LDX ? ldp : d.op == X_STX ? stxp : stp;
-      else tab = d.op == X_LDX ? lds : d.op == X_STX ? stxs : sts;
-    } else if (b.kind == P_STK && !big_stack && at >= -(int64_t)stack_size && at + sz <= 0 && at % sz == 0) {
-      tab = d.op == X_LDX ? ldk : d.op == X_STX ? stxk : stk;
+      // packet bytes: data = slot + head, resolved with the batch head
+      FStatic &s = out.stat[i];
+      s.kind = b.kind == P_PKT ? 1 : 2;
+      s.op = d.op == X_LDX ? 0 : d.op == X_STX ? 1 : 2;
+      s.sz = (uint8_t)sz;
+      s.at = (int32_t)at;
+      s.imm = d.imm;
+      nspec++;
+    } else if (b.kind == P_STK && !big_stack && at >= -stack_size && at + sz <= 0 && at % sz == 0) {
+      const uint32_t *tab = d.op == X_LDX ? ldk : d.op == X_STX ? stxk : stk;
+      f.hoff = 4 + 4 * tab[si];
+      f.target = (uint32_t)(int32_t)at;  // static byte offset from the stack top
+      nspec++;
     } else if (pkt_ok && b.kind == P_CTX && d.op == X_LDX && sz == 8 && (at == 0 || at == 8)) {
       // ctx->data = slot + head, ctx->data_end = data + len (interp.hip setup)
       f.hoff = 4 + 4 * (at == 0 ? F_LDX_CTXDATA : F_LDX_CTXEND);
       nspec++;
-      continue;
+    } else if (b.kind == P_MAPVAL && d.op != X_ST) {
+      const MapRec *m = map_rec(b.id);
+      if (m && at >= 0 && at + sz <= m->value_size) {
+        f.hoff = 4 + 4 * (d.op == X_LDX ? ldm[si] : stxm[si]);
+        nspec++;
+      }
     }
-    if (!tab) continue;
-    f.hoff = 4 + 4 * tab[si];
-    f.target = (uint32_t)(int32_t)at;  // static byte offset (signed for the stack)
-    nspec++;
   }
-  if (specialized) *specialized = nspec;
+  out.specialized = nspec;
+  out.needs_ctx = xdp && ctx_escapes;
+}
+
+static int64_t static_slot_offset(const FStatic &s, uint32_t head) {
+  return (int64_t)s.at + (s.kind == 1 ? (int64_t)head : 0);
+}
+
+uint32_t stage_need(const FastForm &f, uint32_t head) {
+  int64_t ext = 0;
+  for (const FStatic &s : f.stat) {
+    if (!s.kind) continue;
+    const int64_t so = static_slot_offset(s, head);
+    if (so >= 0 && so + s.sz <= (int64_t)kFastStageBytes) ext = std::max<int64_t>(ext, so + s.sz);
+  }
+  return (uint32_t)((ext + 15) & ~15);
+}
+
+void link_fast(const FastForm &f, uint32_t head, uint32_t stage, std::vector<FInsn> &out) {
+  out = f.fast;
+  if (!stage) return;
+  for (size_t i = 0; i < f.stat.size(); i++) {
+    const FStatic &s = f.stat[i];
+    if (!s.kind) continue;
+    const int64_t so = static_slot_offset(s, head);
+    if (so < 0 || so + s.sz > (int64_t)stage) continue;
+    const uint32_t o = (uint32_t)so, sz = s.sz, sh = 8 * (o & 3);
+    FInsn g = out[i];
+    g.imm = (int64_t)((uint64_t)(o >> 2) | ((uint64_t)sh << 32));  // w2 dword index, w3 bit shift
+    g.target = o;                                                // fallback: slot + o
+    if (s.op == 0) {
+      uint32_t id;
+      if (sz == 8) id = (o & 3) ? F_LDXS8U : F_LDXS8A;
+      else if ((o & 3) + sz <= 4) id = sz == 1 ? F_LDXS1 : sz == 2 ? F_LDXS2 : F_LDXS4;
+      else id = sz == 2 ? F_LDXS2X : F_LDXS4X;
+      g.hoff = 4 + 4 * id;
+    } else {
+      const bool fits = sz <= 2 ? (o & 3) + sz <= 4 : (o & 3) == 0;
+      if (!fits) continue;  // straddles dwords: the generic handler ends staging
+      static const uint32_t stx[4] = {F_STXS1, F_STXS2, F_STXS4, F_STXS8};
+      static const uint32_t sti[4] = {F_STS1, F_STS2, F_STS4, F_STS8};
+      const uint32_t si = sz == 1 ? 0 : sz == 2 ? 1 : sz == 4 ? 2 : 3;
+      g.hoff = 4 + 4 * (s.op == 1 ? stx[si] : sti[si]);
+      g.dst_x2 = (1u << (o >> 4)) | (1u << ((o + sz - 1) >> 4));     // dirty chunks
+      g.aux = sz <= 2 ? (int32_t)((((1u << (8 * sz)) - 1)) << sh) : 0;  // byte mask
+      if (s.op == 2) g.src_x2 = (uint32_t)s.imm;
+    }
+    out[i] = g;
+  }
 }
 
 }  // namespace bpftime_amd

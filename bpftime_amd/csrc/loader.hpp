@@ -27,9 +27,29 @@ struct LddwHelpers {
   uint64_t (*code_addr)(uint32_t) = nullptr;
 };
 
+// A packet / slot access at a constant offset (resolved per launch by
+// link_fast once the batch head and staged window are known).
+struct FStatic {
+  uint8_t kind = 0;  // 0 none, 1 packet (ctx->data + at), 2 slot (+ at)
+  uint8_t op = 0;    // 0 LDX, 1 STX, 2 ST
+  uint8_t sz = 0;
+  uint8_t pad = 0;
+  int32_t at = 0;
+  int32_t imm = 0;   // ST immediate
+};
+
+// Threaded-code form of a program for one entry convention.
+struct FastForm {
+  std::vector<FInsn> fast;     // templates (generic handlers for static accesses)
+  std::vector<FStatic> stat;   // per insn
+  uint32_t specialized = 0;    // accesses / calls with statically typed bases
+  bool needs_comb = true;      // per-lane counter adds (LDS combining table)
+  bool needs_ctx = true;       // XDP: the ctx must exist in LDS
+};
+
 struct LoadOut {
   std::vector<DInsn> prog;
-  std::vector<FInsn> fast;   // threaded-code form of `prog` (gen_fast.py)
+  std::vector<uint8_t> lddw_src;  // per pc: the lddw pseudo source (BPF_PSEUDO_MAP_FD = 1, ...)
   uint32_t stack_size = 8;   // per-lane bytes (LDS)
   bool big_stack = false;    // 512-B scratch stack
   uint32_t fused_rmw = 0;
@@ -42,10 +62,18 @@ bool device_helper_supported(uint32_t id);
 // Threaded-code records for the asm fast path: one per DInsn; instructions
 // without a fast handler dispatch to F_SLOW (the C++ interpreter).  `xdp`
 // selects the entry convention (r1 = XDP ctx, else r1 = the unit's slot);
-// loads/stores whose base pointer kind is known statically get
-// specialized handlers (count in *specialized).
-void build_fast(const std::vector<DInsn> &prog, bool xdp, bool big_stack, uint32_t stack_size,
-                std::vector<FInsn> &fast, uint32_t *specialized, bool *needs_comb);
+// loads/stores/calls whose base pointer kind is known statically get
+// specialized handlers (count in out.specialized).
+void build_fast(const LoadOut &lo, bool xdp, FastForm &out);
+
+// Staged bytes the static packet / slot accesses need for a batch head
+// (0..64, multiple of 16).
+uint32_t stage_need(const FastForm &f, uint32_t head);
+
+// Final FInsn array for one launch configuration: static accesses inside a
+// `stage`-byte window get the staged handlers (dword index, shift, masks
+// precomputed), the rest keep their generic templates.
+void link_fast(const FastForm &f, uint32_t head, uint32_t stage, std::vector<FInsn> &out);
 
 // Runs the compat_ubpf.cpp:61-200 patching (call remap check, lddw pseudo
 // sources), ubpf-style validation, pre-decoding and the dataflow analyses

@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -45,8 +46,13 @@ class Mi355xVm {
   bool loaded = false;
   LoadOut prog;
   DInsn *d_prog = nullptr;
-  FInsn *d_fast = nullptr;      // [XDP form | raw/syscall form], prog.prog.size() each
-  uint32_t spec_xdp = 0, spec_raw = 0;  // accesses with statically typed bases
+  // threaded-code forms: XDP entry (r1 = ctx) and raw/syscall entry (r1 = the
+  // unit's slot) differ in the loader's pointer kinds
+  FastForm fx, fr;
+  // linked FInsn arrays per launch configuration (entry form, staged bytes,
+  // batch head): a few per program, built on first use
+  std::mutex link_mu;
+  std::map<uint64_t, FInsn *> links;
   // failed-unit counters, one per in-flight batch: concurrent batches on
   // different streams must not share (and re-zero) one counter
   static constexpr uint32_t kErrSlots = 64;
@@ -71,8 +77,8 @@ class Mi355xVm {
   void unload() {
     if (d_prog) hipFree(d_prog);
     d_prog = nullptr;
-    if (d_fast) hipFree(d_fast);
-    d_fast = nullptr;
+    for (auto &kv : links) hipFree(kv.second);
+    links.clear();
     loaded = false;
     prog = LoadOut();
   }
@@ -108,20 +114,12 @@ class Mi355xVm {
       error = "no HIP device: " + rt().last_error;
       return -1;
     }
-    // two threaded-code forms: XDP entry (r1 = ctx) and raw/syscall entry
-    // (r1 = the unit's slot) differ in the loader's pointer kinds
-    std::vector<FInsn> fraw;
-    bool comb_x = true, comb_r = true;
-    build_fast(out.prog, true, out.big_stack, out.stack_size, out.fast, &spec_xdp, &comb_x);
-    build_fast(out.prog, false, out.big_stack, out.stack_size, fraw, &spec_raw, &comb_r);
-    out.comb_entries = (comb_x || comb_r) ? kComb : 0;
-    out.fast.insert(out.fast.end(), fraw.begin(), fraw.end());
+    build_fast(out, true, fx);
+    build_fast(out, false, fr);
+    out.comb_entries = (fx.needs_comb || fr.needs_comb) ? kComb : 0;
     size_t bytes = out.prog.size() * sizeof(DInsn);
-    size_t fbytes = out.fast.size() * sizeof(FInsn);
     if (hipMalloc((void **)&d_prog, bytes) != hipSuccess ||
-        hipMemcpy(d_prog, out.prog.data(), bytes, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMalloc((void **)&d_fast, fbytes) != hipSuccess ||
-        hipMemcpy(d_fast, out.fast.data(), fbytes, hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(d_prog, out.prog.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
       error = "device upload failed";
       return -1;
     }
@@ -132,6 +130,25 @@ class Mi355xVm {
     prog = std::move(out);
     loaded = true;
     return 0;
+  }
+
+  // the FInsn array for (entry form, staged bytes, head), linked on first use
+  const FInsn *linked(bool xdp, uint32_t head, uint32_t stage) {
+    std::lock_guard<std::mutex> g(link_mu);
+    const uint64_t key = ((uint64_t)xdp << 63) | ((uint64_t)stage << 40) | (stage ? head : 0);
+    auto it = links.find(key);
+    if (it != links.end()) return it->second;
+    std::vector<FInsn> out;
+    link_fast(xdp ? fx : fr, head, stage, out);
+    FInsn *d = nullptr;
+    const size_t bytes = out.size() * sizeof(FInsn);
+    if (hipMalloc((void **)&d, bytes) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, out.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+      hipFree(d);
+      return nullptr;
+    }
+    links[key] = d;
+    return d;
   }
 
   int exec_batch(const ebpf_batch *b);
@@ -152,13 +169,22 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   Runtime &r = rt();
   KParams p{};
   p.prog = d_prog;
-  p.fast = d_fast + (b->ctx_kind == CTX_XDP ? 0 : prog.prog.size());
   {
-    // the asm keeps pending lane groups by FInsn address bits 31:0: only
-    // when the array does not straddle a 4 GiB boundary
-    const uint64_t lo = (uint64_t)(uintptr_t)p.fast, hi = lo + prog.prog.size() * sizeof(FInsn);
-    p.fast_div = (lo >> 32) == ((hi - 1) >> 32) ? 1 : 0;
-    if (getenv("BPFTIME_AMD_NO_ASM_DIVERGENCE")) p.fast_div = 0;
+    // staged window: what the static packet / slot accesses need, when every
+    // slot is 16-B aligned and at least that long (a window never reaches
+    // into the next unit)
+    const bool xdp = b->ctx_kind == CTX_XDP;
+    const uint32_t head = xdp ? b->head : 0;
+    const uint32_t need = stage_need(xdp ? fx : fr, head);
+    const bool aligned = (b->stride % 16) == 0 && ((uint64_t)(uintptr_t)b->data % 16) == 0;
+    p.stage = (need && aligned && b->stride >= need && !getenv("BPFTIME_AMD_NO_STAGING")) ? need : 0;
+    p.fast = linked(xdp, head, p.stage);
+    if (!p.fast) {
+      error = "device upload failed";
+      return -1;
+    }
+    p.needs_ctx = xdp && fx.needs_ctx ? 1 : 0;
+    p.fast_div = getenv("BPFTIME_AMD_NO_ASM_DIVERGENCE") ? 0 : 1;
   }
   p.maps = r.d_maptab;
   p.data = (uint8_t *)b->data;
@@ -451,7 +477,7 @@ int bpftime_amd_vm_info(const struct ebpf_vm *vm, uint32_t *stack_size, int *big
 
 int bpftime_amd_vm_fast_info(const struct ebpf_vm *vm, uint32_t ctx_kind, uint32_t *specialized) {
   if (!vm || !vm->impl->loaded) return -1;
-  if (specialized) *specialized = ctx_kind == CTX_XDP ? vm->impl->spec_xdp : vm->impl->spec_raw;
+  if (specialized) *specialized = ctx_kind == CTX_XDP ? vm->impl->fx.specialized : vm->impl->fr.specialized;
   return 0;
 }
 

@@ -43,8 +43,9 @@ def test_xdp_counter_parity(fresh_oracle, fresh_runtime, n):
     ov, os_, dv, ds, failed, vm = run_xdp_both(po, dev, code, slots)
     assert failed == 0
     assert vm.info()["fused_rmw"] == 1
-    # stack store + lookup key, ctx data/data_end, 6 packet loads, 6 stores
-    assert vm.fast_specialized(dev.CTX_XDP) == 16
+    # stack store, bound-map lookup, flag load through the non-null value,
+    # constant-address counter, ctx data/data_end, 6 packet loads, 6 stores
+    assert vm.fast_specialized(dev.CTX_XDP) == 18
     np.testing.assert_array_equal(dv, ov)
     np.testing.assert_array_equal(ds, os_)
     assert (dv == isa.XDP_TX).all()
