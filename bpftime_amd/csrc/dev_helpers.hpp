@@ -402,4 +402,15 @@ __device__ __forceinline__ void flush_delta(uint64_t a, uint32_t sz, uint64_t de
   }
 }
 
+// one tagged delta {address | (4-byte ? 1 : 0), delta} (LDS combining
+// table entries, the block's combined wave caches)
+__device__ __forceinline__ void flush_delta_tag(uint64_t tag, uint64_t delta) {
+  if (!tag || !delta) return;
+  if (tag & 1)
+    __hip_atomic_fetch_add((uint32_t *)(uintptr_t)(tag & ~1ull), (uint32_t)delta, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  else
+    __hip_atomic_fetch_add((uint64_t *)(uintptr_t)tag, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace bpftime_amd

@@ -231,7 +231,14 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     int occ = bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn);
     if (occ < 1) occ = 1;
     uint64_t want = (b->count + kBlock - 1) / kBlock;
-    uint64_t cap = (uint64_t)cus * (uint64_t)occ;
+    // resident blocks x BPFTIME_AMD_GRID_MULT (default 1): more blocks than
+    // fit at once only add per-block setup for a grid-stride loop
+    static uint32_t mult = 0;
+    if (!mult) {
+      const char *g = getenv("BPFTIME_AMD_GRID_MULT");
+      mult = g && atoi(g) > 0 ? (uint32_t)atoi(g) : 1;
+    }
+    uint64_t cap = (uint64_t)cus * (uint64_t)occ * mult;
     grid = (uint32_t)(want < cap ? want : cap);
   }
   hipError_t e = bpftime_amd_launch_interp(&p, b->ctx_kind, prog.big_stack, grid, ordered ? 1 : 0, s);
