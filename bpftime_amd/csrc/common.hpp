@@ -4,6 +4,13 @@
 #pragma once
 #include <stdint.h>
 
+// functions shared by the host runtime (g++) and the kernel (hipcc)
+#ifdef __HIPCC__
+#define BA_HD __host__ __device__
+#else
+#define BA_HD
+#endif
+
 namespace bpftime_amd {
 
 constexpr uint32_t kMaxInsts = 65536;   // vm/vm-core/include/ebpf-vm.h:33-35
@@ -65,21 +72,39 @@ constexpr uint32_t MT_PERCPU_ARRAY = 6;
 //   HASH/PERCPU_HASH  nbuckets = next_prime(max_entries) slots of slot_size:
 //                  [u32 state][u32 pad][key, padded to 8][value(s), padded to 8]
 //                  state 0 = empty, 1 = filled, 2 = being written
+//                  ix: lookup index beside that layout (see ix_pos), 0 = none
 struct DMap {
   uint32_t type;
   uint32_t key_size;
   uint32_t value_size;
   uint32_t max_entries;
   uint64_t data;        // device address
-  uint64_t nbuckets;
+  uint32_t nbuckets;
+  uint32_t ix_mask;     // lookup index entries - 1 (a power of two minus one)
   uint32_t slot_size;
   uint32_t key_off;     // = 8
   uint32_t val_off;     // = 8 + round8(key_size)
   uint32_t ncpu;        // per-CPU slot count
   uint64_t count_addr;  // device address of the u64 element counter (hash)
-  uint64_t reserved;
+  uint64_t ix;          // device address of the u32 lookup index, 0 = not valid
 };
 static_assert(sizeof(DMap) == 64, "DMap must be 64 bytes");
+
+// Hash-map lookup index.  bpftime_hash_map's linear probing (kept as the
+// storage layout, so get_next_key walks buckets in the reference's order)
+// degrades to cluster walks of thousands of slots as the table fills (65536
+// flows in 65537 buckets at config 3).  Beside it sits an open-addressing
+// table of u32 {bucket + 1} entries, at most half full, keyed by a mix of the
+// same h*31 hash: a lookup that finds its key through it returns the slot the
+// reference probe would return, because the index only holds keys that
+// probe reaches (no deletions since the index was built, or a rebuild that
+// skipped keys orphaned by deletions, bpftime_hash_map.hpp:182-199).
+// Anything else falls back to the reference probe.
+inline BA_HD uint32_t ix_pos(uint64_t h, uint32_t mask) {
+  uint32_t g = ((uint32_t)h ^ ((uint32_t)(h >> 32) * 0x85EBCA6Bu)) * 0x9E3779B1u;
+  return (g ^ (g >> 16)) & mask;
+}
+constexpr uint32_t kIxProbes = 8;  // index probes before the reference probe
 
 // Context kinds for a batch
 constexpr uint32_t CTX_RAW = 0;      // r1 = unit memory, r2 = length

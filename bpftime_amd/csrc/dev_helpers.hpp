@@ -139,8 +139,23 @@ constexpr uint32_t ST_EMPTY = 0, ST_FILLED = 1, ST_BUSY = 2;
 __device__ uint64_t hash_find(const DMap &m, uint64_t key, bool insert, uint64_t init,
                               uint32_t init_bytes, bool *inserted) {
   *inserted = false;
-  uint64_t nb = m.nbuckets;
-  uint64_t idx = key_hash(key, m.key_size) % nb;
+  const uint64_t nb = m.nbuckets;
+  const uint64_t h = key_hash(key, m.key_size);
+  if (m.ix) {
+    // lookup index (common.hpp ix_pos): a hit is the slot the reference
+    // probe below would reach; an empty entry or too many probes fall
+    // through to that probe (an insert in flight is only indexed after it
+    // is published)
+    uint32_t p = ix_pos(h, m.ix_mask);
+    for (uint32_t t = 0; t < kIxProbes; t++) {
+      const uint32_t e = ald32(m.ix + 4ull * p);
+      if (!e) break;
+      const uint64_t s = m.data + (uint64_t)(e - 1) * m.slot_size;
+      if (ald32(s) == ST_FILLED && key_eq(s + m.key_off, key, m.key_size, false)) return s;
+      p = (p + 1) & m.ix_mask;
+    }
+  }
+  uint64_t idx = h % nb;
   uint64_t start = idx;
   uint32_t spins = 0;
   for (;;) {
@@ -181,6 +196,16 @@ __device__ uint64_t hash_find(const DMap &m, uint64_t key, bool insert, uint64_t
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // key/value stores drained first
         __hip_atomic_store(G32(s), ST_FILLED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (m.ix) {  // index the new element (at most nbuckets entries: never full)
+          uint32_t p = ix_pos(h, m.ix_mask);
+          for (uint32_t t = 0; t <= m.ix_mask; t++) {
+            uint32_t z = 0;
+            if (__hip_atomic_compare_exchange_strong(G32(m.ix + 4ull * p), &z, (uint32_t)idx + 1, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+              break;
+            p = (p + 1) & m.ix_mask;
+          }
+        }
         *inserted = true;
         return s;
       }

@@ -780,13 +780,51 @@ class Gen:
                "v_cndmask_b32 v50, v50, v42, vcc", "v_cndmask_b32 v51, v51, v43, vcc",
                "v_cvt_u32_f64 v56, v[50:51]")
 
+    def index_probe(self, kd, done):
+        """The map's lookup index (common.hpp ix_pos), if it has one: up to
+        kIxProbes entries from ix_pos(h) until every lane has found its key
+        (r0 = that slot's value).  An empty entry in any lane, or too many
+        probes, hands the whole wave to the reference probe that follows
+        (h stays in v[48:49]; lanes that already hit are recomputed there)."""
+        loop, fail = self.label("ixl"), self.label("ixf")
+        self.e("s_cmp_eq_u64 s[74:75], 0", f"s_cbranch_scc1 {fail}",
+               "s_mov_b32 s85, 0x85ebca6b", "v_mul_lo_u32 v41, v49, s85", "v_xor_b32 v41, v41, v48",
+               "s_mov_b32 s85, 0x9e3779b1", "v_mul_lo_u32 v41, v41, s85",
+               "v_lshrrev_b32 v50, 16, v41", "v_xor_b32 v41, v41, v50", "v_and_b32 v41, s67, v41",
+               "s_mov_b32 s85, 0",
+               f"{loop}:",
+               "v_mad_u64_u32 v[42:43], s[56:57], v41, 4, s[74:75]",
+               "global_load_dword v50, v[42:43], off sc1",
+               "s_waitcnt vmcnt(0)",
+               "v_cmp_eq_u32 s[56:57], 0, v50",                                 # empty entry
+               "s_cmp_lg_u64 s[56:57], 0", f"s_cbranch_scc1 {fail}",
+               "v_add_u32 v50, -1, v50",
+               "v_mov_b32 v51, s68",
+               "v_mad_u64_u32 v[54:55], s[56:57], v50, v51, s[64:65]",           # slot
+               "global_load_dword v51, v[54:55], off sc1",
+               "global_load_dwordx4 v[56:59], v[54:55], off offset:8 sc1",
+               "s_waitcnt vmcnt(0)",
+               "v_cmp_eq_u32 s[56:57], 1, v51")                                 # FILLED
+        for j in range(kd):
+            self.e(f"v_cmp_eq_u32 vcc, v{56 + j}, v{44 + j}", "s_and_b64 s[56:57], s[56:57], vcc")
+        self.e("s_and_saveexec_b64 s[62:63], s[56:57]",                         # exec = hits
+               f"v_add_co_u32 v{R0}, vcc, s70, v54", f"v_addc_co_u32 v{R0 + 1}, vcc, 0, v55, vcc",
+               "s_andn2_b64 exec, s[62:63], s[56:57]",                          # exec = other keys
+               f"s_cbranch_execz {done}",
+               "v_add_u32 v41, 1, v41", "v_and_b32 v41, s67, v41",
+               "s_add_u32 s85, s85, 1", "s_cmp_ge_u32 s85, 8", f"s_cbranch_scc1 {fail}",
+               f"s_branch {loop}",
+               f"{fail}:", "s_mov_b64 exec, s[60:61]")
+
     def hash_lookup(self):
         done, bail = self.label("hdone"), self.label("hbail")
-        # DMap words 4-11: data, nbuckets, slot_size, key_off, val_off, ncpu
+        # DMap words 4-11: data, nbuckets, ix_mask, slot_size, key_off,
+        # val_off, ncpu; words 14-15: lookup index (0 = none)
         self.e("s_lshl_b32 s85, s62, 6", "s_add_u32 s85, s85, 16",
                "s_load_dwordx8 s[64:71], %[maps], s85",
+               "s_add_u32 s85, s85, 40",
+               "s_load_dwordx2 s[74:75], %[maps], s85",
                "s_waitcnt lgkmcnt(0)",
-               "s_cmp_lg_u32 s67, 0", f"s_cbranch_scc1 {L('slow')}",       # nbuckets >= 2^32
                "v_add_u32 v41, s46, %[stklo]",
                "ds_read_b32 v44, v41", "ds_read_b32 v45, v41 offset:4",
                "ds_read_b32 v46, v41 offset:8", "ds_read_b32 v47, v41 offset:12",
@@ -802,6 +840,7 @@ class Gen:
                        "v_sub_co_u32 v48, vcc, v50, v48", "v_subb_co_u32 v49, vcc, v51, v49, vcc",
                        f"v_bfe_u32 v50, v{44 + i // 4}, {8 * (i % 4)}, 8",
                        "v_add_co_u32 v48, vcc, v48, v50", "v_addc_co_u32 v49, vcc, 0, v49, vcc")
+            self.index_probe(kd, done)
             # idx = h % nbuckets: h = ((hi * 2^16 + lo >> 16) * 2^16 + lo & 0xffff)
             self.e("v_cvt_f64_u32 v[58:59], s66", "v_rcp_f64 v[54:55], v[58:59]",
                    "v_cvt_f64_u32 v[50:51], v49")

@@ -464,6 +464,7 @@ int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &
               ") has no device implementation at PC " + std::to_string(i);
         return -EINVAL;
       }
+      if (cur.imm == 3) out.may_delete = true;
     } else if (cur.code == 0x18) {
       if (i + 1 == n) {
         err = "Unable to patch lddw instructions at " + std::to_string(i) + ", it's the last instruction";

@@ -54,6 +54,7 @@ struct LoadOut {
   bool big_stack = false;    // 512-B scratch stack
   uint32_t fused_rmw = 0;
   uint32_t comb_entries = 0;  // per-block LDS combining entries (0 = none needed)
+  bool may_delete = false;    // calls map_delete_elem: hash lookup indexes stop being valid
 };
 
 // Helper ids the device implements (interp.hip helper switch).

@@ -12,6 +12,7 @@
 #include <errno.h>
 #include <stdlib.h>
 #include <string.h>
+#include <set>
 
 #include <algorithm>
 #include <vector>
@@ -147,6 +148,86 @@ static int64_t host_hash_find(const MapRec &m, const void *key, std::vector<uint
   return -1;
 }
 
+void ix_invalidate(int fd) {
+  Runtime &r = rt();
+  MapRec &m = r.maps[fd];
+  if (!m.ix_addr || !m.ix_valid) return;
+  m.ix_valid = false;
+  m.d.ix = 0;
+  r.push_map(fd);
+  r.ix_stale.insert(fd);
+}
+
+// Rebuild from the table: index exactly the keys the reference probe
+// (bpftime_hash_map.hpp:127-151: from hash % nb, linear, stop at an empty
+// bucket) reaches, i.e. a filled bucket whose key's home bucket lies in the
+// same run of filled buckets at or before it, first occurrence of a key
+// only.  One pass over the runs, starting after an empty bucket; a table
+// without an empty bucket keeps no index.
+static int ix_rebuild(int fd) {
+  Runtime &r = rt();
+  MapRec &m = r.maps[fd];
+  if (hipDeviceSynchronize() != hipSuccess) return -1;  // no batch still writing the table
+  const uint64_t nb = m.d.nbuckets, ss = m.d.slot_size;
+  std::vector<uint8_t> t(m.bytes);
+  if (hipMemcpy(t.data(), (void *)m.d.data, m.bytes, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  auto state = [&](uint64_t i) {
+    uint32_t st;
+    memcpy(&st, t.data() + i * ss, 4);
+    return st;
+  };
+  uint64_t e0 = nb;
+  for (uint64_t i = 0; i < nb; i++)
+    if (state(i) != 1) {
+      e0 = i;
+      break;
+    }
+  r.ix_stale.erase(fd);
+  if (e0 == nb) return 0;  // full table: no index (lookups take the reference probe)
+  const uint64_t isz = (uint64_t)m.d.ix_mask + 1;
+  std::vector<uint32_t> ix(isz, 0);
+  std::set<std::string> run_keys;
+  uint64_t run_start = 1;  // distance from e0 of the current run's first bucket
+  for (uint64_t k = 1; k < nb; k++) {
+    const uint64_t i = (e0 + k) % nb;
+    if (state(i) != 1) {
+      run_keys.clear();
+      run_start = k + 1;
+      continue;
+    }
+    const uint8_t *key = t.data() + i * ss + m.d.key_off;
+    const uint64_t h = hash_bytes(key, m.key_size);
+    const uint64_t home = (h % nb + nb - e0) % nb;  // distance from e0
+    if (home < run_start || home > k) continue;       // orphaned by a deletion
+    if (!run_keys.insert(std::string((const char *)key, m.key_size)).second) continue;  // shadowed
+    uint32_t p = ix_pos(h, m.d.ix_mask);
+    while (ix[p]) p = (p + 1) & m.d.ix_mask;
+    ix[p] = (uint32_t)i + 1;
+  }
+  if (hipMemcpy((void *)m.ix_addr, ix.data(), 4 * isz, hipMemcpyHostToDevice) != hipSuccess) return -1;
+  m.ix_valid = true;
+  m.d.ix = m.ix_addr;
+  return r.push_map(fd);
+}
+
+int Runtime::prepare_ix(bool may_delete) {
+  std::lock_guard<std::mutex> g(mu);
+  if (may_delete) {
+    for (int fd = 0; fd < (int)kMaxFds; fd++)
+      if (kind[fd] == HKind::MAP && maps[fd].ix_valid) ix_invalidate(fd);
+    return 0;
+  }
+  while (!ix_stale.empty()) {
+    const int fd = *ix_stale.begin();
+    if (kind[fd] != HKind::MAP || !maps[fd].ix_addr) {
+      ix_stale.erase(fd);
+      continue;
+    }
+    if (ix_rebuild(fd) < 0) return -1;
+  }
+  return 0;
+}
+
 }  // namespace bpftime_amd
 
 using namespace bpftime_amd;
@@ -228,6 +309,19 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
   d.data = base;
   d.count_addr = extra ? base + ((m.bytes + 127) & ~127ull) : 0;
   if (hipMemset((void *)base, 0, m.bytes + extra + 8) != hipSuccess) return -1;
+  if (extra && !getenv("BPFTIME_AMD_NO_HASH_INDEX")) {
+    // lookup index (common.hpp ix_pos): a power of two >= 2 x buckets, so
+    // it is at most half full; an empty table's index is empty and valid
+    uint64_t isz = 64;
+    while (isz < 2 * (uint64_t)d.nbuckets) isz <<= 1;
+    uint64_t ix = isz <= (1ull << 32) ? r.arena_alloc(4 * isz) : 0;
+    if (ix && hipMemset((void *)ix, 0, 4 * isz) == hipSuccess) {
+      m.ix_addr = ix;
+      m.ix_valid = true;
+      d.ix = ix;
+      d.ix_mask = (uint32_t)(isz - 1);
+    }
+  }
   r.maps[fd] = m;
   r.kind[fd] = HKind::MAP;
   if (r.push_map(fd) < 0) return -1;
@@ -310,6 +404,7 @@ long bpftime_map_update_elem(int fd, const void *key, const void *value, uint64_
     }
     case MT_HASH: {
       // fix_hash_map.cpp:34-39 -> bpftime_hash_map::elem_update; returns 0
+      ix_invalidate(fd);
       std::vector<uint8_t> slot;
       int64_t empty;
       int64_t idx = host_hash_find(*m, key, slot, &empty);
@@ -336,6 +431,7 @@ long bpftime_map_update_elem(int fd, const void *key, const void *value, uint64_
         errno = EINVAL;
         return -1;
       }
+      ix_invalidate(fd);
       std::vector<uint8_t> slot;
       int64_t empty;
       int64_t idx = host_hash_find(*m, key, slot, &empty);
@@ -390,6 +486,7 @@ long bpftime_map_delete_elem(int fd, const void *key) {
         }
         return 0;  // fix_hash_map.cpp:41-45 returns 0 regardless
       }
+      ix_invalidate(fd);
       uint32_t st = 0;
       memcpy(slot.data(), &st, 4);
       write_slot(*m, (uint64_t)idx, slot);
@@ -529,6 +626,7 @@ int bpftime_amd_map_snapshot(int fd, void *out, uint64_t bytes) {
 int bpftime_amd_map_restore(int fd, const void *in, uint64_t bytes) {
   MapRec *m = map_of(fd);
   if (!m || bytes > m->bytes) return -1;
+  ix_invalidate(fd);
   if (hipMemcpy((void *)m->d.data, in, bytes, hipMemcpyHostToDevice) != hipSuccess) return -1;
   if (m->d.count_addr) {
     uint64_t c = 0;

@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -19,6 +20,8 @@ struct MapRec {
   uint64_t flags = 0;
   DMap d{};
   uint64_t bytes = 0;  // storage bytes at d.data
+  uint64_t ix_addr = 0;    // hash lookup index storage (common.hpp ix_pos), 0 = none
+  bool ix_valid = false;   // d.ix = ix_addr while the index holds exactly the reachable keys
 };
 
 struct ProgRec {
@@ -49,7 +52,14 @@ struct Runtime {
   int ensure_device();          // lazily picks the current device, allocates arena + table
   uint64_t arena_alloc(uint64_t bytes);
   int push_map(int fd);         // upload DMap entry for fd
+  std::set<int> ix_stale;       // hash maps whose lookup index needs a rebuild
+  // before a launch: a program that can delete invalidates every hash
+  // lookup index; any other rebuilds the stale ones
+  int prepare_ix(bool may_delete);
 };
+
+// hash lookup index upkeep for host-side writes (maps.cpp)
+void ix_invalidate(int fd);
 
 Runtime &rt();
 void set_error(const std::string &e);

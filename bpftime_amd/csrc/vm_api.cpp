@@ -215,6 +215,10 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     error = "hipMemsetAsync failed";
     return -1;
   }
+  if (r.prepare_ix(prog.may_delete) < 0) {
+    error = "hash lookup index rebuild failed";
+    return -1;
+  }
   const bool ordered = (b->flags & EBPF_BATCH_ORDERED) != 0;
   uint32_t grid = 1;
   if (!ordered) {

@@ -196,3 +196,117 @@ def test_percpu_hash_update_lookup(fresh_oracle, fresh_runtime):
     assert vm.exec_batch(dev.CTX_RAW, d, n, 8, fixed_len=8, rets=dr, flags=dev.BATCH_SYNC | dev.BATCH_ORDERED) == 0
     np.testing.assert_array_equal(dr.download(np.uint64), o)
     assert {k: v for k, v in dm.hash_items().items()} == om.items()
+
+
+# ---- hash lookup index (common.hpp ix_pos): same results as the reference
+# probe, including keys orphaned by deletions (bpftime_hash_map.hpp:182-199)
+
+def _ref_hash(key: bytes) -> int:
+    h = 0
+    for b in key:
+        h = (h * 31 + b) & ((1 << 64) - 1)
+    return h
+
+
+def _lookup_prog(fd):
+    """r0 = *(u64 *)lookup(map, *(u32 *)unit) or 0xdead on a miss (raw ctx)."""
+    a = Asm().ldx(4, 2, 1, 0).stx(4, 10, -4, "r2").mov64(2, "r10").add64(2, -4).ld_map_fd(1, fd).call(1)
+    a.jmp("jeq", 0, 0, "miss").ldx(8, 0, 0, 0).exit()
+    return a.label("miss").mov64(0, 0xDEAD).exit().assemble()
+
+
+def _delete_prog(fd):
+    a = Asm().ldx(4, 2, 1, 0).stx(4, 10, -4, "r2").mov64(2, "r10").add64(2, -4).ld_map_fd(1, fd).call(3)
+    return a.mov64(0, 0).exit().assemble()
+
+
+def _run_raw_both(po, dev, code, keys):
+    units = np.zeros((len(keys), 16), np.uint8)
+    units[:, :4] = np.array(keys, np.uint32).view(np.uint8).reshape(-1, 4)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    want = ovm.run_raw(units.copy(), 16)
+    vm = dev.VM()
+    vm.load(code)
+    d = dev.DeviceBuffer.from_array(units)
+    dr = dev.DeviceBuffer(8 * len(keys))
+    assert vm.exec_batch(dev.CTX_RAW, d, len(keys), 16, fixed_len=16, rets=dr) == 0
+    return dr.download(np.uint64), want
+
+
+def test_hash_index_orphaned_keys(fresh_oracle, fresh_runtime):
+    """Host deletes orphan a colliding key: the device (index rebuilt at the
+    next launch) must miss it exactly like the reference probe."""
+    po, dev = fresh_oracle, fresh_runtime
+    (om,), (dm,) = make_maps([(isa.BPF_MAP_TYPE_HASH, 4, 8, 10)], po, dev)
+    nb = dm.geometry()[0]
+    by_home = {}
+    for k in range(1, 5000):
+        by_home.setdefault(_ref_hash(I32(k)) % nb, []).append(k)
+    a, b, c = next(v for v in by_home.values() if len(v) >= 3)[:3]
+    other = [k for v in by_home.values() for k in v if k not in (a, b, c)][:4]
+    for m in (om, dm):
+        for k in (a, b, c, *other):
+            m.update(I32(k), I64(k * 10))
+    probe = [a, b, c, *other, 777777] * 40
+    got, want = _run_raw_both(po, dev, _lookup_prog(dm.fd), probe)
+    np.testing.assert_array_equal(got, want)
+    for m in (om, dm):
+        m.delete(I32(a))          # b and c are now unreachable
+    got, want = _run_raw_both(po, dev, _lookup_prog(dm.fd), probe)
+    np.testing.assert_array_equal(got, want)
+    assert (got[1::len(probe) // 40] == 0xDEAD).all()
+    for m in (om, dm):
+        m.update(I32(c), I64(5))  # re-inserted at a's bucket, shadows the orphan
+    got, want = _run_raw_both(po, dev, _lookup_prog(dm.fd), probe)
+    np.testing.assert_array_equal(got, want)
+    # the table now holds c twice (the orphan and the shadowing copy), so
+    # compare what lookups see, as the oracle's items() does
+    o_items = om.items()
+    assert {k: dm.lookup(k) for k in o_items} == o_items
+
+
+def test_hash_index_device_deletes(fresh_oracle, fresh_runtime):
+    """A program that deletes invalidates the index; lookups afterwards
+    (index rebuilt from the table) agree with the oracle."""
+    po, dev = fresh_oracle, fresh_runtime
+    (om,), (dm,) = make_maps([(isa.BPF_MAP_TYPE_HASH, 4, 8, 64)], po, dev)
+    keys = list(range(1000, 1060))
+    for m in (om, dm):
+        for k in keys:
+            m.update(I32(k), I64(k))
+    got, want = _run_raw_both(po, dev, _delete_prog(dm.fd), keys[::3])
+    np.testing.assert_array_equal(got, want)
+    got, want = _run_raw_both(po, dev, _lookup_prog(dm.fd), keys * 8)
+    np.testing.assert_array_equal(got, want)
+    o_items = om.items()  # keys orphaned by the deletes map to None
+    assert {k: dm.lookup(k) for k in o_items} == o_items
+
+
+@pytest.mark.parametrize("index", [True, False])
+def test_flow_hash_full_table(fresh_oracle, fresh_runtime, monkeypatch, index):
+    """A nearly full table (config 3's shape at small size): two
+    passes, the second all hits through the lookup index, equal to the
+    oracle with and without the index."""
+    if not index:
+        monkeypatch.setenv("BPFTIME_AMD_NO_HASH_INDEX", "1")
+    po, dev = fresh_oracle, fresh_runtime
+    nflows = 1024
+    (om,), (dm,) = _flow_setup(po, dev, nflows_max=nflows)
+    code = programs.flow_hash(dm.fd)
+    n = 40000
+    slots, lens = gen.flow_packets(n, nflows=nflows, stride=2048)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    vm = dev.VM()
+    vm.load(code)
+    d = dev.DeviceBuffer.from_array(slots)
+    dl = dev.DeviceBuffer.from_array(lens)
+    dv = dev.DeviceBuffer(4 * n)
+    for _ in range(2):
+        ov = ovm.run_xdp(slots.copy(), lens=lens)
+        assert vm.exec_batch(dev.CTX_XDP, d, n, 2048, lens=dl, verdicts=dv) == 0
+        np.testing.assert_array_equal(dv.download(np.uint32), ov)
+    assert _duplicate_keys(dm) == 0
+    assert dm.hash_items() == om.items()
+    assert dm.count() == len(om.items())
