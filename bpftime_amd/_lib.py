@@ -87,6 +87,23 @@ SIGNATURES = [
     ("bpftime_amd_vm_info", C.c_int, [C.c_void_p, u32p, C.POINTER(C.c_int), u32p, u32p]),
     ("bpftime_amd_set_step_limit", None, [C.c_void_p, C.c_uint64]),
     ("bpftime_amd_vm_fast_info", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    ("bpftime_object_open", C.c_void_p, [C.c_char_p]),
+    ("bpftime_object_open_mem", C.c_void_p, [C.c_void_p, C.c_size_t, C.c_char_p]),
+    ("bpftime_object_error", C.c_char_p, [C.c_void_p]),
+    ("bpftime_object_load_relocate_btf", C.c_int, [C.c_void_p, C.c_char_p]),
+    ("bpftime_object_load_relocate_btf_mem", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("bpftime_object_map_count", C.c_int, [C.c_void_p]),
+    ("bpftime_object_map_info", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(BpfMapAttr)]),
+    ("bpftime_object_program_count", C.c_int, [C.c_void_p]),
+    ("bpftime_object_program_info", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
+                                              C.POINTER(C.c_int), C.POINTER(C.c_size_t)]),
+    ("bpftime_object_program_insns", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.c_void_p, C.c_size_t]),
+    ("bpftime_object_load", C.c_int, [C.c_void_p]),
+    ("bpftime_object_find_program_by_name", C.c_int, [C.c_void_p, C.c_char_p]),
+    ("bpftime_object_find_program_by_secname", C.c_int, [C.c_void_p, C.c_char_p]),
+    ("bpftime_object_find_map_fd_by_name", C.c_int, [C.c_void_p, C.c_char_p]),
+    ("bpftime_object_license", C.c_char_p, [C.c_void_p]),
+    ("bpftime_object_close", None, [C.c_void_p]),
     ("bpftime_amd_merge_delta_u64", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     ("bpftime_amd_device_count", C.c_int, []),
     ("bpftime_amd_set_device", C.c_int, [C.c_int]),

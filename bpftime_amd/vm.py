@@ -86,6 +86,16 @@ class Map:
             raise EbpfError(f"map create failed: {_err()}")
         self.type, self.key_size, self.value_size, self.max_entries = type_, key_size, value_size, max_entries
 
+    @classmethod
+    def from_fd(cls, fd: int) -> "Map":
+        """Wrap a map record created elsewhere (e.g. by BpfObject.load)."""
+        if not lib().bpftime_is_map_fd(fd):
+            raise EbpfError(f"fd {fd} is not a map")
+        m = cls.__new__(cls)
+        m.fd = fd
+        m.type = m.key_size = m.value_size = m.max_entries = None
+        return m
+
     @property
     def user_value_size(self) -> int:
         return lib().bpftime_map_value_size_from_syscall(self.fd)

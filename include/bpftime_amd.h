@@ -105,6 +105,45 @@ void bpftime_amd_set_step_limit(struct ebpf_vm *vm, uint64_t limit);
  * fast path under the given ctx kind (packet, slot, ctx or stack bases) */
 int bpftime_amd_vm_fast_info(const struct ebpf_vm *vm, uint32_t ctx_kind, uint32_t *specialized);
 
+/* ---- eBPF ELF objects (csrc/object.cpp) ----
+ * The reference opens objects with libbpf (runtime/object/bpftime_object.hpp:
+ * bpftime_object_open / _close / _find_program_by_name / _by_secname,
+ * bpf_object.cpp:149-260) and relies on libbpf's bpf_object__load for map
+ * creation, map / global-data relocation and CO-RE before BPF_PROG_LOAD
+ * reaches its syscall server.  These entry points do both: open parses the
+ * object (programs, BTF / legacy maps, .bss/.data/.rodata, .rel sections,
+ * .BTF.ext CO-RE field relocations against the target BTF); load creates the
+ * maps and prog records (bpftime_maps_create / bpftime_progs_create) so the
+ * programs run through bpftime_amd_prog_instantiate / bpftime_link_create.
+ * Programs are addressed by prog fd (the reference returns bpftime_prog *). */
+struct bpftime_object;
+/* NULL only if the file cannot be read; parse errors: bpftime_object_error()
+ * non-empty and every other call fails */
+struct bpftime_object *bpftime_object_open(const char *obj_path);
+struct bpftime_object *bpftime_object_open_mem(const void *buf, size_t len, const char *obj_name);
+const char *bpftime_object_error(const struct bpftime_object *obj);
+/* target BTF for CO-RE (libbpf's btf_custom_path, e.g. the xdp-counter
+ * example's base.btf); default: the runtime's own xdp_md layout */
+int bpftime_object_load_relocate_btf(struct bpftime_object *obj, const char *btf_path);
+int bpftime_object_load_relocate_btf_mem(struct bpftime_object *obj, const void *btf, size_t len);
+int bpftime_object_map_count(const struct bpftime_object *obj);
+int bpftime_object_map_info(const struct bpftime_object *obj, int idx, const char **name,
+                            struct bpf_map_attr *attr);
+int bpftime_object_program_count(const struct bpftime_object *obj);
+int bpftime_object_program_info(const struct bpftime_object *obj, int idx, const char **name,
+                                const char **secname, int *prog_type, size_t *insn_cnt);
+/* the relocated instructions of program idx for the given map fds (one per
+ * object map, map_info order); returns the instruction count or -1 */
+int bpftime_object_program_insns(const struct bpftime_object *obj, int idx, const int *map_fds, void *out,
+                                 size_t insn_cap);
+/* create the maps (initialised from .data/.rodata) and prog records; 0 / -1 */
+int bpftime_object_load(struct bpftime_object *obj);
+int bpftime_object_find_program_by_name(const struct bpftime_object *obj, const char *name);      /* prog fd */
+int bpftime_object_find_program_by_secname(const struct bpftime_object *obj, const char *secname); /* prog fd */
+int bpftime_object_find_map_fd_by_name(const struct bpftime_object *obj, const char *name);
+const char *bpftime_object_license(const struct bpftime_object *obj);
+void bpftime_object_close(struct bpftime_object *obj);
+
 /* ---- host merge of per-GPU map shards ---- */
 /* acc += shard - init over u64 words (array counters, additive rule) */
 int bpftime_amd_merge_delta_u64(void *acc, const void *init, const void *shard, uint64_t bytes);
