@@ -274,9 +274,9 @@ class Gen:
         self.e("v_lshrrev_b32 v41, 3, v48", "s_mov_b32 s69, 0x9e3779b1", "v_mul_lo_u32 v41, v41, s69",
                "v_lshrrev_b32 v41, 24, v41", "v_lshlrev_b32 v41, 4, v41", "v_add_u32 v41, %[comb], v41",
                "v_mov_b32 v42, 0", "v_mov_b32 v43, 0")
-        for attempt in range(2):
-            if attempt:
-                self.e("v_xor_b32 v41, 16, v41")              # the neighbouring entry
+        for attempt in range(4):
+            if attempt:                                       # entries e^1, e^2, e^3 (one 64-B group)
+                self.e(f"v_xor_b32 v41, {48 if attempt == 2 else 16}, v41")
             self.e("ds_cmpst_rtn_b64 v[50:51], v41, v[42:43], v[54:55]",      # claim if empty
                    "s_waitcnt lgkmcnt(0)",
                    "v_cmp_eq_u64 s[56:57], 0, v[50:51]",
@@ -292,6 +292,42 @@ class Gen:
                "s_andn2_b64 exec, s[60:61], s[54:55]", f"s_cbranch_execz {done}")
         self.e("global_atomic_add_x2 v[48:49], v[46:47], off" if sz == 8 else "global_atomic_add v[48:49], v46, off",
                f"{done}:", "s_mov_b64 exec, s[60:61]")
+
+    def comb_peel(self, sz):
+        """Per-lane adds of Y to addresses Z (exec = the adding lanes).  When
+        every lane adds the same value (a counter += constant), lanes that
+        share the first lane's address are folded into one add of
+        popcount * value by that lane, up to four distinct addresses per
+        wave (Zipf-hot keys put most of a wave on a few map values); the
+        rest add lane by lane (comb_add).  Masks survive comb_add in lanes
+        of v56."""
+        loop, rest, out = self.label("pl"), self.label("pr"), self.label("po")
+        self.e("v_writelane_b32 v56, exec_lo, 2", "v_writelane_b32 v56, exec_hi, 3",
+               "v_readfirstlane_b32 s64, v46", "v_readfirstlane_b32 s65, v47",
+               "v_cmp_ne_u64 s[54:55], s[64:65], v[46:47]",
+               "s_cmp_lg_u64 s[54:55], 0", f"s_cbranch_scc1 {rest}",       # values differ
+               "s_mov_b32 s85, 0",
+               f"{loop}:",
+               "s_ff1_i32_b64 s69, exec",
+               "v_readlane_b32 s62, v48, s69", "v_readlane_b32 s63, v49, s69",
+               "v_cmp_eq_u64 s[54:55], s[62:63], v[48:49]",
+               "s_bcnt1_i32_b64 s70, s[54:55]",
+               "s_cmp_lt_u32 s70, 2", f"s_cbranch_scc1 {rest}",             # no sharing left
+               "s_andn2_b64 s[56:57], exec, s[54:55]",
+               "v_writelane_b32 v56, s56, 0", "v_writelane_b32 v56, s57, 1",
+               "s_mul_i32 s66, s64, s70", "s_mul_hi_u32 s67, s64, s70",
+               "s_mul_i32 s71, s65, s70", "s_add_u32 s67, s67, s71",
+               "s_lshl_b64 exec, 1, s69",                                   # the first lane adds for all
+               "v_mov_b32 v46, s66", "v_mov_b32 v47, s67")
+        self.comb_add(sz)
+        self.e("v_readlane_b32 s56, v56, 0", "v_readlane_b32 s57, v56, 1",
+               "s_mov_b64 exec, s[56:57]",
+               f"s_cbranch_execz {out}",
+               "s_add_u32 s85, s85, 1", "s_cmp_lt_u32 s85, 4", f"s_cbranch_scc1 {loop}",
+               f"{rest}:")
+        self.comb_add(sz)
+        self.e(f"{out}:", "v_readlane_b32 s56, v56, 2", "v_readlane_b32 s57, v56, 3",
+               "s_mov_b64 exec, s[56:57]")
 
     def flush(self, clear=True):
         """Write dirty staged chunks back to the slots of the exec lanes."""
@@ -940,7 +976,7 @@ class Gen:
         self.e(f"{lane}:")
         if not mv:
             self.check_global(sz)
-        self.comb_add(sz)
+        self.comb_peel(sz)
         self.e(f"{done}:", "s_mov_b32 s48, s46")           # continue after the stx
         self.dispatch()
 
@@ -986,8 +1022,8 @@ class Gen:
                 self.e("v_mov_b32 v47, 0")
             self.wr("s45", 46)
         elif op == "ADD":
-            self.e("v_mov_b32 v46, v44", "v_mov_b32 v47, v45")
-            self.comb_add(sz)
+            self.e("v_mov_b32 v46, v44", "v_mov_b32 v47, v45" if sz == 8 else "v_mov_b32 v47, 0")
+            self.comb_peel(sz)
         else:
             self.e(f"global_atomic_{mn} v[48:49], {val}, off")
         self.next_seq()
