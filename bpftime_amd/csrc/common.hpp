@@ -18,7 +18,8 @@ constexpr uint32_t kStackSize = 512;    // ebpf-vm.h:47-49
 constexpr uint32_t kMaxFds = 1024;      // device map table size
 constexpr uint32_t kBlock = 256;        // threads per workgroup (4 waves)
 constexpr uint32_t kLdsStackMax = 64;   // per-lane stack bytes kept in LDS
-constexpr uint32_t kComb = 256;         // per-block LDS combining entries (counter adds)
+constexpr uint32_t kComb = 256;         // per-block LDS combining entries (counter adds), minimum
+constexpr uint32_t kCombMax = 4096;     // ... and maximum (a power of two in between, vm_api.cpp)
 
 // Internal (pre-decoded) opcodes.  The device switch dispatches on these; the
 // set is dense so the compiler's binary search over cases stays shallow.

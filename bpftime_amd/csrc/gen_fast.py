@@ -260,9 +260,9 @@ class Gen:
         entries of {tag = address | size bit, delta}, flushed by the block at
         its end): Zipf-hot counters cost an LDS add instead of a same-address
         device atomic per lane (those serialize at the memory side).  Entry =
-        a multiplicative hash of the address, second try in the neighbour;
-        lanes finding both taken by other addresses, and misaligned
-        addresses, add to memory directly."""
+        a multiplicative hash of the address, then the other seven entries of
+        its 128-B group; lanes finding all eight taken by other addresses,
+        and misaligned addresses, add to memory directly."""
         done, direct = self.label("cd"), self.label("cx")
         self.e("s_mov_b64 s[60:61], exec", "s_mov_b64 s[54:55], 0",
                "s_cmp_eq_u32 %[combn], 0", f"s_cbranch_scc1 {direct}",
@@ -272,11 +272,12 @@ class Gen:
         if sz == 4:
             self.e("v_or_b32 v54, 1, v54", "v_mov_b32 v47, 0")
         self.e("v_lshrrev_b32 v41, 3, v48", "s_mov_b32 s69, 0x9e3779b1", "v_mul_lo_u32 v41, v41, s69",
-               "v_lshrrev_b32 v41, 24, v41", "v_lshlrev_b32 v41, 4, v41", "v_add_u32 v41, %[comb], v41",
+               "s_ff1_i32_b32 s69, %[combn]", "s_sub_u32 s69, 32, s69",          # 32 - log2(entries)
+               "v_lshrrev_b32 v41, s69, v41", "v_lshlrev_b32 v57, 4, v41", "v_add_u32 v41, %[comb], v57",
                "v_mov_b32 v42, 0", "v_mov_b32 v43, 0")
-        for attempt in range(4):
-            if attempt:                                       # entries e^1, e^2, e^3 (one 64-B group)
-                self.e(f"v_xor_b32 v41, {48 if attempt == 2 else 16}, v41")
+        for attempt in range(8):
+            if attempt:                                       # entries e^1 .. e^7 (one 128-B group)
+                self.e(f"v_xor_b32 v57, {16 * (attempt ^ (attempt - 1))}, v57", "v_add_u32 v41, %[comb], v57")
             self.e("ds_cmpst_rtn_b64 v[50:51], v41, v[42:43], v[54:55]",      # claim if empty
                    "s_waitcnt lgkmcnt(0)",
                    "v_cmp_eq_u64 s[56:57], 0, v[50:51]",

@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <string>
@@ -206,6 +207,27 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   p.fixed_len = b->fixed_len;
   p.stack_size = prog.stack_size;
   p.comb_entries = prog.comb_entries;
+  if (p.comb_entries) {
+    // the largest combining table (256 .. kCombMax entries) that keeps two
+    // blocks (8 waves) resident per CU: a counter that finds no entry is a
+    // device atomic, serialized with every other add to its address, so
+    // table reach beats occupancy (r01c sweep: flow-hash 256 -> 2048
+    // entries 2.1 -> 0.6 ms per 2^22 packets)
+    static std::map<uint64_t, uint32_t> best;  // (kind, big stack, stack bytes) -> entries
+    const uint64_t key = ((uint64_t)b->ctx_kind << 40) | ((uint64_t)prog.big_stack << 32) | prog.stack_size;
+    auto it = best.find(key);
+    if (it == best.end()) {
+      auto dyn = [&](uint32_t e) {
+        return kBlock * ((b->ctx_kind == CTX_XDP ? 48 : 0) + (prog.big_stack ? 0 : prog.stack_size)) + 16 * (size_t)e;
+      };
+      const int base = std::min(2, bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn(kComb)));
+      uint32_t e = kComb;
+      while (e < kCombMax && bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn(2 * e)) >= base) e *= 2;
+      if (getenv("BPFTIME_AMD_COMB_ENTRIES")) e = (uint32_t)atoi(getenv("BPFTIME_AMD_COMB_ENTRIES"));
+      it = best.emplace(key, e).first;
+    }
+    p.comb_entries = it->second;
+  }
   p.ncpu = r.ncpu;
   p.ifindex = b->ingress_ifindex;
   p.rxq = b->rx_queue_index;

@@ -67,7 +67,20 @@ def flow():
     parse = bytes(full[:8 * (look - 3)]) + Asm().mov64(0, 3).exit().assemble()
     vm = dev.VM(); vm.load(full)
     vm.exec_batch(dev.CTX_XDP, pk, N, stride, lens=dl, verdicts=dv)
-    for name, c in (("r0=2", Asm().mov64(0, 2).exit().assemble()), ("full", full)):
+    def patch(code, nop_atomics, no_lookup):
+        c = bytearray(code)
+        first_call = True
+        for i in range(0, len(c), 8):
+            if nop_atomics and c[i] == 0xDB:
+                c[i:i + 8] = bytes([0xBF, 0x00, 0, 0, 0, 0, 0, 0])      # mov64 r0, r0
+            if no_lookup and c[i] == 0x85 and first_call:
+                c[i:i + 8] = bytes([0xB7, 0x00, 0, 0, 1, 0, 0, 0])      # mov64 r0, 1
+                first_call = False
+        return bytes(c)
+    for name, c in (("r0=2", Asm().mov64(0, 2).exit().assemble()),
+                    ("parse+key", patch(full, True, True)),
+                    ("+lookup", patch(full, True, False)),
+                    ("full", full)):
         vm = dev.VM(); vm.load(c)
         try:
             ms = timeit(vm, dev.CTX_XDP, pk, stride, lens=dl, verdicts=dv)
