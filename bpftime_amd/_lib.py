@@ -35,7 +35,8 @@ class EbpfBatch(C.Structure):  # include/ebpf-vm.h struct ebpf_batch
                 ("fixed_len", C.c_uint32), ("ingress_ifindex", C.c_uint32),
                 ("rx_queue_index", C.c_uint32), ("head", C.c_uint32), ("verdicts", C.c_void_p),
                 ("rets", C.c_void_p), ("data_off_out", C.c_void_p), ("len_out", C.c_void_p),
-                ("first_unit", C.c_uint64), ("stream", C.c_void_p)]
+                ("first_unit", C.c_uint64), ("stream", C.c_void_p), ("descs", C.c_void_p),
+                ("umem_bytes", C.c_uint64)]
 
 
 # (name, restype, argtypes) for every exported symbol of include/*.h

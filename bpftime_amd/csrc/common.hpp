@@ -143,6 +143,8 @@ struct KParams {
   uint32_t ordered;       // 1 = a single lane runs the units in index order
   uint32_t stage;         // bytes of each unit staged in VGPRs by the fast path (0 = none)
   uint32_t needs_ctx;     // XDP: the program reads its ctx generically (build it in LDS)
+  const uint64_t *descs;  // AF_XDP descriptors {u64 addr; u32 len; u32 options} or nullptr
+  uint64_t umem_bytes;    // descriptor mode: bytes at data
 };
 
 // Error codes recorded per unit (err_count counts units with any error)

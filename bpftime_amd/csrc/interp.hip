@@ -464,6 +464,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   SRP(err_count); SRV(n); SRV(stride); SRV(first_unit); SRV(data_lo); SRV(data_hi); SRV(arena_lo);
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
+  SRP(descs); SRV(umem_bytes);
 #undef SRP
 #undef SRV
   __shared__ uint64_t Rf[12 * kBlock];  // r0..r10 + a dummy slot per lane
@@ -519,9 +520,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   for (uint64_t u0 = ordered ? 0 : (uint64_t)blockIdx.x * kBlock; u0 < p.n; u0 += ustep) {
     const uint64_t unit = ordered ? u0 : u0 + tid;
     const bool active = ordered ? (tid == 0 && blockIdx.x == 0) : unit < p.n;
-    const uint64_t slot = (uint64_t)(uintptr_t)p.data + unit * p.stride;
+    uint64_t slot = (uint64_t)(uintptr_t)p.data + unit * p.stride;
+    uint64_t chunk = slot;  // XDP ctx buffer_start
     uint32_t len = p.fixed_len;
-    if (active && p.lens) len = p.lens[unit];
+    bool desc_ok = true;
+    if (p.descs) {
+      // AF_XDP descriptor ring: the frame at umem + addr; its chunk bounds
+      // the ctx buffer (aligned-chunk umem)
+      uint64_t addr = 0;
+      len = 0;
+      if (active) {
+        addr = p.descs[2 * unit];
+        len = (uint32_t)p.descs[2 * unit + 1];
+      }
+      desc_ok = addr < p.umem_bytes && len <= p.umem_bytes - addr;
+      if (!desc_ok) addr = len = 0;
+      slot = (uint64_t)(uintptr_t)p.data + addr;
+      chunk = (uint64_t)(uintptr_t)p.data + (p.stride ? addr - addr % p.stride : addr);
+    } else if (active && p.lens) {
+      len = p.lens[unit];
+    }
     const uint64_t vcpu = (p.first_unit + unit) / 64;
     int32_t miss_fd = -1;
     uint64_t miss_hash = 0;
@@ -533,6 +551,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     fu.r10 = stack_top;
     fu.len = len;
     fu.entry = 1u | (p.stage ? 2u : 0u) | (p.fast_div ? 4u : 0u);
+    if (p.descs && p.stage) {
+      // staging needs every lane's window 16-B aligned inside the umem
+      const bool bad = active && ((slot & 15) != 0 || slot + p.stage > (uint64_t)(uintptr_t)p.data + p.umem_bytes);
+      if (__ballot(bad) != 0) fu.entry &= ~2u;
+    }
     if (KIND == CTX_XDP) {
       // the ctx only exists in LDS when the program reads it generically
       // (loader: ctx uses other than the specialised data / data_end loads)
@@ -544,8 +567,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       x->ingress_ifindex = p.ifindex;
       x->rx_queue_index = p.rxq;
       x->egress_ifindex = 0;
-      x->buffer_start = slot;
-      x->buffer_end = slot + p.stride;
+      x->buffer_start = chunk;
+      x->buffer_end = chunk + (p.descs && !p.stride ? len : p.stride);
       }
       fu.r1 = (uint64_t)(uintptr_t)x;
       fu.r2 = 48;
@@ -561,8 +584,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       if (nr == 60 || nr == 231) alive = false;
     }
     c.unit = unit;
-    c.alive = alive;
-    c.err = E_OK;
+    c.alive = alive && desc_ok;
+    c.err = active && !desc_ok ? E_OOB : E_OK;
     c.pc = 0;
     c.lpc = 0;
     c.steps = 0;

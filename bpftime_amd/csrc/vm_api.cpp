@@ -161,8 +161,12 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     error = "no program loaded";
     return -1;
   }
-  if (!b || b->ctx_kind > CTX_SYSCALL || (b->count && (!b->data || !b->stride))) {
+  if (!b || b->ctx_kind > CTX_SYSCALL || (b->count && !b->data) || (b->count && !b->stride && !b->descs)) {
     error = "invalid batch";
+    return -1;
+  }
+  if (b->descs && (b->ctx_kind == CTX_SYSCALL || !b->umem_bytes)) {
+    error = "descriptor batches need an XDP / raw ctx and umem_bytes";
     return -1;
   }
   hipStream_t s = (hipStream_t)b->stream;
@@ -177,8 +181,10 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     const bool xdp = b->ctx_kind == CTX_XDP;
     const uint32_t head = xdp ? b->head : 0;
     const uint32_t need = stage_need(xdp ? fx : fr, head);
-    const bool aligned = (b->stride % 16) == 0 && ((uint64_t)(uintptr_t)b->data % 16) == 0;
-    p.stage = (need && aligned && b->stride >= need && !getenv("BPFTIME_AMD_NO_STAGING")) ? need : 0;
+    // (descriptor batches: the kernel checks each wave's frames)
+    const bool aligned = ((uint64_t)(uintptr_t)b->data % 16) == 0 &&
+                         (b->descs ? true : (b->stride % 16) == 0 && b->stride >= need);
+    p.stage = (need && aligned && !getenv("BPFTIME_AMD_NO_STAGING")) ? need : 0;
     p.fast = linked(xdp, head, p.stage);
     if (!p.fast) {
       error = "device upload failed";
@@ -200,7 +206,9 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   p.stride = b->stride;
   p.first_unit = b->first_unit;
   p.data_lo = (uint64_t)(uintptr_t)b->data;
-  p.data_hi = p.data_lo + b->count * b->stride;
+  p.data_hi = p.data_lo + (b->descs ? b->umem_bytes : b->count * b->stride);
+  p.descs = (const uint64_t *)b->descs;
+  p.umem_bytes = b->umem_bytes;
   p.arena_lo = (uint64_t)(uintptr_t)r.arena;
   p.arena_hi = p.arena_lo + r.arena_size;
   p.step_limit = step_limit;

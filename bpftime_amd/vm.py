@@ -236,14 +236,16 @@ class VM:
                    rets: Optional[DeviceBuffer] = None, data_off_out: Optional[DeviceBuffer] = None,
                    len_out: Optional[DeviceBuffer] = None, flags: int = BATCH_SYNC, first_unit: int = 0,
                    head: int = 0, data_offset: int = 0, ifindex: int = 0, rxq: int = 0,
-                   stream: int = 0) -> int:
+                   stream: int = 0, descs: Optional[DeviceBuffer] = None, umem_bytes: int = 0) -> int:
+        """descs: AF_XDP descriptor mode ({u64 addr; u32 len; u32 options} per
+        unit, frames at data + addr inside umem_bytes; stride = chunk size)."""
         b = EbpfBatch(ctx_kind=kind, flags=flags, count=count, data=data.ptr + data_offset, stride=stride,
                       lens=lens.ptr if lens else None, fixed_len=fixed_len, ingress_ifindex=ifindex,
                       rx_queue_index=rxq, head=head, verdicts=verdicts.ptr if verdicts else None,
                       rets=rets.ptr if rets else None,
                       data_off_out=data_off_out.ptr if data_off_out else None,
                       len_out=len_out.ptr if len_out else None, first_unit=first_unit,
-                      stream=stream or None)
+                      stream=stream or None, descs=descs.ptr if descs else None, umem_bytes=umem_bytes)
         rc = lib().ebpf_exec_batch(C.c_void_p(self.h), C.byref(b))
         if rc < 0:
             e = lib().bpftime_amd_vm_error(C.c_void_p(self.h))

@@ -102,6 +102,20 @@ struct ebpf_batch {
 	uint32_t *len_out;       /* XDP: data_end - data after the program, or NULL */
 	uint64_t first_unit;     /* global index of unit 0 (shards) */
 	void *stream;            /* hipStream_t, NULL = default stream */
+	/* AF_XDP descriptor mode (descs != NULL): `data` is a umem of umem_bytes,
+	 * unit i is the frame at data + descs[i].addr of descs[i].len bytes
+	 * (struct xdp_desc, linux/if_xdp.h), `stride` the umem chunk size
+	 * (ctx buffer_start / buffer_end = the frame's chunk); lens / fixed_len /
+	 * head are not used.  A descriptor outside the umem fails its unit. */
+	const struct ebpf_xdp_desc *descs;
+	uint64_t umem_bytes;
+};
+
+/* linux/if_xdp.h struct xdp_desc */
+struct ebpf_xdp_desc {
+	uint64_t addr;
+	uint32_t len;
+	uint32_t options;
 };
 
 /* Launches the loaded program over `batch`.  Returns 0 when launched (async),
