@@ -90,5 +90,7 @@ def flow():
         print(f"flow    {name:14s} {ms:8.3f} ms {N / ms / 1e3:9.1f} Mpps", flush=True)
 
 
-syscall()
-flow()
+if len(sys.argv) < 2 or sys.argv[1] == "syscall":
+    syscall()
+if len(sys.argv) < 2 or sys.argv[1] == "flow":
+    flow()
