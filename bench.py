@@ -65,7 +65,10 @@ def main():
     from bpftime_amd import gen, isa, programs
     from bpftime_amd import vm as dev
 
-    if dev.lib().bpftime_amd_set_device(local_rank) != 0:
+    # one process per GPU; ranks beyond the visible GPUs share them round-robin
+    # (only to rehearse N>1 on a smaller box: the driver's nodes have one GPU per rank)
+    ngpu = dev.lib().bpftime_amd_device_count()
+    if ngpu <= 0 or dev.lib().bpftime_amd_set_device(local_rank % ngpu) != 0:
         raise SystemExit(f"rank {rank}: cannot select GPU {local_rank}")
 
     n = 1 << args.log2n
