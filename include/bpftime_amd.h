@@ -105,6 +105,17 @@ void bpftime_amd_set_step_limit(struct ebpf_vm *vm, uint64_t limit);
  * fast path under the given ctx kind (packet, slot, ctx or stack bases) */
 int bpftime_amd_vm_fast_info(const struct ebpf_vm *vm, uint32_t ctx_kind, uint32_t *specialized);
 
+/* ---- handler JSON (csrc/shm_json.cpp) ----
+ * The reference's shm export / import format (runtime/include/bpftime_shm.hpp:
+ * 237-241, runtime/src/bpftime_shm_json.cpp:103-327): {"<fd>": {"type":
+ * "bpf_map_handler" | "bpf_prog_handler" | "bpf_link_handler", "name", "attr"}}.
+ * Import recreates maps (in HBM), programs and links at the same fds; a link
+ * to an XDP program becomes a BPF_XDP link (the format drops attach types).
+ * 0 / -1 (errno, bpftime_amd_last_error). */
+int bpftime_import_global_shm_from_json(const char *filename);
+int bpftime_export_global_shm_to_json(const char *filename);
+int bpftime_import_shm_handler_from_json(int fd, const char *json_string);
+
 /* ---- eBPF ELF objects (csrc/object.cpp) ----
  * The reference opens objects with libbpf (runtime/object/bpftime_object.hpp:
  * bpftime_object_open / _close / _find_program_by_name / _by_secname,
