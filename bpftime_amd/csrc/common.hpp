@@ -66,6 +66,7 @@ constexpr uint32_t MT_HASH = 1;
 constexpr uint32_t MT_ARRAY = 2;
 constexpr uint32_t MT_PERCPU_HASH = 5;
 constexpr uint32_t MT_PERCPU_ARRAY = 6;
+constexpr uint32_t MT_LPM_TRIE = 11;
 
 // Device-side map descriptor (64 B), indexed by fd.
 //   ARRAY          data = value_size * max_entries, stride value_size
@@ -74,6 +75,10 @@ constexpr uint32_t MT_PERCPU_ARRAY = 6;
 //                  [u32 state][u32 pad][key, padded to 8][value(s), padded to 8]
 //                  state 0 = empty, 1 = filled, 2 = being written
 //                  ix: lookup index beside that layout (see ix_pos), 0 = none
+//   LPM_TRIE       read-only device replica of the host trie: a 16-B header
+//                  {i32 root node, u32 nodes} then nodes of slot_size bytes
+//                  {u32 prefixlen, u32 intermediate, i32 child[2], prefix data
+//                  at key_off = 16, value at val_off}
 struct DMap {
   uint32_t type;
   uint32_t key_size;

@@ -222,6 +222,41 @@ __device__ uint64_t hash_find(const DMap &m, uint64_t key, bool insert, uint64_t
   }
 }
 
+// LPM trie lookup on the device replica: the walk of lpm_trie_map.cpp:
+// 192-264 (longest prefix match down the trie, the last non-intermediate
+// node on the path wins; an exact full-length match ends the walk).  The
+// replica is read-only during a batch (program-side updates / deletes of an
+// LPM trie are not supported on the device).
+__device__ __forceinline__ uint32_t lpm_bit(const uint8_t *d, uint32_t i) { return (d[i >> 3] >> (7 - (i & 7))) & 1; }
+
+__device__ uint64_t lpm_lookup(const DMap &m, uint64_t key) {
+  const uint32_t dsz = m.key_size - 4, maxp = dsz * 8;
+  const uint32_t kp = *(const u32u *)key;
+  if (kp > maxp) return 0;
+  const uint8_t *kd = (const uint8_t *)(uintptr_t)(key + 4);
+  int32_t node = *(const int32_t *)(uintptr_t)m.data;
+  uint64_t found = 0;
+  for (uint32_t guard = 0; node >= 0 && guard <= maxp + 1; guard++) {
+    const uint64_t nb = m.data + 16 + (uint64_t)node * m.slot_size;
+    const uint32_t np = *(const uint32_t *)(uintptr_t)nb;
+    const bool inter = *(const uint32_t *)(uintptr_t)(nb + 4) != 0;
+    const uint8_t *nd = (const uint8_t *)(uintptr_t)(nb + m.key_off);
+    const uint32_t lim = np < kp ? np : kp;
+    uint32_t ml = 0;
+    while (ml + 8 <= lim && nd[ml >> 3] == kd[ml >> 3]) ml += 8;  // whole bytes first
+    while (ml < lim && lpm_bit(nd, ml) == lpm_bit(kd, ml)) ml++;
+    if (ml == maxp) {
+      found = inter ? 0 : nb;
+      break;
+    }
+    if (ml < np) break;
+    if (!inter) found = nb;
+    if (ml >= kp) break;
+    node = *(const int32_t *)(uintptr_t)(nb + 8 + 4 * lpm_bit(kd, np));
+  }
+  return found ? found + m.val_off : 0;
+}
+
 struct LaneEnv {
   uint64_t vcpu;
   // last lookup miss (map fd, key hash) for the lookup_or_try_init race rule
@@ -256,6 +291,8 @@ __device__ uint64_t helper_lookup(const DMap *maps, uint64_t fd, uint64_t key, L
       if (m.type == MT_PERCPU_HASH) v += (env.vcpu % m.ncpu) * m.value_size;
       return v;
     }
+    case MT_LPM_TRIE:
+      return lpm_lookup(m, key);
   }
   return 0;
 }

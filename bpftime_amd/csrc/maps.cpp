@@ -148,6 +148,256 @@ static int64_t host_hash_find(const MapRec &m, const void *key, std::vector<uint
   return -1;
 }
 
+
+// ---- LPM trie (runtime/src/bpf_map/userspace/lpm_trie_map.cpp) -------------
+// The host keeps the authoritative trie (same node structure and update /
+// logical-delete rules as the reference); the device holds a read-only
+// replica (common.hpp DMap comment) uploaded before the next launch after a
+// change.
+struct LpmTrie {
+  struct Node {
+    uint32_t plen = 0;
+    bool inter = false;
+    int32_t child[2] = {-1, -1};
+    std::vector<uint8_t> data, value;
+  };
+  uint32_t dsz = 0, vsz = 0, max_entries = 0, cap = 0;
+  std::vector<Node> nodes;
+  int32_t root = -1;
+  uint64_t entries = 0;
+
+  int bit(const uint8_t *d, size_t i) const {  // :88-98
+    if (i >= (size_t)dsz * 8) return 0;
+    return (d[i / 8] >> (7 - (i % 8))) & 1;
+  }
+  size_t match(const Node &n, const uint8_t *key) const {  // :101-113
+    uint32_t kp;
+    memcpy(&kp, key, 4);
+    const uint32_t lim = std::min(n.plen, kp);
+    size_t i = 0;
+    while (i < lim && bit(n.data.data(), i) == bit(key + 4, i)) i++;
+    return i;
+  }
+  int32_t make(const uint8_t *key, uint32_t plen, const void *value, bool inter) {
+    if (nodes.size() >= cap) return -1;
+    Node n;
+    n.plen = plen;
+    n.inter = inter;
+    n.data.assign(key + 4, key + 4 + dsz);
+    n.value.assign(vsz, 0);
+    if (!inter && value) memcpy(n.value.data(), value, vsz);
+    nodes.push_back(std::move(n));
+    return (int32_t)nodes.size() - 1;
+  }
+  const Node *lookup(const uint8_t *key) const {  // :192-264
+    uint32_t kp;
+    memcpy(&kp, key, 4);
+    const uint32_t maxp = dsz * 8;
+    if (kp > maxp) {
+      errno = EINVAL;
+      return nullptr;
+    }
+    int32_t node = root;
+    const Node *found = nullptr;
+    while (node >= 0) {
+      const Node &n = nodes[node];
+      const size_t ml = match(n, key);
+      if (ml == maxp) {
+        found = &n;
+        break;
+      }
+      if (ml < n.plen) break;
+      if (!n.inter) found = &n;
+      if (ml < kp)
+        node = n.child[bit(key + 4, n.plen)];
+      else
+        break;
+    }
+    if (!found || found->inter) {
+      errno = ENOENT;
+      return nullptr;
+    }
+    return found;
+  }
+  long update(const uint8_t *key, const void *value, uint64_t flags) {  // :266-488
+    if (flags != 0 && flags != 1 && flags != 2) {
+      errno = EINVAL;
+      return -1;
+    }
+    uint32_t kp;
+    memcpy(&kp, key, 4);
+    const uint32_t maxp = dsz * 8;
+    if (kp > maxp) {
+      errno = EINVAL;
+      return -1;
+    }
+    auto need_room = [&]() {
+      if (flags == 2) {
+        errno = ENOENT;
+        return false;
+      }
+      if (entries >= max_entries) {
+        errno = ENOSPC;
+        return false;
+      }
+      if (nodes.size() + 2 > cap) {  // node pool of the device replica
+        errno = ENOMEM;
+        return false;
+      }
+      return true;
+    };
+    if (root < 0) {
+      if (!need_room()) return -1;
+      root = make(key, kp, value, false);
+      entries++;
+      return 0;
+    }
+    int32_t parent = -1, pbit = 0, node = -1;
+    int32_t cur = root;
+    size_t ml = 0;
+    while (cur >= 0) {
+      node = cur;
+      const Node &n = nodes[cur];
+      ml = match(n, key);
+      if (n.plen != ml || n.plen == kp || n.plen == maxp) break;
+      parent = cur;
+      pbit = bit(key + 4, n.plen);
+      cur = n.child[pbit];
+    }
+    auto set_slot = [&](int32_t v) {
+      if (parent < 0)
+        root = v;
+      else
+        nodes[parent].child[pbit] = v;
+    };
+    auto split = [&](int32_t at) {  // intermediate node at the split point
+      const int32_t nn = make(key, kp, value, false);
+      const int32_t im = make(key, (uint32_t)ml, nullptr, true);
+      if (bit(key + 4, ml)) {
+        nodes[im].child[0] = at;
+        nodes[im].child[1] = nn;
+      } else {
+        nodes[im].child[0] = nn;
+        nodes[im].child[1] = at;
+      }
+      set_slot(im);
+      entries++;
+      return 0L;
+    };
+    if (cur >= 0 && nodes[cur].plen == kp) {  // case 1
+      if (match(nodes[cur], key) == kp) {
+        Node &n = nodes[cur];
+        if (flags == 1) {
+          errno = EEXIST;
+          return -1;
+        }
+        if (flags == 2 && n.inter) {
+          errno = ENOENT;
+          return -1;
+        }
+        if (n.inter) {
+          if (entries >= max_entries) {
+            errno = ENOSPC;
+            return -1;
+          }
+          n.inter = false;
+          entries++;
+        }
+        memcpy(n.value.data(), value, vsz);
+        return 0;
+      }
+      if (!need_room()) return -1;
+      return split(cur);
+    }
+    if (cur < 0) {  // case 2
+      if (!need_room()) return -1;
+      set_slot(make(key, kp, value, false));
+      entries++;
+      return 0;
+    }
+    (void)node;
+    if (ml == kp) {  // case 3: the new prefix becomes cur's parent
+      if (!need_room()) return -1;
+      const int32_t nn = make(key, kp, value, false);
+      nodes[nn].child[bit(nodes[cur].data.data(), ml)] = cur;
+      set_slot(nn);
+      entries++;
+      return 0;
+    }
+    if (!need_room()) return -1;  // case 4
+    return split(cur);
+  }
+  long remove(const uint8_t *key) {  // :490-541: logical deletion
+    uint32_t kp;
+    memcpy(&kp, key, 4);
+    if (kp > dsz * 8) {
+      errno = EINVAL;
+      return -1;
+    }
+    int32_t cur = root, last = -1;
+    while (cur >= 0) {
+      last = cur;
+      const Node &n = nodes[cur];
+      const size_t ml = match(n, key);
+      if (n.plen != ml || n.plen == kp) break;
+      cur = n.child[bit(key + 4, n.plen)];
+      last = cur;
+    }
+    if (last < 0 || nodes[last].plen != kp || match(nodes[last], key) != kp || nodes[last].inter) {
+      errno = ENOENT;
+      return -1;
+    }
+    nodes[last].inter = true;
+    std::fill(nodes[last].value.begin(), nodes[last].value.end(), 0);
+    if (entries) entries--;
+    return 0;
+  }
+  int first_key(uint8_t *next) const {  // :543-590 (only the first key is implemented there)
+    int32_t cur = root;
+    while (cur >= 0) {
+      const Node &n = nodes[cur];
+      if (!n.inter) {
+        memcpy(next, &n.plen, 4);
+        memcpy(next + 4, n.data.data(), dsz);
+        return 0;
+      }
+      cur = n.child[0] >= 0 ? n.child[0] : n.child[1];
+    }
+    errno = ENOENT;
+    return -1;
+  }
+  // device replica image (common.hpp DMap comment)
+  void image(std::vector<uint8_t> &out, uint32_t slot, uint32_t key_off, uint32_t val_off) const {
+    out.assign(16 + (size_t)nodes.size() * slot, 0);
+    const uint32_t nn = (uint32_t)nodes.size();
+    memcpy(out.data(), &root, 4);
+    memcpy(out.data() + 4, &nn, 4);
+    for (size_t i = 0; i < nodes.size(); i++) {
+      uint8_t *b = out.data() + 16 + i * slot;
+      const Node &n = nodes[i];
+      const uint32_t inter = n.inter ? 1 : 0;
+      memcpy(b, &n.plen, 4);
+      memcpy(b + 4, &inter, 4);
+      memcpy(b + 8, n.child, 8);
+      memcpy(b + key_off, n.data.data(), dsz);
+      memcpy(b + val_off, n.value.data(), vsz);
+    }
+  }
+};
+
+static void lpm_touch(int fd) { rt().lpm_stale.insert(fd); }
+
+static int lpm_upload(int fd) {
+  Runtime &r = rt();
+  MapRec &m = r.maps[fd];
+  std::vector<uint8_t> img;
+  m.lpm->image(img, m.d.slot_size, m.d.key_off, m.d.val_off);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;  // no batch still reading the replica
+  if (hipMemcpy((void *)m.d.data, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) return -1;
+  r.lpm_stale.erase(fd);
+  return 0;
+}
+
 void ix_invalidate(int fd) {
   Runtime &r = rt();
   MapRec &m = r.maps[fd];
@@ -216,6 +466,14 @@ int Runtime::prepare_ix(bool may_delete) {
     for (int fd = 0; fd < (int)kMaxFds; fd++)
       if (kind[fd] == HKind::MAP && maps[fd].ix_valid) ix_invalidate(fd);
     return 0;
+  }
+  while (!lpm_stale.empty()) {
+    const int fd = *lpm_stale.begin();
+    if (kind[fd] != HKind::MAP || !maps[fd].lpm) {
+      lpm_stale.erase(fd);
+      continue;
+    }
+    if (lpm_upload(fd) < 0) return -1;
   }
   while (!ix_stale.empty()) {
     const int fd = *ix_stale.begin();
@@ -294,6 +552,25 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
       m.bytes = d.nbuckets * d.slot_size;
       break;
     }
+    case MT_LPM_TRIE: {
+      // lpm_trie_map.cpp:43-81: key = u32 prefixlen + 1..256 data bytes
+      if (m.key_size < 5 || m.key_size > 260 || m.value_size == 0 || m.max_entries == 0) {
+        errno = EINVAL;
+        set_error("LPM trie needs key_size 5..260, value_size > 0, max_entries > 0");
+        return -1;
+      }
+      auto t = std::make_shared<LpmTrie>();
+      t->dsz = m.key_size - 4;
+      t->vsz = m.value_size;
+      t->max_entries = m.max_entries;
+      t->cap = (uint32_t)std::min<uint64_t>(2ull * m.max_entries + 8, 1u << 26);
+      m.lpm = t;
+      d.key_off = 16;
+      d.val_off = 16 + ((t->dsz + 7) & ~7u);
+      d.slot_size = d.val_off + ((m.value_size + 7) & ~7u);
+      m.bytes = 16 + (uint64_t)t->cap * d.slot_size;
+      break;
+    }
     default:
       errno = EINVAL;
       set_error("unsupported map type " + std::to_string(m.type));
@@ -309,6 +586,10 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
   d.data = base;
   d.count_addr = extra ? base + ((m.bytes + 127) & ~127ull) : 0;
   if (hipMemset((void *)base, 0, m.bytes + extra + 8) != hipSuccess) return -1;
+  if (m.lpm) {  // empty replica: root = -1
+    const int32_t none = -1;
+    if (hipMemcpy((void *)base, &none, 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
+  }
   if (extra && !getenv("BPFTIME_AMD_NO_HASH_INDEX")) {
     // lookup index (common.hpp ix_pos): a power of two >= 2 x buckets, so
     // it is at most half full; an empty table's index is empty and valid
@@ -373,6 +654,16 @@ const void *bpftime_map_lookup_elem(int fd, const void *key) {
       buf.assign(slot.begin() + m->d.val_off, slot.begin() + m->d.val_off + vs);
       return buf.data();
     }
+    case MT_LPM_TRIE: {
+      if (!key) {
+        errno = EINVAL;
+        return nullptr;
+      }
+      const LpmTrie::Node *n = m->lpm->lookup((const uint8_t *)key);
+      if (!n) return nullptr;
+      buf = n->value;  // the reference also hands out a copy (lpm_trie_map.cpp:252-263)
+      return buf.data();
+    }
   }
   return nullptr;
 }
@@ -382,6 +673,15 @@ long bpftime_map_update_elem(int fd, const void *key, const void *value, uint64_
   if (!m) return -1;
   uint64_t b = flags & 0xffffffffull;
   bool flags_ok = b == 0 || b == 1 || b == 2;  // map_common_def.hpp:83-94
+  if (m->type == MT_LPM_TRIE) {
+    if (!key || !value) {
+      errno = EINVAL;
+      return -1;
+    }
+    const long rc = m->lpm->update((const uint8_t *)key, value, flags);
+    if (rc == 0) lpm_touch(fd);
+    return rc;
+  }
   switch (m->type) {
     case MT_ARRAY:
     case MT_PERCPU_ARRAY: {
@@ -470,6 +770,15 @@ long bpftime_map_update_elem(int fd, const void *key, const void *value, uint64_
 long bpftime_map_delete_elem(int fd, const void *key) {
   MapRec *m = map_of(fd);
   if (!m) return -1;
+  if (m->type == MT_LPM_TRIE) {
+    if (!key) {
+      errno = EINVAL;
+      return -1;
+    }
+    const long rc = m->lpm->remove((const uint8_t *)key);
+    if (rc == 0) lpm_touch(fd);
+    return rc;
+  }
   switch (m->type) {
     case MT_ARRAY:
     case MT_PERCPU_ARRAY:
@@ -500,6 +809,13 @@ long bpftime_map_delete_elem(int fd, const void *key) {
 int bpftime_map_get_next_key(int fd, const void *key, void *next_key) {
   MapRec *m = map_of(fd);
   if (!m) return -1;
+  if (m->type == MT_LPM_TRIE) {
+    if (!next_key || key) {  // lpm_trie_map.cpp:543-590: only the first key
+      errno = next_key ? ENOENT : EINVAL;
+      return -1;
+    }
+    return m->lpm->first_key((uint8_t *)next_key);
+  }
   switch (m->type) {
     case MT_ARRAY:
     case MT_PERCPU_ARRAY: {  // array_map.cpp:66-81
@@ -654,6 +970,7 @@ int bpftime_amd_map_geometry(int fd, uint64_t *nbuckets, uint32_t *slot_size, ui
 
 uint64_t bpftime_amd_map_count(int fd) {
   MapRec *m = map_of(fd);
+  if (m && m->lpm) return m->lpm->entries;
   if (!m || !m->d.count_addr) return 0;
   return read_count(*m);
 }

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
+#include <memory>
 #include <mutex>
 #include <set>
 #include <string>
@@ -22,6 +23,7 @@ struct MapRec {
   uint64_t bytes = 0;  // storage bytes at d.data
   uint64_t ix_addr = 0;    // hash lookup index storage (common.hpp ix_pos), 0 = none
   bool ix_valid = false;   // d.ix = ix_addr while the index holds exactly the reachable keys
+  std::shared_ptr<struct LpmTrie> lpm;  // LPM_TRIE: the authoritative host trie
 };
 
 struct ProgRec {
@@ -53,6 +55,7 @@ struct Runtime {
   uint64_t arena_alloc(uint64_t bytes);
   int push_map(int fd);         // upload DMap entry for fd
   std::set<int> ix_stale;       // hash maps whose lookup index needs a rebuild
+  std::set<int> lpm_stale;      // LPM tries whose device replica needs an upload
   // before a launch: a program that can delete invalidates every hash
   // lookup index; any other rebuilds the stale ones
   int prepare_ix(bool may_delete);

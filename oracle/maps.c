@@ -19,7 +19,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-enum { T_HASH = 1, T_ARRAY = 2, T_PERCPU_HASH = 5, T_PERCPU_ARRAY = 6 };
+enum { T_HASH = 1, T_ARRAY = 2, T_PERCPU_HASH = 5, T_PERCPU_ARRAY = 6, T_LPM_TRIE = 11 };
 
 struct orc_map {
 	int used;
@@ -32,6 +32,18 @@ struct orc_map {
 	/* PERCPU_HASH: keys[i], vals[i] (ncpu*vsize), insertion ordered */
 	uint8_t *pkeys, *pvals;
 	uint64_t pcount, pcap;
+	/* LPM_TRIE: node pool (lpm_trie_map.cpp keeps heap nodes; same tree) */
+	struct lpm_node *nodes;
+	int64_t nnodes, ncap, root;
+	uint64_t lpm_entries;
+	uint8_t *tl_value; /* the reference returns a thread-local copy */
+};
+
+struct lpm_node {
+	uint32_t prefixlen;
+	int intermediate;
+	int64_t child[2];
+	uint8_t *data; /* data_size prefix bytes, then value_size value bytes */
 };
 
 static struct orc_map g_maps[ORC_MAX_FDS];
@@ -59,8 +71,18 @@ int orc_get_cpu(void)
 	return g_cpu;
 }
 
+static void free_lpm(struct orc_map *m)
+{
+	for (int64_t i = 0; i < m->nnodes; i++)
+		free(m->nodes[i].data);
+	free(m->nodes);
+	free(m->tl_value);
+}
+
 static void free_map(struct orc_map *m)
 {
+	if (m->type == T_LPM_TRIE)
+		free_lpm(m);
 	free(m->data);
 	free(m->pkeys);
 	free(m->pvals);
@@ -143,6 +165,14 @@ int orc_map_create(int fd, uint32_t type, uint32_t ksize, uint32_t vsize, uint32
 		break;
 	case T_PERCPU_HASH:
 		m->ncpu = (uint32_t)g_ncpu;
+		break;
+	case T_LPM_TRIE: /* lpm_trie_map.cpp:43-81: key = u32 prefixlen + 1..256 data bytes */
+		if (ksize < 5 || ksize > 260 || vsize == 0 || max_entries == 0) {
+			g_errno = EINVAL;
+			return -1;
+		}
+		m->root = -1;
+		m->tl_value = calloc(vsize, 1);
 		break;
 	default:
 		return -1;
@@ -252,6 +282,251 @@ static void phash_erase(struct orc_map *m, uint64_t i)
 }
 
 /* ---- helper-side ops (bpf_map_handler::map_*_elem, from_syscall=false) ---- */
+
+/* ---- LPM trie (runtime/src/bpf_map/userspace/lpm_trie_map.cpp) ---- */
+static uint32_t lpm_dsz(const struct orc_map *m)
+{
+	return m->ksize - 4;
+}
+
+static int lpm_bit(const struct orc_map *m, const uint8_t *d, size_t i) /* :88-98 */
+{
+	if (i >= (size_t)lpm_dsz(m) * 8)
+		return 0;
+	return (d[i / 8] >> (7 - (i % 8))) & 1;
+}
+
+static size_t lpm_match(const struct orc_map *m, const struct lpm_node *n, const uint8_t *key) /* :101-113 */
+{
+	uint32_t kp = *(const uint32_t *)key;
+	uint32_t lim = n->prefixlen < kp ? n->prefixlen : kp;
+	size_t i = 0;
+	for (; i < lim; i++)
+		if (lpm_bit(m, n->data, i) != lpm_bit(m, key + 4, i))
+			break;
+	return i;
+}
+
+static int64_t lpm_new(struct orc_map *m, const uint8_t *key, uint32_t plen, const void *value, int inter)
+{
+	if (m->nnodes == m->ncap) {
+		m->ncap = m->ncap ? 2 * m->ncap : 16;
+		m->nodes = realloc(m->nodes, (size_t)m->ncap * sizeof(struct lpm_node));
+	}
+	struct lpm_node *n = &m->nodes[m->nnodes];
+	n->prefixlen = plen;
+	n->intermediate = inter;
+	n->child[0] = n->child[1] = -1;
+	n->data = calloc(lpm_dsz(m) + m->vsize, 1);
+	memcpy(n->data, key + 4, lpm_dsz(m));
+	if (!inter && value)
+		memcpy(n->data + lpm_dsz(m), value, m->vsize);
+	return m->nnodes++;
+}
+
+static void *lpm_lookup(struct orc_map *m, const uint8_t *key) /* :192-264 */
+{
+	const uint32_t maxp = lpm_dsz(m) * 8, kp = *(const uint32_t *)key;
+	if (kp > maxp) {
+		g_errno = EINVAL;
+		return NULL;
+	}
+	int64_t node = m->root, found = -1;
+	while (node >= 0) {
+		struct lpm_node *n = &m->nodes[node];
+		size_t ml = lpm_match(m, n, key);
+		if (ml == maxp) {
+			found = node;
+			break;
+		}
+		if (ml < n->prefixlen)
+			break;
+		if (!n->intermediate)
+			found = node;
+		if (ml < kp)
+			node = n->child[lpm_bit(m, key + 4, n->prefixlen)];
+		else
+			break;
+	}
+	if (found < 0 || m->nodes[found].intermediate) {
+		g_errno = ENOENT;
+		return NULL;
+	}
+	memcpy(m->tl_value, m->nodes[found].data + lpm_dsz(m), m->vsize);
+	return m->tl_value;
+}
+
+static long lpm_update(struct orc_map *m, const uint8_t *key, const void *value, uint64_t flags) /* :266-488 */
+{
+	if (flags != 0 && flags != 1 && flags != 2) {
+		g_errno = EINVAL;
+		return -1;
+	}
+	const uint32_t maxp = lpm_dsz(m) * 8, kp = *(const uint32_t *)key;
+	if (kp > maxp) {
+		g_errno = EINVAL;
+		return -1;
+	}
+#define LPM_NEED_ROOM()                                   \
+	do {                                              \
+		if (flags == 2) {                         \
+			g_errno = ENOENT;                 \
+			return -1;                        \
+		}                                         \
+		if (m->lpm_entries >= m->max_entries) {   \
+			g_errno = ENOSPC;                 \
+			return -1;                        \
+		}                                         \
+	} while (0)
+	if (m->root < 0) {
+		LPM_NEED_ROOM();
+		m->root = lpm_new(m, key, kp, value, 0);
+		m->lpm_entries++;
+		return 0;
+	}
+	int64_t *slotp = &m->root, node = -1;
+	size_t ml = 0;
+	/* walk (slot pointers are indices into nodes[]: re-derived after lpm_new) */
+	int64_t parent = -2;
+	int pbit = 0;
+	while (*slotp >= 0) {
+		node = *slotp;
+		struct lpm_node *n = &m->nodes[node];
+		ml = lpm_match(m, n, key);
+		if (n->prefixlen != ml || n->prefixlen == kp || n->prefixlen == maxp)
+			break;
+		pbit = lpm_bit(m, key + 4, n->prefixlen);
+		parent = node;
+		slotp = &n->child[pbit];
+	}
+#define SLOT_SET(v)                                       \
+	do {                                              \
+		int64_t v_ = (v);                         \
+		if (parent == -2)                         \
+			m->root = v_;                     \
+		else                                      \
+			m->nodes[parent].child[pbit] = v_; \
+	} while (0)
+	const int64_t cur = *slotp;
+	if (cur >= 0 && m->nodes[cur].prefixlen == kp) { /* case 1 */
+		struct lpm_node *n = &m->nodes[cur];
+		if (lpm_match(m, n, key) == kp) {
+			int real = !n->intermediate;
+			if (flags == 1) {
+				g_errno = EEXIST;
+				return -1;
+			}
+			if (flags == 2 && !real) {
+				g_errno = ENOENT;
+				return -1;
+			}
+			if (!real) {
+				if (m->lpm_entries >= m->max_entries) {
+					g_errno = ENOSPC;
+					return -1;
+				}
+				n->intermediate = 0;
+				m->lpm_entries++;
+			}
+			memcpy(n->data + lpm_dsz(m), value, m->vsize);
+			return 0;
+		}
+		LPM_NEED_ROOM();
+		int64_t nn = lpm_new(m, key, kp, value, 0);
+		int64_t im = lpm_new(m, key, (uint32_t)ml, NULL, 1);
+		if (lpm_bit(m, key + 4, ml)) {
+			m->nodes[im].child[0] = cur;
+			m->nodes[im].child[1] = nn;
+		} else {
+			m->nodes[im].child[0] = nn;
+			m->nodes[im].child[1] = cur;
+		}
+		SLOT_SET(im);
+		m->lpm_entries++;
+		return 0;
+	}
+	if (cur < 0) { /* case 2 */
+		LPM_NEED_ROOM();
+		int64_t nn = lpm_new(m, key, kp, value, 0);
+		SLOT_SET(nn);
+		m->lpm_entries++;
+		return 0;
+	}
+	if (ml == kp) { /* case 3: the new prefix becomes cur's parent */
+		LPM_NEED_ROOM();
+		int64_t nn = lpm_new(m, key, kp, value, 0);
+		int nb = lpm_bit(m, m->nodes[cur].data, ml);
+		m->nodes[nn].child[nb] = cur;
+		SLOT_SET(nn);
+		m->lpm_entries++;
+		return 0;
+	}
+	LPM_NEED_ROOM(); /* case 4: intermediate node at the split */
+	int64_t nn = lpm_new(m, key, kp, value, 0);
+	int64_t im = lpm_new(m, key, (uint32_t)ml, NULL, 1);
+	if (lpm_bit(m, key + 4, ml)) {
+		m->nodes[im].child[0] = cur;
+		m->nodes[im].child[1] = nn;
+	} else {
+		m->nodes[im].child[0] = nn;
+		m->nodes[im].child[1] = cur;
+	}
+	SLOT_SET(im);
+	m->lpm_entries++;
+	return 0;
+#undef SLOT_SET
+#undef LPM_NEED_ROOM
+}
+
+static long lpm_delete(struct orc_map *m, const uint8_t *key) /* :490-541: logical deletion */
+{
+	const uint32_t maxp = lpm_dsz(m) * 8, kp = *(const uint32_t *)key;
+	if (kp > maxp) {
+		g_errno = EINVAL;
+		return -1;
+	}
+	int64_t node = m->root, last = -1;
+	while (node >= 0) {
+		struct lpm_node *n = &m->nodes[node];
+		last = node;
+		size_t ml = lpm_match(m, n, key);
+		if (n->prefixlen != ml || n->prefixlen == kp)
+			break;
+		node = n->child[lpm_bit(m, key + 4, n->prefixlen)];
+		last = node;
+	}
+	if (last < 0 || m->nodes[last].prefixlen != kp || lpm_match(m, &m->nodes[last], key) != kp ||
+	    m->nodes[last].intermediate) {
+		g_errno = ENOENT;
+		return -1;
+	}
+	m->nodes[last].intermediate = 1;
+	memset(m->nodes[last].data + lpm_dsz(m), 0, m->vsize);
+	if (m->lpm_entries > 0)
+		m->lpm_entries--;
+	return 0;
+}
+
+static int lpm_next_key(struct orc_map *m, const void *key, uint8_t *next) /* :543-590 */
+{
+	if (m->root < 0 || key) { /* only the first key is implemented by the reference */
+		g_errno = ENOENT;
+		return -1;
+	}
+	int64_t node = m->root;
+	while (node >= 0) {
+		struct lpm_node *n = &m->nodes[node];
+		if (!n->intermediate) {
+			*(uint32_t *)next = n->prefixlen;
+			memcpy(next + 4, n->data, lpm_dsz(m));
+			return 0;
+		}
+		node = n->child[0] >= 0 ? n->child[0] : n->child[1];
+	}
+	g_errno = ENOENT;
+	return -1;
+}
+
 void *orc_map_lookup(int fd, const void *key)
 {
 	struct orc_map *m = get(fd);
@@ -280,6 +555,8 @@ void *orc_map_lookup(int fd, const void *key)
 	}
 	case T_HASH:
 		return hash_lookup(m, key);
+	case T_LPM_TRIE:
+		return key ? lpm_lookup(m, key) : NULL;
 	case T_PERCPU_HASH: { /* per_cpu_hash_map.cpp:48-64 */
 		if (!key) {
 			g_errno = ENOENT;
@@ -320,6 +597,8 @@ long orc_map_update(int fd, const void *key, const void *value, uint64_t flags)
 		memcpy(dst, value, m->vsize);
 		return 0;
 	}
+	case T_LPM_TRIE:
+		return lpm_update(m, key, value, flags);
 	case T_HASH: /* fix_hash_map.cpp:34-39: flags ignored, always 0 */
 		hash_update(m, key, value);
 		return 0;
@@ -349,6 +628,8 @@ long orc_map_delete(int fd, const void *key)
 	case T_HASH: /* fix_hash_map.cpp:41-45 */
 		hash_delete(m, key);
 		return 0;
+	case T_LPM_TRIE:
+		return lpm_delete(m, key);
 	case T_PERCPU_HASH: { /* per_cpu_hash_map.cpp:96-107: zeroes [0, cpu*vsize) */
 		int64_t i = phash_find(m, key);
 		if (i >= 0)
@@ -480,6 +761,8 @@ int orc_map_get_next_key(int fd, const void *key, void *next_key)
 		g_errno = ENOENT;
 		return -1;
 	}
+	case T_LPM_TRIE:
+		return lpm_next_key(m, key, next_key);
 	case T_PERCPU_HASH: {
 		int64_t i = key ? phash_find(m, key) : -1;
 		uint64_t nx = i < 0 ? 0 : (uint64_t)i + 1;
@@ -537,7 +820,7 @@ uint64_t orc_map_count(int fd)
 	struct orc_map *m = get(fd);
 	if (!m)
 		return 0;
-	return m->type == T_PERCPU_HASH ? m->pcount : m->count;
+	return m->type == T_PERCPU_HASH ? m->pcount : m->type == T_LPM_TRIE ? m->lpm_entries : m->count;
 }
 
 /* bpftime_shm.cpp:637-652: the map "pointer" is the fd itself */
