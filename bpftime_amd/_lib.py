@@ -108,6 +108,7 @@ SIGNATURES = [
     ("bpftime_object_find_map_fd_by_name", C.c_int, [C.c_void_p, C.c_char_p]),
     ("bpftime_object_license", C.c_char_p, [C.c_void_p]),
     ("bpftime_object_close", None, [C.c_void_p]),
+    ("bpftime_amd_ringbuf_fetch", C.c_int64, [C.c_int, C.c_void_p, C.c_uint64, u64p]),
     ("bpftime_amd_merge_delta_u64", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     ("bpftime_amd_device_count", C.c_int, []),
     ("bpftime_amd_set_device", C.c_int, [C.c_int]),

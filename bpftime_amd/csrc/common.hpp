@@ -67,6 +67,7 @@ constexpr uint32_t MT_ARRAY = 2;
 constexpr uint32_t MT_PERCPU_HASH = 5;
 constexpr uint32_t MT_PERCPU_ARRAY = 6;
 constexpr uint32_t MT_LPM_TRIE = 11;
+constexpr uint32_t MT_RINGBUF = 27;
 
 // Device-side map descriptor (64 B), indexed by fd.
 //   ARRAY          data = value_size * max_entries, stride value_size
@@ -75,6 +76,9 @@ constexpr uint32_t MT_LPM_TRIE = 11;
 //                  [u32 state][u32 pad][key, padded to 8][value(s), padded to 8]
 //                  state 0 = empty, 1 = filled, 2 = being written
 //                  ix: lookup index beside that layout (see ix_pos), 0 = none
+//   RINGBUF        u64 consumer position at data, u64 producer position at
+//                  data + 128 (own cache lines), 2 x max_entries record bytes
+//                  at data + 256 (ringbuf_map.cpp layout and record format)
 //   LPM_TRIE       read-only device replica of the host trie: a 16-B header
 //                  {i32 root node, u32 nodes} then nodes of slot_size bytes
 //                  {u32 prefixlen, u32 intermediate, i32 child[2], prefix data

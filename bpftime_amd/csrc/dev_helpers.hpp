@@ -257,6 +257,89 @@ __device__ uint64_t lpm_lookup(const DMap &m, uint64_t key) {
   return found ? found + m.val_off : 0;
 }
 
+// ---------------------------------------------------------------------------
+// Ring buffer (runtime/src/bpf_map/userspace/ringbuf_map.cpp, helpers
+// bpf_helper.cpp:451-504).  Records are [u32 len | BUSY | DISCARD][i32 fd]
+// + data, 8-aligned, at data + (pos & mask).  A reservation moves the
+// producer position with a CAS after checking room against the consumer
+// position, like ringbuf::reserve under its spin lock.  The lanes of a wave
+// that reserve from one ring take one CAS for all of them (their records are
+// laid out in lane order); a ring too full for the whole wave falls back to
+// lane-by-lane reservations, so each reservation succeeds or fails exactly
+// as a serial one would at that point.
+// ---------------------------------------------------------------------------
+constexpr uint32_t RB_BUSY = 0x80000000u, RB_DISCARD = 0x40000000u, RB_HDR = 8;
+
+__device__ __forceinline__ uint64_t rb_cas_reserve(const DMap &m, uint64_t total) {
+  // returns the old producer position, or ~0 if total does not fit
+  const uint64_t cons = __hip_atomic_load(G64(m.data), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long p = __hip_atomic_load(G64(m.data + 128), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint32_t spin = 0; spin < (1u << 20); spin++) {
+    if ((uint64_t)m.max_entries - (p - cons) < total) return ~0ull;
+    if (__hip_atomic_compare_exchange_strong(G64(m.data + 128), &p, p + total, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      return p;
+  }
+  return ~0ull;
+}
+
+__device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size) {
+  const bool ok = fd < kMaxFds && maps[fd < kMaxFds ? fd : 0].type == MT_RINGBUF &&
+                  !(size & (RB_BUSY | RB_DISCARD));
+  const DMap m = maps[ok ? fd : 0];
+  const uint64_t total = ok ? (size + RB_HDR + 7) / 8 * 8 : 0;
+  const bool fits = ok && total <= m.max_entries;
+  // one CAS for the wave when every calling lane reserves from the same ring
+  const uint64_t active = __ballot(1);
+  const uint32_t me = __lane_id(), leader = (uint32_t)__builtin_ctzll(active);
+  const uint64_t lfd = __shfl(fd, leader);
+  uint64_t pos = ~0ull;
+  if (__ballot(!fits || fd != lfd) == 0) {
+    uint64_t before = 0, sum = 0;
+    for (uint64_t rest = active; rest; rest &= rest - 1) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(rest);
+      const uint64_t t = __shfl(total, l);
+      if (l < me) before += t;
+      sum += t;
+    }
+    uint64_t base = ~0ull;
+    if (me == leader) base = rb_cas_reserve(m, sum);
+    base = __shfl(base, leader);
+    if (base != ~0ull) pos = base + before;
+  }
+  if (pos == ~0ull && fits) {  // lane by lane (full ring, mixed rings)
+    for (uint64_t rest = __ballot(1); rest; rest &= rest - 1)
+      if ((uint32_t)__builtin_ctzll(rest) == me) pos = rb_cas_reserve(m, total);
+  }
+  if (pos == ~0ull) return 0;
+  const uint64_t mask = m.max_entries - 1, d = m.data + 256;
+  __hip_atomic_store(G32(d + (pos & mask)), (uint32_t)size | RB_BUSY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(G32(d + (pos & mask) + 4), (uint32_t)fd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return d + ((pos + RB_HDR) & mask);
+}
+
+__device__ void rb_submit(const DMap *maps, uint64_t sample, bool discard) {
+  const int32_t fd = *(const int32_t *)(uintptr_t)(sample - 4);  // the header's fd (bpf_helper.cpp:484)
+  if (fd < 0 || fd >= (int32_t)kMaxFds) return;
+  const DMap m = maps[fd];
+  if (m.type != MT_RINGBUF) return;
+  const uint64_t mask = m.max_entries - 1, d = m.data + 256;
+  const uint64_t hdr = d + ((mask + 1 + (sample - d) - RB_HDR) & mask);
+  const uint32_t v = __hip_atomic_load(G32(hdr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the record's bytes before its header
+  __hip_atomic_exchange(G32(hdr), (v & ~RB_BUSY) | (discard ? RB_DISCARD : 0u), __ATOMIC_RELEASE,
+                        __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ uint64_t rb_output(const DMap *maps, uint64_t fd, uint64_t data, uint64_t size) {
+  const uint64_t buf = rb_reserve(maps, fd, size);
+  if (!buf) return (uint64_t)-1;
+  copy_bytes(buf, data, (uint32_t)size);
+  rb_submit(maps, buf, false);
+  return 0;
+}
+
 struct LaneEnv {
   uint64_t vcpu;
   // last lookup miss (map fd, key hash) for the lookup_or_try_init race rule

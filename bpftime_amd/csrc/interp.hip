@@ -53,6 +53,10 @@ __device__ __forceinline__ uint64_t call_helper(uint32_t id, uint64_t a1, uint64
     case 44: return helper_adjust_head(a1, a2);
     case 65: return helper_adjust_tail(a1, a2);
     case 189: return helper_xdp_load_bytes(a1, a2, a3, a4);
+    case 130: return rb_output(maps, a1, a2, a3);
+    case 131: return rb_reserve(maps, a1, a2);
+    case 132: rb_submit(maps, a1, false); return 0;
+    case 133: rb_submit(maps, a1, true); return 0;
   }
   *err = E_BADOP;
   return 0;

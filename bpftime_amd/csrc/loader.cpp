@@ -23,6 +23,7 @@ namespace bpftime_amd {
 bool device_helper_supported(uint32_t id) {
   switch (id) {
     case 1: case 2: case 3: case 5: case 7: case 8: case 28: case 44: case 65: case 189:
+    case 130: case 131: case 132: case 133:
       return true;
   }
   return false;

@@ -552,6 +552,16 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
       m.bytes = d.nbuckets * d.slot_size;
       break;
     }
+    case MT_RINGBUF:
+      // ringbuf_map.cpp: positions + 2 x max_entries data bytes; mask =
+      // max_entries - 1 needs a power of two
+      if (m.max_entries == 0 || (m.max_entries & (m.max_entries - 1))) {
+        errno = EINVAL;
+        set_error("ring buffer size must be a power of two");
+        return -1;
+      }
+      m.bytes = 256 + 2ull * m.max_entries;
+      break;
     case MT_LPM_TRIE: {
       // lpm_trie_map.cpp:43-81: key = u32 prefixlen + 1..256 data bytes
       if (m.key_size < 5 || m.key_size > 260 || m.value_size == 0 || m.max_entries == 0) {
@@ -626,6 +636,10 @@ uint32_t bpftime_map_value_size_from_syscall(int fd) {
 const void *bpftime_map_lookup_elem(int fd, const void *key) {
   MapRec *m = map_of(fd);
   if (!m) return nullptr;
+  if (m->type == MT_RINGBUF) {  // ringbuf_map.cpp: lookup / update / delete / next key unsupported
+    errno = ENOTSUP;
+    return nullptr;
+  }
   std::vector<uint8_t> &buf = tl_lookup_buf;
   switch (m->type) {
     case MT_ARRAY:
@@ -671,6 +685,10 @@ const void *bpftime_map_lookup_elem(int fd, const void *key) {
 long bpftime_map_update_elem(int fd, const void *key, const void *value, uint64_t flags) {
   MapRec *m = map_of(fd);
   if (!m) return -1;
+  if (m->type == MT_RINGBUF) {
+    errno = ENOTSUP;
+    return -1;
+  }
   uint64_t b = flags & 0xffffffffull;
   bool flags_ok = b == 0 || b == 1 || b == 2;  // map_common_def.hpp:83-94
   if (m->type == MT_LPM_TRIE) {
@@ -770,6 +788,10 @@ long bpftime_map_update_elem(int fd, const void *key, const void *value, uint64_
 long bpftime_map_delete_elem(int fd, const void *key) {
   MapRec *m = map_of(fd);
   if (!m) return -1;
+  if (m->type == MT_RINGBUF) {
+    errno = ENOTSUP;
+    return -1;
+  }
   if (m->type == MT_LPM_TRIE) {
     if (!key) {
       errno = EINVAL;
@@ -809,6 +831,10 @@ long bpftime_map_delete_elem(int fd, const void *key) {
 int bpftime_map_get_next_key(int fd, const void *key, void *next_key) {
   MapRec *m = map_of(fd);
   if (!m) return -1;
+  if (m->type == MT_RINGBUF) {
+    errno = ENOTSUP;
+    return -1;
+  }
   if (m->type == MT_LPM_TRIE) {
     if (!next_key || key) {  // lpm_trie_map.cpp:543-590: only the first key
       errno = next_key ? ENOENT : EINVAL;
@@ -966,6 +992,45 @@ int bpftime_amd_map_geometry(int fd, uint64_t *nbuckets, uint32_t *slot_size, ui
   if (val_off) *val_off = m->d.val_off;
   if (ncpu) *ncpu = m->d.ncpu;
   return 0;
+}
+
+// ringbuf::fetch_data (ringbuf_map.cpp): committed records from the consumer
+// position on, stopping at a record still being written; discarded records
+// are skipped.  Each delivered record is written to out as [u32 len][bytes].
+int64_t bpftime_amd_ringbuf_fetch(int fd, void *out, uint64_t cap, uint64_t *used) {
+  MapRec *m = map_of(fd);
+  if (used) *used = 0;
+  if (!m || m->type != MT_RINGBUF) {
+    errno = EINVAL;
+    return -1;
+  }
+  if (hipDeviceSynchronize() != hipSuccess) return -1;  // producers of queued batches first
+  uint64_t pos[2];
+  std::vector<uint8_t> data(2ull * m->max_entries);
+  if (hipMemcpy(&pos[0], (void *)m->d.data, 8, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(&pos[1], (void *)(m->d.data + 128), 8, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(data.data(), (void *)(m->d.data + 256), data.size(), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  const uint64_t mask = m->max_entries - 1;
+  uint64_t cons = pos[0], off = 0;
+  int64_t cnt = 0;
+  while (cons < pos[1]) {
+    uint32_t len;
+    memcpy(&len, data.data() + (cons & mask), 4);
+    if (len & 0x80000000u) break;  // BUSY
+    const uint32_t n = len & 0x3fffffffu;
+    if (!(len & 0x40000000u)) {     // not DISCARD
+      if (off + 4 + n > cap) break;
+      memcpy((uint8_t *)out + off, &n, 4);
+      memcpy((uint8_t *)out + off + 4, data.data() + (cons & mask) + 8, n);
+      off += 4 + n;
+      cnt++;
+    }
+    cons += ((uint64_t)n + 8 + 7) / 8 * 8;
+  }
+  if (hipMemcpy((void *)m->d.data, &cons, 8, hipMemcpyHostToDevice) != hipSuccess) return -1;
+  if (used) *used = off;
+  return cnt;
 }
 
 uint64_t bpftime_amd_map_count(int fd) {

@@ -482,6 +482,8 @@ int bpftime_amd_register_default_helpers(struct ebpf_vm *vm) {
     const char *name;
   } h[] = {{8, "bpf_get_smp_processor_id"}, {28, "bpf_csum_diff"},    {44, "bpf_xdp_adjust_head"},
            {65, "bpf_xdp_adjust_tail"},      {5, "bpf_ktime_get_ns"}, {7, "bpf_get_prandom_u32"},
+           {131, "bpf_ringbuf_reserve"},     {132, "bpf_ringbuf_submit"}, {133, "bpf_ringbuf_discard"},
+           {130, "bpf_ringbuf_output"},
            {1, "bpf_map_lookup_elem"},       {2, "bpf_map_update_elem"}, {3, "bpf_map_delete_elem"}};
   int err = 0;
   for (auto &e : h) err |= ebpf_register(vm, e.id, e.name, nullptr);

@@ -69,6 +69,7 @@ BPF_MAP_TYPE_ARRAY = 2
 BPF_MAP_TYPE_PERCPU_HASH = 5
 BPF_MAP_TYPE_PERCPU_ARRAY = 6
 BPF_MAP_TYPE_LPM_TRIE = 11
+BPF_MAP_TYPE_RINGBUF = 27
 BPF_ANY, BPF_NOEXIST, BPF_EXIST = 0, 1, 2
 BPF_F_MMAPABLE = 1 << 10
 

@@ -96,6 +96,20 @@ class Map:
         m.type = m.key_size = m.value_size = m.max_entries = None
         return m
 
+    def ringbuf_fetch(self, cap: int = 1 << 24) -> list:
+        """Consume committed ring-buffer records (BPF_MAP_TYPE_RINGBUF)."""
+        buf = C.create_string_buffer(cap)
+        used = C.c_uint64(0)
+        n = lib().bpftime_amd_ringbuf_fetch(self.fd, buf, cap, C.byref(used))
+        if n < 0:
+            raise EbpfError(f"ringbuf fetch failed: {_err()}")
+        raw, out, off = buf.raw[:used.value], [], 0
+        for _ in range(n):
+            ln = int.from_bytes(raw[off:off + 4], "little")
+            out.append(raw[off + 4:off + 4 + ln])
+            off += 4 + ln
+        return out
+
     @property
     def user_value_size(self) -> int:
         return lib().bpftime_map_value_size_from_syscall(self.fd)

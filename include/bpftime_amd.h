@@ -95,7 +95,7 @@ int bpftime_amd_xdp_links(int *link_fds, int *prog_fds, uint32_t *ifindexes, int
 /* instantiate a prog record into a loaded "mi355x" VM with the default
  * helper groups registered (bpf_attach_ctx.cpp:40-57 equivalent). */
 struct ebpf_vm *bpftime_amd_prog_instantiate(int prog_fd, char **errmsg);
-/* registers the device helper set (ids 1,2,3,5,7,8,28,44,65) on a VM */
+/* registers the device helper set (ids 1,2,3,5,7,8,28,44,65,130-133) on a VM */
 int bpftime_amd_register_default_helpers(struct ebpf_vm *vm);
 /* loader facts: per-lane stack bytes, big (scratch) stack, fused RMW count */
 int bpftime_amd_vm_info(const struct ebpf_vm *vm, uint32_t *stack_size, int *big_stack,
@@ -154,6 +154,12 @@ int bpftime_object_find_program_by_secname(const struct bpftime_object *obj, con
 int bpftime_object_find_map_fd_by_name(const struct bpftime_object *obj, const char *name);
 const char *bpftime_object_license(const struct bpftime_object *obj);
 void bpftime_object_close(struct bpftime_object *obj);
+
+/* ring buffer consumer (ringbuf::fetch_data, ringbuf_map.cpp): committed
+ * records from the consumer position on, each written to `out` as
+ * [u32 len][len bytes]; advances the consumer position; returns the record
+ * count (-1: not a ring buffer).  Waits for queued batches first. */
+int64_t bpftime_amd_ringbuf_fetch(int fd, void *out, uint64_t cap, uint64_t *used);
 
 /* ---- host merge of per-GPU map shards ---- */
 /* acc += shard - init over u64 words (array counters, additive rule) */

@@ -120,6 +120,38 @@ static uint64_t h_adjust_tail(uint64_t ctx, uint64_t delta_, uint64_t a, uint64_
 	return 0;
 }
 
+/* bpf_helper.cpp:451-504 (map "pointer" = fd; flags other than 0 only warn) */
+static uint64_t h_rb_output(uint64_t rb, uint64_t data, uint64_t size, uint64_t flags, uint64_t c)
+{
+	(void)flags, (void)c;
+	void *buf = orc_ringbuf_reserve((int)rb, size);
+	if (!buf)
+		return (uint64_t)-1;
+	memcpy(buf, (const void *)(uintptr_t)data, size);
+	orc_ringbuf_submit(buf, 0);
+	return 0;
+}
+
+static uint64_t h_rb_reserve(uint64_t rb, uint64_t size, uint64_t flags, uint64_t b, uint64_t c)
+{
+	(void)flags, (void)b, (void)c;
+	return (uint64_t)(uintptr_t)orc_ringbuf_reserve((int)rb, size);
+}
+
+static uint64_t h_rb_submit(uint64_t data, uint64_t flags, uint64_t a, uint64_t b, uint64_t c)
+{
+	(void)flags, (void)a, (void)b, (void)c;
+	orc_ringbuf_submit((const void *)(uintptr_t)data, 0);
+	return 0;
+}
+
+static uint64_t h_rb_discard(uint64_t data, uint64_t flags, uint64_t a, uint64_t b, uint64_t c)
+{
+	(void)flags, (void)a, (void)b, (void)c;
+	orc_ringbuf_submit((const void *)(uintptr_t)data, 1);
+	return 0;
+}
+
 int orc_vm_register_default_helpers(struct orc_vm *vm)
 {
 	int err = 0;
@@ -130,6 +162,10 @@ int orc_vm_register_default_helpers(struct orc_vm *vm)
 	err |= orc_vm_register(vm, 65, "bpf_xdp_adjust_tail", h_adjust_tail);
 	err |= orc_vm_register(vm, 5, "bpf_ktime_get_ns", h_ktime);
 	err |= orc_vm_register(vm, 7, "bpf_get_prandom_u32", h_prandom);
+	err |= orc_vm_register(vm, 131, "bpf_ringbuf_reserve", h_rb_reserve);
+	err |= orc_vm_register(vm, 132, "bpf_ringbuf_submit", h_rb_submit);
+	err |= orc_vm_register(vm, 133, "bpf_ringbuf_discard", h_rb_discard);
+	err |= orc_vm_register(vm, 130, "bpf_ringbuf_output", h_rb_output);
 	/* shm maps helper group (bpf_helper.cpp:1359-1401) */
 	err |= orc_vm_register(vm, 1, "bpf_map_lookup_elem", h_lookup);
 	err |= orc_vm_register(vm, 2, "bpf_map_update_elem", h_update);

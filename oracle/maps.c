@@ -19,7 +19,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-enum { T_HASH = 1, T_ARRAY = 2, T_PERCPU_HASH = 5, T_PERCPU_ARRAY = 6, T_LPM_TRIE = 11 };
+enum { T_HASH = 1, T_ARRAY = 2, T_PERCPU_HASH = 5, T_PERCPU_ARRAY = 6, T_LPM_TRIE = 11, T_RINGBUF = 27 };
 
 struct orc_map {
 	int used;
@@ -37,6 +37,8 @@ struct orc_map {
 	int64_t nnodes, ncap, root;
 	uint64_t lpm_entries;
 	uint8_t *tl_value; /* the reference returns a thread-local copy */
+	/* RINGBUF (ringbuf_map.cpp): consumer / producer positions, 2 x max_ent data */
+	uint64_t rb_cons, rb_prod;
 };
 
 struct lpm_node {
@@ -166,6 +168,13 @@ int orc_map_create(int fd, uint32_t type, uint32_t ksize, uint32_t vsize, uint32
 	case T_PERCPU_HASH:
 		m->ncpu = (uint32_t)g_ncpu;
 		break;
+	case T_RINGBUF: /* ringbuf_map.cpp ringbuf::ringbuf: data = 2 x max_ent bytes */
+		if (max_entries == 0 || (max_entries & (max_entries - 1))) {
+			g_errno = EINVAL;
+			return -1;
+		}
+		m->data = calloc((size_t)max_entries * 2, 1);
+		break;
 	case T_LPM_TRIE: /* lpm_trie_map.cpp:43-81: key = u32 prefixlen + 1..256 data bytes */
 		if (ksize < 5 || ksize > 260 || vsize == 0 || max_entries == 0) {
 			g_errno = EINVAL;
@@ -282,6 +291,83 @@ static void phash_erase(struct orc_map *m, uint64_t i)
 }
 
 /* ---- helper-side ops (bpf_map_handler::map_*_elem, from_syscall=false) ---- */
+
+
+/* ---- ring buffer (runtime/src/bpf_map/userspace/ringbuf_map.cpp) ---- */
+#define RB_BUSY 0x80000000u
+#define RB_DISCARD 0x40000000u
+#define RB_HDR 8
+
+void *orc_ringbuf_reserve(int fd, uint64_t size) /* ringbuf::reserve */
+{
+	struct orc_map *m = get(fd);
+	if (!m || m->type != T_RINGBUF)
+		return NULL;
+	if (size & (RB_BUSY | RB_DISCARD)) {
+		g_errno = E2BIG;
+		return NULL;
+	}
+	uint64_t mask = m->max_entries - 1;
+	uint64_t avail = m->max_entries - (m->rb_prod - m->rb_cons);
+	uint64_t total = (size + RB_HDR + 7) / 8 * 8;
+	if (total > m->max_entries) {
+		g_errno = E2BIG;
+		return NULL;
+	}
+	if (avail < total) {
+		g_errno = ENOSPC;
+		return NULL;
+	}
+	uint8_t *hdr = m->data + (m->rb_prod & mask);
+	*(uint32_t *)hdr = (uint32_t)size | RB_BUSY;
+	*(int32_t *)(hdr + 4) = fd;
+	uint8_t *ptr = m->data + ((m->rb_prod + RB_HDR) & mask);
+	m->rb_prod += total;
+	return ptr;
+}
+
+void orc_ringbuf_submit(const void *sample, int discard) /* ringbuf::submit (fd from the header) */
+{
+	int fd = ((const int32_t *)sample)[-1];
+	struct orc_map *m = get(fd);
+	if (!m || m->type != T_RINGBUF)
+		return;
+	uint64_t mask = m->max_entries - 1;
+	uint64_t off = (mask + 1 + (uint64_t)((const uint8_t *)sample - m->data) - RB_HDR) & mask;
+	uint32_t *len = (uint32_t *)(m->data + off);
+	uint32_t v = *len & ~RB_BUSY;
+	if (discard)
+		v |= RB_DISCARD;
+	*len = v;
+}
+
+/* ringbuf::fetch_data: committed, non-discarded records in order, each
+ * written to out as [u32 len][len bytes]; returns the record count */
+int64_t orc_ringbuf_fetch(int fd, uint8_t *out, uint64_t cap, uint64_t *used)
+{
+	struct orc_map *m = get(fd);
+	*used = 0;
+	if (!m || m->type != T_RINGBUF)
+		return -1;
+	uint64_t mask = m->max_entries - 1;
+	int64_t cnt = 0;
+	while (m->rb_cons < m->rb_prod) {
+		uint32_t len = *(uint32_t *)(m->data + (m->rb_cons & mask));
+		if (len & RB_BUSY)
+			break;
+		uint32_t n = len & ~(RB_BUSY | RB_DISCARD);
+		if (!(len & RB_DISCARD)) {
+			if (*used + 4 + n > cap)
+				break;
+			memcpy(out + *used, &n, 4);
+			memcpy(out + *used + 4, m->data + (m->rb_cons & mask) + RB_HDR, n);
+			*used += 4 + n;
+			cnt++;
+		}
+		m->rb_cons += ((uint64_t)n + RB_HDR + 7) / 8 * 8;
+	}
+	return cnt;
+}
 
 /* ---- LPM trie (runtime/src/bpf_map/userspace/lpm_trie_map.cpp) ---- */
 static uint32_t lpm_dsz(const struct orc_map *m)
@@ -557,6 +643,9 @@ void *orc_map_lookup(int fd, const void *key)
 		return hash_lookup(m, key);
 	case T_LPM_TRIE:
 		return key ? lpm_lookup(m, key) : NULL;
+	case T_RINGBUF:
+		g_errno = ENOTSUP;
+		return NULL;
 	case T_PERCPU_HASH: { /* per_cpu_hash_map.cpp:48-64 */
 		if (!key) {
 			g_errno = ENOENT;

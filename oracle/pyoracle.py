@@ -55,6 +55,7 @@ def lib():
             "orc_map_raw": (vp, [C.c_int, C.POINTER(C.c_size_t)]),
             "orc_map_buckets": (u64, [C.c_int]),
             "orc_map_count": (u64, [C.c_int]),
+            "orc_ringbuf_fetch": (C.c_int64, [C.c_int, vp, u64, C.POINTER(C.c_uint64)]),
             "orc_map_ptr_by_fd": (u64, [u32]),
             "orc_map_val": (u64, [u64]),
             "orc_next_prime": (u64, [u64]),
@@ -202,6 +203,18 @@ class OracleMap:
 
     def count(self) -> int:
         return lib().orc_map_count(self.fd)
+
+    def ringbuf_fetch(self, cap: int = 1 << 24) -> list:
+        """Consume committed ring-buffer records (ringbuf::fetch_data)."""
+        buf = C.create_string_buffer(cap)
+        used = C.c_uint64(0)
+        n = lib().orc_ringbuf_fetch(self.fd, buf, cap, C.byref(used))
+        raw, out, off = buf.raw[:used.value], [], 0
+        for _ in range(max(n, 0)):
+            ln = int.from_bytes(raw[off:off + 4], "little")
+            out.append(raw[off + 4:off + 4 + ln])
+            off += 4 + ln
+        return out
 
     @staticmethod
     def errno() -> int:
