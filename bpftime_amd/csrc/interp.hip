@@ -456,6 +456,19 @@ __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const Fas
   return why;
 }
 
+// xdp_md_userspace of one unit (runtime/extension/userspace_xdp.h:6-17)
+__device__ __forceinline__ void write_xdp_ctx(XdpCtx *x, uint64_t slot, uint32_t len, uint64_t chunk,
+                                              const KParams &p) {
+  x->data = slot + p.head;
+  x->data_end = slot + p.head + len;
+  x->data_meta = 0;
+  x->ingress_ifindex = p.ifindex;
+  x->rx_queue_index = p.rxq;
+  x->egress_ifindex = 0;
+  x->buffer_start = chunk;
+  x->buffer_end = chunk + (p.descs && !p.stride ? len : p.stride);
+}
+
 template <uint32_t KIND, bool BIGSTACK>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_interp(KParams pin) {
   // Copy every kernel argument through an SGPR barrier: without it the
@@ -564,16 +577,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       // the ctx only exists in LDS when the program reads it generically
       // (loader: ctx uses other than the specialised data / data_end loads)
       XdpCtx *x = (XdpCtx *)my_ctx;
-      if (p.needs_ctx) {
-      x->data = slot + p.head;
-      x->data_end = slot + p.head + len;
-      x->data_meta = 0;
-      x->ingress_ifindex = p.ifindex;
-      x->rx_queue_index = p.rxq;
-      x->egress_ifindex = 0;
-      x->buffer_start = chunk;
-      x->buffer_end = chunk + (p.descs && !p.stride ? len : p.stride);
-      }
+      if (p.needs_ctx) write_xdp_ctx(x, slot, len, chunk, p);
       fu.r1 = (uint64_t)(uintptr_t)x;
       fu.r2 = 48;
     } else {
@@ -595,6 +599,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     c.steps = 0;
 
     bool uni = true;
+    // the asm tier computes specialised ctx->data / data_end loads from the
+    // slot; the C++ tier reads the ctx, so it is written before the C++ tier
+    // first runs an instruction of this unit
+    bool ctx_ready = KIND != CTX_XDP || p.needs_ctx;
+    auto ctx_for_cpp = [&]() {
+      if (KIND == CTX_XDP && !ctx_ready) {
+        write_xdp_ctx((XdpCtx *)my_ctx, slot, len, chunk, p);
+        ctx_ready = true;
+      }
+    };
     while (__ballot(c.alive) != 0) {
       uint32_t r;
       if (uni) {
@@ -613,8 +627,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
           c.alive = false;
           break;
         }
+        ctx_for_cpp();
         r = run_loop<true, true>(c);
       } else {
+        ctx_for_cpp();
         r = run_loop<false>(c);
       }
       if (r == R_STEP) continue;

@@ -506,3 +506,35 @@ def test_ctx_reads_after_divergence(fresh_oracle, fresh_runtime, monkeypatch, as
     dv = dev.DeviceBuffer(4 * n)
     assert vm.exec_batch(dev.CTX_XDP, d, n, 64, lens=dl, verdicts=dv) == 0
     np.testing.assert_array_equal(dv.download(np.uint32), want)
+
+
+@pytest.mark.parametrize("asm_groups", [True, False])
+def test_ctx_reads_inside_divergent_groups(fresh_oracle, fresh_runtime, monkeypatch, asm_groups):
+    """ctx->data read inside each of six lane groups (before they
+    reconverge), so the C++ tier executes ctx loads itself."""
+    if not asm_groups:
+        monkeypatch.setenv("BPFTIME_AMD_NO_ASM_DIVERGENCE", "1")
+    po, dev = fresh_oracle, fresh_runtime
+    a = Asm().mov64(6, "r1").ldx(8, 2, 1, 0).ldx(1, 3, 2, 0)
+    for k in range(5):
+        a.jmp("jeq", 3, k, f"g{k}")
+    a.mov64(0, 9).ja("tail")
+    for k in range(5):
+        a.label(f"g{k}").ldx(8, 2, 6, 0).ldx(8, 4, 6, 8).alu64("sub", 4, "r2")
+        a.ldx(1, 5, 2, k + 1).alu64("lsh", 5, 8).alu64("or", 5, "r4").mov64(0, "r5").add64(0, k).ja("tail")
+    a.label("tail").exit()
+    code = a.assemble()
+    n = 4096
+    pk = gen.xdp_packets(n, seed=78)
+    pk[:, 0] %= 7
+    lens = (np.arange(n) % 50 + 14).astype(np.uint32)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    want = ovm.run_xdp(pk.copy(), lens=lens)
+    vm = dev.VM()
+    vm.load(code)
+    d = dev.DeviceBuffer.from_array(pk)
+    dl = dev.DeviceBuffer.from_array(lens)
+    dv = dev.DeviceBuffer(4 * n)
+    assert vm.exec_batch(dev.CTX_XDP, d, n, 64, lens=dl, verdicts=dv) == 0
+    np.testing.assert_array_equal(dv.download(np.uint32), want)
