@@ -538,3 +538,96 @@ def test_ctx_reads_inside_divergent_groups(fresh_oracle, fresh_runtime, monkeypa
     dv = dev.DeviceBuffer(4 * n)
     assert vm.exec_batch(dev.CTX_XDP, d, n, 64, lens=dl, verdicts=dv) == 0
     np.testing.assert_array_equal(dv.download(np.uint32), want)
+
+
+def _random_xdp_program(rng, map_fd, nins=50):
+    """Random XDP program of the shapes a verifier accepts: scalars in
+    r0-r5, r6 = ctx, r7 / r8 = data / data_end (re-read from the ctx at
+    random points), 64 B bounds-checked once, packet loads / stores at
+    constant offsets, stack traffic, forward branches on scalars, and
+    array-map counters (lookup + fused add)."""
+    a = Asm().mov64(6, "r1").ldx(8, 7, 1, 0).ldx(8, 8, 1, 8)
+    a.mov64(9, "r7").add64(9, 64).mov64(0, 1).jmp("jgt", 9, "r8", "out")
+    for r in range(6):
+        a.mov64(r, int(rng.integers(-100, 100)))
+    labels, pending = 0, []
+    for i in range(nins):
+        k = int(rng.integers(0, 12))
+        dst = int(rng.integers(0, 6))
+        src = "r%d" % int(rng.integers(0, 6))
+        if k < 3:
+            op = ["add", "sub", "xor", "or", "and", "lsh", "rsh", "mul"][int(rng.integers(0, 8))]
+            v = src if rng.integers(0, 2) else int(rng.integers(0, 31))
+            (a.alu32 if rng.integers(0, 2) else a.alu64)(op, dst, v)
+        elif k < 5:
+            sz = [1, 2, 4, 8][int(rng.integers(0, 4))]
+            a.ldx(sz, dst, 7, int(rng.integers(0, 64 - sz + 1)))
+        elif k < 6:
+            sz = [1, 2, 4, 8][int(rng.integers(0, 4))]
+            a.stx(sz, 7, int(rng.integers(0, 64 - sz + 1)), src)
+        elif k < 7:
+            a.ldx(8, 7, 6, 0) if rng.integers(0, 2) else a.ldx(8, 8, 6, 8)
+        elif k < 8:
+            off = -8 * int(rng.integers(1, 6))
+            a.stx(8, 10, off, src).ldx(8, dst, 10, off)
+        elif k < 10:
+            name = f"L{labels}"
+            labels += 1
+            op = JMP[int(rng.integers(0, len(JMP)))]
+            v = src if rng.integers(0, 2) else int(rng.integers(-5, 5))
+            (a.jmp32 if rng.integers(0, 2) else a.jmp)(op, dst, v, name)
+            pending.append((name, i + int(rng.integers(1, 6))))
+        else:
+            # counters[(dst & 3)] += 1 (lookup_elem, fused ldx / add / stx)
+            skip = f"M{labels}"
+            labels += 1
+            a.mov64(9, f"r{dst}").alu64("and", 9, 3).stx(4, 10, -48, "r9")
+            a.ld_map_fd(1, map_fd).mov64(2, "r10").add64(2, -48).call(1)
+            a.jmp("jeq", 0, 0, skip).ldx(8, 1, 0, 0).add64(1, int(rng.integers(1, 9))).stx(8, 0, 0, "r1")
+            a.label(skip)
+            for r in range(6):
+                a.mov64(r, int(rng.integers(-100, 100)))
+        for name, at in list(pending):
+            if at <= i:
+                a.label(name)
+                pending.remove((name, at))
+    for name, _ in pending:
+        a.label(name)
+    a.alu64("xor", 0, "r1").alu64("add", 0, "r2").alu64("xor", 0, "r3").alu64("add", 0, "r4")
+    a.alu64("xor", 0, "r5").ldx(8, 2, 6, 8).ldx(8, 3, 6, 0).alu64("sub", 2, "r3").alu64("add", 0, "r2")
+    a.label("out").exit()
+    return a.assemble()
+
+
+@pytest.mark.parametrize("asm_groups", [True, False])
+def test_random_xdp_programs(fresh_oracle, fresh_runtime, monkeypatch, asm_groups):
+    """Random verifier-shaped XDP programs: verdicts, packet bytes and map
+    counters bit-exact against the oracle, with lane groups in asm and in
+    the C++ tier."""
+    if not asm_groups:
+        monkeypatch.setenv("BPFTIME_AMD_NO_ASM_DIVERGENCE", "1")
+    po, dev = fresh_oracle, fresh_runtime
+    rng = np.random.default_rng(2024)
+    n = 2048
+    for t in range(64):
+        po.reset()
+        dev.reset_runtime()
+        (om,), (dm,) = make_maps([(isa.BPF_MAP_TYPE_ARRAY, 4, 8, 4)], po, dev)
+        code = _random_xdp_program(rng, dm.fd)
+        pk = gen.xdp_packets(n, seed=100 + t)
+        lens = np.where(np.arange(n) % 13 == 0, 40, 64).astype(np.uint32)
+        ovm = po.OracleVM()
+        ovm.load(code)
+        opk = pk.copy()
+        want = ovm.run_xdp(opk, lens=lens)
+        vm = dev.VM()
+        vm.load(code)
+        d = dev.DeviceBuffer.from_array(pk)
+        dl = dev.DeviceBuffer.from_array(lens)
+        dv = dev.DeviceBuffer(4 * n)
+        assert vm.exec_batch(dev.CTX_XDP, d, n, 64, lens=dl, verdicts=dv) == 0, t
+        np.testing.assert_array_equal(dv.download(np.uint32), want, err_msg=f"program {t}")
+        np.testing.assert_array_equal(d.download().reshape(n, 64), opk, err_msg=f"program {t}")
+        for k in range(4):
+            key = struct.pack("<I", k)
+            assert dm.lookup(key) == om.lookup(key), (t, k)
