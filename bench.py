@@ -36,6 +36,7 @@ def parse():
     ap.add_argument("--unchecked", action="store_true", help="skip the global-window check")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe-inclusive) leg")
     ap.add_argument("--e2e-chunk-log2", type=int, default=20, help="packets per H2D chunk = 2^k")
+    ap.add_argument("--e2e-streams", type=int, default=3, help="streams the host-memory leg rotates over")
     args = ap.parse_args()
     args.log2n_set = args.log2n is not None
     if args.log2n is None:
@@ -130,7 +131,7 @@ def main():
     shard = bss.snapshot()
     e2e = None
     if not args.no_e2e:
-        e2e = e2e_leg(dev, vm, bss, n, first, args.e2e_chunk_log2, dist)
+        e2e = e2e_leg(dev, vm, bss, n, first, args.e2e_chunk_log2, dist, nstreams=args.e2e_streams)
     times = [wall]
     shards = [shard]
     oks = [ok_verdicts and ok_counter and ok_bytes]
@@ -217,7 +218,7 @@ def main():
         dist.destroy_process_group()
 
 
-def e2e_leg(dev, vm, bss, n, first, chunk_log2, dist, passes=3):
+def e2e_leg(dev, vm, bss, n, first, chunk_log2, dist, passes=3, nstreams=2):
     """Path that starts and ends in host memory: pinned host frames -> chunked
     hipMemcpyAsync H2D -> interpreter -> verdicts (and, in the second mode,
     the rewritten frames) D2H, double-buffered on two streams.  Reported
@@ -234,9 +235,9 @@ def e2e_leg(dev, vm, bss, n, first, chunk_log2, dist, passes=3):
     hverd = L.bpftime_amd_host_alloc(4 * n)
     if not host or not hverd:
         return {"error": "pinned host allocation failed"}
-    dbuf = [dev.DeviceBuffer(chunk * PKT) for _ in range(2)]
-    dver = [dev.DeviceBuffer(4 * chunk) for _ in range(2)]
-    streams = [L.bpftime_amd_stream_create() for _ in range(2)]
+    dbuf = [dev.DeviceBuffer(chunk * PKT) for _ in range(nstreams)]
+    dver = [dev.DeviceBuffer(4 * chunk) for _ in range(nstreams)]
+    streams = [L.bpftime_amd_stream_create() for _ in range(nstreams)]
     try:
         for c in range(nch):  # host frames = the same seeded stream as the resident leg
             L.bpftime_amd_gen_xdp(dbuf[0].ptr, chunk, PKT, PKT, gen.SEED_CFG2, first + c * chunk, None)
@@ -245,7 +246,7 @@ def e2e_leg(dev, vm, bss, n, first, chunk_log2, dist, passes=3):
 
         def one_pass(frames_back):
             for c in range(nch):
-                b, s = c % 2, streams[c % 2]
+                b, s = c % nstreams, streams[c % nstreams]
                 off = c * chunk
                 L.bpftime_amd_memcpy_htod_async(dbuf[b].ptr, host + off * PKT, chunk * PKT, s)
                 vm.exec_batch(dev.CTX_XDP, dbuf[b], chunk, PKT, fixed_len=PKT, verdicts=dver[b], flags=0,
@@ -256,7 +257,7 @@ def e2e_leg(dev, vm, bss, n, first, chunk_log2, dist, passes=3):
             for s in streams:
                 L.bpftime_amd_stream_sync(s)
 
-        out = {"chunk_packets": chunk, "streams": 2, "passes": passes}
+        out = {"chunk_packets": chunk, "streams": nstreams, "passes": passes}
         c0 = int(np.frombuffer(bss.lookup(b"\0\0\0\0"), dtype=np.uint64)[0])
         for mode, back in (("verdicts_out", False), ("frames_and_verdicts_out", True)):
             one_pass(back)  # warm-up
@@ -280,12 +281,12 @@ def e2e_leg(dev, vm, bss, n, first, chunk_log2, dist, passes=3):
 def merge_e2e(e2es, world, n):
     if any(e is None or "error" in e for e in e2es):
         return next((e for e in e2es if e is not None), None)
-    out = {"unit": "Mpps", "chunk_packets": e2es[0]["chunk_packets"], "streams": 2,
+    out = {"unit": "Mpps", "chunk_packets": e2es[0]["chunk_packets"], "streams": e2es[0]["streams"],
            "ok": all(e["ok"] for e in e2es)}
     for mode in ("verdicts_out", "frames_and_verdicts_out"):
         t = max(e[mode + "_s"] for e in e2es)
         out[mode] = round(world * n / t / 1e6, 3)
-    out["note"] = ("pinned host frames -> hipMemcpyAsync H2D -> interpreter -> D2H, 2 streams; "
+    out["note"] = ("pinned host frames -> hipMemcpyAsync H2D -> interpreter -> D2H, round-robin streams; "
                    "PCIe-inclusive, not the headline value")
     return out
 
