@@ -230,10 +230,143 @@ def syscall_agg(args, dev, gen, isa, programs):
     }
 
 
+def _lpm_routes(rng, nroutes):
+    """Every /8 (so each address has a route) plus random /12../28 prefixes;
+    values 1..3 = DROP / PASS / TX."""
+    routes = [(8, i << 24, 1 + (i % 3)) for i in range(256)]
+    while len(routes) < nroutes:
+        plen = int(rng.integers(12, 29))
+        net = int(rng.integers(0, 1 << 32)) & ((0xFFFFFFFF << (32 - plen)) & 0xFFFFFFFF)
+        routes.append((plen, net, int(rng.integers(1, 4))))
+    return routes
+
+
+def lpm_route(args, dev, gen, isa, programs):
+    """LPM_TRIE routing: 2^24 random 64-B IPv4 frames,
+    16384 routes, one lookup per frame on the device replica."""
+    n = 1 << (args.log2n if args.log2n_set else 24)
+    rng = np.random.default_rng(0x5EED0006)
+    routes = _lpm_routes(rng, 16384)
+    dev.reset_runtime()
+    rt = dev.Map(isa.BPF_MAP_TYPE_LPM_TRIE, 8, 4, len(routes), name="routes")
+    for plen, net, v in routes:
+        rt.update(struct.pack("<I", plen) + struct.pack(">I", net), struct.pack("<I", v))
+    code = programs.lpm_route(rt.fd)
+    vm = dev.VM()
+    vm.load(code)
+    pk = dev.DeviceBuffer(n * 64)
+    if dev.lib().bpftime_amd_gen_xdp(pk.ptr, n, 64, 64, gen.SEED_CFG2 ^ 0x6, 0, None):
+        raise SystemExit("generator failed")
+    dv = dev.DeviceBuffer(4 * n)
+
+    def step():
+        vm.exec_batch(dev.CTX_XDP, pk, n, 64, fixed_len=64, verdicts=dv, flags=0)
+
+    wall, kern_s = _timed(dev, step, args.steps, args.warmup)
+    from oracle import pyoracle as po   # checker: the oracle over a sample of the same frames
+    sn = min(n, 1 << 18)
+    sample = pk.download(count=sn * 64).reshape(sn, 64)
+    po.reset()
+    om = po.OracleMap(isa.BPF_MAP_TYPE_LPM_TRIE, 8, 4, len(routes), fd=rt.fd)
+    for plen, net, v in routes:
+        om.update(struct.pack("<I", plen) + struct.pack(">I", net), struct.pack("<I", v))
+    ovm = po.OracleVM()
+    ovm.load(code)
+    t0 = time.perf_counter()
+    want = ovm.run_xdp(sample.copy(), fixed_len=64)
+    cpu_s = time.perf_counter() - t0
+    verd = dv.download(np.uint32)
+    ok = bool((verd[:sn] == want).all()) and bool(np.isin(verd, [1, 2, 3]).all())
+    cpu = None if args.no_cpu_baseline else {
+        "value": round(sn / cpu_s / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
+        "sample": f"the oracle over the first 2^{int(np.log2(sn))} frames ({cpu_s:.2f} s)"}
+    algo = 2 + 4 + 4.0   # ethertype + daddr + verdict (the 640-KB trie is on-chip)
+    achieved = algo * n / kern_s / 1e9
+    return {
+        "metric": "device-resident Mpps, LPM-trie routing XDP prog (16384 IPv4 routes), 64B pkts",
+        "value": round(n * args.steps / wall / 1e6, 3), "unit": "Mpps", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic (seeded splitmix64 64-B IPv4 frames; routes: every /8 + random /12../28)",
+        "config": {"workload": "lpm-route over 2^%d device-resident 64-B frames" % int(np.log2(n)),
+                   "packets": n, "routes": len(routes)},
+        "parity": {"sample_verdicts_exact": ok, "sample": sn, "ok": ok,
+                   "verdicts": {str(k): int((verd == k).sum()) for k in (1, 2, 3)}},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "kernel_avg_ms": round(kern_s * 1e3, 4), "algo_bytes_per_pkt": algo},
+        "cpu_baseline": cpu,
+    }
+
+
+def ringbuf_sample(args, dev, gen, isa, programs):
+    """RINGBUF sampling: 2^24 64-B frames, every 64th
+    (by its first byte) sends its 12 MAC bytes through bpf_ringbuf_output;
+    the 256-MiB ring holds every run's records (the consumer drains it once,
+    after the timed runs)."""
+    n = 1 << (args.log2n if args.log2n_set else 24)
+    os.environ.setdefault("BPFTIME_AMD_ARENA_MB", "1024")   # the ring's 2 x 256 MiB of records
+    dev.reset_runtime()
+    runs = args.steps + args.warmup
+    size = 1 << 28
+    rb = dev.Map(isa.BPF_MAP_TYPE_RINGBUF, 0, 0, size, name="samples")
+    code = programs.ringbuf_sampler(rb.fd, every_log2=6)
+    vm = dev.VM()
+    vm.load(code)
+    pk = dev.DeviceBuffer(n * 64)
+    if dev.lib().bpftime_amd_gen_xdp(pk.ptr, n, 64, 64, gen.SEED_CFG2, 0, None):
+        raise SystemExit("generator failed")
+    dv = dev.DeviceBuffer(4 * n)
+
+    def step():
+        vm.exec_batch(dev.CTX_XDP, pk, n, 64, fixed_len=64, verdicts=dv, flags=0)
+
+    wall, kern_s = _timed(dev, step, args.steps, args.warmup)
+    first = pk.download(count=n * 64).reshape(n, 64)[:, 0]
+    picked = int((first % 64 == 0).sum())
+    recs = rb.ringbuf_fetch(cap=size * 2)
+    fits = min(runs * picked, size // 24)
+    verd = dv.download(np.uint32)
+    ok = len(recs) == fits and all(r[0] % 64 == 0 for r in recs[:4096]) and \
+        (runs * picked > fits or bool((verd == isa.XDP_PASS).all()))
+    algo = 1 + 4 + 24 / 64   # first byte + verdict + a 24-B record for one frame in 64
+    achieved = algo * n / kern_s / 1e9
+    cpu = None
+    if not args.no_cpu_baseline:   # the oracle over a sample of the same frames
+        from oracle import pyoracle as po
+        sn = min(n, 1 << 18)
+        sample = pk.download(count=sn * 64).reshape(sn, 64)
+        po.reset()
+        om = po.OracleMap(isa.BPF_MAP_TYPE_RINGBUF, 0, 0, 1 << 24, fd=rb.fd)
+        ovm = po.OracleVM()
+        ovm.load(code)
+        t0 = time.perf_counter()
+        ovm.run_xdp(sample.copy(), fixed_len=64)
+        cpu_s = time.perf_counter() - t0
+        ok = ok and len(om.ringbuf_fetch()) == int((sample[:, 0] % 64 == 0).sum())
+        cpu = {"value": round(sn / cpu_s / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
+               "sample": f"the oracle over the first 2^{int(np.log2(sn))} frames ({cpu_s:.2f} s)"}
+    return {
+        "metric": "device-resident Mpps, ring-buffer sampling XDP prog (1/64 frames), 64B pkts",
+        "value": round(n * args.steps / wall / 1e6, 3), "unit": "Mpps", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic (seeded splitmix64 64-B frames, seed 0x5EED0002)",
+        "config": {"workload": "ringbuf-sample over 2^%d device-resident 64-B frames, 256-MiB ring"
+                               % int(np.log2(n)), "packets": n, "records_per_run": picked},
+        "parity": {"records": len(recs), "expected_records": fits, "ok": ok},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "kernel_avg_ms": round(kern_s * 1e3, 4), "algo_bytes_per_pkt": algo},
+        "cpu_baseline": cpu,
+    }
+
+
 def run(args):
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         raise SystemExit("--workload %s runs on one GPU (BASELINE configs[2]/[4])" % args.workload)
     from bpftime_amd import gen, isa, programs
     from bpftime_amd import vm as dev
-    fn = {"flow-hash": flow_hash, "syscall-agg": syscall_agg}[args.workload]
+    fn = {"flow-hash": flow_hash, "syscall-agg": syscall_agg, "lpm-route": lpm_route,
+          "ringbuf-sample": ringbuf_sample}[args.workload]
     print(json.dumps(fn(args, dev, gen, isa, programs)))

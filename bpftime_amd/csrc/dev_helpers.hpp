@@ -269,16 +269,23 @@ __device__ uint64_t lpm_lookup(const DMap &m, uint64_t key) {
 // as a serial one would at that point.
 // ---------------------------------------------------------------------------
 constexpr uint32_t RB_BUSY = 0x80000000u, RB_DISCARD = 0x40000000u, RB_HDR = 8;
+constexpr uint64_t kRbMaxWaves = 256 * 32;                 // CUs x resident waves per CU (upper bound)
+constexpr uint64_t kRbWaveMax = 4096;                      // largest wave reservation on the fast path
+constexpr uint64_t kRbSlack = kRbMaxWaves * kRbWaveMax;    // 32 MiB
 
 __device__ __forceinline__ uint64_t rb_cas_reserve(const DMap &m, uint64_t total) {
   // returns the old producer position, or ~0 if total does not fit
   const uint64_t cons = __hip_atomic_load(G64(m.data), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   unsigned long long p = __hip_atomic_load(G64(m.data + 128), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t backoff = 1;
   for (uint32_t spin = 0; spin < (1u << 20); spin++) {
     if ((uint64_t)m.max_entries - (p - cons) < total) return ~0ull;
     if (__hip_atomic_compare_exchange_strong(G64(m.data + 128), &p, p + total, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT))
       return p;
+    // lost to another wave: back off (thousands of waves share this word)
+    for (uint32_t i = 0; i < backoff; i++) __builtin_amdgcn_s_sleep(2);
+    backoff = backoff < 64 ? 2 * backoff : 64;
   }
   return ~0ull;
 }
@@ -303,7 +310,20 @@ __device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size) {
       sum += t;
     }
     uint64_t base = ~0ull;
-    if (me == leader) base = rb_cas_reserve(m, sum);
+    if (me == leader) {
+      // Plenty of room: a fetch-and-add (same-address atomics serialize at
+      // the memory side, ~12 ns each, while a CAS retry loop under the
+      // contention of thousands of waves costs microseconds per record).
+      // Safe because at most kRbMaxWaves reservations of <= kRbWaveMax
+      // bytes can be between their room check and their add, so an add
+      // admitted with kRbSlack bytes to spare never overruns the consumer.
+      const uint64_t cons = __hip_atomic_load(G64(m.data), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t prod = __hip_atomic_load(G64(m.data + 128), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (sum <= kRbWaveMax && (uint64_t)m.max_entries - (prod - cons) >= sum + kRbSlack)
+        base = __hip_atomic_fetch_add(G64(m.data + 128), sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        base = rb_cas_reserve(m, sum);
+    }
     base = __shfl(base, leader);
     if (base != ~0ull) pos = base + before;
   }

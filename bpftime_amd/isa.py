@@ -61,6 +61,10 @@ BPF_FUNC_get_smp_processor_id = 8
 BPF_FUNC_csum_diff = 28
 BPF_FUNC_xdp_adjust_head = 44
 BPF_FUNC_xdp_adjust_tail = 65
+BPF_FUNC_ringbuf_output = 130
+BPF_FUNC_ringbuf_reserve = 131
+BPF_FUNC_ringbuf_submit = 132
+BPF_FUNC_ringbuf_discard = 133
 BPF_FUNC_xdp_load_bytes = 189
 
 # map types (linux/bpf.h)

@@ -17,7 +17,7 @@ semantics after libbpf relocation / CO-RE, not byte-identical clang output.
 from __future__ import annotations
 
 from .isa import (Asm, BPF_ANY, BPF_FUNC_map_lookup_elem, BPF_FUNC_map_update_elem,
-                  BPF_NOEXIST, ATOMIC_ADD, XDP_DROP, XDP_PASS, XDP_TX, XDP_ABORTED)
+                  BPF_FUNC_ringbuf_output, BPF_NOEXIST, ATOMIC_ADD, XDP_DROP, XDP_PASS, XDP_TX, XDP_ABORTED)
 
 ETH_P_IP_LE = 0x0008  # htons(0x0800) as read by a little-endian ldxh
 IPPROTO_TCP, IPPROTO_UDP = 6, 17
@@ -197,6 +197,34 @@ def syscall_agg(counts_fd: int) -> bytes:
     a.label("ret")
     a.mov64(0, 0)
     a.exit()
+    return a.assemble()
+
+
+def lpm_route(routes_fd: int) -> bytes:
+    """XDP routing: verdict = u32 value of the longest prefix (LPM_TRIE,
+    key {u32 prefixlen = 32, be32 daddr}) containing the IPv4 destination;
+    PASS when there is no route or the frame is not IPv4."""
+    a = Asm().ldx(8, 2, 1, 0).ldx(8, 3, 1, 8).mov64(0, XDP_PASS)
+    a.mov64(4, "r2").add64(4, 34).jmp("jgt", 4, "r3", "out")
+    a.ldx(2, 4, 2, 12).jmp("jne", 4, ETH_P_IP_LE, "out")
+    a.st(4, 10, -8, 32).ldx(4, 4, 2, 30).stx(4, 10, -4, "r4")
+    a.ld_map_fd(1, routes_fd).mov64(2, "r10").add64(2, -8).call(BPF_FUNC_map_lookup_elem)
+    a.mov64(1, "r0").mov64(0, XDP_PASS).jmp("jeq", 1, 0, "out").ldx(4, 0, 1, 0)
+    a.label("out").exit()
+    return a.assemble()
+
+
+def ringbuf_sampler(rb_fd: int, every_log2: int = 4) -> bytes:
+    """XDP sampler: frames whose first byte is 0 modulo 2^every_log2 send
+    their first 12 bytes (the MACs) to a ring buffer with
+    bpf_ringbuf_output (bpf_helper.cpp:451-467); verdict PASS, DROP when
+    the ring had no room."""
+    a = Asm().ldx(8, 2, 1, 0).ldx(8, 3, 1, 8).mov64(0, XDP_PASS)
+    a.mov64(4, "r2").add64(4, 14).jmp("jgt", 4, "r3", "out")
+    a.ldx(1, 4, 2, 0).alu64("and", 4, (1 << every_log2) - 1).jmp("jne", 4, 0, "out")
+    a.ld_map_fd(1, rb_fd).mov64(3, 12).mov64(4, 0).call(BPF_FUNC_ringbuf_output)
+    a.mov64(1, "r0").mov64(0, XDP_PASS).jmp("jeq", 1, 0, "out").mov64(0, XDP_DROP)
+    a.label("out").exit()
     return a.assemble()
 
 
