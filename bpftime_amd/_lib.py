@@ -36,7 +36,7 @@ class EbpfBatch(C.Structure):  # include/ebpf-vm.h struct ebpf_batch
                 ("rx_queue_index", C.c_uint32), ("head", C.c_uint32), ("verdicts", C.c_void_p),
                 ("rets", C.c_void_p), ("data_off_out", C.c_void_p), ("len_out", C.c_void_p),
                 ("first_unit", C.c_uint64), ("stream", C.c_void_p), ("descs", C.c_void_p),
-                ("umem_bytes", C.c_uint64)]
+                ("umem_bytes", C.c_uint64), ("sys_nr", C.c_int64)]
 
 
 # (name, restype, argtypes) for every exported symbol of include/*.h
@@ -109,6 +109,9 @@ SIGNATURES = [
     ("bpftime_object_license", C.c_char_p, [C.c_void_p]),
     ("bpftime_object_close", None, [C.c_void_p]),
     ("bpftime_amd_ringbuf_fetch", C.c_int64, [C.c_int, C.c_void_p, C.c_uint64, u64p]),
+    ("bpftime_amd_syscall_attach", C.c_int, [C.c_int, C.c_int64]),
+    ("bpftime_amd_syscall_detach", C.c_int, [C.c_int]),
+    ("bpftime_amd_syscall_dispatch", C.c_int64, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]),
     ("bpftime_amd_merge_delta_u64", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     ("bpftime_amd_device_count", C.c_int, []),
     ("bpftime_amd_set_device", C.c_int, [C.c_int]),

@@ -154,6 +154,7 @@ struct KParams {
   uint32_t needs_ctx;     // XDP: the program reads its ctx generically (build it in LDS)
   const uint64_t *descs;  // AF_XDP descriptors {u64 addr; u32 len; u32 options} or nullptr
   uint64_t umem_bytes;    // descriptor mode: bytes at data
+  int64_t sys_nr;         // CTX_SYSCALL: run only records with this id (-1: every record)
 };
 
 // Error codes recorded per unit (err_count counts units with any error)

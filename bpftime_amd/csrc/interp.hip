@@ -482,6 +482,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
   SRP(descs); SRV(umem_bytes);
+  p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
 #undef SRP
 #undef SRV
   __shared__ uint64_t Rf[12 * kBlock];  // r0..r10 + a dummy slot per lane
@@ -589,7 +590,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     if (KIND == CTX_SYSCALL && active) {
       // exit / exit_group bypass every callback (syscall_trace_attach_impl.cpp:25)
       const int64_t nr = *(const int64_t *)(slot + 8);
-      if (nr == 60 || nr == 231) alive = false;
+      if (nr == 60 || nr == 231 || (p.sys_nr >= 0 && nr != p.sys_nr)) alive = false;
     }
     c.unit = unit;
     c.alive = alive && desc_ok;
@@ -677,7 +678,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         atomicAdd(p.err_count, 1u);
       } else if (KIND == CTX_SYSCALL) {
         const int64_t nr = *(const int64_t *)(slot + 8);
-        if (nr == 60 || nr == 231) {
+        if (nr == 60 || nr == 231 || (p.sys_nr >= 0 && nr != p.sys_nr)) {
           if (p.verdicts) p.verdicts[unit] = 0;
           if (p.rets) p.rets[unit] = 0;
         }

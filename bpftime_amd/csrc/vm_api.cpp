@@ -209,6 +209,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   p.data_hi = p.data_lo + (b->descs ? b->umem_bytes : b->count * b->stride);
   p.descs = (const uint64_t *)b->descs;
   p.umem_bytes = b->umem_bytes;
+  p.sys_nr = (b->flags & EBPF_BATCH_SYS_NR) && b->ctx_kind == CTX_SYSCALL ? b->sys_nr : -1;
   p.arena_lo = (uint64_t)(uintptr_t)r.arena;
   p.arena_hi = p.arena_lo + r.arena_size;
   p.step_limit = step_limit;

@@ -16,7 +16,7 @@ from . import isa
 from ._lib import BpfLinkCreateArgs, BpfMapAttr, EbpfBatch, lib
 
 CTX_RAW, CTX_XDP, CTX_SYSCALL = 0, 1, 2
-BATCH_SYNC, BATCH_ORDERED, BATCH_UNCHECKED = 0x1, 0x2, 0x4
+BATCH_SYNC, BATCH_ORDERED, BATCH_UNCHECKED, BATCH_SYS_NR = 0x1, 0x2, 0x4, 0x8
 
 
 class EbpfError(RuntimeError):
@@ -250,7 +250,8 @@ class VM:
                    rets: Optional[DeviceBuffer] = None, data_off_out: Optional[DeviceBuffer] = None,
                    len_out: Optional[DeviceBuffer] = None, flags: int = BATCH_SYNC, first_unit: int = 0,
                    head: int = 0, data_offset: int = 0, ifindex: int = 0, rxq: int = 0,
-                   stream: int = 0, descs: Optional[DeviceBuffer] = None, umem_bytes: int = 0) -> int:
+                   stream: int = 0, descs: Optional[DeviceBuffer] = None, umem_bytes: int = 0,
+                   sys_nr: Optional[int] = None) -> int:
         """descs: AF_XDP descriptor mode ({u64 addr; u32 len; u32 options} per
         unit, frames at data + addr inside umem_bytes; stride = chunk size)."""
         b = EbpfBatch(ctx_kind=kind, flags=flags, count=count, data=data.ptr + data_offset, stride=stride,
@@ -259,7 +260,10 @@ class VM:
                       rets=rets.ptr if rets else None,
                       data_off_out=data_off_out.ptr if data_off_out else None,
                       len_out=len_out.ptr if len_out else None, first_unit=first_unit,
-                      stream=stream or None, descs=descs.ptr if descs else None, umem_bytes=umem_bytes)
+                      stream=stream or None, descs=descs.ptr if descs else None, umem_bytes=umem_bytes,
+                      sys_nr=-1 if sys_nr is None else sys_nr)
+        if sys_nr is not None:
+            b.flags |= BATCH_SYS_NR
         rc = lib().ebpf_exec_batch(C.c_void_p(self.h), C.byref(b))
         if rc < 0:
             e = lib().bpftime_amd_vm_error(C.c_void_p(self.h))

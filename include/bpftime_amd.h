@@ -161,6 +161,17 @@ void bpftime_object_close(struct bpftime_object *obj);
  * count (-1: not a ring buffer).  Waits for queued batches first. */
 int64_t bpftime_amd_ringbuf_fetch(int fd, void *out, uint64_t cap, uint64_t *used);
 
+/* ---- syscall tracepoint dispatch (csrc/syscall_dispatch.cpp) ----
+ * syscall_trace_attach_impl.cpp:18-95: attach a program to the sys_enter
+ * tracepoint of `sys_nr` (-1: every syscall); a replay batch of n 64-B
+ * trace_event_raw_sys_enter records (device memory) runs the per-syscall
+ * programs on their records, then the global ones, skipping exit /
+ * exit_group; r0 is ignored.  Returns the failed-unit count with
+ * EBPF_BATCH_SYNC in flags, else 0; -1 on errors. */
+int bpftime_amd_syscall_attach(int prog_fd, int64_t sys_nr);   /* attach id or -1 */
+int bpftime_amd_syscall_detach(int id);
+int64_t bpftime_amd_syscall_dispatch(const void *records, uint64_t n, uint32_t flags, void *stream);
+
 /* ---- host merge of per-GPU map shards ---- */
 /* acc += shard - init over u64 words (array counters, additive rule) */
 int bpftime_amd_merge_delta_u64(void *acc, const void *init, const void *shard, uint64_t bytes);

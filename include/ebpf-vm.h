@@ -84,6 +84,7 @@ ebpf_jit_fn ebpf_load_aot_object(struct ebpf_vm *vm, const void *buf, size_t buf
 #define EBPF_BATCH_SYNC 0x1    /* wait for completion; return the failed-unit count */
 #define EBPF_BATCH_ORDERED 0x2 /* one lane, units in index order (exact sequential semantics) */
 #define EBPF_BATCH_UNCHECKED 0x4 /* skip the global-window confinement check */
+#define EBPF_BATCH_SYS_NR 0x8    /* EBPF_CTX_SYSCALL: only records whose id == sys_nr run (per-syscall attach) */
 
 struct ebpf_batch {
 	uint32_t ctx_kind;       /* EBPF_CTX_* */
@@ -109,6 +110,7 @@ struct ebpf_batch {
 	 * head are not used.  A descriptor outside the umem fails its unit. */
 	const struct ebpf_xdp_desc *descs;
 	uint64_t umem_bytes;
+	int64_t sys_nr;          /* with EBPF_BATCH_SYS_NR: the syscall nr a per-syscall program is attached to */
 };
 
 /* linux/if_xdp.h struct xdp_desc */
