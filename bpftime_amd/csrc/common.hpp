@@ -64,6 +64,7 @@ static_assert(sizeof(DInsn) == 16, "DInsn must be 16 bytes");
 // Map types (linux/bpf.h)
 constexpr uint32_t MT_HASH = 1;
 constexpr uint32_t MT_ARRAY = 2;
+constexpr uint32_t MT_PROG_ARRAY = 3;
 constexpr uint32_t MT_PERCPU_HASH = 5;
 constexpr uint32_t MT_PERCPU_ARRAY = 6;
 constexpr uint32_t MT_LPM_TRIE = 11;
@@ -79,6 +80,8 @@ constexpr uint32_t MT_RINGBUF = 27;
 //   RINGBUF        u64 consumer position at data, u64 producer position at
 //                  data + 128 (own cache lines), 2 x max_entries record bytes
 //                  at data + 256 (ringbuf_map.cpp layout and record format)
+//   PROG_ARRAY     int32 prog fd per index, -1 = empty (prog_array.cpp's
+//                  INVALID_ENTRY; host-authoritative, read-only on the device)
 //   LPM_TRIE       read-only device replica of the host trie: a 16-B header
 //                  {i32 root node, u32 nodes} then nodes of slot_size bytes
 //                  {u32 prefixlen, u32 intermediate, i32 child[2], prefix data
@@ -115,6 +118,22 @@ inline BA_HD uint32_t ix_pos(uint64_t h, uint32_t mask) {
   return (g ^ (g >> 16)) & mask;
 }
 constexpr uint32_t kIxProbes = 8;  // index probes before the reference probe
+
+// bpf_tail_call (helper 12, bpf_helper.cpp:568-650).  The reference runs the
+// target as a nested exec over a 64-B copy of the ctx and returns its r0 to
+// the caller (depth <= 32).  Here the caller and every program a PROG_ARRAY
+// can name are linked into one image at launch (vm_api.cpp), the targets'
+// exits become calls of kRetHelper, and a call pushes a per-lane frame
+// {r1..r10, return pc, ctx bytes, stack bytes} that the matching return pops:
+// the callee runs on the same stack and ctx, restored afterwards, which is
+// what a copy gives it.
+constexpr uint32_t kTailHelper = 12;
+constexpr int32_t kRetHelper = 0x7fff0001;  // internal: a linked target's exit
+constexpr uint32_t kTailDepth = 32;          // MAX_TAIL_CALL_CNT
+constexpr uint32_t kTailGrid = 256;          // blocks per launch of an image with tail calls
+constexpr uint32_t kFrameCtx = 64;
+constexpr uint32_t kFrameHdr = 96;           // r1..r10, ctx address, ret pc, ctx bytes
+constexpr uint32_t kFrameBytes = kFrameHdr + kFrameCtx + kStackSize;
 
 // Context kinds for a batch
 constexpr uint32_t CTX_RAW = 0;      // r1 = unit memory, r2 = length
@@ -155,6 +174,8 @@ struct KParams {
   const uint64_t *descs;  // AF_XDP descriptors {u64 addr; u32 len; u32 options} or nullptr
   uint64_t umem_bytes;    // descriptor mode: bytes at data
   int64_t sys_nr;         // CTX_SYSCALL: run only records with this id (-1: every record)
+  const int32_t *tail_entry;  // prog fd -> entry pc in the linked image, -1 = not linked (nullable)
+  uint8_t *frames;        // tail-call frames: [lane][kTailDepth][kFrameBytes]
 };
 
 // Error codes recorded per unit (err_count counts units with any error)

@@ -396,6 +396,12 @@ __device__ uint64_t helper_lookup(const DMap *maps, uint64_t fd, uint64_t key, L
     }
     case MT_LPM_TRIE:
       return lpm_lookup(m, key);
+    case MT_PROG_ARRAY: {  // prog_array.cpp:113-143: the slot's prog fd
+      const int32_t k = (int32_t)*(const u32u *)key;
+      if (k < 0 || (uint32_t)k >= m.max_entries) return 0;
+      const uint64_t a = m.data + 4ull * (uint32_t)k;
+      return *(const int32_t *)a >= 0 ? a : 0;
+    }
   }
   return 0;
 }

@@ -481,7 +481,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   SRP(err_count); SRV(n); SRV(stride); SRV(first_unit); SRV(data_lo); SRV(data_hi); SRV(arena_lo);
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
-  SRP(descs); SRV(umem_bytes);
+  SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
 #undef SRP
 #undef SRV
@@ -561,6 +561,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const uint64_t vcpu = (p.first_unit + unit) / 64;
     int32_t miss_fd = -1;
     uint64_t miss_hash = 0;
+    uint32_t tdepth = 0;  // tail-call frames this lane has pushed
 
     // ---- per-unit setup: r1, r2, r10 (other registers zero) are set by the
     // fast path's fresh entry, which every unit starts with ----
@@ -646,6 +647,75 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       }
       // ---- R_CALL: helper call (bpf_helper.cpp helpers; csrc/dev_helpers.hpp) ----
       const bool csel = uni ? c.alive : (c.alive && c.lpc == c.call_pc);
+      const uint32_t cid = __builtin_amdgcn_readfirstlane(c.call_id);  // uniform by construction
+      if (p.tail_entry && (cid == kTailHelper || cid == (uint32_t)kRetHelper)) {
+        // bpf_tail_call (bpf_helper.cpp:568-650) in a linked image
+        // (common.hpp kTailHelper): push a frame and enter the target, or
+        // pop one at a target's exit.  Lanes may go to different pcs.
+        uint32_t next = c.lpc;
+        if (csel) {
+          ctx_for_cpp();
+          uint64_t *R = &Rf[tid];
+          uint8_t *frames = p.frames + (uint64_t)(blockIdx.x * kBlock + tid) * kTailDepth * kFrameBytes;
+          const uint32_t sbytes = BIGSTACK ? kStackSize : p.stack_size;
+          if (cid == kTailHelper) {
+            next = c.call_pc + 1;
+            const uint64_t fd = R[2 * kBlock], a1 = R[1 * kBlock];
+            const int32_t k = (int32_t)R[3 * kBlock];  // `int idx = index`
+            int32_t entry = -1;
+            if (fd < kMaxFds && p.maps[fd].type == MT_PROG_ARRAY && k >= 0 && (uint32_t)k < p.maps[fd].max_entries) {
+              const int32_t t = *(const int32_t *)(p.maps[fd].data + 4ull * (uint32_t)k);
+              if (t >= 0 && t < (int32_t)kMaxFds) entry = p.tail_entry[t];
+            }
+            // the 64-B ctx copy: the lane's LDS XDP ctx (48 B), else the
+            // bytes of [a1, a1 + 64) the program may access (a unit shorter
+            // than 64 B keeps to its window), outside its stack
+            const bool lds_ctx = KIND == CTX_XDP && a1 == (uint64_t)(uintptr_t)my_ctx;
+            uint32_t cb = 48;
+            if (!lds_ctx)
+              for (cb = 0; cb < kFrameCtx && c.win.ok(a1 + cb, 8); cb += 8) {
+              }
+            const bool in_stack = a1 + 64 > stack_top - sbytes && a1 < stack_top;
+            if (entry >= 0 && tdepth < kTailDepth && a1 != 0 && !in_stack) {
+              uint64_t *fh = (uint64_t *)(frames + (uint64_t)tdepth * kFrameBytes);
+              for (int r = 1; r <= 10; r++) fh[r - 1] = R[r * kBlock];
+              fh[10] = a1;
+              fh[11] = (uint64_t)next | ((uint64_t)cb << 32);
+              for (uint32_t i = 0; i < cb; i += 8) fh[kFrameHdr / 8 + i / 8] = mem_load(a1 + i, 8);
+              const uint64_t sb = stack_top - sbytes;
+              for (uint32_t i = 0; i < sbytes; i += 8)
+                fh[(kFrameHdr + kFrameCtx) / 8 + i / 8] = *(const uint64_t *)(sb + i);
+              for (int r = 0; r <= 10; r++) R[r * kBlock] = 0;
+              R[1 * kBlock] = a1;
+              R[2 * kBlock] = 64;  // bpftime_prog_exec(context, sizeof(context), ...)
+              R[10 * kBlock] = stack_top;
+              tdepth++;
+              next = (uint32_t)entry;
+            } else {
+              R[0] = (uint64_t)-1;
+            }
+          } else if (tdepth == 0) {
+            c.err = E_BADOP;
+            c.alive = false;
+          } else {
+            tdepth--;
+            const uint64_t *fh = (const uint64_t *)(frames + (uint64_t)tdepth * kFrameBytes);
+            const uint64_t rv = R[0];
+            for (int r = 1; r <= 10; r++) R[r * kBlock] = fh[r - 1];
+            const uint64_t a1 = fh[10];
+            next = (uint32_t)fh[11];
+            const uint32_t cb = (uint32_t)(fh[11] >> 32);
+            for (uint32_t i = 0; i < cb; i += 8) mem_store(a1 + i, 8, fh[kFrameHdr / 8 + i / 8]);
+            const uint64_t sb = stack_top - sbytes;
+            for (uint32_t i = 0; i < sbytes; i += 8)
+              *(uint64_t *)(sb + i) = fh[(kFrameHdr + kFrameCtx) / 8 + i / 8];
+            R[0] = rv;
+          }
+        }
+        c.lpc = csel ? next : c.lpc;
+        uni = false;
+        continue;
+      }
       if (csel) {
         LaneEnv env;
         env.vcpu = vcpu;

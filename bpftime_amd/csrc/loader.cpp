@@ -24,6 +24,7 @@ bool device_helper_supported(uint32_t id) {
   switch (id) {
     case 1: case 2: case 3: case 5: case 7: case 8: case 28: case 44: case 65: case 189:
     case 130: case 131: case 132: case 133:
+    case kTailHelper:
       return true;
   }
   return false;
@@ -230,6 +231,8 @@ static int helper_arity(uint32_t id) {
     case 5: case 7: case 8: return 0;          // ktime_get_ns, get_prandom_u32, get_smp_processor_id
     case 1: case 3: case 44: case 65: return 2;  // map_lookup/delete_elem, xdp_adjust_head/tail
     case 2: case 189: return 4;                // map_update_elem, xdp_load_bytes
+    case kTailHelper: return 3;                // tail_call(ctx, prog_array, index)
+    case (uint32_t)kRetHelper: return 0;       // a linked tail-call target's exit
     default: return 5;                         // csum_diff and anything else
   }
 }
@@ -280,6 +283,7 @@ static void use_def(const DInsn &d, RegSet &use, RegSet &def) {
       // a helper reads only its declared arguments; r1-r5 survive the call
       // (ubpf semantics, restated by oracle/interp.c: helpers get copies)
       for (int r = 1; r <= helper_arity((uint32_t)d.hi); r++) U(r);
+      if (d.hi == kRetHelper) U(0);
       D(0);
       break;
     case X_EXIT: U(0); break;
@@ -296,6 +300,10 @@ static void successors(const std::vector<DInsn> &p, uint32_t i, uint32_t s[2], i
   ns = 0;
   switch (d.op) {
     case X_EXIT: return;
+    case X_CALL:
+      if (d.hi == kRetHelper) return;  // a linked target's exit
+      if (i + 1 < p.size()) s[ns++] = i + 1;
+      return;
     case X_JA: s[ns++] = d.tgt; return;
     case X_RMW_ADD: if (d.tgt < p.size()) s[ns++] = d.tgt; return;
     case X_LDDW: if (i + 2 < p.size()) s[ns++] = i + 2; return;
@@ -440,7 +448,7 @@ static int stack_depth(const std::vector<DInsn> &p, const std::vector<bool> &rea
 
 int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &helper_id_map,
                  const std::map<size_t, std::string> &helper_names, const LddwHelpers &lddw,
-                 LoadOut &out, std::string &err) {
+                 LoadOut &out, std::string &err, const std::vector<uint32_t> &entries) {
   if (n > kMaxInsts) {
     err = fmt("too many instructions (max %u)", kMaxInsts);
     return -1;
@@ -450,7 +458,10 @@ int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &
   // compat_ubpf.cpp:72-190
   for (size_t i = 0; i < n; i++) {
     RawInsn &cur = in[i];
-    if (cur.code == 0x85) {
+    if (cur.code == 0x85 && cur.imm == kRetHelper && !entries.empty()) {
+      // linked image (vm_api.cpp link_tail_image): a target's exit
+    } else if (cur.code == 0x85) {
+      if (cur.imm == (int32_t)kTailHelper) out.tail_call = true;
       if (helper_id_map.find((size_t)(uint32_t)cur.imm) == helper_id_map.end() || cur.imm < 0) {
         if (cur.imm >= 64) {
           err = "invalid call immediate at PC " + std::to_string(i);
@@ -537,6 +548,11 @@ int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &
   {
     std::vector<uint32_t> st{0};
     reach[0] = true;
+    for (uint32_t e : entries)  // linked tail-call targets
+      if (e < n && !reach[e]) {
+        reach[e] = true;
+        st.push_back(e);
+      }
     while (!st.empty()) {
       uint32_t i = st.back();
       st.pop_back();
@@ -602,7 +618,8 @@ int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &
     i += 2;
   }
 
-  int depth = stack_depth(p, reach);
+  int depth = entries.empty() ? stack_depth(p, reach) : -1;  // an image: every program on a 512-B stack
+  out.multi_entry = !entries.empty();
   if (depth < 0 || depth > (int)kLdsStackMax) {
     out.big_stack = true;
     out.stack_size = kStackSize;
@@ -886,6 +903,8 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
   for (const DInsn &d : prog)
     if (d.op == X_CALL && (d.hi == 44 || d.hi == 65)) pkt_ok = false;
   std::vector<std::vector<PVal>> in;
+  // a linked tail-call image has entries the pointer kinds do not start from
+  if (lo.multi_entry) return;
   if (!pointer_kinds(prog, lo.lddw_src, xdp, pkt_ok, in)) return;  // ctx rewritten: generic handlers only
   // per-lane counter adds (fused counters, atomic adds without fetch) whose
   // target is not a wave-uniform constant use the LDS combining table

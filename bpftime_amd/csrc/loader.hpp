@@ -55,6 +55,8 @@ struct LoadOut {
   uint32_t fused_rmw = 0;
   uint32_t comb_entries = 0;  // per-block LDS combining entries (0 = none needed)
   bool may_delete = false;    // calls map_delete_elem: hash lookup indexes stop being valid
+  bool tail_call = false;     // calls bpf_tail_call: linked with the prog arrays' targets at launch
+  bool multi_entry = false;   // a linked image (tail-call targets are extra entries)
 };
 
 // Helper ids the device implements (interp.hip helper switch).
@@ -81,6 +83,6 @@ void link_fast(const FastForm &f, uint32_t head, uint32_t stage, std::vector<FIn
 // (liveness for RMW fusion, stack depth).  Returns 0 or <0 with `err`.
 int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &helper_id_map,
                  const std::map<size_t, std::string> &helper_names, const LddwHelpers &lddw,
-                 LoadOut &out, std::string &err);
+                 LoadOut &out, std::string &err, const std::vector<uint32_t> &entries = {});
 
 }  // namespace bpftime_amd

@@ -552,6 +552,15 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
       m.bytes = d.nbuckets * d.slot_size;
       break;
     }
+    case MT_PROG_ARRAY:
+      // prog_array.cpp:101-110: key and value are both 4 bytes
+      if (m.key_size != 4 || m.value_size != 4) {
+        errno = EINVAL;
+        set_error("Key size and value size of prog_array must be 4");
+        return -1;
+      }
+      m.bytes = 4ull * m.max_entries;
+      break;
     case MT_RINGBUF:
       // ringbuf_map.cpp: positions + 2 x max_entries data bytes; mask =
       // max_entries - 1 needs a power of two
@@ -596,6 +605,10 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
   d.data = base;
   d.count_addr = extra ? base + ((m.bytes + 127) & ~127ull) : 0;
   if (hipMemset((void *)base, 0, m.bytes + extra + 8) != hipSuccess) return -1;
+  if (m.type == MT_PROG_ARRAY) {  // every slot INVALID_ENTRY (-1)
+    if (hipMemset((void *)base, 0xff, m.bytes) != hipSuccess) return -1;
+    r.prog_gen++;
+  }
   if (m.lpm) {  // empty replica: root = -1
     const int32_t none = -1;
     if (hipMemcpy((void *)base, &none, 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
@@ -633,6 +646,87 @@ uint32_t bpftime_map_value_size_from_syscall(int fd) {
   return m->value_size;  // map_handler.cpp:69-84
 }
 
+// ---- PROG_ARRAY (runtime/src/bpf_map/userspace/prog_array.cpp) -------------
+// Slots hold bpftime prog fds (the reference encodes them as -fd-2 beside
+// kernel prog ids; kernel programs do not exist here).
+static thread_local int32_t tl_prog_fd;
+
+static int32_t prog_array_read(const MapRec &m, int32_t k) {
+  int32_t v = -1;
+  if (hipMemcpy(&v, (const void *)(m.d.data + 4ull * (uint32_t)k), 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return v;
+}
+
+// prog_array.cpp:113-143
+static const void *prog_array_lookup(const MapRec &m, const void *key) {
+  int32_t k;
+  memcpy(&k, key, 4);
+  if (k < 0 || (uint32_t)k >= m.max_entries) {
+    errno = EINVAL;
+    return nullptr;
+  }
+  const int32_t v = prog_array_read(m, k);
+  if (v < 0 || !bpftime_is_prog_fd(v)) {
+    errno = ENOENT;
+    return nullptr;
+  }
+  tl_prog_fd = v;
+  return &tl_prog_fd;
+}
+
+// prog_array.cpp:146-176 (flags are not looked at); a value that is not a
+// bpftime prog fd would be asked of the kernel, which has no such fd here
+static long prog_array_update(MapRec &m, const void *key, const void *value) {
+  int32_t k, v;
+  memcpy(&k, key, 4);
+  if (k < 0 || (uint32_t)k >= m.max_entries) {
+    errno = EINVAL;
+    return -1;
+  }
+  memcpy(&v, value, 4);
+  if (!bpftime_is_prog_fd(v)) {
+    errno = EBADF;
+    return -1;
+  }
+  if (hipMemcpy((void *)(m.d.data + 4ull * (uint32_t)k), &v, 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
+  rt().prog_gen++;
+  return 0;
+}
+
+// prog_array.cpp:180-189
+static long prog_array_delete(MapRec &m, const void *key) {
+  int32_t k;
+  memcpy(&k, key, 4);
+  if (k < 0 || (uint32_t)k >= m.max_entries) {
+    errno = EINVAL;
+    return -1;
+  }
+  const int32_t none = -1;
+  if (hipMemcpy((void *)(m.d.data + 4ull * (uint32_t)k), &none, 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
+  rt().prog_gen++;
+  return 0;
+}
+
+// prog_array.cpp:191-211: the last key is checked before the range
+static int prog_array_next_key(const MapRec &m, const void *key, void *next_key) {
+  int32_t out = 0;
+  if (key) {
+    int32_t k;
+    memcpy(&k, key, 4);
+    if ((size_t)(k + 1) == m.max_entries) {
+      errno = ENOENT;
+      return -1;
+    }
+    if (k < 0 || (uint32_t)k >= m.max_entries) {
+      errno = EINVAL;
+      return -1;
+    }
+    out = k + 1;
+  }
+  memcpy(next_key, &out, 4);
+  return 0;
+}
+
 const void *bpftime_map_lookup_elem(int fd, const void *key) {
   MapRec *m = map_of(fd);
   if (!m) return nullptr;
@@ -640,6 +734,7 @@ const void *bpftime_map_lookup_elem(int fd, const void *key) {
     errno = ENOTSUP;
     return nullptr;
   }
+  if (m->type == MT_PROG_ARRAY) return prog_array_lookup(*m, key);
   std::vector<uint8_t> &buf = tl_lookup_buf;
   switch (m->type) {
     case MT_ARRAY:
@@ -689,6 +784,7 @@ long bpftime_map_update_elem(int fd, const void *key, const void *value, uint64_
     errno = ENOTSUP;
     return -1;
   }
+  if (m->type == MT_PROG_ARRAY) return prog_array_update(*m, key, value);
   uint64_t b = flags & 0xffffffffull;
   bool flags_ok = b == 0 || b == 1 || b == 2;  // map_common_def.hpp:83-94
   if (m->type == MT_LPM_TRIE) {
@@ -788,6 +884,7 @@ long bpftime_map_update_elem(int fd, const void *key, const void *value, uint64_
 long bpftime_map_delete_elem(int fd, const void *key) {
   MapRec *m = map_of(fd);
   if (!m) return -1;
+  if (m->type == MT_PROG_ARRAY) return prog_array_delete(*m, key);
   if (m->type == MT_RINGBUF) {
     errno = ENOTSUP;
     return -1;
@@ -842,6 +939,7 @@ int bpftime_map_get_next_key(int fd, const void *key, void *next_key) {
     }
     return m->lpm->first_key((uint8_t *)next_key);
   }
+  if (m->type == MT_PROG_ARRAY) return prog_array_next_key(*m, key, next_key);
   switch (m->type) {
     case MT_ARRAY:
     case MT_PERCPU_ARRAY: {  // array_map.cpp:66-81
@@ -894,6 +992,7 @@ void bpftime_close(int fd) {
   Runtime &r = rt();
   std::lock_guard<std::mutex> g(r.mu);
   if (fd < 0 || fd >= (int)kMaxFds) return;
+  r.prog_gen++;
   if (r.kind[fd] == HKind::MAP) {
     r.maps[fd] = MapRec();
     r.push_map(fd);
@@ -1052,6 +1151,7 @@ int bpftime_progs_create(int fd, const void *insns, size_t insn_cnt, const char 
   p.type = prog_type;
   r.progs[fd] = std::move(p);
   r.kind[fd] = HKind::PROG;
+  r.prog_gen++;
   return fd;
 }
 

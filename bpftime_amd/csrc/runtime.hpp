@@ -50,6 +50,8 @@ struct Runtime {
   uint64_t arena_size = 0, arena_used = 0;
   uint32_t ncpu = 64;
   std::string last_error;
+  uint64_t prog_gen = 1;        // bumped when a prog, a prog array or its contents change
+  uint8_t *d_frames = nullptr;  // tail-call frames (kTailGrid * kBlock lanes), allocated on first use
 
   int ensure_device();          // lazily picks the current device, allocates arena + table
   uint64_t arena_alloc(uint64_t bytes);

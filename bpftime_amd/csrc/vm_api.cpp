@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -62,6 +63,12 @@ class Mi355xVm {
   // staging for ebpf_exec
   uint8_t *d_stage = nullptr;
   size_t stage_size = 0;
+  // bpf_tail_call: the loaded code, and the image linked with every prog
+  // array target (common.hpp kTailHelper), rebuilt when rt().prog_gen moves
+  std::vector<RawInsn> raw;
+  bool has_tail = false;
+  uint64_t image_gen = 0;
+  int32_t *d_tail_entry = nullptr;
 
   Mi355xVm() {
     // bpftime_prog.cpp:126-127 defaults, pointed at the device registry
@@ -74,6 +81,7 @@ class Mi355xVm {
     unload();
     if (d_err) hipFree(d_err);
     if (d_stage) hipFree(d_stage);
+    if (d_tail_entry) hipFree(d_tail_entry);
   }
   void unload() {
     if (d_prog) hipFree(d_prog);
@@ -82,6 +90,9 @@ class Mi355xVm {
     links.clear();
     loaded = false;
     prog = LoadOut();
+    raw.clear();
+    has_tail = false;
+    image_gen = 0;
   }
   int register_external_function(size_t index, const std::string &name, void *fn) {
     // compat_ubpf.cpp:50-59: allocate the next id; ubpf caps helpers at 64
@@ -128,8 +139,98 @@ class Mi355xVm {
       error = "device alloc failed";
       return -1;
     }
+    has_tail = out.tail_call;
+    raw.assign((const RawInsn *)code, (const RawInsn *)code + code_len / 8);
     prog = std::move(out);
     loaded = true;
+    return 0;
+  }
+
+  // Link the loaded program with every program a PROG_ARRAY names: one
+  // image, the targets appended (raw jumps are relative, so they need no
+  // relocation) with their exits turned into kRetHelper calls, plus a
+  // prog fd -> entry pc table.  A target that does not load alone is left
+  // out, so tail calls to it return -1 like a failed bpftime_prog_load
+  // (bpf_helper.cpp:623-628).
+  int link_tail_image() {
+    Runtime &r = rt();
+    if (image_gen == r.prog_gen && d_tail_entry) return 0;
+    std::map<size_t, size_t> hm = helper_id_map;
+    std::map<size_t, std::string> names = helper_names;
+    for (uint32_t id : {1u, 2u, 3u, 5u, 7u, 8u, 12u, 28u, 44u, 65u, 130u, 131u, 132u, 133u, 189u})
+      if (!hm.count(id)) hm[id] = 63;  // the runtime's helper groups (bpf_helper.cpp:606-620)
+    std::set<int32_t> targets;
+    for (uint32_t fd = 0; fd < kMaxFds; fd++) {
+      if (r.kind[fd] != HKind::MAP || r.maps[fd].type != MT_PROG_ARRAY) continue;
+      std::vector<int32_t> slots(r.maps[fd].max_entries);
+      if (!slots.empty() &&
+          hipMemcpy(slots.data(), (const void *)r.maps[fd].d.data, 4 * slots.size(), hipMemcpyDeviceToHost) != hipSuccess) {
+        error = "prog array read failed";
+        return -1;
+      }
+      for (int32_t v : slots)
+        if (v >= 0 && v < (int32_t)kMaxFds && r.kind[v] == HKind::PROG) targets.insert(v);
+    }
+    std::vector<RawInsn> img(raw);
+    std::vector<uint32_t> entries;
+    std::vector<int32_t> entry(kMaxFds, -1);
+    for (int32_t t : targets) {
+      const std::vector<uint8_t> &bytes = r.progs[t].insns;
+      const size_t n = bytes.size() / 8;
+      if (img.size() + n + 1 > kMaxInsts) continue;
+      LoadOut alone;
+      std::string err;
+      if (load_program((const RawInsn *)bytes.data(), n, hm, names, lddw, alone, err) < 0) continue;
+      entry[t] = (int32_t)img.size();
+      entries.push_back((uint32_t)img.size());
+      const RawInsn *code = (const RawInsn *)bytes.data();
+      for (size_t i = 0; i < n; i++) {
+        RawInsn x = code[i];
+        if (x.code == 0x95) {  // exit -> return to the caller's frame
+          x = RawInsn{};
+          x.code = 0x85;
+          x.imm = kRetHelper;
+        }
+        img.push_back(x);
+        if (code[i].code == 0x18 && i + 1 < n) img.push_back(code[++i]);
+      }
+    }
+    if (!entries.empty()) {
+      RawInsn ex{};
+      ex.code = 0x95;
+      img.push_back(ex);
+    }
+    LoadOut out;
+    std::string err;
+    if (load_program(img.data(), img.size(), hm, names, lddw, out, err, entries) < 0) {
+      error = "tail-call image: " + err;
+      return -1;
+    }
+    FastForm nx, nr;
+    build_fast(out, true, nx);
+    build_fast(out, false, nr);
+    out.comb_entries = (nx.needs_comb || nr.needs_comb) ? kComb : 0;
+    DInsn *dp = nullptr;
+    const size_t bytes = out.prog.size() * sizeof(DInsn);
+    if (!d_tail_entry && hipMalloc((void **)&d_tail_entry, 4 * kMaxFds) != hipSuccess) d_tail_entry = nullptr;
+    if (!r.d_frames && hipMalloc((void **)&r.d_frames, (size_t)kTailGrid * kBlock * kTailDepth * kFrameBytes) != hipSuccess)
+      r.d_frames = nullptr;
+    if (!d_tail_entry || !r.d_frames || hipMalloc((void **)&dp, bytes) != hipSuccess ||
+        hipMemcpy(dp, out.prog.data(), bytes, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_tail_entry, entry.data(), 4 * kMaxFds, hipMemcpyHostToDevice) != hipSuccess) {
+      if (dp) hipFree(dp);
+      error = "device upload failed";
+      return -1;
+    }
+    std::lock_guard<std::mutex> g(link_mu);
+    if (d_prog) hipFree(d_prog);
+    d_prog = dp;
+    for (auto &kv : links) hipFree(kv.second);
+    links.clear();
+    fx = std::move(nx);
+    fr = std::move(nr);
+    prog = std::move(out);
+    image_gen = r.prog_gen;
     return 0;
   }
 
@@ -172,8 +273,13 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   hipStream_t s = (hipStream_t)b->stream;
   if (b->count == 0) return 0;
   Runtime &r = rt();
+  if (has_tail && link_tail_image() < 0) return -1;
   KParams p{};
   p.prog = d_prog;
+  if (has_tail) {
+    p.tail_entry = d_tail_entry;
+    p.frames = r.d_frames;
+  }
   {
     // staged window: what the static packet / slot accesses need, when every
     // slot is 16-B aligned and at least that long (a window never reaches
@@ -276,6 +382,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       if (atoi(g) > 0) mult = (uint32_t)atoi(g);
     uint64_t cap = (uint64_t)cus * (uint64_t)occ * mult;
     grid = (uint32_t)(want < cap ? want : cap);
+    if (has_tail && grid > kTailGrid) grid = kTailGrid;  // one frame stack per lane of the grid
   }
   hipError_t e = bpftime_amd_launch_interp(&p, b->ctx_kind, prog.big_stack, grid, ordered ? 1 : 0, s);
   if (e != hipSuccess) {
@@ -484,7 +591,7 @@ int bpftime_amd_register_default_helpers(struct ebpf_vm *vm) {
   } h[] = {{8, "bpf_get_smp_processor_id"}, {28, "bpf_csum_diff"},    {44, "bpf_xdp_adjust_head"},
            {65, "bpf_xdp_adjust_tail"},      {5, "bpf_ktime_get_ns"}, {7, "bpf_get_prandom_u32"},
            {131, "bpf_ringbuf_reserve"},     {132, "bpf_ringbuf_submit"}, {133, "bpf_ringbuf_discard"},
-           {130, "bpf_ringbuf_output"},
+           {130, "bpf_ringbuf_output"},      {12, "bpf_tail_call"},
            {1, "bpf_map_lookup_elem"},       {2, "bpf_map_update_elem"}, {3, "bpf_map_delete_elem"}};
   int err = 0;
   for (auto &e : h) err |= ebpf_register(vm, e.id, e.name, nullptr);

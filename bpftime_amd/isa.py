@@ -58,6 +58,7 @@ BPF_FUNC_ktime_get_ns = 5
 BPF_FUNC_trace_printk = 6
 BPF_FUNC_get_prandom_u32 = 7
 BPF_FUNC_get_smp_processor_id = 8
+BPF_FUNC_tail_call = 12
 BPF_FUNC_csum_diff = 28
 BPF_FUNC_xdp_adjust_head = 44
 BPF_FUNC_xdp_adjust_tail = 65
@@ -70,6 +71,7 @@ BPF_FUNC_xdp_load_bytes = 189
 # map types (linux/bpf.h)
 BPF_MAP_TYPE_HASH = 1
 BPF_MAP_TYPE_ARRAY = 2
+BPF_MAP_TYPE_PROG_ARRAY = 3
 BPF_MAP_TYPE_PERCPU_HASH = 5
 BPF_MAP_TYPE_PERCPU_ARRAY = 6
 BPF_MAP_TYPE_LPM_TRIE = 11

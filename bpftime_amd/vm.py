@@ -180,6 +180,12 @@ class Map:
         lib().bpftime_close(self.fd)
 
 
+def close_fd(fd: int) -> None:
+    """bpftime_close: a map, prog or link record (a closed prog leaves the
+    prog arrays that name it, prog_array.cpp:127-131)."""
+    lib().bpftime_close(fd)
+
+
 def reset_runtime() -> None:
     lib().bpftime_amd_reset()
 

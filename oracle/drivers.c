@@ -36,6 +36,13 @@ int orc_run_xdp(struct orc_vm *vm, uint8_t *base, uint64_t n, uint64_t stride, c
 	for (uint64_t i = 0; i < n; i++) {
 		uint8_t *slot = base + i * stride;
 		uint32_t len = lens ? lens[i] : fixed_len;
+		/* bpf_tail_call copies 64 bytes from the 48-B ctx (bpf_helper.cpp:631-634):
+		 * keep that read inside one zeroed object */
+		union {
+			struct xdp_md_userspace md;
+			uint8_t bytes[64];
+		} u;
+		memset(&u, 0, sizeof(u));
 		struct xdp_md_userspace ctx = {
 			.data = (uintptr_t)slot,
 			.data_end = (uintptr_t)slot + len,
@@ -46,13 +53,14 @@ int orc_run_xdp(struct orc_vm *vm, uint8_t *base, uint64_t n, uint64_t stride, c
 			.buffer_start = (uintptr_t)slot,
 			.buffer_end = (uintptr_t)slot + stride,
 		};
-		uint64_t v = exec_or_zero(vm, &ctx, sizeof(ctx));
+		u.md = ctx;
+		uint64_t v = exec_or_zero(vm, &u.md, sizeof(u.md));
 		if (verdicts)
 			verdicts[i] = (uint32_t)v;
 		if (out_data_off)
-			out_data_off[i] = (int32_t)(ctx.data - (uintptr_t)slot);
+			out_data_off[i] = (int32_t)(u.md.data - (uintptr_t)slot);
 		if (out_len)
-			out_len[i] = (uint32_t)(ctx.data_end - ctx.data);
+			out_len[i] = (uint32_t)(u.md.data_end - u.md.data);
 	}
 	return 0;
 }

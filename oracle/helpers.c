@@ -152,6 +152,74 @@ static uint64_t h_rb_discard(uint64_t data, uint64_t flags, uint64_t a, uint64_t
 	return 0;
 }
 
+/* ---- programs + bpf_tail_call (runtime/src/bpf_helper.cpp:568-650) ---- */
+static struct {
+	int used;
+	uint8_t *insns;
+	uint32_t n;
+} g_progs[ORC_MAX_FDS];
+
+int orc_prog_create(int fd, const void *insns, uint32_t n)
+{
+	if (fd < 0 || fd >= ORC_MAX_FDS)
+		return -1;
+	orc_prog_close(fd);
+	g_progs[fd].insns = malloc((size_t)n * 8 + 1);
+	memcpy(g_progs[fd].insns, insns, (size_t)n * 8);
+	g_progs[fd].n = n;
+	g_progs[fd].used = 1;
+	return fd;
+}
+
+void orc_prog_close(int fd)
+{
+	if (fd < 0 || fd >= ORC_MAX_FDS || !g_progs[fd].used)
+		return;
+	free(g_progs[fd].insns);
+	g_progs[fd].used = 0;
+}
+
+int orc_is_prog_fd(int fd)
+{
+	return fd >= 0 && fd < ORC_MAX_FDS && g_progs[fd].used;
+}
+
+static __thread uint32_t g_tail_depth;
+
+static uint64_t h_tail_call(uint64_t ctx, uint64_t prog_array, uint64_t index, uint64_t a4, uint64_t a5)
+{
+	int fd = (int)prog_array;
+	if (!orc_map_is_prog_array(fd))
+		return (uint64_t)-1;
+	int idx = (int)index;
+	const int32_t *p = orc_map_lookup(fd, &idx);
+	if (!p)
+		return (uint64_t)-1;
+	int to = *p;
+	if (!orc_is_prog_fd(to))
+		return (uint64_t)-1;
+	if (g_tail_depth >= 32) /* MAX_TAIL_CALL_CNT */
+		return (uint64_t)-1;
+	g_tail_depth++;
+	uint64_t rv = (uint64_t)-1;
+	struct orc_vm *vm = orc_vm_create();
+	char err[256];
+	if (orc_vm_register_default_helpers(vm) == 0 &&
+	    orc_vm_load(vm, g_progs[to].insns, g_progs[to].n * 8, err, sizeof(err)) == 0) {
+		uint8_t context[64];
+		if (ctx)
+			memcpy(context, (const void *)(uintptr_t)ctx, sizeof(context));
+		else
+			memset(context, 0, sizeof(context));
+		uint64_t ret = 0;
+		if (orc_vm_exec(vm, context, sizeof(context), &ret) == 0)
+			rv = ret;
+	}
+	orc_vm_destroy(vm);
+	g_tail_depth--;
+	return rv;
+}
+
 int orc_vm_register_default_helpers(struct orc_vm *vm)
 {
 	int err = 0;
@@ -166,6 +234,7 @@ int orc_vm_register_default_helpers(struct orc_vm *vm)
 	err |= orc_vm_register(vm, 132, "bpf_ringbuf_submit", h_rb_submit);
 	err |= orc_vm_register(vm, 133, "bpf_ringbuf_discard", h_rb_discard);
 	err |= orc_vm_register(vm, 130, "bpf_ringbuf_output", h_rb_output);
+	err |= orc_vm_register(vm, 12, "bpf_tail_call", h_tail_call);
 	/* shm maps helper group (bpf_helper.cpp:1359-1401) */
 	err |= orc_vm_register(vm, 1, "bpf_map_lookup_elem", h_lookup);
 	err |= orc_vm_register(vm, 2, "bpf_map_update_elem", h_update);

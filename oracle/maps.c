@@ -19,7 +19,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-enum { T_HASH = 1, T_ARRAY = 2, T_PERCPU_HASH = 5, T_PERCPU_ARRAY = 6, T_LPM_TRIE = 11, T_RINGBUF = 27 };
+enum { T_HASH = 1, T_ARRAY = 2, T_PROG_ARRAY = 3, T_PERCPU_HASH = 5, T_PERCPU_ARRAY = 6, T_LPM_TRIE = 11, T_RINGBUF = 27 };
 
 struct orc_map {
 	int used;
@@ -93,6 +93,8 @@ static void free_map(struct orc_map *m)
 
 void orc_maps_reset(void)
 {
+	for (int fd = 0; fd < ORC_MAX_FDS; fd++)
+		orc_prog_close(fd);
 	for (int i = 0; i < ORC_MAX_FDS; i++)
 		free_map(&g_maps[i]);
 }
@@ -167,6 +169,14 @@ int orc_map_create(int fd, uint32_t type, uint32_t ksize, uint32_t vsize, uint32
 		break;
 	case T_PERCPU_HASH:
 		m->ncpu = (uint32_t)g_ncpu;
+		break;
+	case T_PROG_ARRAY: /* prog_array.cpp:101-110: every slot INVALID_ENTRY (-1) */
+		if (ksize != 4 || vsize != 4) {
+			g_errno = EINVAL;
+			return -1;
+		}
+		m->data = malloc((size_t)max_entries * 4 + 1);
+		memset(m->data, 0xff, (size_t)max_entries * 4);
 		break;
 	case T_RINGBUF: /* ringbuf_map.cpp ringbuf::ringbuf: data = 2 x max_ent bytes */
 		if (max_entries == 0 || (max_entries & (max_entries - 1))) {
@@ -613,12 +623,84 @@ static int lpm_next_key(struct orc_map *m, const void *key, uint8_t *next) /* :5
 	return -1;
 }
 
+/* ---- PROG_ARRAY (prog_array.cpp); slots hold bpftime prog fds ---- */
+static __thread int32_t tl_prog_fd;
+
+int orc_map_is_prog_array(int fd)
+{
+	struct orc_map *m = get(fd);
+	return m && m->type == T_PROG_ARRAY;
+}
+
+static void *parr_lookup(struct orc_map *m, const void *key) /* prog_array.cpp:113-143 */
+{
+	int32_t k = *(const int32_t *)key;
+	if (k < 0 || (uint32_t)k >= m->max_entries) {
+		g_errno = EINVAL;
+		return NULL;
+	}
+	int32_t v = ((const int32_t *)m->data)[k];
+	if (v < 0 || !orc_is_prog_fd(v)) {
+		g_errno = ENOENT;
+		return NULL;
+	}
+	tl_prog_fd = v;
+	return &tl_prog_fd;
+}
+
+static long parr_update(struct orc_map *m, const void *key, const void *value) /* :146-176 */
+{
+	int32_t k = *(const int32_t *)key, v = *(const int32_t *)value;
+	if (k < 0 || (uint32_t)k >= m->max_entries) {
+		g_errno = EINVAL;
+		return -1;
+	}
+	if (!orc_is_prog_fd(v)) { /* would be asked of the kernel: no such fd */
+		g_errno = EBADF;
+		return -1;
+	}
+	((int32_t *)m->data)[k] = v;
+	return 0;
+}
+
+static long parr_delete(struct orc_map *m, const void *key) /* :180-189 */
+{
+	int32_t k = *(const int32_t *)key;
+	if (k < 0 || (uint32_t)k >= m->max_entries) {
+		g_errno = EINVAL;
+		return -1;
+	}
+	((int32_t *)m->data)[k] = -1;
+	return 0;
+}
+
+static int parr_next_key(struct orc_map *m, const void *key, void *next) /* :191-211 */
+{
+	if (!key) {
+		*(int32_t *)next = 0;
+		return 0;
+	}
+	int32_t k = *(const int32_t *)key;
+	if ((size_t)(k + 1) == m->max_entries) {
+		g_errno = ENOENT;
+		return -1;
+	}
+	if (k < 0 || (uint32_t)k >= m->max_entries) {
+		g_errno = EINVAL;
+		return -1;
+	}
+	*(int32_t *)next = k + 1;
+	return 0;
+}
+
 void *orc_map_lookup(int fd, const void *key)
 {
 	struct orc_map *m = get(fd);
 	if (!m)
 		return NULL;
 	switch (m->type) {
+	case T_PROG_ARRAY:
+		return parr_lookup(m, key);
 	case T_ARRAY: { /* array_map.cpp:27-35 */
 		uint32_t k = *(const uint32_t *)key;
 		if (k >= m->max_entries) {
@@ -668,6 +750,8 @@ long orc_map_update(int fd, const void *key, const void *value, uint64_t flags)
 	if (!m)
 		return -1;
 	switch (m->type) {
+	case T_PROG_ARRAY:
+		return parr_update(m, key, value);
 	case T_ARRAY: /* array_map.cpp:37-56 */
 	case T_PERCPU_ARRAY: { /* per_cpu_array_map.cpp:50-73 */
 		if (!check_update_flags(flags))
@@ -710,6 +794,8 @@ long orc_map_delete(int fd, const void *key)
 	if (!m)
 		return -1;
 	switch (m->type) {
+	case T_PROG_ARRAY:
+		return parr_delete(m, key);
 	case T_ARRAY:
 	case T_PERCPU_ARRAY: /* array_map.cpp:58-64 */
 		g_errno = EINVAL;
@@ -821,6 +907,8 @@ int orc_map_get_next_key(int fd, const void *key, void *next_key)
 	if (!m)
 		return -1;
 	switch (m->type) {
+	case T_PROG_ARRAY:
+		return parr_next_key(m, key, next_key);
 	case T_ARRAY:
 	case T_PERCPU_ARRAY: /* array_map.cpp:66-81 */
 		if (!key || *(const uint32_t *)key >= m->max_entries) {

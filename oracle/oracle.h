@@ -80,6 +80,12 @@ void *orc_map_raw(int fd, size_t *bytes);
 /* hash maps: bucket count (= next_prime(max_entries)), element count */
 uint64_t orc_map_buckets(int fd);
 uint64_t orc_map_count(int fd);
+/* programs for bpf_tail_call (bpftime_progs_create records; bpf_helper.cpp:568-650):
+ * the target runs as a nested exec over a 64-B copy of the ctx, depth <= 32 */
+int orc_prog_create(int fd, const void *insns, uint32_t insn_cnt);
+void orc_prog_close(int fd);
+int orc_is_prog_fd(int fd);
+int orc_map_is_prog_array(int fd);
 /* lddw helpers (runtime/src/bpftime_shm.cpp:637-676) */
 uint64_t orc_map_ptr_by_fd(uint32_t fd);
 uint64_t orc_map_val(uint64_t map_ptr);

@@ -57,6 +57,9 @@ def lib():
             "orc_map_count": (u64, [C.c_int]),
             "orc_ringbuf_fetch": (C.c_int64, [C.c_int, vp, u64, C.POINTER(C.c_uint64)]),
             "orc_map_ptr_by_fd": (u64, [u32]),
+            "orc_prog_create": (C.c_int, [C.c_int, vp, u32]),
+            "orc_prog_close": (None, [C.c_int]),
+            "orc_is_prog_fd": (C.c_int, [C.c_int]),
             "orc_map_val": (u64, [u64]),
             "orc_next_prime": (u64, [u64]),
             "orc_hash_bytes": (u64, [vp, u64]),
@@ -223,6 +226,15 @@ class OracleMap:
 
 def reset() -> None:
     lib().orc_maps_reset()
+
+
+def prog_create(fd: int, code: bytes) -> int:
+    """A bpftime_progs_create record (the target of bpf_tail_call)."""
+    return lib().orc_prog_create(fd, bytes(code), len(code) // 8)
+
+
+def prog_close(fd: int) -> None:
+    lib().orc_prog_close(fd)
 
 
 def set_ncpu(n: int) -> None:

@@ -1,0 +1,127 @@
+"""bpf_tail_call + BPF_MAP_TYPE_PROG_ARRAY on the device against the oracle:
+the reference's user-to-user tail-call test
+(runtime/unit-test/tailcall/test_user_to_user_tailcall.cpp), then an XDP
+batch whose lanes take different targets (a packet writer, a map counter, an
+empty slot, a 32-deep self recursion), and relinking after the prog array
+or a target changes."""
+import errno
+import struct
+
+import numpy as np
+import pytest
+
+from bpftime_amd import gen, isa
+from bpftime_amd.isa import Asm
+
+import _tailcall as tc
+
+pytestmark = pytest.mark.gpu
+
+I32 = lambda v: struct.pack("<i", v)  # noqa: E731
+PA_FD, TARGET_FD = 1001, 1002
+
+
+def test_device_prog_array_map_kat(fresh_runtime):
+    dev = fresh_runtime
+    with pytest.raises(Exception):
+        dev.Map(isa.BPF_MAP_TYPE_PROG_ARRAY, 4, 8, 4)
+    m = dev.Map(isa.BPF_MAP_TYPE_PROG_ARRAY, 4, 4, 4, fd=PA_FD)
+    assert m.fd == PA_FD
+    assert m.update(I32(0), I32(TARGET_FD)) < 0
+    assert dev.prog_create(tc.ref_kat_target(), "tail_call_target", 1, fd=TARGET_FD) == TARGET_FD
+    assert m.update(I32(0), I32(TARGET_FD)) == 0
+    assert m.lookup(I32(0)) == I32(TARGET_FD)
+    assert m.lookup(I32(1)) is None and m.lookup(I32(4)) is None
+    assert m.next_key(None) == I32(0) and m.next_key(I32(2)) == I32(3) and m.next_key(I32(3)) is None
+    assert m.delete(I32(0)) == 0 and m.lookup(I32(0)) is None
+    assert m.update(I32(0), I32(TARGET_FD)) == 0
+    dev.close_fd(TARGET_FD)
+    assert m.lookup(I32(0)) is None
+
+
+@pytest.mark.parametrize("tail_then_exit", [True, False])
+def test_reference_tailcall_kat_device(fresh_oracle, fresh_runtime, tail_then_exit):
+    po, dev = fresh_oracle, fresh_runtime
+    m = dev.Map(isa.BPF_MAP_TYPE_PROG_ARRAY, 4, 4, 4, fd=PA_FD)
+    dev.prog_create(tc.ref_kat_target(), "tail_call_target", 1, fd=TARGET_FD)
+    assert m.update(I32(0), I32(TARGET_FD)) == 0
+    vm = dev.VM()
+    vm.load(tc.ref_kat_caller(PA_FD, tail_then_exit))
+    rc, ret = vm.exec(bytearray(64))
+    assert rc == 0 and ret == (0x1234 if tail_then_exit else 0xdead)
+    # a batch of raw units takes the same path
+    n = 300
+    d = dev.DeviceBuffer(64 * n)
+    d.zero()
+    rets = dev.DeviceBuffer(8 * n)
+    assert vm.exec_batch(dev.CTX_RAW, d, n, 64, fixed_len=64, rets=rets) == 0
+    assert (rets.download(np.uint64) == (0x1234 if tail_then_exit else 0xdead)).all()
+    # closing the target: the slot reads empty and the call returns -1
+    dev.close_fd(TARGET_FD)
+    rc, ret = vm.exec(bytearray(64))
+    assert rc == 0 and ret == ((1 << 64) - 1 if tail_then_exit else 0xdead)
+
+
+def _xdp_pair(po, dev):
+    pa_o = po.OracleMap(isa.BPF_MAP_TYPE_PROG_ARRAY, 4, 4, 4, fd=PA_FD)
+    pa_d = dev.Map(isa.BPF_MAP_TYPE_PROG_ARRAY, 4, 4, 4, fd=PA_FD)
+    cnt_d = dev.Map(isa.BPF_MAP_TYPE_ARRAY, 4, 8, 4)
+    cnt_o = po.OracleMap(isa.BPF_MAP_TYPE_ARRAY, 4, 8, 4, fd=cnt_d.fd)
+    progs = {900: tc.target_write(0xA1), 901: tc.target_count(cnt_d.fd),
+             903: tc.target_recurse(PA_FD, cnt_d.fd, 3), 904: tc.target_write(0xB2)}
+    for fd, code in progs.items():
+        po.prog_create(fd, code)
+        assert dev.prog_create(code, f"t{fd}", 6, fd=fd) == fd
+    for k, fd in ((0, 900), (1, 901), (3, 903)):
+        assert pa_o.update(I32(k), I32(fd)) == 0 and pa_d.update(I32(k), I32(fd)) == 0
+    return (pa_o, cnt_o), (pa_d, cnt_d)
+
+
+def _run_both(po, dev, ovm, dvm, n, seed, cnt_o, cnt_d):
+    pk = gen.xdp_packets(n, seed=seed)
+    pk[:, 0] = np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8)
+    opk = pk.copy()
+    ov = ovm.run_xdp(opk, fixed_len=64, ifindex=5)
+    d = dev.DeviceBuffer.from_array(pk)
+    dv = dev.DeviceBuffer(4 * n)
+    assert dvm.exec_batch(dev.CTX_XDP, d, n, 64, fixed_len=64, verdicts=dv, ifindex=5) == 0
+    np.testing.assert_array_equal(dv.download(np.uint32), ov)
+    np.testing.assert_array_equal(d.download().reshape(n, 64), opk)
+    for i in range(4):
+        assert cnt_d.lookup(I32(i)) == cnt_o.lookup(I32(i)), i
+    return ov, opk
+
+
+@pytest.mark.parametrize("n", [1, 64, 1000, 70000])
+def test_xdp_tailcall_parity(fresh_oracle, fresh_runtime, n):
+    po, dev = fresh_oracle, fresh_runtime
+    (pa_o, cnt_o), (pa_d, cnt_d) = _xdp_pair(po, dev)
+    code = tc.xdp_caller(PA_FD, cnt_d.fd)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    dvm = dev.VM()
+    dvm.load(code)
+    ov, opk = _run_both(po, dev, ovm, dvm, n, 11 + n, cnt_o, cnt_d)
+    idx = opk[:, 0] & 3
+    assert (ov[idx == 3] == 31 + 1005).all() and (ov[idx == 2] == (0xFFFFFFFF + 1005) & 0xFFFFFFFF).all()
+
+
+def test_xdp_tailcall_relink(fresh_oracle, fresh_runtime):
+    """Prog array writes between launches relink the image: slot 1 now names
+    another writer, slot 0 is deleted, then the recursion target is closed."""
+    po, dev = fresh_oracle, fresh_runtime
+    (pa_o, cnt_o), (pa_d, cnt_d) = _xdp_pair(po, dev)
+    code = tc.xdp_caller(PA_FD, cnt_d.fd)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    dvm = dev.VM()
+    dvm.load(code)
+    _run_both(po, dev, ovm, dvm, 4096, 1, cnt_o, cnt_d)
+    for m in (pa_o, pa_d):
+        assert m.update(I32(1), I32(904)) == 0 and m.delete(I32(0)) == 0
+    ov, opk = _run_both(po, dev, ovm, dvm, 4096, 2, cnt_o, cnt_d)
+    assert (opk[(opk[:, 0] & 3) == 1, 1] == 0xB2).all()
+    po.prog_close(903)
+    dev.close_fd(903)
+    ov, opk = _run_both(po, dev, ovm, dvm, 4096, 3, cnt_o, cnt_d)
+    assert (ov[(opk[:, 0] & 3) == 3] == (0xFFFFFFFF + 1005) & 0xFFFFFFFF).all()
