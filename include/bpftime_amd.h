@@ -51,8 +51,10 @@ struct bpf_link_create_args {
 
 /* ---- maps: bpftime_shm.hpp:316-345 ---- */
 /* create a map at `fd` (-1: lowest unused fd).  Supported types: HASH (1,
- * fix-size hash, map_handler.cpp:54-58), ARRAY (2), PERCPU_HASH (5),
- * PERCPU_ARRAY (6).  Returns fd or -1 (errno set). */
+ * fix-size hash, map_handler.cpp:54-58), ARRAY (2), PROG_ARRAY (3, prog
+ * fds, prog_array.cpp; the targets of bpf_tail_call, linked into the caller's
+ * image at launch), PERCPU_HASH (5), PERCPU_ARRAY (6), LPM_TRIE (11),
+ * RINGBUF (27).  Returns fd or -1 (errno set). */
 int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr);
 /* syscall-side ops (from_syscall = true), bpftime_shm.cpp:115-140 */
 const void *bpftime_map_lookup_elem(int fd, const void *key);
