@@ -112,6 +112,7 @@ SIGNATURES = [
     ("bpftime_amd_syscall_attach", C.c_int, [C.c_int, C.c_int64]),
     ("bpftime_amd_syscall_detach", C.c_int, [C.c_int]),
     ("bpftime_amd_syscall_dispatch", C.c_int64, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]),
+    ("bpftime_amd_handle_sysbpf", C.c_long, [C.c_int, C.c_void_p, C.c_uint32]),
     ("bpftime_amd_merge_delta_u64", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     ("bpftime_amd_device_count", C.c_int, []),
     ("bpftime_amd_set_device", C.c_int, [C.c_int]),
@@ -155,7 +156,7 @@ def lib() -> C.CDLL:
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback exists)")
-        l = C.CDLL(LIB_PATH)
+        l = C.CDLL(LIB_PATH, use_errno=True)
         for name, res, args in SIGNATURES + EXTRA:
             f = getattr(l, name)
             f.restype = res

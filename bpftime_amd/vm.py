@@ -8,6 +8,7 @@ libbpftime_amd.so; nothing executes eBPF on the CPU.
 from __future__ import annotations
 
 import ctypes as C
+import struct
 from typing import Optional
 
 import numpy as np
@@ -336,3 +337,45 @@ class Event:
             lib().bpftime_amd_event_destroy(C.c_void_p(self.h))
         except Exception:
             pass
+
+
+# ---- bpf(2) commands (syscall_context.cpp:429-668) --------------------------
+BPF_MAP_CREATE, BPF_MAP_LOOKUP_ELEM, BPF_MAP_UPDATE_ELEM, BPF_MAP_DELETE_ELEM = 0, 1, 2, 3
+BPF_MAP_GET_NEXT_KEY, BPF_PROG_LOAD, BPF_MAP_FREEZE, BPF_LINK_CREATE = 4, 5, 22, 28
+
+
+def sys_bpf(cmd: int, attr: bytearray) -> tuple:
+    """bpftime_amd_handle_sysbpf over a union bpf_attr image; (ret, errno)."""
+    buf = (C.c_char * len(attr)).from_buffer(attr)
+    C.set_errno(0)
+    r = lib().bpftime_amd_handle_sysbpf(cmd, C.addressof(buf), len(attr))
+    return r, C.get_errno()
+
+
+def attr_map_create(type_: int, key_size: int, value_size: int, max_entries: int, flags: int = 0,
+                    name: str = "") -> bytearray:
+    a = bytearray(128)
+    struct.pack_into("<IIIII", a, 0, type_, key_size, value_size, max_entries, flags)
+    nm = name.encode()[:15]
+    a[28:28 + len(nm)] = nm
+    return a
+
+
+def attr_map_elem(fd: int, key_addr: int, value_addr: int = 0, flags: int = 0) -> bytearray:
+    a = bytearray(128)
+    struct.pack_into("<IIQQQ", a, 0, fd, 0, key_addr, value_addr, flags)
+    return a
+
+
+def attr_prog_load(prog_type: int, insns_addr: int, insn_cnt: int, name: str = "") -> bytearray:
+    a = bytearray(128)
+    struct.pack_into("<IIQ", a, 0, prog_type, insn_cnt, insns_addr)
+    nm = name.encode()[:15]
+    a[48:48 + len(nm)] = nm
+    return a
+
+
+def attr_link_create(prog_fd: int, target: int, attach_type: int, flags: int = 0) -> bytearray:
+    a = bytearray(128)
+    struct.pack_into("<IIII", a, 0, prog_fd, target, attach_type, flags)
+    return a

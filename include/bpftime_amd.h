@@ -72,6 +72,15 @@ void bpftime_close(int fd);
 int bpftime_progs_create(int fd, const void *insns, size_t insn_cnt, const char *prog_name, int prog_type);
 int bpftime_link_create(int fd, struct bpf_link_create_args *args);
 
+/* ---- bpf(2) commands from an interposed loader ----
+ * syscall_context::handle_sysbpf's userspace branch
+ * (runtime/syscall-server/syscall_context.cpp:429-668): `attr` is the
+ * kernel's union bpf_attr.  BPF_MAP_CREATE / BPF_PROG_LOAD / BPF_LINK_CREATE
+ * return a new fd; lookups copy the value out (ENOENT when absent); update,
+ * delete and get-next-key return the map operation's status; BPF_MAP_FREEZE
+ * returns 0; other commands -1 with errno ENOTSUP. */
+long bpftime_amd_handle_sysbpf(int cmd, void *attr, uint32_t size);
+
 /* ---- lddw helpers for the device VM (bpftime_shm.cpp:637-676) ---- */
 uint64_t bpftime_amd_map_ptr_by_fd(uint32_t fd); /* the fd itself, ~0 if not a map */
 uint64_t bpftime_amd_map_val(uint64_t map_ptr);  /* DEVICE address of the first value */

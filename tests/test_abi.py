@@ -3,6 +3,7 @@ function include/*.h declares; VM-level error paths that run before any
 device work behave like the reference (compat_ubpf.cpp:61-200,
 ebpf-vm.cpp:6-98)."""
 import ctypes as C
+import errno
 import os
 import re
 
@@ -86,3 +87,21 @@ def test_compile_and_aot_unsupported():
     assert b"interpreter" in C.string_at(err.value)
     assert not l.ebpf_load_aot_object(C.c_void_p(vm), None, 0)
     l.ebpf_destroy(C.c_void_p(vm))
+
+
+def test_sysbpf_errors_before_device_work():
+    """bpf(2) commands the data path does not serve, and element ops on an
+    fd that is no map (syscall_context.cpp:490-514: ENOENT)."""
+    import struct
+    from bpftime_amd import vm
+    r, e = vm.sys_bpf(99, bytearray(128))
+    assert r == -1 and e == errno.ENOTSUP
+    key = bytearray(4)
+    kb = (C.c_char * 4).from_buffer(key)
+    val = bytearray(8)
+    vb = (C.c_char * 8).from_buffer(val)
+    r, e = vm.sys_bpf(vm.BPF_MAP_LOOKUP_ELEM, vm.attr_map_elem(777, C.addressof(kb), C.addressof(vb)))
+    assert r == -1 and e == errno.ENOENT
+    assert vm.sys_bpf(vm.BPF_MAP_FREEZE, bytearray(128))[0] == 0
+    assert _lib.lib().bpftime_amd_handle_sysbpf(vm.BPF_MAP_CREATE, None, 0) == -1
+    assert struct.calcsize("<IIQQQ") == 32
