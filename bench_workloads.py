@@ -362,11 +362,86 @@ def ringbuf_sample(args, dev, gen, isa, programs):
     }
 
 
+def tail_call(args, dev, gen, isa, programs):
+    """bpf_tail_call jump table: 2^24 64-B frames; the
+    caller tail-calls slot data[0] & 3 of a PROG_ARRAY {0: a packet writer,
+    1: a map counter, 2: empty (-1), 3: a counter that tail-calls slot 0}
+    with per-CPU counters,
+    so lanes of one wave take different targets and chains of two."""
+    n = 1 << (args.log2n if args.log2n_set else 24)
+    dev.reset_runtime()
+    pa = dev.Map(isa.BPF_MAP_TYPE_PROG_ARRAY, 4, 4, 4, name="jmp_table")
+    # per-CPU counters, the XDP idiom for hot counters (virtual CPU = unit / 64)
+    cnt = dev.Map(isa.BPF_MAP_TYPE_PERCPU_ARRAY, 4, 8, 4, name="counts")
+    targets = {0: programs.tail_target_write(0xA1), 1: programs.tail_target_count(cnt.fd),
+               3: programs.tail_target_recurse(pa.fd, cnt.fd, 0)}
+    pfd = {}
+    for k, code in targets.items():
+        pfd[k] = dev.prog_create(code, "t%d" % k, 6)
+        pa.update(struct.pack("<i", k), struct.pack("<i", pfd[k]))
+    code = programs.tail_xdp_caller(pa.fd, cnt.fd)
+    vm = dev.VM()
+    vm.load(code)
+    pk = dev.DeviceBuffer(n * 64)
+    if dev.lib().bpftime_amd_gen_xdp(pk.ptr, n, 64, 64, gen.SEED_CFG2 ^ 0x7, 0, None):
+        raise SystemExit("generator failed")
+    dv = dev.DeviceBuffer(4 * n)
+
+    def step():
+        vm.exec_batch(dev.CTX_XDP, pk, n, 64, fixed_len=64, verdicts=dv, flags=0, ifindex=5)
+
+    wall, kern_s = _timed(dev, step, args.steps, args.warmup)
+    runs = args.steps + args.warmup
+    frames = pk.download().reshape(n, 64)
+    idx = frames[:, 0] & 3
+    hist = np.bincount(idx, minlength=4).astype(np.uint64)
+    want_v = np.array([64 + 0xA1, 2, 0xFFFFFFFF, 64 + 0xA1 + 1], dtype=np.uint64)[idx] + 1005
+    verd = dv.download(np.uint32)
+    got = [int(np.frombuffer(cnt.lookup(struct.pack("<i", i)), dtype=np.uint64).sum()) for i in range(4)]
+    want_c = [runs * int(hist[0]), runs * 2 * int(hist[1]), runs * int(hist[2] + hist[3]), runs * int(hist[3])]
+    ok = bool((verd == (want_v & 0xFFFFFFFF).astype(np.uint32)).all()) and got == want_c and \
+        bool((frames[(idx == 0) | (idx == 3), 1] == 0xA1).all())
+    cpu = None
+    if not args.no_cpu_baseline:   # the oracle over a sample of the same frames
+        from oracle import pyoracle as po
+        sn = min(n, 1 << 18)
+        po.reset()
+        opa = po.OracleMap(isa.BPF_MAP_TYPE_PROG_ARRAY, 4, 4, 4, fd=pa.fd)
+        po.OracleMap(isa.BPF_MAP_TYPE_PERCPU_ARRAY, 4, 8, 4, fd=cnt.fd)
+        for k, c in targets.items():
+            po.prog_create(pfd[k], c)
+            opa.update(struct.pack("<i", k), struct.pack("<i", pfd[k]))
+        ovm = po.OracleVM()
+        ovm.load(code)
+        t0 = time.perf_counter()
+        ov = ovm.run_xdp(frames[:sn].copy(), fixed_len=64, ifindex=5)
+        cpu_s = time.perf_counter() - t0
+        ok = ok and bool((ov == verd[:sn]).all())
+        cpu = {"value": round(sn / cpu_s / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
+               "sample": f"the oracle over the first 2^{int(np.log2(sn))} frames ({cpu_s:.2f} s)"}
+    algo = 1 + 4 + 0.5   # first byte + verdict + the writer's byte for half the frames (counters on-chip)
+    achieved = algo * n / kern_s / 1e9
+    return {
+        "metric": "device-resident Mpps, bpf_tail_call jump-table XDP prog (4 slots), 64B pkts",
+        "value": round(n * args.steps / wall / 1e6, 3), "unit": "Mpps", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic (seeded splitmix64 64-B frames)",
+        "config": {"workload": "tail-call over 2^%d device-resident 64-B frames" % int(np.log2(n)),
+                   "packets": n, "slots": 4},
+        "parity": {"verdicts_exact": ok, "counters": got, "ok": ok},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "kernel_avg_ms": round(kern_s * 1e3, 4), "algo_bytes_per_pkt": algo},
+        "cpu_baseline": cpu,
+    }
+
+
 def run(args):
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         raise SystemExit("--workload %s runs on one GPU (BASELINE configs[2]/[4])" % args.workload)
     from bpftime_amd import gen, isa, programs
     from bpftime_amd import vm as dev
     fn = {"flow-hash": flow_hash, "syscall-agg": syscall_agg, "lpm-route": lpm_route,
-          "ringbuf-sample": ringbuf_sample}[args.workload]
+          "ringbuf-sample": ringbuf_sample, "tail-call": tail_call}[args.workload]
     print(json.dumps(fn(args, dev, gen, isa, programs)))

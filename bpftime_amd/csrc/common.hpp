@@ -130,7 +130,7 @@ constexpr uint32_t kIxProbes = 8;  // index probes before the reference probe
 constexpr uint32_t kTailHelper = 12;
 constexpr int32_t kRetHelper = 0x7fff0001;  // internal: a linked target's exit
 constexpr uint32_t kTailDepth = 32;          // MAX_TAIL_CALL_CNT
-constexpr uint32_t kTailGrid = 256;          // blocks per launch of an image with tail calls
+constexpr uint32_t kTailGrid = 1024;         // blocks per launch of an image with tail calls
 constexpr uint32_t kFrameCtx = 64;
 constexpr uint32_t kFrameHdr = 96;           // r1..r10, ctx address, ret pc, ctx bytes
 constexpr uint32_t kFrameBytes = kFrameHdr + kFrameCtx + kStackSize;
@@ -175,7 +175,8 @@ struct KParams {
   uint64_t umem_bytes;    // descriptor mode: bytes at data
   int64_t sys_nr;         // CTX_SYSCALL: run only records with this id (-1: every record)
   const int32_t *tail_entry;  // prog fd -> entry pc in the linked image, -1 = not linked (nullable)
-  uint8_t *frames;        // tail-call frames: [lane][kTailDepth][kFrameBytes]
+  uint8_t *frames;        // tail-call frames: [kTailDepth][frame_words][kTailGrid * kBlock lanes] u64
+  uint32_t frame_words;   // header + ctx + the image's stack bytes, / 8
 };
 
 // Error codes recorded per unit (err_count counts units with any error)

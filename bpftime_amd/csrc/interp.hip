@@ -300,6 +300,25 @@ __device__ __forceinline__ uint32_t run_loop(Ctx &c) {
                                    : (uint64_t)__hip_atomic_exchange((uint32_t *)ea, (uint32_t)v, __ATOMIC_RELAXED,
                                                                      __HIP_MEMORY_SCOPE_AGENT);
           WRO(d.src, old, v);
+        } else if (d.hi == 0x00) {
+          // add without fetch: lanes adding to one address are summed across
+          // the wave and one of them adds (same-address device atomics
+          // serialize at the memory side); the final value is the same
+          uint64_t pend = __ballot(sel && ok);
+          while (pend) {
+            const int leader = __builtin_ctzll(pend);
+            const uint64_t la = readlane64(a, leader);
+            const bool mine = ((pend >> __lane_id()) & 1) && a == la;
+            const uint64_t m = __ballot(mine);
+            const uint64_t sum = wave_sum64(mine ? (w64 ? v : (uint64_t)(uint32_t)v) : 0);
+            if ((int)__lane_id() == leader) {
+              if (w64)
+                __hip_atomic_fetch_add((uint64_t *)la, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              else
+                __hip_atomic_fetch_add((uint32_t *)la, (uint32_t)sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            pend &= ~m;
+          }
         } else {
           uint64_t old;
           const uint32_t aop = (uint32_t)d.hi & ~1u;
@@ -481,7 +500,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   SRP(err_count); SRV(n); SRV(stride); SRV(first_unit); SRV(data_lo); SRV(data_hi); SRV(arena_lo);
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
-  SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames);
+  SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
 #undef SRP
 #undef SRV
@@ -656,7 +675,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         if (csel) {
           ctx_for_cpp();
           uint64_t *R = &Rf[tid];
-          uint8_t *frames = p.frames + (uint64_t)(blockIdx.x * kBlock + tid) * kTailDepth * kFrameBytes;
+          // frames word-interleaved across the grid's lanes ([depth][word][lane]):
+          // a wave's save of one word is one coalesced 512-B store
+          uint64_t *const fbase = (uint64_t *)p.frames + (blockIdx.x * kBlock + tid);
+          constexpr uint64_t kLanes = (uint64_t)kTailGrid * kBlock;
+          auto FW = [&](uint32_t d, uint32_t w) -> uint64_t & {
+            return fbase[((uint64_t)d * p.frame_words + w) * kLanes];
+          };
           const uint32_t sbytes = BIGSTACK ? kStackSize : p.stack_size;
           if (cid == kTailHelper) {
             next = c.call_pc + 1;
@@ -677,14 +702,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
               }
             const bool in_stack = a1 + 64 > stack_top - sbytes && a1 < stack_top;
             if (entry >= 0 && tdepth < kTailDepth && a1 != 0 && !in_stack) {
-              uint64_t *fh = (uint64_t *)(frames + (uint64_t)tdepth * kFrameBytes);
-              for (int r = 1; r <= 10; r++) fh[r - 1] = R[r * kBlock];
-              fh[10] = a1;
-              fh[11] = (uint64_t)next | ((uint64_t)cb << 32);
-              for (uint32_t i = 0; i < cb; i += 8) fh[kFrameHdr / 8 + i / 8] = mem_load(a1 + i, 8);
+              const uint32_t d = tdepth;
+              for (int r = 1; r <= 10; r++) FW(d, r - 1) = R[r * kBlock];
+              FW(d, 10) = a1;
+              FW(d, 11) = (uint64_t)next | ((uint64_t)cb << 32);
+              for (uint32_t i = 0; i < cb; i += 8) FW(d, kFrameHdr / 8 + i / 8) = mem_load(a1 + i, 8);
               const uint64_t sb = stack_top - sbytes;
               for (uint32_t i = 0; i < sbytes; i += 8)
-                fh[(kFrameHdr + kFrameCtx) / 8 + i / 8] = *(const uint64_t *)(sb + i);
+                FW(d, (kFrameHdr + kFrameCtx) / 8 + i / 8) = *(const uint64_t *)(sb + i);
               for (int r = 0; r <= 10; r++) R[r * kBlock] = 0;
               R[1 * kBlock] = a1;
               R[2 * kBlock] = 64;  // bpftime_prog_exec(context, sizeof(context), ...)
@@ -699,16 +724,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             c.alive = false;
           } else {
             tdepth--;
-            const uint64_t *fh = (const uint64_t *)(frames + (uint64_t)tdepth * kFrameBytes);
+            const uint32_t d = tdepth;
             const uint64_t rv = R[0];
-            for (int r = 1; r <= 10; r++) R[r * kBlock] = fh[r - 1];
-            const uint64_t a1 = fh[10];
-            next = (uint32_t)fh[11];
-            const uint32_t cb = (uint32_t)(fh[11] >> 32);
-            for (uint32_t i = 0; i < cb; i += 8) mem_store(a1 + i, 8, fh[kFrameHdr / 8 + i / 8]);
+            for (int r = 1; r <= 10; r++) R[r * kBlock] = FW(d, r - 1);
+            const uint64_t a1 = FW(d, 10);
+            const uint64_t w11 = FW(d, 11);
+            next = (uint32_t)w11;
+            const uint32_t cb = (uint32_t)(w11 >> 32);
+            for (uint32_t i = 0; i < cb; i += 8) mem_store(a1 + i, 8, FW(d, kFrameHdr / 8 + i / 8));
             const uint64_t sb = stack_top - sbytes;
             for (uint32_t i = 0; i < sbytes; i += 8)
-              *(uint64_t *)(sb + i) = fh[(kFrameHdr + kFrameCtx) / 8 + i / 8];
+              *(uint64_t *)(sb + i) = FW(d, (kFrameHdr + kFrameCtx) / 8 + i / 8);
             R[0] = rv;
           }
         }

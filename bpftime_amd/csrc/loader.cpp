@@ -903,8 +903,14 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
   for (const DInsn &d : prog)
     if (d.op == X_CALL && (d.hi == 44 || d.hi == 65)) pkt_ok = false;
   std::vector<std::vector<PVal>> in;
-  // a linked tail-call image has entries the pointer kinds do not start from
-  if (lo.multi_entry) return;
+  // a linked tail-call image has entries the pointer kinds do not start from:
+  // generic handlers, and adds without fetch in the C++ tier, which sums a
+  // wave's adds to one address (the combining table needs the kinds)
+  if (lo.multi_entry) {
+    for (size_t i = 0; i < prog.size(); i++)
+      if (prog[i].op == X_ATOMIC && prog[i].hi == 0x00) out.fast[i].hoff = 4 + 4 * F_SLOW;
+    return;
+  }
   if (!pointer_kinds(prog, lo.lddw_src, xdp, pkt_ok, in)) return;  // ctx rewritten: generic handlers only
   // per-lane counter adds (fused counters, atomic adds without fetch) whose
   // target is not a wave-uniform constant use the LDS combining table

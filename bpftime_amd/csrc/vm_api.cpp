@@ -67,6 +67,8 @@ class Mi355xVm {
   // array target (common.hpp kTailHelper), rebuilt when rt().prog_gen moves
   std::vector<RawInsn> raw;
   bool has_tail = false;
+  uint32_t base_stack = 0;
+  uint32_t frame_words = 0;  // the loaded program's own stack need (kStackSize + 1: unknown)
   uint64_t image_gen = 0;
   int32_t *d_tail_entry = nullptr;
 
@@ -140,6 +142,7 @@ class Mi355xVm {
       return -1;
     }
     has_tail = out.tail_call;
+    base_stack = out.big_stack ? kStackSize + 1 : out.stack_size;
     raw.assign((const RawInsn *)code, (const RawInsn *)code + code_len / 8);
     prog = std::move(out);
     loaded = true;
@@ -174,6 +177,7 @@ class Mi355xVm {
     std::vector<RawInsn> img(raw);
     std::vector<uint32_t> entries;
     std::vector<int32_t> entry(kMaxFds, -1);
+    uint32_t stack_need = base_stack;  // the deepest program of the image
     for (int32_t t : targets) {
       const std::vector<uint8_t> &bytes = r.progs[t].insns;
       const size_t n = bytes.size() / 8;
@@ -181,6 +185,7 @@ class Mi355xVm {
       LoadOut alone;
       std::string err;
       if (load_program((const RawInsn *)bytes.data(), n, hm, names, lddw, alone, err) < 0) continue;
+      stack_need = std::max(stack_need, alone.big_stack ? kStackSize + 1 : alone.stack_size);
       entry[t] = (int32_t)img.size();
       entries.push_back((uint32_t)img.size());
       const RawInsn *code = (const RawInsn *)bytes.data();
@@ -206,6 +211,11 @@ class Mi355xVm {
       error = "tail-call image: " + err;
       return -1;
     }
+    if (stack_need <= kLdsStackMax) {
+      // every program's stack fits the LDS stack: the frames save that many bytes
+      out.big_stack = false;
+      out.stack_size = std::max<uint32_t>(8, stack_need);
+    }
     FastForm nx, nr;
     build_fast(out, true, nx);
     build_fast(out, false, nr);
@@ -213,8 +223,17 @@ class Mi355xVm {
     DInsn *dp = nullptr;
     const size_t bytes = out.prog.size() * sizeof(DInsn);
     if (!d_tail_entry && hipMalloc((void **)&d_tail_entry, 4 * kMaxFds) != hipSuccess) d_tail_entry = nullptr;
-    if (!r.d_frames && hipMalloc((void **)&r.d_frames, (size_t)kTailGrid * kBlock * kTailDepth * kFrameBytes) != hipSuccess)
-      r.d_frames = nullptr;
+    // frames: header + ctx copy + the stack bytes the image uses, per depth and lane
+    frame_words = (kFrameHdr + kFrameCtx + (out.big_stack ? kStackSize : out.stack_size)) / 8;
+    const uint64_t fbytes = (uint64_t)kTailGrid * kBlock * kTailDepth * frame_words * 8;
+    if (r.frames_bytes < fbytes) {
+      if (r.d_frames) hipFree(r.d_frames);
+      r.frames_bytes = 0;
+      if (hipMalloc((void **)&r.d_frames, fbytes) != hipSuccess)
+        r.d_frames = nullptr;
+      else
+        r.frames_bytes = fbytes;
+    }
     if (!d_tail_entry || !r.d_frames || hipMalloc((void **)&dp, bytes) != hipSuccess ||
         hipMemcpy(dp, out.prog.data(), bytes, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_tail_entry, entry.data(), 4 * kMaxFds, hipMemcpyHostToDevice) != hipSuccess) {
@@ -279,6 +298,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   if (has_tail) {
     p.tail_entry = d_tail_entry;
     p.frames = r.d_frames;
+    p.frame_words = frame_words;
   }
   {
     // staged window: what the static packet / slot accesses need, when every
