@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libbpftime_amd.so")
+LIB_PATH = os.environ.get("BPFTIME_AMD_LIB") or os.path.join(_HERE, "lib", "libbpftime_amd.so")
 
 u8p = C.POINTER(C.c_uint8)
 u32p = C.POINTER(C.c_uint32)
@@ -158,6 +158,8 @@ def lib() -> C.CDLL:
             raise RuntimeError(f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback exists)")
         l = C.CDLL(LIB_PATH, use_errno=True)
         for name, res, args in SIGNATURES + EXTRA:
+            if os.environ.get("BPFTIME_AMD_LIB") and not hasattr(l, name):
+                continue  # an older build loaded for A/B timing
             f = getattr(l, name)
             f.restype = res
             f.argtypes = args
