@@ -71,6 +71,7 @@ class Mi355xVm {
   uint32_t frame_words = 0;  // the loaded program's own stack need (kStackSize + 1: unknown)
   uint64_t image_gen = 0;
   int32_t *d_tail_entry = nullptr;
+  std::mutex tail_mu;
 
   Mi355xVm() {
     // bpftime_prog.cpp:126-127 defaults, pointed at the device registry
@@ -156,6 +157,7 @@ class Mi355xVm {
   // out, so tail calls to it return -1 like a failed bpftime_prog_load
   // (bpf_helper.cpp:623-628).
   int link_tail_image() {
+    std::lock_guard<std::mutex> tg(tail_mu);  // concurrent batches of one VM relink once
     Runtime &r = rt();
     if (image_gen == r.prog_gen && d_tail_entry) return 0;
     std::map<size_t, size_t> hm = helper_id_map;
