@@ -1015,6 +1015,7 @@ void bpftime_amd_reset(void) {
   }
   if (r.d_maptab) hipMemset(r.d_maptab, 0, sizeof(DMap) * kMaxFds);
   r.arena_used = 0;
+  r.prog_gen++;  // tail-call images linked before the reset relink
 }
 
 // ---- lddw helpers: bpftime_shm.cpp:637-676 --------------------------------
