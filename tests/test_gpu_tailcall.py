@@ -125,3 +125,42 @@ def test_xdp_tailcall_relink(fresh_oracle, fresh_runtime):
     dev.close_fd(903)
     ov, opk = _run_both(po, dev, ovm, dvm, 4096, 3, cnt_o, cnt_d)
     assert (ov[(opk[:, 0] & 3) == 3] == (0xFFFFFFFF + 1005) & 0xFFFFFFFF).all()
+
+
+def test_image_atomic_adds_summed_per_address(fresh_oracle, fresh_runtime):
+    """In a linked image, adds without fetch run in the C++ tier summed per
+    address across the wave: 4-byte adds to eight lane-dependent slots and
+    8-byte adds to one slot equal the oracle's sequential sums."""
+    po, dev = fresh_oracle, fresh_runtime
+    pa_d = dev.Map(isa.BPF_MAP_TYPE_PROG_ARRAY, 4, 4, 1, fd=PA_FD)
+    pa_o = po.OracleMap(isa.BPF_MAP_TYPE_PROG_ARRAY, 4, 4, 1, fd=PA_FD)
+    c32_d = dev.Map(isa.BPF_MAP_TYPE_ARRAY, 4, 48, 1)
+    c32_o = po.OracleMap(isa.BPF_MAP_TYPE_ARRAY, 4, 48, 1, fd=c32_d.fd)
+    seven = Asm().mov64(0, 7).exit().assemble()
+    po.prog_create(TARGET_FD, seven)
+    dev.prog_create(seven, "seven", 6, fd=TARGET_FD)
+    for m in (pa_o, pa_d):
+        assert m.update(I32(0), I32(TARGET_FD)) == 0
+    a = Asm().mov64(6, "r1")
+    a.ldx(8, 7, 6, 0).ldx(8, 3, 6, 8).mov64(4, "r7").add64(4, 1).jmp("jgt", 4, "r3", "out")
+    a.ldx(1, 8, 7, 0).alu64("and", 8, 7).alu64("lsh", 8, 2)       # r8 = 4 * (data[0] & 7)
+    a.mov64(1, "r6").ld_map_fd(2, PA_FD).mov64(3, 0).call(tc.TAIL)
+    a.mov64(9, "r0")
+    a.ld_map_value(1, c32_d.fd, 0).alu64("add", 1, "r8").atomic(4, 0x00, 1, 0, 9)
+    a.ld_map_value(1, c32_d.fd, 0).mov64(2, 1).atomic(8, 0x00, 1, 32, 2)
+    a.label("out").mov64(0, 2).exit()
+    code = a.assemble()
+    ovm = po.OracleVM()
+    ovm.load(code)
+    dvm = dev.VM()
+    dvm.load(code)
+    n = 20000
+    pk = gen.xdp_packets(n, seed=3)
+    ov = ovm.run_xdp(pk.copy(), fixed_len=64)
+    d = dev.DeviceBuffer.from_array(pk)
+    dv = dev.DeviceBuffer(4 * n)
+    assert dvm.exec_batch(dev.CTX_XDP, d, n, 64, fixed_len=64, verdicts=dv) == 0
+    np.testing.assert_array_equal(dv.download(np.uint32), ov)
+    assert c32_d.lookup(I32(0)) == c32_o.lookup(I32(0))
+    got = np.frombuffer(c32_d.lookup(I32(0)), dtype=np.uint32)
+    assert int(got[:8].sum()) == 7 * n and struct.unpack_from("<Q", c32_d.lookup(I32(0)), 32)[0] == n
