@@ -88,6 +88,8 @@ SIGNATURES = [
     ("bpftime_amd_vm_info", C.c_int, [C.c_void_p, u32p, C.POINTER(C.c_int), u32p, u32p]),
     ("bpftime_amd_set_step_limit", None, [C.c_void_p, C.c_uint64]),
     ("bpftime_amd_vm_fast_info", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    ("bpftime_amd_vm_counter_info", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32),
+                                              C.POINTER(C.c_uint32)]),
     ("bpftime_import_global_shm_from_json", C.c_int, [C.c_char_p]),
     ("bpftime_export_global_shm_to_json", C.c_int, [C.c_char_p]),
     ("bpftime_import_shm_handler_from_json", C.c_int, [C.c_int, C.c_char_p]),

@@ -34,7 +34,8 @@ enum XOp : uint8_t {
   X_LE, X_BE,
   // memory
   X_LDX, X_ST, X_STX, X_ATOMIC, X_LDDW,
-  // fused "ldx r,[b+o]; add r,v; stx [b+o],r" with r dead afterwards
+  // fused "ldx r,[b+o]; add r,v; stx [b+o],r": one atomic add (A_FETCH: r
+  // stays live and receives the old value + v)
   X_RMW_ADD,
   // control
   X_JA, X_JEQ, X_JGT, X_JGE, X_JSET, X_JNE, X_JSGT, X_JSGE, X_JLT, X_JLE, X_JSLT, X_JSLE,
@@ -47,6 +48,13 @@ enum XOp : uint8_t {
 constexpr uint8_t A_SRCREG = 0x01;  // second operand is a register
 constexpr uint8_t A_W32 = 0x02;     // 32-bit ALU / JMP32
 constexpr uint8_t A_SIZE_SHIFT = 4; // memory access size = 1 << ((aux >> 4) & 3)
+constexpr uint8_t A_FETCH = 0x08;   // X_RMW_ADD: the loaded register stays live (DInsn::hi = it):
+                                    // r = fetch_add(addr, v) + v, the ldx/add/stx in one atomic
+
+// FInsn::w1 flags (per entry form and launch, loader.cpp build_fast / link_fast)
+constexpr uint32_t FW_NODEFER = 1;  // counter add: apply it to memory now (a later access of
+                                    // the same unit may read or overwrite it, or the batch is
+                                    // ORDERED): no per-wave delta cache, no LDS combining table
 
 // 16-byte pre-decoded instruction: fetched with one s_load_dwordx4.
 struct DInsn {

@@ -135,7 +135,8 @@ def handler_ids():
     ids += ["LDDW", "JA", "CALL_LOOKUP", "CALL_LOOKUP_STK", "CALL_LOOKUP_AK", "EXIT"]
     for sz in (4, 8):
         for k in ("R", "I"):
-            ids += [f"RMW{sz}_{k}", f"RMWMV{sz}_{k}", f"RMWK{sz}_{k}"]
+            ids += [f"RMW{sz}_{k}", f"RMWMV{sz}_{k}", f"RMWK{sz}_{k}", f"RMWD{sz}_{k}"]
+        ids += [f"ATOMD{sz}"]
     for w in ("64", "32"):
         for cc in JCC:
             for k in ("R", "I"):
@@ -254,7 +255,7 @@ class Gen:
                "s_andn2_b64 s[54:55], exec, s[54:55]",
                f"s_cbranch_scc1 {L('slow')}")
 
-    def comb_add(self, sz):
+    def comb_add(self, sz, direct_only=False):
         """Per-lane add of Y (v46, v[46:47] for 8 B) at the global address Z
         through the workgroup's LDS combining table (interp.hip: %[combn]
         entries of {tag = address | size bit, delta}, flushed by the block at
@@ -262,7 +263,11 @@ class Gen:
         device atomic per lane (those serialize at the memory side).  Entry =
         a multiplicative hash of the address, then the other seven entries of
         its 128-B group; lanes finding all eight taken by other addresses,
-        and misaligned addresses, add to memory directly."""
+        and misaligned addresses, add to memory directly.  direct_only: every
+        lane adds to memory now (FW_NODEFER counters)."""
+        if direct_only:
+            self.e("global_atomic_add_x2 v[48:49], v[46:47], off" if sz == 8 else "global_atomic_add v[48:49], v46, off")
+            return
         done, direct = self.label("cd"), self.label("cx")
         self.e("s_mov_b64 s[60:61], exec", "s_mov_b64 s[54:55], 0",
                "s_cmp_eq_u32 %[combn], 0", f"s_cbranch_scc1 {direct}",
@@ -294,7 +299,7 @@ class Gen:
         self.e("global_atomic_add_x2 v[48:49], v[46:47], off" if sz == 8 else "global_atomic_add v[48:49], v46, off",
                f"{done}:", "s_mov_b64 exec, s[60:61]")
 
-    def comb_peel(self, sz):
+    def comb_peel(self, sz, direct_only=False):
         """Per-lane adds of Y to addresses Z (exec = the adding lanes).  When
         every lane adds the same value (a counter += constant), lanes that
         share the first lane's address are folded into one add of
@@ -320,13 +325,13 @@ class Gen:
                "s_mul_i32 s71, s65, s70", "s_add_u32 s67, s67, s71",
                "s_lshl_b64 exec, 1, s69",                                   # the first lane adds for all
                "v_mov_b32 v46, s66", "v_mov_b32 v47, s67")
-        self.comb_add(sz)
+        self.comb_add(sz, direct_only)
         self.e("v_readlane_b32 s56, v56, 0", "v_readlane_b32 s57, v56, 1",
                "s_mov_b64 exec, s[56:57]",
                f"s_cbranch_execz {out}",
                "s_add_u32 s85, s85, 1", "s_cmp_lt_u32 s85, 4", f"s_cbranch_scc1 {loop}",
                f"{rest}:")
-        self.comb_add(sz)
+        self.comb_add(sz, direct_only)
         self.e(f"{out}:", "v_readlane_b32 s56, v56, 2", "v_readlane_b32 s57, v56, 3",
                "s_mov_b64 exec, s[56:57]")
 
@@ -1001,6 +1006,40 @@ class Gen:
         self.e(f"{done}:", "s_mov_b32 s48, s46")
         self.dispatch()
 
+    def rmwd(self, sz, k):
+        """Fused counter that must reach memory now (FW_NODEFER: a later
+        access of the unit may read or overwrite it, or the batch is
+        ORDERED): lanes sharing an address and value fold into one device
+        atomic, the rest add lane by lane, and the adds are drained before
+        the next instruction.  Targets in the unit's staged bytes, LDS or
+        scratch leave for the C++ tier."""
+        glb = self.label("dg")
+        self.rd("s44", 48)
+        self.rmw_value(k)
+        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[42:43]")
+        self.staged_or(sz, L("slow"), glb)
+        self.e(f"{glb}:")
+        self.check_global(sz)
+        self.comb_peel(sz, direct_only=True)
+        self.e("s_waitcnt vmcnt(0)", "s_mov_b32 s48, s46")   # continue after the stx
+        self.dispatch()
+
+    def atomd(self, sz):
+        """BPF_ATOMIC add without fetch that must reach memory now
+        (FW_NODEFER)."""
+        glb = self.label("adg")
+        self.rd("s44", 48)
+        self.rd("s45", 46)
+        if sz == 4:
+            self.e("v_mov_b32 v47, 0")
+        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[42:43]")
+        self.staged_or(sz, L("slow"), glb)
+        self.e(f"{glb}:")
+        self.check_global(sz)
+        self.comb_peel(sz, direct_only=True)
+        self.e("s_waitcnt vmcnt(0)")
+        self.next_seq()
+
     def atomic(self, sz, op, fetch, mv=False):
         """BPF_ATOMIC add/or/and/xor (+ BPF_FETCH) on global memory: one
         device-scope atomic per lane (array_map values, hash values).  LDS or
@@ -1196,6 +1235,8 @@ class Gen:
             e(f"{L('h_' + name)}:")
             if name == "SLOW":
                 e(f"s_branch {L('slow')}")
+            elif name.startswith("ATOMD"):
+                self.atomd(int(name[5]))
             elif name.startswith("ATOMMV"):
                 self.atomic(int(name[6]), "ADD", False, mv=True)
             elif name.startswith("ATOM"):
@@ -1248,6 +1289,8 @@ class Gen:
                 self.call_lookup_ak()
             elif name == "EXIT":
                 self.exit_()
+            elif name.startswith("RMWD"):
+                self.rmwd(int(name[4]), name[6])
             elif name.startswith("RMWMV"):
                 self.rmw(int(name[5]), name[7], mv=True)
             elif name.startswith("RMWK"):

@@ -85,6 +85,7 @@ constexpr uint32_t R_DONE = 0, R_DIVERGE = 1, R_RECONV = 2, R_CALL = 3, R_STEP =
 struct Ctx {
   uint64_t *R;           // this lane's register file column: R[i * kBlock]
   prog_ptr prog;
+  const FInsn *fast;     // per-launch threaded form (w1: FW_* flags)
   Win win;
   uint64_t dummy;        // flat address of this lane's dummy LDS slot
   uint32_t *verdicts;
@@ -226,9 +227,63 @@ __device__ __forceinline__ uint32_t run_loop(Ctx &c) {
       case X_RMW_ADD: {
         // Counters hit by a whole wave (e.g. cntrs_array[0]) are summed across
         // the wave into the per-wave delta cache; otherwise one atomic per lane.
+        // FW_NODEFER counters (a later access of the unit can observe them,
+        // or the batch is ORDERED) and fetch forms reach memory here.
         const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
         const uint64_t a = RG(d.dst) + (int64_t)d.off;
         const uint64_t v = OPB(RG(d.src));
+        const bool fetch = (d.aux & A_FETCH) != 0;
+        const uint32_t fw = __builtin_amdgcn_readfirstlane(c.fast[cur].w1);  // uniform by construction
+        if (fetch || (fw & FW_NODEFER)) {
+          const bool ok = c.win.ok(a, sz);
+          const bool local = is_lds_addr(a) || is_scratch_addr(a);  // the unit's own stack: no other writer
+          uint64_t old = 0;
+          if (sel && ok && local) {
+            old = mem_load(a, sz);
+            mem_store(a, sz, old + v);
+          }
+          // global: lanes adding to one address take one atomic in lane
+          // order (each lane's old value = the leader's result + the adds of
+          // the lanes before it: a serial order of the wave's units)
+          uint64_t pend = __ballot(sel && ok && !local);
+          while (pend) {
+            const int leader = __builtin_ctzll(pend);
+            const uint64_t la = readlane64(a, leader);
+            const bool mine = ((pend >> __lane_id()) & 1) && a == la;
+            const uint64_t m = __ballot(mine);
+            const uint64_t add = mine ? (sz == 8 ? v : (uint64_t)(uint32_t)v) : 0;
+            uint64_t incl = add;
+            for (int o = 1; o < 64; o <<= 1) {
+              const uint64_t t = __shfl_up(incl, (unsigned)o, 64);
+              if ((int)__lane_id() >= o) incl += t;
+            }
+            const uint64_t total = readlane64(incl, 63);
+            uint64_t base = 0;
+            if ((int)__lane_id() == leader) {
+              if (sz == 8)
+                base = __hip_atomic_fetch_add((uint64_t *)la, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              else
+                base = __hip_atomic_fetch_add((uint32_t *)la, (uint32_t)total, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+            }
+            base = readlane64(base, leader);
+            if (mine) old = base + incl - add;
+            pend &= ~m;
+          }
+          if (fetch) {
+            // ldx zero-extends; the add is 64-bit unless it was ALU32
+            const uint64_t o = sz == 8 ? old : (uint64_t)(uint32_t)old;
+            const uint64_t r = (d.aux & A_W32) ? (uint64_t)(uint32_t)(o + v) : o + v;
+            WRO(d.hi, r, RG(d.hi));
+          }
+          if (__ballot(sel && !ok) != 0) {
+            c.err = (sel && !ok) ? E_OOB : c.err;
+            c.alive = c.alive && !(sel && !ok);
+            if (__ballot(c.alive) == 0) return R_DONE;
+          }
+          npc = d.tgt;
+          break;
+        }
         const uint64_t selm = __ballot(sel);
         const int first = __builtin_ctzll(selm);
         const uint64_t a0 = readlane64(a, first);
@@ -523,6 +578,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   Ctx c;
   c.R = &Rf[tid];
   c.prog = (prog_ptr)p.prog;
+  c.fast = p.fast;
   c.win = Win{p.data_lo, p.data_hi, p.arena_lo, p.arena_hi, p.checked != 0};
   c.dummy = (uint64_t)(uintptr_t)&Rf[11 * kBlock + tid];
   c.verdicts = p.verdicts;

@@ -290,6 +290,7 @@ static void use_def(const DInsn &d, RegSet &use, RegSet &def) {
     case X_RMW_ADD:
       U(d.dst);
       if (d.aux & A_SRCREG) U(d.src);
+      if (d.aux & A_FETCH) D(d.hi);
       break;
     default: break;
   }
@@ -383,6 +384,7 @@ static int stack_depth(const std::vector<DInsn> &p, const std::vector<bool> &rea
       case X_RMW_ADD:
         base_access(d.dst, 0);
         if ((d.aux & A_SRCREG) && (st[d.src].kind == 1 || st[d.src].kind == 3)) escape = true;
+        if (d.aux & A_FETCH) st[d.hi] = SVal{2, 0};
         break;
       case X_STX:
         base_access(d.dst, 0);
@@ -591,7 +593,11 @@ int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &
     }
   }
 
-  // RMW fusion: ldx r,[b+o]; add r,v; stx [b+o],r  with r dead after the stx
+  // RMW fusion: ldx r,[b+o]; add r,v; stx [b+o],r is one atomic add (the
+  // reference's ld/add/st is not atomic, but it runs one unit at a time: a
+  // parallel batch needs the add to be indivisible to give the same total).
+  // r dead after the stx: a plain add; r live: a fetch-add that also leaves
+  // old + v in r (A_FETCH), which is what the three instructions compute.
   uint32_t fused = 0;
   for (uint32_t i = 0; i + 2 < n; i++) {
     const DInsn &a = p[i], &b = p[i + 1], &c = p[i + 2];
@@ -604,14 +610,15 @@ int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &
     if (r == base || b.dst != r || c.src != r || c.dst != base || c.off != a.off) continue;
     if ((b.aux & A_SRCREG) && b.src == r) continue;
     if (is_target[i + 1] || is_target[i + 2]) continue;
-    if (live_out[i + 2] & (1u << r)) continue;
+    const bool fetch = (live_out[i + 2] & (1u << r)) != 0;
     DInsn f{};
     f.op = X_RMW_ADD;
     f.dst = base;
     f.off = a.off;
-    f.aux = (uint8_t)((sz << A_SIZE_SHIFT) | (b.aux & A_SRCREG));
+    f.aux = (uint8_t)((sz << A_SIZE_SHIFT) | (b.aux & A_SRCREG) | (fetch ? (A_FETCH | (b.aux & A_W32)) : 0));
     f.src = b.src;
     f.imm = b.imm;
+    f.hi = r;
     f.tgt = (uint16_t)(i + 3);
     p[i] = f;
     fused++;
@@ -811,8 +818,11 @@ static bool pointer_kinds(const std::vector<DInsn> &p, const std::vector<uint8_t
       }
       case X_ST:
       case X_STX:
+        if (st[d.dst].kind == P_CTX) ctx_written = true;
+        break;
       case X_RMW_ADD:
         if (st[d.dst].kind == P_CTX) ctx_written = true;
+        if (d.aux & A_FETCH) st[d.hi] = kOther;
         break;
       case X_ATOMIC:
         if (st[d.dst].kind == P_CTX) ctx_written = true;
@@ -877,10 +887,150 @@ static bool pointer_kinds(const std::vector<DInsn> &p, const std::vector<uint8_t
   return !ctx_written;
 }
 
+// ---------------------------------------------------------------------------
+// Counter deferral.  Counter adds (fused ldx/add/stx and BPF_ATOMIC add
+// without fetch) may be summed per wave or per block and reach memory when
+// the wave / block ends (interp.hip delta cache, gen_fast.py comb_add) only
+// while nothing the same unit executes afterwards can observe the location:
+// a unit must see its own increments (bpftime_prog.cpp:231-260 runs ld/add/st
+// one unit at a time).  Locations are abstracted from the pointer kinds: a
+// constant address (lddw), a map value range (map fd, offset range), the
+// unit's own memory (stack, ctx, packet, slot: never a map) or anything.
+// ---------------------------------------------------------------------------
+namespace {
+struct Loc {
+  enum : uint8_t { LOCAL, CONST, MAPVAL, ANY } cls;
+  int32_t fd;
+  int64_t lo, hi;  // byte range (CONST: absolute addresses; MAPVAL: offsets in the value)
+};
+constexpr int64_t kUnknownLen = 1 << 16;
+}  // namespace
+
+static Loc loc_of(const std::vector<DInsn> &p, const PVal &b, int64_t off, int64_t len) {
+  switch (b.kind) {
+    case P_CTX: case P_PKT: case P_SLOT: case P_STK:
+      return Loc{Loc::LOCAL, -1, 0, 0};
+    case P_CONST: {
+      const DInsn &l = p[b.id];
+      const int64_t a = (int64_t)((uint64_t)(uint32_t)l.imm | ((uint64_t)(uint32_t)l.hi << 32)) + b.k + off;
+      return Loc{Loc::CONST, -1, a, a + len};
+    }
+    case P_MAPVAL: case P_MVNULL:
+      return Loc{Loc::MAPVAL, b.id, (int64_t)b.k + off, (int64_t)b.k + off + len};
+    default:
+      return Loc{Loc::ANY, -1, 0, 0};
+  }
+}
+
+static bool may_alias(const Loc &a, const Loc &b) {
+  if (a.cls == Loc::ANY || b.cls == Loc::ANY) return true;
+  if (a.cls == Loc::LOCAL || b.cls == Loc::LOCAL) return a.cls == b.cls;
+  if (a.cls == Loc::CONST && b.cls == Loc::CONST) return a.lo < b.hi && b.lo < a.hi;
+  if (a.cls == Loc::MAPVAL && b.cls == Loc::MAPVAL) return a.fd == b.fd && a.lo < b.hi && b.lo < a.hi;
+  const Loc &c = a.cls == Loc::CONST ? a : b, &m = a.cls == Loc::CONST ? b : a;
+  const MapRec *r = map_rec(m.fd);
+  if (!r) return true;
+  return c.lo < (int64_t)(r->d.data + r->bytes) && (int64_t)r->d.data < c.hi;
+}
+
+// Memory the instruction at i reads or writes, other than as a counter add.
+static void accesses(const std::vector<DInsn> &p, uint32_t i, const std::vector<PVal> &st, std::vector<Loc> &out) {
+  out.clear();
+  const DInsn &d = p[i];
+  const int64_t sz = 1 << ((d.aux >> A_SIZE_SHIFT) & 3);
+  switch (d.op) {
+    case X_LDX: out.push_back(loc_of(p, st[d.src], d.off, sz)); return;
+    case X_ST: case X_STX: out.push_back(loc_of(p, st[d.dst], d.off, sz)); return;
+    case X_ATOMIC:
+      if (d.hi != 0x00) out.push_back(loc_of(p, st[d.dst], d.off, sz));
+      return;
+    case X_RMW_ADD:
+      if (d.aux & A_FETCH) out.push_back(loc_of(p, st[d.dst], d.off, sz));
+      return;
+    case X_CALL: break;
+    default: return;
+  }
+  const uint32_t id = (uint32_t)d.hi;
+  auto arg = [&](int r) { out.push_back(loc_of(p, st[r], 0, kUnknownLen)); };
+  auto map_values = [&]() {  // the values of the map in r1
+    if (st[1].kind == P_MAPFD) out.push_back(Loc{Loc::MAPVAL, st[1].id, 0, kUnknownLen});
+    else out.push_back(Loc{Loc::ANY, -1, 0, 0});
+  };
+  switch (id) {
+    case 5: case 7: case 8: case 131: case 44: case 65: return;  // no memory (ctx helpers: unit-local)
+    case 1: arg(2); return;
+    case 2: arg(2); arg(3); map_values(); return;
+    case 3: arg(2); map_values(); return;
+    case 28: arg(1); arg(3); return;
+    case 130: arg(2); return;
+    case 132: case 133: arg(1); return;
+    case 189: arg(3); return;
+    default:
+      if ((int32_t)id == kRetHelper) return;
+      out.push_back(Loc{Loc::ANY, -1, 0, 0});  // tail calls and anything else
+  }
+}
+
+// nodefer[i] for every counter-add site i: an access that may alias it is
+// reachable from it (loops included).
+static std::vector<bool> counter_nodefer(const std::vector<DInsn> &p, const std::vector<std::vector<PVal>> &in) {
+  const uint32_t n = (uint32_t)p.size();
+  auto reached = [&](uint32_t i) { return !(in[i][0].kind == P_UNDEF && in[i][1].kind == P_UNDEF); };
+  std::vector<std::vector<Loc>> acc(n);
+  for (uint32_t i = 0; i < n; i++)
+    if (reached(i)) accesses(p, i, in[i], acc[i]);
+  std::vector<bool> nodefer(n, false);
+  std::vector<uint32_t> seen(n, UINT32_MAX), work;
+  for (uint32_t i = 0; i < n; i++) {
+    const DInsn &d = p[i];
+    const bool add = (d.op == X_RMW_ADD && !(d.aux & A_FETCH)) || (d.op == X_ATOMIC && d.hi == 0x00);
+    if (!add || !reached(i)) continue;
+    const int64_t sz = 1 << ((d.aux >> A_SIZE_SHIFT) & 3);
+    const Loc me = loc_of(p, in[i][d.dst], d.off, sz);
+    if (me.cls == Loc::LOCAL || me.cls == Loc::ANY) {  // the unit's own memory / unknown: nothing to gain
+      nodefer[i] = true;
+      continue;
+    }
+    bool hit = false;
+    work.clear();
+    uint32_t s[2];
+    int ns;
+    successors(p, i, s, ns);
+    for (int j = 0; j < ns; j++) work.push_back(s[j]);
+    while (!work.empty() && !hit) {
+      const uint32_t k = work.back();
+      work.pop_back();
+      if (seen[k] == i) continue;
+      seen[k] = i;
+      for (const Loc &l : acc[k])
+        if (may_alias(me, l)) hit = true;
+      successors(p, k, s, ns);
+      for (int j = 0; j < ns; j++) work.push_back(s[j]);
+    }
+    nodefer[i] = hit;
+  }
+  return nodefer;
+}
+
+static uint32_t direct_add_handler(const DInsn &d) {
+  const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
+  if (sz != 4 && sz != 8) return F_SLOW;
+  if (d.op == X_ATOMIC) return sz == 8 ? F_ATOMD8 : F_ATOMD4;
+  if (d.aux & A_FETCH) return F_SLOW;
+  const bool r = (d.aux & A_SRCREG) != 0;
+  return sz == 8 ? (r ? F_RMWD8_R : F_RMWD8_I) : (r ? F_RMWD4_R : F_RMWD4_I);
+}
+
+static bool is_counter_add(const DInsn &d) {
+  return d.op == X_RMW_ADD || (d.op == X_ATOMIC && d.hi == 0x00);
+}
+
 void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
   const std::vector<DInsn> &prog = lo.prog;
   out.fast.assign(prog.size(), FInsn{});
   out.stat.assign(prog.size(), FStatic{});
+  out.add_site.assign(prog.size(), 0);
+  for (size_t i = 0; i < prog.size(); i++) out.add_site[i] = is_counter_add(prog[i]) ? 1 : 0;
   out.specialized = 0;
   out.needs_comb = true;
   out.needs_ctx = xdp;
@@ -906,19 +1056,35 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
   // a linked tail-call image has entries the pointer kinds do not start from:
   // generic handlers, and adds without fetch in the C++ tier, which sums a
   // wave's adds to one address (the combining table needs the kinds)
+  auto make_direct = [&](size_t i) {
+    out.fast[i].hoff = 4 + 4 * direct_add_handler(prog[i]);
+    out.fast[i].w1 |= FW_NODEFER;
+  };
   if (lo.multi_entry) {
     for (size_t i = 0; i < prog.size(); i++)
-      if (prog[i].op == X_ATOMIC && prog[i].hi == 0x00) out.fast[i].hoff = 4 + 4 * F_SLOW;
+      if (out.add_site[i]) make_direct(i);
+    out.needs_comb = false;
     return;
   }
-  if (!pointer_kinds(prog, lo.lddw_src, xdp, pkt_ok, in)) return;  // ctx rewritten: generic handlers only
+  if (!pointer_kinds(prog, lo.lddw_src, xdp, pkt_ok, in)) {
+    // ctx rewritten: generic handlers only, no pointer kinds to prove a
+    // counter unobserved
+    for (size_t i = 0; i < prog.size(); i++)
+      if (out.add_site[i]) make_direct(i);
+    out.needs_comb = false;
+    return;
+  }
+  const std::vector<bool> nodefer = counter_nodefer(prog, in);
+  for (size_t i = 0; i < prog.size(); i++)
+    if (out.add_site[i] && (nodefer[i] || (prog[i].aux & A_FETCH))) make_direct(i);
   // per-lane counter adds (fused counters, atomic adds without fetch) whose
   // target is not a wave-uniform constant use the LDS combining table
   bool comb = false;
   for (size_t i = 0; i < prog.size(); i++) {
     const DInsn &d = prog[i];
-    const bool add = d.op == X_RMW_ADD || (d.op == X_ATOMIC && d.hi == 0x00);
-    if (add && in[i][d.dst].kind != P_CONST && in[i][d.dst].kind != P_UNDEF) comb = true;
+    if (out.add_site[i] && !(out.fast[i].w1 & FW_NODEFER) && in[i][d.dst].kind != P_CONST &&
+        in[i][d.dst].kind != P_UNDEF)
+      comb = true;
   }
   out.needs_comb = comb;
   uint32_t nspec = 0;
@@ -976,6 +1142,7 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
     }
     if (d.op == X_RMW_ADD || (d.op == X_ATOMIC && d.hi == 0x00)) {
       if (sz != 4 && sz != 8) continue;
+      if (f.w1 & FW_NODEFER) continue;  // direct handler chosen above
       const PVal b = st[d.dst];
       const int64_t at = (int64_t)b.k + d.off;
       const MapRec *m = b.kind == P_MAPVAL ? map_rec(b.id) : nullptr;
@@ -1053,8 +1220,15 @@ uint32_t stage_need(const FastForm &f, uint32_t head) {
   return (uint32_t)((ext + 15) & ~15);
 }
 
-void link_fast(const FastForm &f, uint32_t head, uint32_t stage, std::vector<FInsn> &out) {
+void link_fast(const FastForm &f, uint32_t head, uint32_t stage, bool ordered, const std::vector<DInsn> &prog,
+               std::vector<FInsn> &out) {
   out = f.fast;
+  if (ordered)  // the reference's sequential order: every counter add reaches memory at once
+    for (size_t i = 0; i < out.size(); i++)
+      if (i < f.add_site.size() && f.add_site[i]) {
+        out[i].hoff = 4 + 4 * direct_add_handler(prog[i]);
+        out[i].w1 |= FW_NODEFER;
+      }
   if (!stage) return;
   for (size_t i = 0; i < f.stat.size(); i++) {
     const FStatic &s = f.stat[i];

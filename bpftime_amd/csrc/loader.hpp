@@ -45,6 +45,7 @@ struct FastForm {
   uint32_t specialized = 0;    // accesses / calls with statically typed bases
   bool needs_comb = true;      // per-lane counter adds (LDS combining table)
   bool needs_ctx = true;       // XDP: the ctx must exist in LDS
+  std::vector<uint8_t> add_site;  // per insn: a counter add (fused RMW, atomic add without fetch)
 };
 
 struct LoadOut {
@@ -76,7 +77,9 @@ uint32_t stage_need(const FastForm &f, uint32_t head);
 // Final FInsn array for one launch configuration: static accesses inside a
 // `stage`-byte window get the staged handlers (dword index, shift, masks
 // precomputed), the rest keep their generic templates.
-void link_fast(const FastForm &f, uint32_t head, uint32_t stage, std::vector<FInsn> &out);
+// `ordered`: every counter add gets its direct (FW_NODEFER) handler.
+void link_fast(const FastForm &f, uint32_t head, uint32_t stage, bool ordered, const std::vector<DInsn> &prog,
+               std::vector<FInsn> &out);
 
 // Runs the compat_ubpf.cpp:61-200 patching (call remap check, lddw pseudo
 // sources), ubpf-style validation, pre-decoding and the dataflow analyses

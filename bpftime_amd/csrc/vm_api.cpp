@@ -256,13 +256,13 @@ class Mi355xVm {
   }
 
   // the FInsn array for (entry form, staged bytes, head), linked on first use
-  const FInsn *linked(bool xdp, uint32_t head, uint32_t stage) {
+  const FInsn *linked(bool xdp, uint32_t head, uint32_t stage, bool ordered) {
     std::lock_guard<std::mutex> g(link_mu);
-    const uint64_t key = ((uint64_t)xdp << 63) | ((uint64_t)stage << 40) | (stage ? head : 0);
+    const uint64_t key = ((uint64_t)xdp << 63) | ((uint64_t)ordered << 62) | ((uint64_t)stage << 40) | (stage ? head : 0);
     auto it = links.find(key);
     if (it != links.end()) return it->second;
     std::vector<FInsn> out;
-    link_fast(xdp ? fx : fr, head, stage, out);
+    link_fast(xdp ? fx : fr, head, stage, ordered, prog.prog, out);
     FInsn *d = nullptr;
     const size_t bytes = out.size() * sizeof(FInsn);
     if (hipMalloc((void **)&d, bytes) != hipSuccess) return nullptr;
@@ -313,7 +313,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     const bool aligned = ((uint64_t)(uintptr_t)b->data % 16) == 0 &&
                          (b->descs ? true : (b->stride % 16) == 0 && b->stride >= need);
     p.stage = (need && aligned && !getenv("BPFTIME_AMD_NO_STAGING")) ? need : 0;
-    p.fast = linked(xdp, head, p.stage);
+    p.fast = linked(xdp, head, p.stage, (b->flags & EBPF_BATCH_ORDERED) != 0);
     if (!p.fast) {
       error = "device upload failed";
       return -1;
@@ -343,7 +343,8 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   p.step_limit = step_limit;
   p.fixed_len = b->fixed_len;
   p.stack_size = prog.stack_size;
-  p.comb_entries = prog.comb_entries;
+  // ORDERED: every counter add goes straight to memory (link_fast), no table
+  p.comb_entries = (b->flags & EBPF_BATCH_ORDERED) ? 0 : prog.comb_entries;
   if (p.comb_entries) {
     // the largest combining table (256 .. kCombMax entries) that keeps two
     // blocks (8 waves) resident per CU: a counter that finds no entry is a
@@ -652,6 +653,17 @@ int bpftime_amd_vm_info(const struct ebpf_vm *vm, uint32_t *stack_size, int *big
 int bpftime_amd_vm_fast_info(const struct ebpf_vm *vm, uint32_t ctx_kind, uint32_t *specialized) {
   if (!vm || !vm->impl->loaded) return -1;
   if (specialized) *specialized = ctx_kind == CTX_XDP ? vm->impl->fx.specialized : vm->impl->fr.specialized;
+  return 0;
+}
+
+int bpftime_amd_vm_counter_info(const struct ebpf_vm *vm, uint32_t ctx_kind, uint32_t *deferred, uint32_t *direct) {
+  if (!vm || !vm->impl->loaded) return -1;
+  const FastForm &f = ctx_kind == CTX_XDP ? vm->impl->fx : vm->impl->fr;
+  uint32_t nd = 0, nn = 0;
+  for (size_t i = 0; i < f.add_site.size(); i++)
+    if (f.add_site[i]) ((f.fast[i].w1 & FW_NODEFER) ? nn : nd)++;
+  if (deferred) *deferred = nd;
+  if (direct) *direct = nn;
   return 0;
 }
 

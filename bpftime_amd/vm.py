@@ -249,6 +249,13 @@ class VM:
             raise EbpfError("vm_fast_info failed")
         return n.value
 
+    def counter_info(self, kind: int) -> tuple:
+        """(deferred, direct) counter-add sites for the entry form of `kind`."""
+        d, n = C.c_uint32(), C.c_uint32()
+        if lib().bpftime_amd_vm_counter_info(C.c_void_p(self.h), kind, C.byref(d), C.byref(n)):
+            raise EbpfError("vm_counter_info failed")
+        return d.value, n.value
+
     def set_step_limit(self, n: int) -> None:
         lib().bpftime_amd_set_step_limit(C.c_void_p(self.h), n)
 

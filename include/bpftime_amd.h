@@ -115,6 +115,10 @@ void bpftime_amd_set_step_limit(struct ebpf_vm *vm, uint64_t limit);
 /* loads/stores (and array-lookup keys) the loader typed statically for the
  * fast path under the given ctx kind (packet, slot, ctx or stack bases) */
 int bpftime_amd_vm_fast_info(const struct ebpf_vm *vm, uint32_t ctx_kind, uint32_t *specialized);
+/* Counter adds of the loaded program for one entry form: `deferred` may be
+ * summed per wave / block before they reach memory (nothing the unit runs
+ * afterwards can observe them), `direct` reach memory at once. */
+int bpftime_amd_vm_counter_info(const struct ebpf_vm *vm, uint32_t ctx_kind, uint32_t *deferred, uint32_t *direct);
 
 /* ---- handler JSON (csrc/shm_json.cpp) ----
  * The reference's shm export / import format (runtime/include/bpftime_shm.hpp:
