@@ -185,7 +185,22 @@ struct KParams {
   const int32_t *tail_entry;  // prog fd -> entry pc in the linked image, -1 = not linked (nullable)
   uint8_t *frames;        // tail-call frames: [kTailDepth][frame_words][kTailGrid * kBlock lanes] u64
   uint32_t frame_words;   // header + ctx + the image's stack bytes, / 8
+  uint64_t *flush_log;    // block-end counter deltas: [grid][log_words] (k_comb_merge adds them), or nullptr
+  uint32_t log_words;     // u64 words per block: count, then {tag, delta} pairs
+  uint32_t dbg;           // BPFTIME_AMD_DBG experiment bits (0 in production)
 };
+
+// Block-end counter deltas.  Every block holds its counter deltas (the wave
+// caches of uniform counters, the LDS combining table) until it ends; with a
+// flush log it appends them to its own log region instead of adding them to
+// memory, and k_comb_merge (a second launch on the same stream) merges
+// kMergeGroup blocks' logs in an LDS table before adding: the same addresses
+// are hot in every block, and same-address device atomics serialize at the
+// memory side (a map of a few hundred values sits in a handful of channels).
+constexpr uint32_t kWaveCacheEntries = (kBlock / 64) * 2;
+constexpr uint32_t kMergeGroup = 16;
+constexpr uint32_t kMergeEntries = 4096;  // merge table entries (64 KiB of LDS)
+inline uint32_t log_words_for(uint32_t comb_entries) { return 1 + 2 * (kWaveCacheEntries + comb_entries); }
 
 // Error codes recorded per unit (err_count counts units with any error)
 constexpr uint32_t E_OK = 0;

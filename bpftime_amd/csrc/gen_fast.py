@@ -257,46 +257,85 @@ class Gen:
 
     def comb_add(self, sz, direct_only=False):
         """Per-lane add of Y (v46, v[46:47] for 8 B) at the global address Z
-        through the workgroup's LDS combining table (interp.hip: %[combn]
-        entries of {tag = address | size bit, delta}, flushed by the block at
-        its end): Zipf-hot counters cost an LDS add instead of a same-address
-        device atomic per lane (those serialize at the memory side).  Entry =
-        a multiplicative hash of the address, then the other seven entries of
-        its 128-B group; lanes finding all eight taken by other addresses,
-        and misaligned addresses, add to memory directly.  direct_only: every
-        lane adds to memory now (FW_NODEFER counters)."""
+        through the workgroup's LDS combining table (interp.hip: %[combn] u32
+        tags, then %[combn] u64 deltas, flushed when the block ends): Zipf-hot
+        counters cost an LDS add instead of a same-address device atomic per
+        lane (those serialize at the memory side, ~12 ns each).  A tag is the
+        counter's offset in the map arena | 2 | (4-byte ? 1 : 0).  The table
+        is 8-way set associative: a lane reads the eight tags of its set (two
+        ds_read_b128, one wait), adds to the way holding its counter (a tag
+        never changes once set: no atomic claim), else claims an empty way
+        with a compare-and-swap (a lane that loses the race to another
+        counter re-reads its set once), else adds to memory directly; so do
+        misaligned lanes and counters outside the arena.  Lanes sharing a
+        counter are serialized by the LDS itself.  direct_only: every lane
+        adds to memory now (FW_NODEFER counters)."""
+        glob_add = ("global_atomic_add_x2 v[48:49], v[46:47], off" if sz == 8
+                    else "global_atomic_add v[48:49], v46, off")
         if direct_only:
-            self.e("global_atomic_add_x2 v[48:49], v[46:47], off" if sz == 8 else "global_atomic_add v[48:49], v46, off")
+            self.e(glob_add)
             return
-        done, direct = self.label("cd"), self.label("cx")
+        done, direct, retry = self.label("cd"), self.label("cx"), self.label("cr")
+        nohit, noclaim = self.label("cnh"), self.label("cnc")
         self.e("s_mov_b64 s[60:61], exec", "s_mov_b64 s[54:55], 0",
                "s_cmp_eq_u32 %[combn], 0", f"s_cbranch_scc1 {direct}",
                f"v_and_b32 v41, {sz - 1}, v48", "v_cmp_eq_u32 vcc, 0, v41",            # aligned lanes
                "s_and_b64 exec, exec, vcc", f"s_cbranch_execz {direct}",
-               "v_mov_b32 v54, v48", "v_mov_b32 v55, v49")
+               "s_mov_b64 s[72:73], %[alo]",
+               "v_mov_b32 v55, s73",
+               "v_subrev_co_u32 v54, vcc, s72, v48", "v_subb_co_u32 v55, vcc, v49, v55, vcc",
+               "v_cmp_eq_u32 vcc, 0, v55",                                       # inside the arena's 4 GiB
+               "s_and_b64 exec, exec, vcc", f"s_cbranch_execz {direct}",
+               f"v_or_b32 v54, {3 if sz == 4 else 2}, v54")
         if sz == 4:
-            self.e("v_or_b32 v54, 1, v54", "v_mov_b32 v47, 0")
+            self.e("v_mov_b32 v47, 0")
         self.e("v_lshrrev_b32 v41, 3, v48", "s_mov_b32 s69, 0x9e3779b1", "v_mul_lo_u32 v41, v41, s69",
                "s_ff1_i32_b32 s69, %[combn]", "s_sub_u32 s69, 32, s69",          # 32 - log2(entries)
-               "v_lshrrev_b32 v41, s69, v41", "v_lshlrev_b32 v57, 4, v41", "v_add_u32 v41, %[comb], v57",
-               "v_mov_b32 v42, 0", "v_mov_b32 v43, 0")
-        for attempt in range(8):
-            if attempt:                                       # entries e^1 .. e^7 (one 128-B group)
-                self.e(f"v_xor_b32 v57, {16 * (attempt ^ (attempt - 1))}, v57", "v_add_u32 v41, %[comb], v57")
-            self.e("ds_cmpst_rtn_b64 v[50:51], v41, v[42:43], v[54:55]",      # claim if empty
-                   "s_waitcnt lgkmcnt(0)",
-                   "v_cmp_eq_u64 s[56:57], 0, v[50:51]",
-                   "v_cmp_eq_u64 vcc, v[54:55], v[50:51]",
-                   "s_or_b64 s[56:57], s[56:57], vcc",                        # entry is ours
-                   "s_or_b64 s[54:55], s[54:55], s[56:57]",
-                   "s_mov_b64 s[62:63], exec",
-                   "s_and_b64 exec, exec, s[56:57]")
-            skip = self.label("cs")
-            self.e(f"s_cbranch_execz {skip}", "ds_add_u64 v41, v[46:47] offset:8", f"{skip}:",
-                   "s_andn2_b64 exec, s[62:63], s[56:57]", f"s_cbranch_execz {direct}")
+               "v_lshrrev_b32 v41, s69, v41", "v_and_b32 v41, -8, v41",          # first way of the set
+               "v_lshlrev_b32 v55, 3, v41", "v_lshlrev_b32 v41, 2, v41",
+               "v_add_u32 v41, %[comb], v41",                                   # the set's tags
+               "s_lshl_b32 s70, %[combn], 2", "s_add_u32 s70, s70, %[comb]",
+               "v_add_u32 v55, s70, v55",                                       # ... and its deltas
+               "s_mov_b32 s85, 0",
+               f"{retry}:",
+               "s_mov_b64 s[62:63], exec",                                       # lanes of this pass
+               "ds_read_b128 v[56:59], v41", "ds_read_b128 v[42:45], v41 offset:16",
+               "s_waitcnt lgkmcnt(0)",
+               "v_mov_b32 v50, -1", "v_mov_b32 v51, 0")
+        tags = ["v56", "v57", "v58", "v59", "v42", "v43", "v44", "v45"]
+        for k in range(7, -1, -1):                                               # first empty way
+            self.e(f"v_cmp_eq_u32 vcc, 0, {tags[k]}", f"v_cndmask_b32_e64 v50, v50, {k}, vcc")
+        for k in range(7, -1, -1):                                               # the counter's way wins
+            self.e(f"v_cmp_eq_u32 vcc, v54, {tags[k]}", f"v_cndmask_b32_e64 v50, v50, {k}, vcc",
+                   "v_cndmask_b32_e64 v51, v51, 1, vcc")
+        self.e("v_lshlrev_b32 v56, 2, v50", "v_add_u32 v56, v41, v56",           # the way's tag
+               "v_lshlrev_b32 v57, 3, v50", "v_add_u32 v57, v55, v57",           # ... and its delta
+               "v_cmp_eq_u32 s[56:57], 1, v51", "s_and_b64 exec, s[62:63], s[56:57]",
+               f"s_cbranch_execz {nohit}",
+               "ds_add_u64 v57, v[46:47]",
+               f"{nohit}:",
+               "s_or_b64 s[54:55], s[54:55], exec",
+               "s_mov_b64 exec, s[62:63]",                                      # compares write only exec lanes
+               "v_cmp_ne_u32 s[56:57], -1, v50", "s_andn2_b64 s[56:57], s[56:57], s[54:55]",
+               "s_and_b64 exec, s[62:63], s[56:57]",                            # lanes claiming an empty way
+               f"s_cbranch_execz {noclaim}",
+               "v_mov_b32 v42, 0",
+               "ds_cmpst_rtn_b32 v50, v56, v42, v54",
+               "s_waitcnt lgkmcnt(0)",
+               "v_cmp_eq_u32 s[56:57], 0, v50", "v_cmp_eq_u32 vcc, v54, v50",
+               "s_or_b64 s[56:57], s[56:57], vcc",                              # claimed (or claimed for us)
+               "s_and_b64 s[64:65], exec, s[56:57]",
+               "s_andn2_b64 s[66:67], exec, s[56:57]",                           # lost to another counter
+               "s_mov_b64 exec, s[64:65]", f"s_cbranch_execz {noclaim}",
+               "ds_add_u64 v57, v[46:47]",
+               "s_or_b64 s[54:55], s[54:55], exec",
+               "s_cmp_eq_u64 s[66:67], 0", f"s_cbranch_scc1 {noclaim}",
+               "s_add_u32 s85, s85, 1", "s_cmp_gt_u32 s85, 1", f"s_cbranch_scc1 {noclaim}",
+               "s_mov_b64 exec, s[66:67]", f"s_branch {retry}",
+               f"{noclaim}:")
         self.e(f"{direct}:",
-               "s_andn2_b64 exec, s[60:61], s[54:55]", f"s_cbranch_execz {done}")
-        self.e("global_atomic_add_x2 v[48:49], v[46:47], off" if sz == 8 else "global_atomic_add v[48:49], v46, off",
+               "s_andn2_b64 exec, s[60:61], s[54:55]", f"s_cbranch_execz {done}",
+               glob_add,
                f"{done}:", "s_mov_b64 exec, s[60:61]")
 
     def comb_peel(self, sz, direct_only=False):
@@ -982,7 +1021,7 @@ class Gen:
         self.e(f"{lane}:")
         if not mv:
             self.check_global(sz)
-        self.comb_peel(sz)
+        self.comb_add(sz)
         self.e(f"{done}:", "s_mov_b32 s48, s46")           # continue after the stx
         self.dispatch()
 
@@ -1063,7 +1102,7 @@ class Gen:
             self.wr("s45", 46)
         elif op == "ADD":
             self.e("v_mov_b32 v46, v44", "v_mov_b32 v47, v45" if sz == 8 else "v_mov_b32 v47, 0")
-            self.comb_peel(sz)
+            self.comb_add(sz)
         else:
             self.e(f"global_atomic_{mn} v[48:49], {val}, off")
         self.next_seq()

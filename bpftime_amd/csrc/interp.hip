@@ -555,7 +555,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   SRP(err_count); SRV(n); SRV(stride); SRV(first_unit); SRV(data_lo); SRV(data_hi); SRV(arena_lo);
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
-  SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words);
+  SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(flush_log); SRV(log_words);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
 #undef SRP
 #undef SRV
@@ -566,10 +566,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   uint8_t *my_ctx = dyn + tid * CTXB;
   uint8_t *my_stack = dyn + kBlock * CTXB + tid * p.stack_size;
   // combining table for per-lane counter adds (gen_fast.py comb_add), after
-  // the ctx and stack areas: {tag = address | (4-byte ? 1 : 0), delta},
-  // flushed when the block ends; sized 0 for programs that never need it
-  uint64_t *comb = (uint64_t *)(dyn + kBlock * (CTXB + (BIGSTACK ? 0 : p.stack_size)));
-  for (uint32_t i = tid; i < 2 * p.comb_entries; i += kBlock) comb[i] = 0;
+  // the ctx and stack areas: comb_entries u32 tags {arena offset | 2 |
+  // (4-byte ? 1 : 0)} (8-way sets), then comb_entries u64 deltas, flushed
+  // when the block ends; sized 0 for programs that never need it
+  uint32_t *comb = (uint32_t *)(dyn + kBlock * (CTXB + (BIGSTACK ? 0 : p.stack_size)));
+  uint64_t *comb_d = (uint64_t *)(comb + p.comb_entries);
+  for (uint32_t i = tid; i < 3 * p.comb_entries; i += kBlock) comb[i] = 0;
+  // a table tag as a flush tag {address | (4-byte ? 1 : 0)}
+  auto comb_tag = [&](uint32_t t) -> uint64_t { return t ? (p.arena_lo + (t & ~3u)) | (t & 1u) : 0; };
   __syncthreads();
   uint64_t big_stack[BIGSTACK ? kStackSize / 8 : 1];
   const uint64_t stack_top = BIGSTACK ? (uint64_t)(uintptr_t)(big_stack + kStackSize / 8)
@@ -848,6 +852,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   // MI355X_MICROARCH.md 'fanin'), so one add per block instead of per wave
   // shortens the kernel's tail four-fold
   __shared__ uint64_t wdelta[kBlock / 64][2][2];  // {tag = address | (4-byte ? 1 : 0), delta}
+  __shared__ uint32_t nlog;
   if ((tid & 63) == 0) {
     const uint32_t w = tid >> 6;
     wdelta[w][0][0] = c.c0a && c.c0d ? (c.c0a | (c.c0s == 4 ? 1 : 0)) : 0;
@@ -855,10 +860,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     wdelta[w][1][0] = c.c1a && c.c1d ? (c.c1a | (c.c1s == 4 ? 1 : 0)) : 0;
     wdelta[w][1][1] = c.c1d;
   }
+  if (tid == 0) nlog = 0;
   __syncthreads();
+  uint64_t *e = &wdelta[0][0][0];
+  constexpr uint32_t NE = kWaveCacheEntries;
   if (tid == 0) {
-    uint64_t *e = &wdelta[0][0][0];
-    constexpr uint32_t NE = kBlock / 64 * 2;
     for (uint32_t i = 0; i < NE; i++) {
       if (!e[2 * i]) continue;
       for (uint32_t j = i + 1; j < NE; j++)
@@ -866,17 +872,115 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
           e[2 * i + 1] += e[2 * j + 1];
           e[2 * j] = 0;
         }
-      flush_delta_tag(e[2 * i], e[2 * i + 1]);
+      if (!p.flush_log) flush_delta_tag(e[2 * i], e[2 * i + 1]);
     }
   }
-  for (uint32_t e = tid; e < p.comb_entries; e += kBlock) flush_delta_tag(comb[2 * e], comb[2 * e + 1]);
+  if (!p.flush_log) {
+    if (!(p.dbg & 1))
+      for (uint32_t i = tid; i < p.comb_entries; i += kBlock) flush_delta_tag(comb_tag(comb[i]), comb_d[i]);
+    return;
+  }
+  // append the nonzero deltas (wave caches, then the table) to this block's
+  // log region; k_comb_merge adds them.  A block holding many addresses adds
+  // them itself: a map with that many hot values spans many memory channels,
+  // so its atomics do not queue on a few words, and merging would not fold them
+  __syncthreads();
+  uint64_t *reg = p.flush_log + (uint64_t)blockIdx.x * p.log_words;
+  const uint32_t total = NE + p.comb_entries;
+  auto entry = [&](uint32_t i, uint64_t &tag, uint64_t &delta) {
+    tag = delta = 0;
+    if (i < NE) {
+      tag = e[2 * i];
+      delta = e[2 * i + 1];
+    } else if (i < total) {
+      tag = comb_tag(comb[i - NE]);
+      delta = comb_d[i - NE];
+    }
+  };
+  for (uint32_t r0 = 0; r0 < total; r0 += kBlock) {
+    uint64_t tag, delta;
+    entry(r0 + tid, tag, delta);
+    const uint64_t m = __ballot(tag && delta);
+    if ((tid & 63) == 0 && m) atomicAdd(&nlog, (uint32_t)__builtin_popcountll(m));
+  }
+  __syncthreads();
+  const uint32_t used = nlog;
+  __syncthreads();
+  if (used > kMergeEntries / 8) {
+    for (uint32_t i = tid; i < total; i += kBlock) {
+      uint64_t tag, delta;
+      entry(i, tag, delta);
+      flush_delta_tag(tag, delta);
+    }
+    if (tid == 0) reg[0] = 0;
+    return;
+  }
+  if (tid == 0) nlog = 0;
+  __syncthreads();
+  for (uint32_t r0 = 0; r0 < total; r0 += kBlock) {
+    uint64_t tag, delta;
+    entry(r0 + tid, tag, delta);
+    const bool nz = tag && delta;
+    const uint64_t m = __ballot(nz);
+    uint32_t base = 0;
+    if ((tid & 63) == 0 && m) base = atomicAdd(&nlog, (uint32_t)__builtin_popcountll(m));
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (nz) {
+      const uint32_t k = base + (uint32_t)__builtin_popcountll(m & ((1ull << __lane_id()) - 1));
+      reg[1 + 2 * k] = tag;
+      reg[2 + 2 * k] = delta;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) reg[0] = nlog;
 }
+
+// Second level of the block-end flush (common.hpp kMergeGroup): block m
+// merges the logs of blocks [m * group, (m + 1) * group) in a 4-way LDS table
+// and adds each address's sum with one device atomic; an entry whose set is
+// full adds at once.
+__global__ __launch_bounds__(kBlock) void k_comb_merge(const uint64_t *log, uint32_t log_words, uint32_t nblocks,
+                                                       uint32_t group) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t mt[];  // tags[kMergeEntries], deltas[kMergeEntries]
+  constexpr uint32_t E = kMergeEntries;
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < 2 * E; i += kBlock) mt[i] = 0;
+  __syncthreads();
+  const uint32_t b0 = blockIdx.x * group, b1 = min(nblocks, b0 + group);
+  for (uint32_t b = b0; b < b1; b++) {
+    const uint64_t *reg = log + (uint64_t)b * log_words;
+    const uint32_t n = (uint32_t)reg[0];
+    for (uint32_t i = tid; i < n; i += kBlock) {
+      const uint64_t tag = reg[1 + 2 * i], d = reg[2 + 2 * i];
+      const uint32_t set = ((uint32_t)((tag >> 3) * 0x9E3779B1u) >> (32 - 10)) * 4;  // E / 4 = 2^10 sets
+      bool done = false;
+      for (uint32_t w = 0; w < 4 && !done; w++) {
+        uint64_t *t = &mt[set + w];
+        uint64_t cur = __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == 0) {
+          uint64_t z = 0;
+          __hip_atomic_compare_exchange_strong(t, &z, tag, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+          cur = z == 0 ? tag : z;
+        }
+        if (cur == tag) {
+          __hip_atomic_fetch_add(&mt[E + set + w], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          done = true;
+        }
+      }
+      if (!done) flush_delta_tag(tag, d);
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < E; i += kBlock) flush_delta_tag(mt[i], mt[E + i]);
+}
+static_assert(kMergeEntries == 4u << 10, "k_comb_merge hashes into 2^10 sets of 4");
 
 // ---------------------------------------------------------------------------
 // Host-side launch wrappers
 // ---------------------------------------------------------------------------
 static size_t dyn_lds_bytes(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries) {
-  return kBlock * ((kind == CTX_XDP ? 48 : 0) + (big_stack ? 0 : stack_size)) + 16 * (size_t)comb_entries;
+  return kBlock * ((kind == CTX_XDP ? 48 : 0) + (big_stack ? 0 : stack_size)) + 12 * (size_t)comb_entries;
 }
 
 extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind, bool big_stack, uint32_t grid,
@@ -894,6 +998,14 @@ extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind,
     if (big_stack) L(CTX_RAW, true); else L(CTX_RAW, false);
   }
 #undef L
+  return hipGetLastError();
+}
+
+extern "C" hipError_t bpftime_amd_launch_merge(const uint64_t *log, uint32_t log_words, uint32_t nblocks,
+                                                hipStream_t stream) {
+  const uint32_t grid = (nblocks + kMergeGroup - 1) / kMergeGroup;
+  hipLaunchKernelGGL(k_comb_merge, dim3(grid), dim3(kBlock), 2 * kMergeEntries * sizeof(uint64_t), stream, log,
+                     log_words, nblocks, kMergeGroup);
   return hipGetLastError();
 }
 

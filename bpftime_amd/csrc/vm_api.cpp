@@ -25,6 +25,8 @@ namespace bpftime_amd {
 extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind, bool big_stack, uint32_t grid,
                                                 uint32_t ordered, hipStream_t stream);
 extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds);
+extern "C" hipError_t bpftime_amd_launch_merge(const uint64_t *log, uint32_t log_words, uint32_t nblocks,
+                                                hipStream_t stream);
 
 struct HelperReg {
   std::string name;
@@ -72,6 +74,27 @@ class Mi355xVm {
   uint64_t image_gen = 0;
   int32_t *d_tail_entry = nullptr;
   std::mutex tail_mu;
+  // block-end flush logs (common.hpp kMergeGroup), one per stream: a batch's
+  // two launches use it in stream order, batches on other streams have their own
+  struct StreamBuf {
+    void *p = nullptr;
+    uint64_t bytes = 0;
+  };
+  std::mutex log_mu;
+  std::map<hipStream_t, StreamBuf> logs;
+  uint64_t *flush_log(hipStream_t s, uint64_t bytes) {
+    std::lock_guard<std::mutex> g(log_mu);
+    StreamBuf &b = logs[s];
+    if (b.bytes < bytes) {
+      // the stream may still run a batch that uses the old buffer
+      if (b.p && (hipStreamSynchronize(s) != hipSuccess || hipFree(b.p) != hipSuccess)) return nullptr;
+      b.p = nullptr;
+      b.bytes = 0;
+      if (hipMalloc(&b.p, bytes) != hipSuccess) return nullptr;
+      b.bytes = bytes;
+    }
+    return (uint64_t *)b.p;
+  }
 
   Mi355xVm() {
     // bpftime_prog.cpp:126-127 defaults, pointed at the device registry
@@ -85,6 +108,8 @@ class Mi355xVm {
     if (d_err) hipFree(d_err);
     if (d_stage) hipFree(d_stage);
     if (d_tail_entry) hipFree(d_tail_entry);
+    for (auto &kv : logs)
+      if (kv.second.p) hipFree(kv.second.p);
   }
   void unload() {
     if (d_prog) hipFree(d_prog);
@@ -356,7 +381,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     auto it = best.find(key);
     if (it == best.end()) {
       auto dyn = [&](uint32_t e) {
-        return kBlock * ((b->ctx_kind == CTX_XDP ? 48 : 0) + (prog.big_stack ? 0 : prog.stack_size)) + 16 * (size_t)e;
+        return kBlock * ((b->ctx_kind == CTX_XDP ? 48 : 0) + (prog.big_stack ? 0 : prog.stack_size)) + 12 * (size_t)e;
       };
       const int base = std::min(2, bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn(kComb)));
       uint32_t e = kComb;
@@ -371,6 +396,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   p.rxq = b->rx_queue_index;
   p.head = b->head;
   p.checked = (b->flags & EBPF_BATCH_UNCHECKED) ? 0 : 1;
+  if (const char *d = getenv("BPFTIME_AMD_DBG")) p.dbg = (uint32_t)strtoul(d, nullptr, 0);
   if (hipMemsetAsync(err, 0, 4, s) != hipSuccess) {
     error = "hipMemsetAsync failed";
     return -1;
@@ -391,7 +417,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       cus = prop.multiProcessorCount;
     }
     const size_t dyn = kBlock * ((b->ctx_kind == CTX_XDP ? 48 : 0) + (prog.big_stack ? 0 : prog.stack_size)) +
-                       16 * (size_t)prog.comb_entries;
+                       12 * (size_t)prog.comb_entries;
     int occ = bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn);
     if (occ < 1) occ = 1;
     uint64_t want = (b->count + kBlock - 1) / kBlock;
@@ -407,7 +433,18 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     grid = (uint32_t)(want < cap ? want : cap);
     if (has_tail && grid > kTailGrid) grid = kTailGrid;  // one frame stack per lane of the grid
   }
+  // a block-end flush log when the blocks hold per-lane counter tables:
+  // merged by a second launch instead of every block adding its table
+  if (p.comb_entries && grid > kMergeGroup && !getenv("BPFTIME_AMD_NO_MERGE")) {
+    p.log_words = log_words_for(p.comb_entries);
+    p.flush_log = flush_log(s, (uint64_t)grid * p.log_words * 8);
+    if (!p.flush_log) {
+      error = "flush log allocation failed";
+      return -1;
+    }
+  }
   hipError_t e = bpftime_amd_launch_interp(&p, b->ctx_kind, prog.big_stack, grid, ordered ? 1 : 0, s);
+  if (e == hipSuccess && p.flush_log) e = bpftime_amd_launch_merge(p.flush_log, p.log_words, grid, s);
   if (e != hipSuccess) {
     error = std::string("kernel launch failed: ") + hipGetErrorString(e);
     return -1;

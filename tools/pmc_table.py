@@ -1,0 +1,70 @@
+"""Per-launch PMC means of the interpreter kernel for one tools/prof_workload.sh
+run, as a table and as JSON (the `traffic` figure bench_workloads.py reads).
+
+    python tools/pmc_table.py gpurun_out/prof_<tag>_<workload> <units per launch> [out.json]
+
+FETCH_SIZE / WRITE_SIZE are kilobytes; FETCH_SIZE is doubled (gfx950 reports
+half the bytes of wide reads, MI355X_MICROARCH.md HBM section).
+"""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+from collections import defaultdict
+
+HOT = "k_interp"
+
+
+def means(d):
+    per = defaultdict(lambda: defaultdict(float))
+    big = 0
+    rows = []
+    for f in glob.glob(os.path.join(d, "*_counter_collection.csv")):
+        with open(f) as fh:
+            rows += [(r, os.path.basename(f)) for r in csv.DictReader(fh) if HOT in r["Kernel_Name"]]
+    for r, _ in rows:
+        big = max(big, int(r["Grid_Size"]))
+    for r, f in rows:
+        if int(r["Grid_Size"]) == big:
+            per[r["Counter_Name"]][(r["Dispatch_Id"], f)] += float(r["Counter_Value"])
+    return {c: statistics.mean(v.values()) for c, v in per.items()}
+
+
+def kernel_ms(d):
+    f = os.path.join(d, "kt_kernel_stats.csv")
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        for r in csv.DictReader(fh):
+            if HOT in r["Name"]:
+                return float(r["AverageNs"]) / 1e6, int(r["Calls"])
+    return None
+
+
+def main():
+    d, units = sys.argv[1], int(sys.argv[2])
+    cs = means(d)
+    km = kernel_ms(d)
+    out = {"dir": d, "units": units, "kernel_avg_ms": km[0] if km else None, "calls": km[1] if km else None,
+           "counters": cs}
+    w = cs.get("SQ_WAVES")
+    print(f"kernel avg ms: {km}")
+    for c in sorted(cs):
+        extra = f"  per-wave {cs[c] / w:10.1f}" if w and c.startswith("SQ_") and c != "SQ_WAVES" else ""
+        print(f"{c:36s} {cs[c]:16.1f}{extra}")
+    if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+        fb, wb = cs["FETCH_SIZE"] * 2048, cs["WRITE_SIZE"] * 1024
+        out["hbm_bytes_per_launch"] = fb + wb
+        out["bytes_per_unit"] = (fb + wb) / units
+        print(f"HBM bytes/launch {fb + wb:.4g} (fetch x2 {fb:.4g}, write {wb:.4g}), per unit {(fb + wb) / units:.1f}")
+        if km:
+            print(f"HBM GB/s {(fb + wb) / km[0] / 1e6:.1f}")
+    if len(sys.argv) > 3:
+        with open(sys.argv[3], "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,34 @@
+#!/bin/bash
+# rocprofv3 passes for one bench workload: kernel-trace stats, then separate
+# PMC passes (MI355X_MICROARCH.md §rocprofv3: one block budget per pass).
+#   tools/prof_workload.sh <workload> <tag> [extra bench args]
+set -u
+W=${1:-flow-hash}
+TAG=${2:-r02}
+shift 2 || true
+EXTRA="$*"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+D=gpurun_out/prof_${TAG}_${W}
+ARGS="--workload $W --steps 3 --warmup 1 --no-cpu-baseline $EXTRA"
+run() {  # name, counters...
+  local name=$1; shift
+  if [ "$name" = kt ]; then
+    timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o kt -- python3 bench.py $ARGS > $D.kt.log 2>&1
+  else
+    timeout -s KILL 240 rocprofv3 --pmc "$@" --output-format csv -d $D -o $name -- python3 bench.py $ARGS > $D.$name.log 2>&1
+  fi
+  local rc=$?
+  echo "$name rc=$rc"
+  return $rc
+}
+mkdir -p $D
+run kt || exit $?
+run sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY || exit $?
+run sq2 SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_WAVES || exit $?
+run fetch FETCH_SIZE || exit $?
+run write WRITE_SIZE || exit $?
+run tcp TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum || true
+U=${UNITS:-16777216}
+python3 tools/pmc_table.py $D $U $D.pmc.json > $D.summary.txt 2>&1 || true
+cat $D.summary.txt
