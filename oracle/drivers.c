@@ -31,7 +31,7 @@ static inline uint64_t exec_or_zero(struct orc_vm *vm, void *mem, size_t len)
 
 int orc_run_xdp(struct orc_vm *vm, uint8_t *base, uint64_t n, uint64_t stride, const uint32_t *lens,
 		uint32_t fixed_len, uint32_t *verdicts, int32_t *out_data_off, uint32_t *out_len,
-		uint32_t ifindex, uint32_t rxq)
+		uint32_t ifindex, uint32_t rxq, uint32_t head)
 {
 	for (uint64_t i = 0; i < n; i++) {
 		uint8_t *slot = base + i * stride;
@@ -44,8 +44,8 @@ int orc_run_xdp(struct orc_vm *vm, uint8_t *base, uint64_t n, uint64_t stride, c
 		} u;
 		memset(&u, 0, sizeof(u));
 		struct xdp_md_userspace ctx = {
-			.data = (uintptr_t)slot,
-			.data_end = (uintptr_t)slot + len,
+			.data = (uintptr_t)slot + head,
+			.data_end = (uintptr_t)slot + head + len,
 			.data_meta = 0,
 			.ingress_ifindex = ifindex,
 			.rx_queue_index = rxq,
@@ -122,7 +122,7 @@ double orc_time_xdp(struct orc_vm *vm, uint8_t *base, uint64_t n, uint64_t strid
 	}
 	struct timespec t0, t1;
 	clock_gettime(CLOCK_MONOTONIC, &t0);
-	orc_run_xdp(vm, base, n, stride, NULL, fixed_len, verdicts, NULL, NULL, 0, 0);
+	orc_run_xdp(vm, base, n, stride, NULL, fixed_len, verdicts, NULL, NULL, 0, 0, 0);
 	clock_gettime(CLOCK_MONOTONIC, &t1);
 	if (pinned)
 		sched_setaffinity(0, sizeof(old), &old);

@@ -120,6 +120,24 @@ static uint64_t h_adjust_tail(uint64_t ctx, uint64_t delta_, uint64_t a, uint64_
 	return 0;
 }
 
+/* bpf_helper.cpp:778-788 (no fragmented packets) */
+static uint64_t h_xdp_load_bytes(uint64_t ctx, uint64_t off_, uint64_t buf, uint64_t len_, uint64_t c)
+{
+	(void)c;
+	struct xdp_md_userspace *x = (struct xdp_md_userspace *)(uintptr_t)ctx;
+	uint32_t offset = (uint32_t)off_, len = (uint32_t)len_;
+	uint64_t data = x->data + offset;
+	if (data + len > x->data_end)
+		return (uint64_t)(int64_t)-EINVAL;
+	memcpy((void *)(uintptr_t)buf, (const void *)(uintptr_t)data, len);
+	return 0;
+}
+
+int orc_vm_register_xdp_load_bytes(struct orc_vm *vm)
+{
+	return orc_vm_register(vm, 189, "bpf_xdp_load_bytes", h_xdp_load_bytes);
+}
+
 /* bpf_helper.cpp:451-504 (map "pointer" = fd; flags other than 0 only warn) */
 static uint64_t h_rb_output(uint64_t rb, uint64_t data, uint64_t size, uint64_t flags, uint64_t c)
 {

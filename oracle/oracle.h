@@ -42,6 +42,9 @@ void orc_vm_destroy(struct orc_vm *vm);
 int orc_vm_register(struct orc_vm *vm, unsigned index, const char *name, orc_helper_fn fn);
 /* registers bpftime helper ids 1,2,3,5,7,8,28,44,65 (bpf_helper.cpp:1177-1401) */
 int orc_vm_register_default_helpers(struct orc_vm *vm);
+/* bpf_xdp_load_bytes (id 189): defined in bpf_helper.cpp:778-788 but not in
+ * any default helper group; an embedder registers it explicitly. */
+int orc_vm_register_xdp_load_bytes(struct orc_vm *vm);
 void orc_vm_set_unwind_index(struct orc_vm *vm, int idx);
 /* ebpf_load: 0 / <0, errbuf receives the message (compat_ubpf.cpp:61-200) */
 int orc_vm_load(struct orc_vm *vm, const void *code, uint32_t code_len, char *errbuf, size_t errlen);
@@ -97,10 +100,12 @@ uint64_t orc_hash_bytes(const void *key, uint64_t n);
  * with data = base + i*stride, data_end = data + len, buffer_[start,end) =
  * the slot; verdicts[i] = (u32) r0 (0 on exec error, bpftime_prog.cpp:237-257).
  * lens == NULL -> fixed_len for every packet. out_data_off / out_len (nullable)
- * receive data-slot and data_end-data after the program (adjust_head/tail). */
+ * receive data-slot and data_end-data after the program (adjust_head/tail).
+ * head: data starts `head` bytes into the slot (headroom for adjust_head). */
 int orc_run_xdp(struct orc_vm *vm, uint8_t *base, uint64_t n, uint64_t stride,
                 const uint32_t *lens, uint32_t fixed_len, uint32_t *verdicts,
-                int32_t *out_data_off, uint32_t *out_len, uint32_t ifindex, uint32_t rxq);
+                int32_t *out_data_off, uint32_t *out_len, uint32_t ifindex, uint32_t rxq,
+                uint32_t head);
 /* raw: r1 = base + i*stride, r2 = len; rets[i] = r0 */
 int orc_run_raw(struct orc_vm *vm, uint8_t *base, uint64_t n, uint64_t stride, uint32_t len,
                 uint64_t *rets);

@@ -63,7 +63,8 @@ def lib():
             "orc_map_val": (u64, [u64]),
             "orc_next_prime": (u64, [u64]),
             "orc_hash_bytes": (u64, [vp, u64]),
-            "orc_run_xdp": (C.c_int, [vp, vp, u64, u64, vp, u32, vp, vp, vp, u32, u32]),
+            "orc_run_xdp": (C.c_int, [vp, vp, u64, u64, vp, u32, vp, vp, vp, u32, u32, u32]),
+            "orc_vm_register_xdp_load_bytes": (C.c_int, [vp]),
             "orc_run_raw": (C.c_int, [vp, vp, u64, u64, u32, vp]),
             "orc_run_syscall": (C.c_int, [vp, vp, u64, vp, vp]),
             "orc_time_xdp": (C.c_double, [vp, vp, u64, u64, u32, vp, C.c_int]),
@@ -102,8 +103,12 @@ class OracleVM:
         rc = lib().orc_vm_exec(self.h, buf, len(mem), C.byref(r))
         return rc, r.value
 
+    def register_xdp_load_bytes(self) -> None:
+        """bpf_xdp_load_bytes (id 189), defined but not in a default group."""
+        lib().orc_vm_register_xdp_load_bytes(self.h)
+
     def run_xdp(self, slots: np.ndarray, lens: Optional[np.ndarray] = None, fixed_len: int = 0,
-                want_meta: bool = False, ifindex: int = 0, rxq: int = 0, ncpu: int = 0):
+                want_meta: bool = False, ifindex: int = 0, rxq: int = 0, ncpu: int = 0, head: int = 0):
         """slots: (n, stride) uint8, modified in place; returns verdicts (and meta).
         With ncpu > 0 the virtual CPU of unit i is (i // 64) % ncpu, like the
         device's helper 8 / per-CPU slot assignment."""
@@ -119,10 +124,10 @@ class OracleVM:
                 lib().orc_run_xdp(self.h, slots[w0:].ctypes.data, m, stride,
                                   None if lens is None else lens[w0:].ctypes.data, fixed_len,
                                   v[w0:].ctypes.data, None if off is None else off[w0:].ctypes.data,
-                                  None if ln is None else ln[w0:].ctypes.data, ifindex, rxq)
+                                  None if ln is None else ln[w0:].ctypes.data, ifindex, rxq, head)
         else:
             lib().orc_run_xdp(self.h, slots.ctypes.data, n, stride, _p(lens), fixed_len, v.ctypes.data,
-                              _p(off), _p(ln), ifindex, rxq)
+                              _p(off), _p(ln), ifindex, rxq, head)
         return (v, off, ln) if want_meta else v
 
     def run_raw(self, units: np.ndarray, length: int) -> np.ndarray:
