@@ -183,10 +183,11 @@ struct KParams {
   uint64_t umem_bytes;    // descriptor mode: bytes at data
   int64_t sys_nr;         // CTX_SYSCALL: run only records with this id (-1: every record)
   const int32_t *tail_entry;  // prog fd -> entry pc in the linked image, -1 = not linked (nullable)
-  uint8_t *frames;        // tail-call frames: [kTailDepth][frame_words][kTailGrid * kBlock lanes] u64
+  uint8_t *frames;        // tail-call frames: [kTailDepth][frame_words][grid * kBlock lanes] u64 (per stream)
   uint32_t frame_words;   // header + ctx + the image's stack bytes, / 8
   uint64_t *flush_log;    // block-end counter deltas: [grid][log_words] (k_comb_merge adds them), or nullptr
   uint32_t log_words;     // u64 words per block: count, then {tag, delta} pairs
+  uint64_t *lane_scratch; // a u64 per lane of the grid (PROG_ARRAY lookups hand out a copy there), or nullptr
   uint32_t dbg;           // BPFTIME_AMD_DBG experiment bits (0 in production)
 };
 

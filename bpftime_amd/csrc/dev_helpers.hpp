@@ -44,14 +44,18 @@ __device__ __forceinline__ void mem_store(uint64_t a, uint32_t sz, uint64_t v) {
   }
 }
 
+// Global windows a program may access: the batch, the map arena, and the
+// lanes' scratch words (PROG_ARRAY lookup copies; C++ tier only -- the asm
+// window check leaves those accesses to it).
 struct Win {
-  uint64_t lo1, hi1, lo2, hi2;
+  uint64_t lo1, hi1, lo2, hi2, lo3, hi3;
   bool checked;
   __device__ __forceinline__ bool ok(uint64_t a, uint32_t sz) const {
     if (!checked) return true;
     if (is_lds_addr(a) || is_scratch_addr(a)) return true;
     uint64_t e = a + sz;
-    return (a >= lo1 && e <= hi1 && e >= a) || (a >= lo2 && e <= hi2 && e >= a);
+    return (a >= lo1 && e <= hi1 && e >= a) || (a >= lo2 && e <= hi2 && e >= a) ||
+           (a >= lo3 && e <= hi3 && e >= a);
   }
 };
 
@@ -362,6 +366,7 @@ __device__ uint64_t rb_output(const DMap *maps, uint64_t fd, uint64_t data, uint
 
 struct LaneEnv {
   uint64_t vcpu;
+  uint64_t scratch;  // this lane's scratch word (KParams::lane_scratch), 0 = none
   // last lookup miss (map fd, key hash) for the lookup_or_try_init race rule
   int32_t miss_fd;
   uint64_t miss_hash;
@@ -396,11 +401,17 @@ __device__ uint64_t helper_lookup(const DMap *maps, uint64_t fd, uint64_t key, L
     }
     case MT_LPM_TRIE:
       return lpm_lookup(m, key);
-    case MT_PROG_ARRAY: {  // prog_array.cpp:113-143: the slot's prog fd
+    case MT_PROG_ARRAY: {  // prog_array.cpp:113-143: a copy of the slot's prog fd
       const int32_t k = (int32_t)*(const u32u *)key;
       if (k < 0 || (uint32_t)k >= m.max_entries) return 0;
-      const uint64_t a = m.data + 4ull * (uint32_t)k;
-      return *(const int32_t *)a >= 0 ? a : 0;
+      const int32_t v = *(const volatile int32_t *)(m.data + 4ull * (uint32_t)k);
+      if (v < 0) return 0;
+      // the copy: this lane's scratch word when the launch has them (the
+      // reference's thread-local), else the array's shadow half (maps.cpp);
+      // either way a write through the pointer never reaches the array
+      const uint64_t c = env.scratch ? env.scratch : m.data + 4ull * m.max_entries + 4ull * (uint32_t)k;
+      *(volatile int32_t *)c = v;
+      return c;
     }
   }
   return 0;

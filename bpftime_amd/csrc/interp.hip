@@ -555,7 +555,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   SRP(err_count); SRV(n); SRV(stride); SRV(first_unit); SRV(data_lo); SRV(data_hi); SRV(arena_lo);
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
-  SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(flush_log); SRV(log_words);
+  SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(flush_log); SRV(log_words); SRP(lane_scratch);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
 #undef SRP
 #undef SRV
@@ -583,7 +583,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   c.R = &Rf[tid];
   c.prog = (prog_ptr)p.prog;
   c.fast = p.fast;
-  c.win = Win{p.data_lo, p.data_hi, p.arena_lo, p.arena_hi, p.checked != 0};
+  {
+    const uint64_t sl = (uint64_t)(uintptr_t)p.lane_scratch;
+    c.win = Win{p.data_lo, p.data_hi, p.arena_lo, p.arena_hi, sl, sl ? sl + 8ull * gridDim.x * kBlock : 0,
+                p.checked != 0};
+  }
   c.dummy = (uint64_t)(uintptr_t)&Rf[11 * kBlock + tid];
   c.verdicts = p.verdicts;
   c.rets = p.rets;
@@ -738,7 +742,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
           // frames word-interleaved across the grid's lanes ([depth][word][lane]):
           // a wave's save of one word is one coalesced 512-B store
           uint64_t *const fbase = (uint64_t *)p.frames + (blockIdx.x * kBlock + tid);
-          constexpr uint64_t kLanes = (uint64_t)kTailGrid * kBlock;
+          const uint64_t kLanes = (uint64_t)gridDim.x * kBlock;  // frames sized for this launch (vm_api.cpp)
           auto FW = [&](uint32_t d, uint32_t w) -> uint64_t & {
             return fbase[((uint64_t)d * p.frame_words + w) * kLanes];
           };
@@ -805,6 +809,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       if (csel) {
         LaneEnv env;
         env.vcpu = vcpu;
+        env.scratch = p.lane_scratch ? (uint64_t)(uintptr_t)(p.lane_scratch + (uint64_t)blockIdx.x * kBlock + tid) : 0;
         env.miss_fd = miss_fd;
         env.miss_hash = miss_hash;
         uint32_t cerr = E_OK;

@@ -596,7 +596,12 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
       return -1;
   }
   uint64_t extra = (m.type == MT_HASH || m.type == MT_PERCPU_HASH) ? 128 : 0;
-  uint64_t base = r.arena_alloc(m.bytes + extra + 8);
+  // PROG_ARRAY: a second copy of the slots after them, where device-side
+  // map_lookup_elem hands out the looked-up fd (the reference returns a
+  // thread-local copy, prog_array.cpp:113-143: a write through the pointer
+  // must not change the array)
+  const uint64_t shadow = m.type == MT_PROG_ARRAY ? m.bytes : 0;
+  uint64_t base = r.arena_alloc(m.bytes + extra + shadow + 8);
   if (!base) {
     errno = ENOMEM;
     set_error("map arena exhausted (BPFTIME_AMD_ARENA_MB)");
@@ -604,9 +609,9 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
   }
   d.data = base;
   d.count_addr = extra ? base + ((m.bytes + 127) & ~127ull) : 0;
-  if (hipMemset((void *)base, 0, m.bytes + extra + 8) != hipSuccess) return -1;
+  if (hipMemset((void *)base, 0, m.bytes + extra + shadow + 8) != hipSuccess) return -1;
   if (m.type == MT_PROG_ARRAY) {  // every slot INVALID_ENTRY (-1)
-    if (hipMemset((void *)base, 0xff, m.bytes) != hipSuccess) return -1;
+    if (hipMemset((void *)base, 0xff, 2 * m.bytes) != hipSuccess) return -1;
     r.prog_gen++;
   }
   if (m.lpm) {  // empty replica: root = -1

@@ -51,8 +51,6 @@ struct Runtime {
   uint32_t ncpu = 64;
   std::string last_error;
   uint64_t prog_gen = 1;        // bumped when a prog, a prog array or its contents change
-  uint8_t *d_frames = nullptr;  // tail-call frames (kTailGrid * kBlock lanes), allocated on first use
-  uint64_t frames_bytes = 0;
 
   int ensure_device();          // lazily picks the current device, allocates arena + table
   uint64_t arena_alloc(uint64_t bytes);

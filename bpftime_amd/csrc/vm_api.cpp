@@ -11,7 +11,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <set>
 #include <string>
@@ -33,6 +35,92 @@ struct HelperReg {
   void *fn;
 };
 
+// A loaded program in device form.  Tail-call images (common.hpp
+// kTailHelper) are rebuilt when a prog array changes; a batch holds a
+// reference to the image it launches, so a relink by another thread never
+// frees what an exec_batch in flight is reading (hipFree waits for the
+// device, so launches already queued are safe too).
+struct Image {
+  LoadOut prog;
+  DInsn *d_prog = nullptr;
+  // threaded-code forms: XDP entry (r1 = ctx) and raw/syscall entry (r1 = the
+  // unit's slot) differ in the loader's pointer kinds
+  FastForm fx, fr;
+  int32_t *d_tail_entry = nullptr;  // prog fd -> entry pc (tail-call images)
+  uint32_t frame_words = 0;         // tail-call frame: header + ctx + the image's stack bytes, / 8
+  uint64_t gen = 0;                 // rt().prog_gen it was linked at
+  // linked FInsn arrays per launch configuration (entry form, ORDERED,
+  // staged bytes, batch head): a few per program, built on first use
+  std::mutex link_mu;
+  std::map<uint64_t, FInsn *> links;
+
+  ~Image() {
+    if (d_prog) hipFree(d_prog);
+    if (d_tail_entry) hipFree(d_tail_entry);
+    for (auto &kv : links) hipFree(kv.second);
+  }
+  const FInsn *linked(bool xdp, uint32_t head, uint32_t stage, bool ordered) {
+    std::lock_guard<std::mutex> g(link_mu);
+    const uint64_t key =
+        ((uint64_t)xdp << 63) | ((uint64_t)ordered << 62) | ((uint64_t)stage << 40) | (stage ? head : 0);
+    auto it = links.find(key);
+    if (it != links.end()) return it->second;
+    std::vector<FInsn> out;
+    link_fast(xdp ? fx : fr, head, stage, ordered, prog.prog, out);
+    FInsn *d = nullptr;
+    const size_t bytes = out.size() * sizeof(FInsn);
+    if (hipMalloc((void **)&d, bytes) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, out.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+      hipFree(d);
+      return nullptr;
+    }
+    links[key] = d;
+    return d;
+  }
+  // device copy of the decoded program + both threaded forms
+  int upload(LoadOut &&out, std::string &err) {
+    build_fast(out, true, fx);
+    build_fast(out, false, fr);
+    out.comb_entries = (fx.needs_comb || fr.needs_comb) ? kComb : 0;
+    const size_t bytes = out.prog.size() * sizeof(DInsn);
+    if (hipMalloc((void **)&d_prog, bytes) != hipSuccess ||
+        hipMemcpy(d_prog, out.prog.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+      err = "device upload failed";
+      return -1;
+    }
+    prog = std::move(out);
+    return 0;
+  }
+};
+
+// device buffers kept per stream: a batch's launches use them in stream
+// order, batches on other streams have their own
+struct StreamBufs {
+  struct Buf {
+    void *p = nullptr;
+    uint64_t bytes = 0;
+  };
+  std::mutex mu;
+  std::map<hipStream_t, Buf> bufs;
+  ~StreamBufs() {
+    for (auto &kv : bufs)
+      if (kv.second.p) hipFree(kv.second.p);
+  }
+  void *get(hipStream_t s, uint64_t bytes) {
+    std::lock_guard<std::mutex> g(mu);
+    Buf &b = bufs[s];
+    if (b.bytes < bytes) {
+      // the stream may still run a batch that uses the old buffer
+      if (b.p && (hipStreamSynchronize(s) != hipSuccess || hipFree(b.p) != hipSuccess)) return nullptr;
+      b.p = nullptr;
+      b.bytes = 0;
+      if (hipMalloc(&b.p, bytes) != hipSuccess) return nullptr;
+      b.bytes = bytes;
+    }
+    return b.p;
+  }
+};
+
 class Mi355xVm {
  public:
   std::string error;
@@ -48,53 +136,29 @@ class Mi355xVm {
   uint64_t step_limit = 1ull << 22;
 
   bool loaded = false;
-  LoadOut prog;
-  DInsn *d_prog = nullptr;
-  // threaded-code forms: XDP entry (r1 = ctx) and raw/syscall entry (r1 = the
-  // unit's slot) differ in the loader's pointer kinds
-  FastForm fx, fr;
-  // linked FInsn arrays per launch configuration (entry form, staged bytes,
-  // batch head): a few per program, built on first use
-  std::mutex link_mu;
-  std::map<uint64_t, FInsn *> links;
+  std::mutex img_mu;                 // guards img (replaced by tail-call relinks)
+  std::shared_ptr<Image> img;
+  std::shared_ptr<Image> image() {
+    std::lock_guard<std::mutex> g(img_mu);
+    return img;
+  }
   // failed-unit counters, one per in-flight batch: concurrent batches on
   // different streams must not share (and re-zero) one counter
   static constexpr uint32_t kErrSlots = 64;
   uint32_t *d_err = nullptr;
-  uint32_t err_slot = 0;
+  std::atomic<uint32_t> err_slot{0};
   // staging for ebpf_exec
+  std::mutex stage_mu;
   uint8_t *d_stage = nullptr;
   size_t stage_size = 0;
-  // bpf_tail_call: the loaded code, and the image linked with every prog
-  // array target (common.hpp kTailHelper), rebuilt when rt().prog_gen moves
+  // bpf_tail_call: the loaded code, relinked with the prog arrays' targets
+  // when rt().prog_gen moves
   std::vector<RawInsn> raw;
   bool has_tail = false;
-  uint32_t base_stack = 0;
-  uint32_t frame_words = 0;  // the loaded program's own stack need (kStackSize + 1: unknown)
-  uint64_t image_gen = 0;
-  int32_t *d_tail_entry = nullptr;
-  std::mutex tail_mu;
-  // block-end flush logs (common.hpp kMergeGroup), one per stream: a batch's
-  // two launches use it in stream order, batches on other streams have their own
-  struct StreamBuf {
-    void *p = nullptr;
-    uint64_t bytes = 0;
-  };
-  std::mutex log_mu;
-  std::map<hipStream_t, StreamBuf> logs;
-  uint64_t *flush_log(hipStream_t s, uint64_t bytes) {
-    std::lock_guard<std::mutex> g(log_mu);
-    StreamBuf &b = logs[s];
-    if (b.bytes < bytes) {
-      // the stream may still run a batch that uses the old buffer
-      if (b.p && (hipStreamSynchronize(s) != hipSuccess || hipFree(b.p) != hipSuccess)) return nullptr;
-      b.p = nullptr;
-      b.bytes = 0;
-      if (hipMalloc(&b.p, bytes) != hipSuccess) return nullptr;
-      b.bytes = bytes;
-    }
-    return (uint64_t *)b.p;
-  }
+  uint32_t base_stack = 0;  // the loaded program's own stack need (kStackSize + 1: unknown)
+  std::string link_note;    // targets left out of the last image, and why
+  // block-end flush logs (common.hpp kMergeGroup) and tail-call frames
+  StreamBufs logs, frames, scratch;
 
   Mi355xVm() {
     // bpftime_prog.cpp:126-127 defaults, pointed at the device registry
@@ -107,20 +171,13 @@ class Mi355xVm {
     unload();
     if (d_err) hipFree(d_err);
     if (d_stage) hipFree(d_stage);
-    if (d_tail_entry) hipFree(d_tail_entry);
-    for (auto &kv : logs)
-      if (kv.second.p) hipFree(kv.second.p);
   }
   void unload() {
-    if (d_prog) hipFree(d_prog);
-    d_prog = nullptr;
-    for (auto &kv : links) hipFree(kv.second);
-    links.clear();
+    std::lock_guard<std::mutex> g(img_mu);
+    img.reset();
     loaded = false;
-    prog = LoadOut();
     raw.clear();
     has_tail = false;
-    image_gen = 0;
   }
   int register_external_function(size_t index, const std::string &name, void *fn) {
     // compat_ubpf.cpp:50-59: allocate the next id; ubpf caps helpers at 64
@@ -154,44 +211,60 @@ class Mi355xVm {
       error = "no HIP device: " + rt().last_error;
       return -1;
     }
-    build_fast(out, true, fx);
-    build_fast(out, false, fr);
-    out.comb_entries = (fx.needs_comb || fr.needs_comb) ? kComb : 0;
-    size_t bytes = out.prog.size() * sizeof(DInsn);
-    if (hipMalloc((void **)&d_prog, bytes) != hipSuccess ||
-        hipMemcpy(d_prog, out.prog.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
-      error = "device upload failed";
-      return -1;
-    }
     if (!d_err && hipMalloc((void **)&d_err, 4 * kErrSlots) != hipSuccess) {
       error = "device alloc failed";
       return -1;
     }
     has_tail = out.tail_call;
     base_stack = out.big_stack ? kStackSize + 1 : out.stack_size;
+    auto im = std::make_shared<Image>();
+    if (im->upload(std::move(out), error) < 0) return -1;
     raw.assign((const RawInsn *)code, (const RawInsn *)code + code_len / 8);
-    prog = std::move(out);
+    {
+      std::lock_guard<std::mutex> g(img_mu);
+      img = std::move(im);
+    }
     loaded = true;
     return 0;
   }
 
-  // Link the loaded program with every program a PROG_ARRAY names: one
-  // image, the targets appended (raw jumps are relative, so they need no
-  // relocation) with their exits turned into kRetHelper calls, plus a
-  // prog fd -> entry pc table.  A target that does not load alone is left
-  // out, so tail calls to it return -1 like a failed bpftime_prog_load
-  // (bpf_helper.cpp:623-628).
-  int link_tail_image() {
-    std::lock_guard<std::mutex> tg(tail_mu);  // concurrent batches of one VM relink once
+  // Link the loaded program with the programs its prog arrays can reach:
+  // the arrays it loads by fd (lddw src 1), the targets they name, and
+  // transitively the arrays those targets load.  One image, the targets
+  // appended (raw jumps are relative, so they need no relocation) with their
+  // exits turned into kRetHelper calls, plus a prog fd -> entry pc table.  A
+  // target that does not load alone is left out, so tail calls to it return
+  // -1 like a failed bpftime_prog_load (bpf_helper.cpp:623-628); the reason
+  // is kept in link_note.  Called with img_mu held.
+  int link_tail_image_locked() {
     Runtime &r = rt();
-    if (image_gen == r.prog_gen && d_tail_entry) return 0;
+    if (img && img->gen == r.prog_gen && img->d_tail_entry) return 0;
     std::map<size_t, size_t> hm = helper_id_map;
     std::map<size_t, std::string> names = helper_names;
     for (uint32_t id : {1u, 2u, 3u, 5u, 7u, 8u, 12u, 28u, 44u, 65u, 130u, 131u, 132u, 133u, 189u})
       if (!hm.count(id)) hm[id] = 63;  // the runtime's helper groups (bpf_helper.cpp:606-620)
-    std::set<int32_t> targets;
-    for (uint32_t fd = 0; fd < kMaxFds; fd++) {
-      if (r.kind[fd] != HKind::MAP || r.maps[fd].type != MT_PROG_ARRAY) continue;
+    // prog arrays named by lddw src 1 in `code`
+    auto arrays_of = [&](const RawInsn *code, size_t n, std::set<int32_t> &out) {
+      // (the fd as BPF_PSEUDO_MAP_FD, or as a plain 64-bit immediate the way
+      // runtime/unit-test/tailcall/test_user_to_user_tailcall.cpp loads it)
+      for (size_t i = 0; i + 1 < n; i++)
+        if (code[i].code == 0x18) {
+          const uint64_t v = (uint64_t)(uint32_t)code[i].imm | ((uint64_t)(uint32_t)code[i + 1].imm << 32);
+          const bool as_fd = code[i].src == 1 || (code[i].src == 0 && v < kMaxFds);
+          const int32_t fd = code[i].imm;
+          if (as_fd && fd >= 0 && fd < (int32_t)kMaxFds && r.kind[fd] == HKind::MAP &&
+              r.maps[fd].type == MT_PROG_ARRAY)
+            out.insert(fd);
+          i++;
+        }
+    };
+    std::set<int32_t> arrays, seen_arrays, targets;
+    arrays_of(raw.data(), raw.size(), arrays);
+    link_note.clear();
+    while (!arrays.empty()) {
+      const int32_t fd = *arrays.begin();
+      arrays.erase(arrays.begin());
+      if (!seen_arrays.insert(fd).second) continue;
       std::vector<int32_t> slots(r.maps[fd].max_entries);
       if (!slots.empty() &&
           hipMemcpy(slots.data(), (const void *)r.maps[fd].d.data, 4 * slots.size(), hipMemcpyDeviceToHost) != hipSuccess) {
@@ -199,42 +272,51 @@ class Mi355xVm {
         return -1;
       }
       for (int32_t v : slots)
-        if (v >= 0 && v < (int32_t)kMaxFds && r.kind[v] == HKind::PROG) targets.insert(v);
+        if (v >= 0 && v < (int32_t)kMaxFds && r.kind[v] == HKind::PROG && targets.insert(v).second) {
+          const std::vector<uint8_t> &b = r.progs[v].insns;
+          arrays_of((const RawInsn *)b.data(), b.size() / 8, arrays);
+        }
     }
-    std::vector<RawInsn> img(raw);
+    std::vector<RawInsn> code(raw);
     std::vector<uint32_t> entries;
     std::vector<int32_t> entry(kMaxFds, -1);
     uint32_t stack_need = base_stack;  // the deepest program of the image
     for (int32_t t : targets) {
       const std::vector<uint8_t> &bytes = r.progs[t].insns;
       const size_t n = bytes.size() / 8;
-      if (img.size() + n + 1 > kMaxInsts) continue;
+      if (code.size() + n + 1 > kMaxInsts) {
+        link_note += "prog " + std::to_string(t) + ": image would exceed " + std::to_string(kMaxInsts) + " insns; ";
+        continue;
+      }
       LoadOut alone;
       std::string err;
-      if (load_program((const RawInsn *)bytes.data(), n, hm, names, lddw, alone, err) < 0) continue;
+      if (load_program((const RawInsn *)bytes.data(), n, hm, names, lddw, alone, err) < 0) {
+        link_note += "prog " + std::to_string(t) + ": " + err + "; ";
+        continue;
+      }
       stack_need = std::max(stack_need, alone.big_stack ? kStackSize + 1 : alone.stack_size);
-      entry[t] = (int32_t)img.size();
-      entries.push_back((uint32_t)img.size());
-      const RawInsn *code = (const RawInsn *)bytes.data();
+      entry[t] = (int32_t)code.size();
+      entries.push_back((uint32_t)code.size());
+      const RawInsn *c = (const RawInsn *)bytes.data();
       for (size_t i = 0; i < n; i++) {
-        RawInsn x = code[i];
+        RawInsn x = c[i];
         if (x.code == 0x95) {  // exit -> return to the caller's frame
           x = RawInsn{};
           x.code = 0x85;
           x.imm = kRetHelper;
         }
-        img.push_back(x);
-        if (code[i].code == 0x18 && i + 1 < n) img.push_back(code[++i]);
+        code.push_back(x);
+        if (c[i].code == 0x18 && i + 1 < n) code.push_back(c[++i]);
       }
     }
     if (!entries.empty()) {
       RawInsn ex{};
       ex.code = 0x95;
-      img.push_back(ex);
+      code.push_back(ex);
     }
     LoadOut out;
     std::string err;
-    if (load_program(img.data(), img.size(), hm, names, lddw, out, err, entries) < 0) {
+    if (load_program(code.data(), code.size(), hm, names, lddw, out, err, entries) < 0) {
       error = "tail-call image: " + err;
       return -1;
     }
@@ -243,60 +325,17 @@ class Mi355xVm {
       out.big_stack = false;
       out.stack_size = std::max<uint32_t>(8, stack_need);
     }
-    FastForm nx, nr;
-    build_fast(out, true, nx);
-    build_fast(out, false, nr);
-    out.comb_entries = (nx.needs_comb || nr.needs_comb) ? kComb : 0;
-    DInsn *dp = nullptr;
-    const size_t bytes = out.prog.size() * sizeof(DInsn);
-    if (!d_tail_entry && hipMalloc((void **)&d_tail_entry, 4 * kMaxFds) != hipSuccess) d_tail_entry = nullptr;
-    // frames: header + ctx copy + the stack bytes the image uses, per depth and lane
-    frame_words = (kFrameHdr + kFrameCtx + (out.big_stack ? kStackSize : out.stack_size)) / 8;
-    const uint64_t fbytes = (uint64_t)kTailGrid * kBlock * kTailDepth * frame_words * 8;
-    if (r.frames_bytes < fbytes) {
-      if (r.d_frames) hipFree(r.d_frames);
-      r.frames_bytes = 0;
-      if (hipMalloc((void **)&r.d_frames, fbytes) != hipSuccess)
-        r.d_frames = nullptr;
-      else
-        r.frames_bytes = fbytes;
-    }
-    if (!d_tail_entry || !r.d_frames || hipMalloc((void **)&dp, bytes) != hipSuccess ||
-        hipMemcpy(dp, out.prog.data(), bytes, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(d_tail_entry, entry.data(), 4 * kMaxFds, hipMemcpyHostToDevice) != hipSuccess) {
-      if (dp) hipFree(dp);
+    auto im = std::make_shared<Image>();
+    im->frame_words = (kFrameHdr + kFrameCtx + (out.big_stack ? kStackSize : out.stack_size)) / 8;
+    im->gen = r.prog_gen;
+    if (im->upload(std::move(out), error) < 0) return -1;
+    if (hipMalloc((void **)&im->d_tail_entry, 4 * kMaxFds) != hipSuccess ||
+        hipMemcpy(im->d_tail_entry, entry.data(), 4 * kMaxFds, hipMemcpyHostToDevice) != hipSuccess) {
       error = "device upload failed";
       return -1;
     }
-    std::lock_guard<std::mutex> g(link_mu);
-    if (d_prog) hipFree(d_prog);
-    d_prog = dp;
-    for (auto &kv : links) hipFree(kv.second);
-    links.clear();
-    fx = std::move(nx);
-    fr = std::move(nr);
-    prog = std::move(out);
-    image_gen = r.prog_gen;
+    img = std::move(im);
     return 0;
-  }
-
-  // the FInsn array for (entry form, staged bytes, head), linked on first use
-  const FInsn *linked(bool xdp, uint32_t head, uint32_t stage, bool ordered) {
-    std::lock_guard<std::mutex> g(link_mu);
-    const uint64_t key = ((uint64_t)xdp << 63) | ((uint64_t)ordered << 62) | ((uint64_t)stage << 40) | (stage ? head : 0);
-    auto it = links.find(key);
-    if (it != links.end()) return it->second;
-    std::vector<FInsn> out;
-    link_fast(xdp ? fx : fr, head, stage, ordered, prog.prog, out);
-    FInsn *d = nullptr;
-    const size_t bytes = out.size() * sizeof(FInsn);
-    if (hipMalloc((void **)&d, bytes) != hipSuccess) return nullptr;
-    if (hipMemcpy(d, out.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
-      hipFree(d);
-      return nullptr;
-    }
-    links[key] = d;
-    return d;
   }
 
   int exec_batch(const ebpf_batch *b);
@@ -319,31 +358,37 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   hipStream_t s = (hipStream_t)b->stream;
   if (b->count == 0) return 0;
   Runtime &r = rt();
-  if (has_tail && link_tail_image() < 0) return -1;
-  KParams p{};
-  p.prog = d_prog;
-  if (has_tail) {
-    p.tail_entry = d_tail_entry;
-    p.frames = r.d_frames;
-    p.frame_words = frame_words;
+  std::shared_ptr<Image> imp;
+  {
+    std::lock_guard<std::mutex> g(img_mu);
+    if (has_tail && link_tail_image_locked() < 0) return -1;
+    imp = img;
   }
+  if (!imp) {
+    error = "no program loaded";
+    return -1;
+  }
+  Image &im = *imp;
+  const LoadOut &prog = im.prog;
+  KParams p{};
+  p.prog = im.d_prog;
   {
     // staged window: what the static packet / slot accesses need, when every
     // slot is 16-B aligned and at least that long (a window never reaches
     // into the next unit)
     const bool xdp = b->ctx_kind == CTX_XDP;
     const uint32_t head = xdp ? b->head : 0;
-    const uint32_t need = stage_need(xdp ? fx : fr, head);
+    const uint32_t need = stage_need(xdp ? im.fx : im.fr, head);
     // (descriptor batches: the kernel checks each wave's frames)
     const bool aligned = ((uint64_t)(uintptr_t)b->data % 16) == 0 &&
                          (b->descs ? true : (b->stride % 16) == 0 && b->stride >= need);
     p.stage = (need && aligned && !getenv("BPFTIME_AMD_NO_STAGING")) ? need : 0;
-    p.fast = linked(xdp, head, p.stage, (b->flags & EBPF_BATCH_ORDERED) != 0);
+    p.fast = im.linked(xdp, head, p.stage, (b->flags & EBPF_BATCH_ORDERED) != 0);
     if (!p.fast) {
       error = "device upload failed";
       return -1;
     }
-    p.needs_ctx = xdp && fx.needs_ctx ? 1 : 0;
+    p.needs_ctx = xdp && im.fx.needs_ctx ? 1 : 0;
     p.fast_div = getenv("BPFTIME_AMD_NO_ASM_DIVERGENCE") ? 0 : 1;
   }
   p.maps = r.d_maptab;
@@ -353,7 +398,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   p.rets = b->rets;
   p.out_data_off = b->data_off_out;
   p.out_len = b->len_out;
-  uint32_t *err = d_err + (err_slot++ % kErrSlots);
+  uint32_t *err = d_err + (err_slot.fetch_add(1) % kErrSlots);
   p.err_count = err;
   p.n = b->count;
   p.stride = b->stride;
@@ -431,13 +476,36 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       if (atoi(g) > 0) mult = (uint32_t)atoi(g);
     uint64_t cap = (uint64_t)cus * (uint64_t)occ * mult;
     grid = (uint32_t)(want < cap ? want : cap);
-    if (has_tail && grid > kTailGrid) grid = kTailGrid;  // one frame stack per lane of the grid
+    if (im.d_tail_entry && grid > kTailGrid) grid = kTailGrid;  // one frame stack per lane of the grid
   }
+  if (im.d_tail_entry) {
+    // tail-call frames for the lanes of this launch ([depth][word][lane]),
+    // one buffer per stream: concurrent batches never share frames
+    p.tail_entry = im.d_tail_entry;
+    p.frame_words = im.frame_words;
+    const uint64_t fbytes = (uint64_t)grid * kBlock * kTailDepth * im.frame_words * 8;
+    p.frames = (uint8_t *)frames.get(s, fbytes);
+    if (!p.frames) {
+      error = "tail-call frame allocation failed (" + std::to_string(fbytes >> 20) + " MiB)";
+      return -1;
+    }
+  }
+  // a scratch word per lane while prog arrays exist (device map_lookup_elem
+  // on one hands out a copy of the fd there, prog_array.cpp:113-143)
+  for (uint32_t fd = 0; fd < kMaxFds; fd++)
+    if (r.kind[fd] == HKind::MAP && r.maps[fd].type == MT_PROG_ARRAY) {
+      p.lane_scratch = (uint64_t *)scratch.get(s, (uint64_t)grid * kBlock * 8);
+      if (!p.lane_scratch) {
+        error = "lane scratch allocation failed";
+        return -1;
+      }
+      break;
+    }
   // a block-end flush log when the blocks hold per-lane counter tables:
   // merged by a second launch instead of every block adding its table
   if (p.comb_entries && grid > kMergeGroup && !getenv("BPFTIME_AMD_NO_MERGE")) {
     p.log_words = log_words_for(p.comb_entries);
-    p.flush_log = flush_log(s, (uint64_t)grid * p.log_words * 8);
+    p.flush_log = (uint64_t *)logs.get(s, (uint64_t)grid * p.log_words * 8);
     if (!p.flush_log) {
       error = "flush log allocation failed";
       return -1;
@@ -489,6 +557,7 @@ int Mi355xVm::exec_one(void *mem, size_t mem_len, uint64_t *ret) {
     slot_bytes = mem_len;
     len = (uint32_t)mem_len;
   }
+  std::lock_guard<std::mutex> sg(stage_mu);  // one ebpf_exec at a time per VM uses the staging buffer
   size_t need = ((slot_bytes + 255) & ~(size_t)255) + 64;
   if (need > stage_size) {
     if (d_stage) hipFree(d_stage);
@@ -680,22 +749,25 @@ struct ebpf_vm *bpftime_amd_prog_instantiate(int prog_fd, char **errmsg) {
 int bpftime_amd_vm_info(const struct ebpf_vm *vm, uint32_t *stack_size, int *big_stack, uint32_t *fused_rmw,
                         uint32_t *n_insns) {
   if (!vm || !vm->impl->loaded) return -1;
-  if (stack_size) *stack_size = vm->impl->prog.stack_size;
-  if (big_stack) *big_stack = vm->impl->prog.big_stack;
-  if (fused_rmw) *fused_rmw = vm->impl->prog.fused_rmw;
-  if (n_insns) *n_insns = (uint32_t)vm->impl->prog.prog.size();
+  auto im = vm->impl->image();
+  if (stack_size) *stack_size = im->prog.stack_size;
+  if (big_stack) *big_stack = im->prog.big_stack;
+  if (fused_rmw) *fused_rmw = im->prog.fused_rmw;
+  if (n_insns) *n_insns = (uint32_t)im->prog.prog.size();
   return 0;
 }
 
 int bpftime_amd_vm_fast_info(const struct ebpf_vm *vm, uint32_t ctx_kind, uint32_t *specialized) {
   if (!vm || !vm->impl->loaded) return -1;
-  if (specialized) *specialized = ctx_kind == CTX_XDP ? vm->impl->fx.specialized : vm->impl->fr.specialized;
+  auto im = vm->impl->image();
+  if (specialized) *specialized = ctx_kind == CTX_XDP ? im->fx.specialized : im->fr.specialized;
   return 0;
 }
 
 int bpftime_amd_vm_counter_info(const struct ebpf_vm *vm, uint32_t ctx_kind, uint32_t *deferred, uint32_t *direct) {
   if (!vm || !vm->impl->loaded) return -1;
-  const FastForm &f = ctx_kind == CTX_XDP ? vm->impl->fx : vm->impl->fr;
+  auto im = vm->impl->image();
+  const FastForm &f = ctx_kind == CTX_XDP ? im->fx : im->fr;
   uint32_t nd = 0, nn = 0;
   for (size_t i = 0; i < f.add_site.size(); i++)
     if (f.add_site[i]) ((f.fast[i].w1 & FW_NODEFER) ? nn : nd)++;

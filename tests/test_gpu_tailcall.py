@@ -164,3 +164,59 @@ def test_image_atomic_adds_summed_per_address(fresh_oracle, fresh_runtime):
     assert c32_d.lookup(I32(0)) == c32_o.lookup(I32(0))
     got = np.frombuffer(c32_d.lookup(I32(0)), dtype=np.uint32)
     assert int(got[:8].sum()) == 7 * n and struct.unpack_from("<Q", c32_d.lookup(I32(0)), 32)[0] == n
+
+
+def test_tailcall_batches_on_two_streams(fresh_oracle, fresh_runtime):
+    """Two tail-call batches in flight at once on two streams (the same VM
+    and a second VM): each launch has its own frames (per-stream buffers),
+    so neither resumes the other's callers."""
+    po, dev = fresh_oracle, fresh_runtime
+    (pa_o, cnt_o), (pa_d, cnt_d) = _xdp_pair(po, dev)
+    code = tc.xdp_caller(PA_FD, cnt_d.fd)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    vms = [dev.VM(), dev.VM()]
+    for v in vms:
+        v.load(code)
+    streams = [dev.lib().bpftime_amd_stream_create() for _ in range(3)]
+    n = 50000
+    jobs = []
+    for i, (vm, s) in enumerate(((vms[0], streams[0]), (vms[0], streams[1]), (vms[1], streams[2]))):
+        pk = gen.xdp_packets(n, seed=100 + i)
+        pk[:, 0] = np.random.default_rng(100 + i).integers(0, 256, n, dtype=np.uint8)
+        opk = pk.copy()
+        ov = ovm.run_xdp(opk, fixed_len=64, ifindex=5)
+        d = dev.DeviceBuffer.from_array(pk)
+        dv = dev.DeviceBuffer(4 * n)
+        assert vm.exec_batch(dev.CTX_XDP, d, n, 64, fixed_len=64, verdicts=dv, ifindex=5, flags=0, stream=s) == 0
+        jobs.append((d, dv, ov, opk))
+    for s in streams:
+        assert dev.lib().bpftime_amd_stream_sync(s) == 0
+        dev.lib().bpftime_amd_stream_destroy(s)
+    for d, dv, ov, opk in jobs:
+        np.testing.assert_array_equal(dv.download(np.uint32), ov)
+        np.testing.assert_array_equal(d.download().reshape(n, 64), opk)
+    for i in range(4):
+        assert cnt_d.lookup(I32(i)) == cnt_o.lookup(I32(i)), i
+
+
+def test_prog_array_lookup_returns_a_copy(fresh_oracle, fresh_runtime):
+    """map_lookup_elem on a PROG_ARRAY hands out a copy of the fd
+    (prog_array.cpp:113-143, a thread-local): writing through it leaves the
+    array and the following tail call unchanged; r0 = the fd read back +
+    the target's result."""
+    po, dev = fresh_oracle, fresh_runtime
+    (pa_o, cnt_o), (pa_d, cnt_d) = _xdp_pair(po, dev)
+    a = isa.Asm().mov64(6, "r1").st(4, 10, -4, 0)
+    a.ld_map_fd(1, PA_FD).mov64(2, "r10").add64(2, -4).call(isa.BPF_FUNC_map_lookup_elem)
+    a.mov64(7, 0).jmp("jeq", 0, 0, "call").ldx(4, 7, 0, 0).st(4, 0, 0, 901)   # overwrite the copy
+    a.label("call").mov64(1, "r6").ld_map_fd(2, PA_FD).mov64(3, 0).call(12)
+    a.alu64("lsh", 7, 16).alu64("add", 0, "r7").exit()
+    code = a.assemble()
+    ovm = po.OracleVM()
+    ovm.load(code)
+    dvm = dev.VM()
+    dvm.load(code)
+    ov, opk = _run_both(po, dev, ovm, dvm, 3000, 5, cnt_o, cnt_d)
+    assert ((ov >> 16) == 900).all() and ((ov & 0xFFFF) == 64 + 0xA1).all()
+    assert pa_d.lookup(I32(0)) == I32(900)
