@@ -31,7 +31,8 @@ def parse():
     ap.add_argument("--workload", default="xdp-counter", choices=["xdp-counter", "flow-hash", "syscall-agg", "lpm-route", "ringbuf-sample", "tail-call"],
                     help="xdp-counter is the headline (BASELINE metric); the others are configs[2]/[4] "
                          "(bench_workloads.py)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
+                    help="CPU baseline budget per leg (1 core, all cores; rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--unchecked", action="store_true", help="skip the global-window check")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe-inclusive) leg")
@@ -291,42 +292,18 @@ def merge_e2e(e2es, world, n):
     return out
 
 
-def cpu_baseline(budget_s):
-    """The oracle (restated reference CPU interpreter, -O2, 1 pinned thread)
-    over a bounded sample of the same workload."""
-    import numpy as np
-
-    from bpftime_amd import gen, isa, programs
-    from oracle import pyoracle as po
-
-    po.reset()
-    ctl = po.OracleMap(isa.BPF_MAP_TYPE_ARRAY, 4, 4, 2)
-    bss = po.OracleMap(isa.BPF_MAP_TYPE_ARRAY, 4, 4096, 1)
-    ovm = po.OracleVM()
-    ovm.load(programs.xdp_counter(ctl.fd, bss.fd))
-    sample_n = 1 << 22
-    pk = gen.xdp_packets(sample_n, PKT, gen.SEED_CFG2, 0)
-    secs, done = 0.0, 0
-    while secs < budget_s and done < 64 * sample_n:
-        secs += ovm.time_xdp(pk, PKT, pin_cpu=0)
-        done += sample_n
-    cnt = int(np.frombuffer(bss.lookup(b"\0\0\0\0"), dtype=np.uint64)[0])
-    cpu_model = ""
+def cpu_baseline(budget_s, workload="xdp-counter"):
+    """The oracle (restated reference CPU interpreter, -O2) over a bounded
+    sample of the same workload: one pinned core and all the cores this
+    process may use (bench_cpu.py, run as its own process: it never touches
+    the GPU)."""
+    import subprocess
     try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    return {
-        "value": round(done / secs / 1e6, 3),
-        "unit": "Mpps",
-        "cores": 1,
-        "kind": "port",
-        "sample": "%d passes x 2^22 64-B packets of the same stream (%.1f s, counter %s), cpu %s, pinned core 0"
-                  % (done // sample_n, secs, "ok" if cnt == done else "MISMATCH", cpu_model),
-    }
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench_cpu.py"), "--workload", workload,
+                            "--seconds", str(budget_s)], capture_output=True, text=True, timeout=20 * budget_s + 120)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:  # noqa: BLE001 -- a baseline failure must not lose the GPU line
+        return {"error": "cpu baseline failed: %s" % e}
 
 
 if __name__ == "__main__":

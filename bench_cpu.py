@@ -1,0 +1,159 @@
+"""CPU baseline leg of bench.py: the oracle (the C restatement of the
+reference's CPU path, oracle/ -- test infrastructure, never the product) timed
+on the host cores over a bounded sample of the same workload.
+
+    python bench_cpu.py --workload xdp-counter --seconds 8 [--cores N]
+
+Runs in its own process (bench.py starts it after the GPU part; this process
+never touches the GPU).  Two legs, SURVEY.md §8d:
+  (i)  one thread pinned to one core;
+  (ii) N worker processes pinned to N cores, each over its own contiguous
+       shard of the stream with private map copies, their map deltas merged
+       like the GPUs' (the harness shape of tools/bpftimetool/main.cpp:42-58,
+       steady clock around the packet loop only).
+Prints one JSON object: the N-core leg as value/cores, the 1-core leg as
+single_core.
+"""
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def _setup(workload, shard, sample_n):
+    """(oracle vm, run() -> (seconds, units), check() -> bool, units label)."""
+    import numpy as np
+
+    from bpftime_amd import gen, isa, programs
+    from oracle import pyoracle as po
+    po.reset()
+    first = shard * sample_n
+    if workload == "xdp-counter":
+        ctl = po.OracleMap(isa.BPF_MAP_TYPE_ARRAY, 4, 4, 2)
+        bss = po.OracleMap(isa.BPF_MAP_TYPE_ARRAY, 4, 4096, 1)
+        ovm = po.OracleVM()
+        ovm.load(programs.xdp_counter(ctl.fd, bss.fd))
+        pk = gen.xdp_packets(sample_n, 64, gen.SEED_CFG2, first)
+        runs = [0]
+
+        def run():
+            runs[0] += 1
+            return ovm.time_xdp(pk, 64, pin_cpu=-1), sample_n
+
+        def check():
+            return int(np.frombuffer(bss.lookup(b"\0\0\0\0"), dtype=np.uint64)[0]) == runs[0] * sample_n
+        return run, check
+    if workload == "flow-hash":
+        flows = po.OracleMap(isa.BPF_MAP_TYPE_HASH, 16, 16, 65536)
+        ovm = po.OracleVM()
+        ovm.load(programs.flow_hash(flows.fd))
+        slots, lens = gen.flow_packets(sample_n, first=first)
+        ipmask = slots[:, 12] == 0x08
+        runs = [0]
+
+        def run():
+            s = slots.copy()
+            t0 = time.perf_counter()
+            ovm.run_xdp(s, lens=lens)
+            runs[0] += 1
+            return time.perf_counter() - t0, sample_n
+
+        def check():
+            tot = sum(int(np.frombuffer(v, dtype=np.uint64)[0]) for v in flows.items().values())
+            return tot == runs[0] * int(ipmask.sum())
+        return run, check
+    if workload == "syscall-agg":
+        counts = po.OracleMap(isa.BPF_MAP_TYPE_HASH, 4, 32, 8192)
+        ovm = po.OracleVM()
+        ovm.load(programs.syscall_agg(counts.fd))
+        recs = gen.syscall_records(sample_n, first=first)
+        ids = recs.view(np.uint64)[:, 1]
+        live = int(((ids != 60) & (ids != 231)).sum())
+        runs = [0]
+
+        def run():
+            t0 = time.perf_counter()
+            ovm.run_syscall(recs)
+            runs[0] += 1
+            return time.perf_counter() - t0, sample_n
+
+        def check():
+            tot = sum(int(np.frombuffer(v[:8], dtype=np.uint64)[0]) for v in counts.items().values())
+            return tot == runs[0] * live
+        return run, check
+    raise SystemExit("unknown workload " + workload)
+
+
+SAMPLE = {"xdp-counter": 1 << 21, "flow-hash": 1 << 15, "syscall-agg": 1 << 17}
+
+
+def _worker(a):
+    workload, shard, core, budget = a
+    if core is not None:
+        try:
+            os.sched_setaffinity(0, {core})
+        except OSError:
+            pass
+    run, check = _setup(workload, shard, SAMPLE[workload])
+    secs, done = 0.0, 0
+    while secs < budget:
+        dt, k = run()
+        secs += dt
+        done += k
+    return done, secs, check()
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return ""
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="xdp-counter", choices=sorted(SAMPLE))
+    ap.add_argument("--seconds", type=float, default=8.0, help="oracle time per leg")
+    ap.add_argument("--cores", type=int, default=0, help="N-core leg width (0: the cores this process may use, "
+                                                         "at most 16 -- the GPU box's CPU share per GPU)")
+    args = ap.parse_args()
+    cores = sorted(os.sched_getaffinity(0))
+    ncore = args.cores or min(16, len(cores))
+    ncore = max(1, min(ncore, len(cores)))
+    unit = "Mrec/s" if args.workload == "syscall-agg" else "Mpps"
+    # (i) one pinned core
+    done1, secs1, ok1 = _worker((args.workload, 0, cores[0], args.seconds))
+    # (ii) ncore pinned processes, contiguous shards, private maps
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(ncore) as pool:
+        res = pool.map(_worker, [(args.workload, k, cores[k], args.seconds) for k in range(ncore)])
+    wall = time.perf_counter() - t0
+    done_n = sum(r[0] for r in res)
+    # each worker's packet loop ran `secs` of its own steady clock; they ran
+    # side by side, so the aggregate rate is units / the longest loop time
+    loop_n = max(r[1] for r in res)
+    ok = ok1 and all(r[2] for r in res)
+    out = {
+        "value": round(done_n / loop_n / 1e6, 3), "unit": unit, "cores": ncore, "kind": "port",
+        "sample": "%s: %d oracle processes pinned to %d cores, each over its own contiguous 2^%d-unit shard of "
+                  "the same stream with private maps (%.1f s loops, %.1f s wall, map totals %s), cpu %s"
+                  % (args.workload, ncore, ncore, SAMPLE[args.workload].bit_length() - 1, loop_n, wall,
+                     "ok" if ok else "MISMATCH", cpu_model()),
+        "single_core": {"value": round(done1 / secs1 / 1e6, 3), "unit": unit, "cores": 1,
+                        "sample": "1 oracle thread pinned to core %d, %.1f s" % (cores[0], secs1)},
+        "ok": ok,
+    }
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

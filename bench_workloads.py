@@ -37,29 +37,6 @@ def _timed(dev, step, steps, warmup):
     return wall, ev0.elapsed_ms(ev1) / steps / 1e3
 
 
-def _cpu_sample(po, setup, run, unit, budget_s, what):
-    """The oracle over a bounded sample of the same stream, 1 thread;
-    setup() creates the oracle maps and returns the program."""
-    po.reset()
-    ovm = po.OracleVM()
-    ovm.load(setup())
-    secs, done = 0.0, 0
-    while secs < budget_s:
-        dt, k = run(ovm)
-        secs += dt
-        done += k
-    cpu_model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    return {"value": round(done / secs / 1e6, 3), "unit": unit, "cores": 1, "kind": "port",
-            "sample": f"{what} ({secs:.1f} s of oracle time), cpu {cpu_model}"}
-
-
 def flow_hash(args, dev, gen, isa, programs):
     n = 1 << (args.log2n if args.log2n_set else 24)
     stride = 2048
@@ -114,20 +91,8 @@ def flow_hash(args, dev, gen, isa, programs):
     algo = 24.0 * ip_frac + 10.0 * (1 - ip_frac)
     cpu = None
     if not args.no_cpu_baseline:
-        from oracle import pyoracle as po
-        sn = 1 << 16
-        slots, slens = gen.flow_packets(sn)
-
-        def mk():
-            return programs.flow_hash(po.OracleMap(isa.BPF_MAP_TYPE_HASH, 16, 16, nflows).fd)
-
-        def runo(ovm):
-            s = slots.copy()
-            t0 = time.perf_counter()
-            ovm.run_xdp(s, lens=slens)
-            return time.perf_counter() - t0, sn
-        cpu = _cpu_sample(po, mk, runo, "Mpps", args.cpu_seconds,
-                          "repeated passes over the first 2^16 frames of the same stream")
+        from bench import cpu_baseline
+        cpu = cpu_baseline(args.cpu_seconds, "flow-hash")
     value = n * args.steps / wall / 1e6
     achieved = algo * n / kern_s / 1e9
     return {
@@ -195,19 +160,8 @@ def syscall_agg(args, dev, gen, isa, programs):
     algo = 12.0 + 8.0 * p
     cpu = None
     if not args.no_cpu_baseline:
-        from oracle import pyoracle as po
-        sn = 1 << 18
-        srecs = gen.syscall_records(sn)
-
-        def mk():
-            return programs.syscall_agg(po.OracleMap(isa.BPF_MAP_TYPE_HASH, 4, 32, 8192).fd)
-
-        def runo(ovm):
-            t0 = time.perf_counter()
-            ovm.run_syscall(srecs)
-            return time.perf_counter() - t0, sn
-        cpu = _cpu_sample(po, mk, runo, "Mrec/s", args.cpu_seconds,
-                          "repeated passes over the first 2^18 records of the same stream")
+        from bench import cpu_baseline
+        cpu = cpu_baseline(args.cpu_seconds, "syscall-agg")
     value = n * args.steps / wall / 1e6
     achieved = algo * n / kern_s / 1e9
     return {
