@@ -133,28 +133,18 @@ def main():
     e2e = None
     if not args.no_e2e:
         e2e = e2e_leg(dev, vm, bss, n, first, args.e2e_chunk_log2, dist, nstreams=args.e2e_streams)
-    times = [wall]
-    shards = [shard]
-    oks = [ok_verdicts and ok_counter and ok_bytes]
-    e2es = [e2e]
-    if dist:
-        gathered = [None] * world
-        dist.all_gather_object(gathered, (wall, shard.tobytes(), oks[0], e2e))
-        times = [g[0] for g in gathered]
-        shards = [np.frombuffer(g[1], dtype=np.uint8) for g in gathered]
-        oks = [g[2] for g in gathered]
-        e2es = [g[3] for g in gathered]
+    gathered = gather_ranks(dist, world, (wall, shard.tobytes(), ok_verdicts and ok_counter and ok_bytes, e2e))
+    times = [g[0] for g in gathered]
+    shards = [np.frombuffer(g[1], dtype=np.uint8) for g in gathered]
+    oks = [g[2] for g in gathered]
+    e2es = [g[3] for g in gathered]
     if rank != 0:
         if dist:
             dist.barrier()
             dist.destroy_process_group()
         return
 
-    # host merge of per-GPU map shards: final = init + sum(shard - init)
-    merged = init_bss.copy()
-    for s in shards:
-        dev.lib().bpftime_amd_merge_delta_u64(merged.ctypes.data, init_bss.ctypes.data, s.ctypes.data,
-                                              merged.nbytes)
+    merged = merge_counter_shards(init_bss, shards)
     merged_cnt = int(merged.view(np.uint64)[0])
     parity = all(oks) and merged_cnt == world * total_runs * n
 
@@ -217,6 +207,23 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def gather_ranks(dist, world, payload):
+    """Every rank's (wall seconds, map shard bytes, parity, e2e) on every
+    rank: the control plane over gloo, no data-path collective."""
+    if not dist or world == 1:
+        return [payload]
+    gathered = [None] * world
+    dist.all_gather_object(gathered, payload)
+    return gathered
+
+
+def merge_counter_shards(init, shards, width=8):
+    """Host merge of the per-GPU map shards: final = init + sum(shard - init),
+    counter by counter (xdp-counter's cntrs_array is u64)."""
+    from bpftime_amd import shard as sh
+    return sh.merge_array_delta(init, shards, width)
 
 
 def e2e_leg(dev, vm, bss, n, first, chunk_log2, dist, passes=3, nstreams=2):

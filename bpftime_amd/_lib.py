@@ -116,6 +116,7 @@ SIGNATURES = [
     ("bpftime_amd_syscall_dispatch", C.c_int64, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]),
     ("bpftime_amd_handle_sysbpf", C.c_long, [C.c_int, C.c_void_p, C.c_uint32]),
     ("bpftime_amd_merge_delta_u64", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
+    ("bpftime_amd_merge_delta", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32]),
     ("bpftime_amd_device_count", C.c_int, []),
     ("bpftime_amd_set_device", C.c_int, [C.c_int]),
     ("bpftime_amd_dev_alloc", C.c_void_p, [C.c_uint64]),

@@ -1203,12 +1203,30 @@ int bpftime_amd_xdp_links(int *link_fds, int *prog_fds, uint32_t *ifindexes, int
 }
 
 // ---- host merge ------------------------------------------------------------
+// final = init + sum(shard - init), counter by counter at the map's counter
+// width (a u32 counter's combined delta wraps at 2^32 instead of carrying
+// into its neighbour)
+#define MERGE_DELTA(T)                                                     \
+  do {                                                                     \
+    T *a = (T *)acc;                                                       \
+    const T *i0 = (const T *)init, *s = (const T *)shard;                  \
+    for (uint64_t k = 0; k < bytes / sizeof(T); k++) a[k] = (T)(a[k] + (T)(s[k] - i0[k])); \
+  } while (0)
+
+int bpftime_amd_merge_delta(void *acc, const void *init, const void *shard, uint64_t bytes, uint32_t width) {
+  if (!acc || !init || !shard || !width || bytes % width) return -1;
+  switch (width) {
+    case 1: MERGE_DELTA(uint8_t); return 0;
+    case 2: MERGE_DELTA(uint16_t); return 0;
+    case 4: MERGE_DELTA(uint32_t); return 0;
+    case 8: MERGE_DELTA(uint64_t); return 0;
+  }
+  return -1;
+}
+#undef MERGE_DELTA
+
 int bpftime_amd_merge_delta_u64(void *acc, const void *init, const void *shard, uint64_t bytes) {
-  if (bytes % 8) return -1;
-  uint64_t *a = (uint64_t *)acc;
-  const uint64_t *i0 = (const uint64_t *)init, *s = (const uint64_t *)shard;
-  for (uint64_t k = 0; k < bytes / 8; k++) a[k] += s[k] - i0[k];
-  return 0;
+  return bpftime_amd_merge_delta(acc, init, shard, bytes, 8);
 }
 
 }  // extern "C"

@@ -190,6 +190,10 @@ int64_t bpftime_amd_syscall_dispatch(const void *records, uint64_t n, uint32_t f
 /* ---- host merge of per-GPU map shards ---- */
 /* acc += shard - init over u64 words (array counters, additive rule) */
 int bpftime_amd_merge_delta_u64(void *acc, const void *init, const void *shard, uint64_t bytes);
+/* The same rule counter by counter at `width` bytes (1, 2, 4, 8): a u32
+ * counter's combined delta wraps at 2^32 instead of carrying into the next
+ * field.  -1 when bytes is not a multiple of width. */
+int bpftime_amd_merge_delta(void *acc, const void *init, const void *shard, uint64_t bytes, uint32_t width);
 
 /* ---- device utilities (HIP runtime plumbing for callers without one) ---- */
 int bpftime_amd_device_count(void);

@@ -99,3 +99,61 @@ def test_shard_range_covers_exactly():
             assert sum(c for _, c in spans) == n
             for (f0, c0), (f1, _) in zip(spans, spans[1:]):
                 assert f0 + c0 == f1
+
+
+def _bench_worker(rank, world, port, q):
+    """bench.py's own N>1 control plane: gather_ranks over gloo, then the
+    rank-0 merge (merge_counter_shards) of per-rank .bss shards."""
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+
+    import bench
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        init = np.zeros(4096, np.uint8)
+        init.view(np.uint64)[:3] = (7, 1 << 40, 5)
+        shard = init.copy()
+        shard.view(np.uint64)[0] += 1000 * (rank + 1)      # this rank's packets
+        shard.view(np.uint64)[1] += rank                    # a second counter
+        got = bench.gather_ranks(dist, world, (0.5 + rank, shard.tobytes(), True, None))
+        if rank == 0:
+            merged = bench.merge_counter_shards(init, [np.frombuffer(g[1], np.uint8) for g in got])
+            q.put((merged.view(np.uint64)[:3].tolist(), [g[0] for g in got]))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_control_plane_two_ranks():
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    counters, times = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert counters == [7 + 1000 + 2000, (1 << 40) + 1, 5]
+    assert times == [0.5, 1.5]   # bench.py reports world * n * steps / max(times)
+
+
+def test_merge_at_counter_width():
+    """u32 counters whose combined delta crosses 2^32 wrap at 32 bits and
+    leave the neighbouring counter alone (a u64-word merge would carry)."""
+    from bpftime_amd import shard
+    init = np.array([0xFFFFFFF0, 5], np.uint32).view(np.uint8)
+    s1 = np.array([0xFFFFFFF8, 5], np.uint32).view(np.uint8)   # +8
+    s2 = np.array([0xFFFFFFFC, 6], np.uint32).view(np.uint8)   # +0xC, neighbour +1
+    got = shard.merge_array_delta(init, [s1, s2], width=4).view(np.uint32)
+    assert got.tolist() == [(0xFFFFFFF0 + 8 + 0xC) & 0xFFFFFFFF, 6]   # the total crosses 2^32
+    wrong = shard.merge_array_delta(init, [s1, s2], width=8).view(np.uint32)
+    assert wrong.tolist() != got.tolist()
+    h = shard.merge_hash_additive({b"k": init.tobytes()}, [{b"k": s1.tobytes()}, {b"k": s2.tobytes()}], 8, width=4)
+    assert np.frombuffer(h[b"k"], np.uint32).tolist() == got.tolist()
+    assert shard.counter_width(12) == 4 and shard.counter_width(16) == 8
+    with pytest.raises(ValueError):
+        shard.counter_width(6)
