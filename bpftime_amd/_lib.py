@@ -115,6 +115,13 @@ SIGNATURES = [
     ("bpftime_amd_syscall_detach", C.c_int, [C.c_int]),
     ("bpftime_amd_syscall_dispatch", C.c_int64, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]),
     ("bpftime_amd_handle_sysbpf", C.c_long, [C.c_int, C.c_void_p, C.c_uint32]),
+    ("bpftime_map_get_info", C.c_int, [C.c_int, C.POINTER(BpfMapAttr), C.POINTER(C.c_char_p),
+                                        C.POINTER(C.c_int)]),
+    ("bpftime_get_array_map_raw_data", C.c_void_p, [C.c_int]),
+    ("bpftime_amd_map_msync", C.c_int, [C.c_int]),
+    ("bpftime_amd_perf_event_syscall", C.c_int, [C.c_int, C.c_int64]),
+    ("bpftime_is_perf_event_fd", C.c_int, [C.c_int]),
+    ("bpftime_attach_perf_to_bpf", C.c_int, [C.c_int, C.c_int]),
     ("bpftime_amd_merge_delta_u64", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     ("bpftime_amd_merge_delta", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32]),
     ("bpftime_amd_device_count", C.c_int, []),

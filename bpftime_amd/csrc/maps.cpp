@@ -10,6 +10,7 @@
 // race a running batch (the reference's syscall path likewise takes the map
 // lock, map_handler.hpp:45-62).
 #include <errno.h>
+#include <sys/mman.h>
 #include <stdlib.h>
 #include <string.h>
 #include <set>
@@ -515,6 +516,12 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
   m.value_size = attr.value_size;
   m.max_entries = attr.max_ents;
   m.flags = attr.flags;
+  m.ifindex = attr.ifindex;
+  m.btf_vmlinux_value_type_id = attr.btf_vmlinux_value_type_id;
+  m.btf_id = attr.btf_id;
+  m.btf_key_type_id = attr.btf_key_type_id;
+  m.btf_value_type_id = attr.btf_value_type_id;
+  m.map_extra = attr.map_extra;
   DMap &d = m.d;
   d.type = m.type;
   d.key_size = m.key_size;
@@ -993,31 +1000,53 @@ int bpftime_map_get_next_key(int fd, const void *key, void *next_key) {
   return -1;
 }
 
+static void drop_host_view(Runtime &r, int fd) {
+  MapRec &m = r.maps[fd];
+  if (m.host_view) munmap(m.host_view, m.host_view_bytes);
+  m.host_view = nullptr;
+  m.host_view_bytes = 0;
+  m.host_shadow.clear();
+  r.host_views.erase(fd);
+}
+
 void bpftime_close(int fd) {
   Runtime &r = rt();
-  std::lock_guard<std::mutex> g(r.mu);
-  if (fd < 0 || fd >= (int)kMaxFds) return;
-  r.prog_gen++;
-  if (r.kind[fd] == HKind::MAP) {
-    r.maps[fd] = MapRec();
-    r.push_map(fd);
-  } else if (r.kind[fd] == HKind::PROG) {
-    r.progs[fd] = ProgRec();
-  } else if (r.kind[fd] == HKind::LINK) {
-    r.links[fd] = LinkRec();
+  int detach = 0;
+  {
+    std::lock_guard<std::mutex> g(r.mu);
+    if (fd < 0 || fd >= (int)kMaxFds) return;
+    r.prog_gen++;
+    if (r.kind[fd] == HKind::MAP) {
+      drop_host_view(r, fd);
+      r.maps[fd] = MapRec();
+      r.push_map(fd);
+    } else if (r.kind[fd] == HKind::PROG) {
+      r.progs[fd] = ProgRec();
+    } else if (r.kind[fd] == HKind::LINK) {
+      detach = r.links[fd].attach_id;
+      r.links[fd] = LinkRec();
+    } else if (r.kind[fd] == HKind::PERF) {
+      r.perfs[fd] = PerfRec();
+    }
+    r.kind[fd] = HKind::NONE;
   }
-  r.kind[fd] = HKind::NONE;
+  if (detach) bpftime_amd_syscall_detach(detach);  // a perf link: its syscall attachment
 }
 
 void bpftime_amd_reset(void) {
   Runtime &r = rt();
   std::lock_guard<std::mutex> g(r.mu);
+  std::vector<int> detach;
   for (uint32_t i = 0; i < kMaxFds; i++) {
+    if (r.kind[i] == HKind::MAP) drop_host_view(r, (int)i);
+    if (r.kind[i] == HKind::LINK && r.links[i].attach_id) detach.push_back(r.links[i].attach_id);
     r.kind[i] = HKind::NONE;
     r.maps[i] = MapRec();
     r.progs[i] = ProgRec();
     r.links[i] = LinkRec();
+    r.perfs[i] = PerfRec();
   }
+  for (int id : detach) bpftime_amd_syscall_detach(id);
   if (r.d_maptab) hipMemset(r.d_maptab, 0, sizeof(DMap) * kMaxFds);
   r.arena_used = 0;
   r.prog_gen++;  // tail-call images linked before the reset relink
@@ -1200,6 +1229,164 @@ int bpftime_amd_xdp_links(int *link_fds, int *prog_fds, uint32_t *ifindexes, int
     n++;
   }
   return n;
+}
+
+// ---- map info (bpftime_shm.cpp:287-306) -------------------------------------
+int bpftime_map_get_info(int fd, struct bpf_map_attr *out_attr, const char **out_name, int *type) {
+  MapRec *m = map_of(fd);
+  if (!m) {
+    errno = ENOENT;
+    return -1;
+  }
+  if (out_attr) {
+    memset(out_attr, 0, sizeof(*out_attr));
+    out_attr->type = (int)m->type;
+    out_attr->key_size = m->key_size;
+    out_attr->value_size = m->value_size;
+    out_attr->max_ents = m->max_entries;
+    out_attr->flags = m->flags;
+    out_attr->ifindex = m->ifindex;
+    out_attr->btf_vmlinux_value_type_id = m->btf_vmlinux_value_type_id;
+    out_attr->btf_id = m->btf_id;
+    out_attr->btf_key_type_id = m->btf_key_type_id;
+    out_attr->btf_value_type_id = m->btf_value_type_id;
+    out_attr->map_extra = m->map_extra;
+  }
+  if (out_name) *out_name = m->name.c_str();
+  if (type) *type = (int)m->type;
+  return 0;
+}
+
+// ---- host views of ARRAY maps (bpftime_shm.cpp:347-353 via the mocked
+// mmap64, syscall_context.cpp:915-920) ---------------------------------------
+// The reference hands a loader the array's bytes in its shared-memory
+// segment.  Here they live in HBM: the view is page-aligned host memory
+// holding the same bytes, exchanged with the device at batch boundaries --
+// what a host write changed reaches the device before the next launch, what
+// a batch changed reaches the view when a synchronous batch returns or on
+// bpftime_amd_map_msync.
+void *bpftime_get_array_map_raw_data(int fd) {
+  Runtime &r = rt();
+  std::lock_guard<std::mutex> g(r.mu);
+  MapRec *m = map_of(fd);
+  if (!m || m->type != MT_ARRAY) {
+    errno = EINVAL;
+    return nullptr;
+  }
+  if (m->host_view) return m->host_view;
+  const uint64_t pg = 4096, len = std::max<uint64_t>(pg, (m->bytes + pg - 1) / pg * pg);
+  void *p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) {
+    errno = ENOMEM;
+    return nullptr;
+  }
+  m->host_shadow.resize(m->bytes);
+  if (m->bytes && hipMemcpy(m->host_shadow.data(), (void *)m->d.data, m->bytes, hipMemcpyDeviceToHost) != hipSuccess) {
+    munmap(p, len);
+    errno = EIO;
+    return nullptr;
+  }
+  memcpy(p, m->host_shadow.data(), m->bytes);
+  m->host_view = (uint8_t *)p;
+  m->host_view_bytes = len;
+  r.host_views.insert(fd);
+  return p;
+}
+
+// host writes -> device: the bytes that differ from the last exchange
+static int view_push(MapRec &m) {
+  uint64_t lo = m.bytes, hi = 0;
+  for (uint64_t i = 0; i < m.bytes; i++)
+    if (m.host_view[i] != m.host_shadow[i]) {
+      lo = std::min(lo, i);
+      hi = i + 1;
+    }
+  if (lo >= hi) return 0;
+  if (hipMemcpy((void *)(m.d.data + lo), m.host_view + lo, hi - lo, hipMemcpyHostToDevice) != hipSuccess) return -1;
+  memcpy(m.host_shadow.data() + lo, m.host_view + lo, hi - lo);
+  return 0;
+}
+
+static int view_pull(MapRec &m) {
+  if (hipMemcpy(m.host_shadow.data(), (void *)m.d.data, m.bytes, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  memcpy(m.host_view, m.host_shadow.data(), m.bytes);
+  return 0;
+}
+
+int Runtime::host_views_push() {
+  std::lock_guard<std::mutex> g(mu);
+  for (int fd : host_views)
+    if (view_push(maps[fd]) < 0) return -1;
+  return 0;
+}
+
+int Runtime::host_views_pull() {
+  std::lock_guard<std::mutex> g(mu);
+  for (int fd : host_views)
+    if (view_pull(maps[fd]) < 0) return -1;
+  return 0;
+}
+
+int bpftime_amd_map_msync(int fd) {
+  Runtime &r = rt();
+  std::lock_guard<std::mutex> g(r.mu);
+  MapRec *m = map_of(fd);
+  if (!m || !m->host_view) {
+    errno = EINVAL;
+    return -1;
+  }
+  if (hipDeviceSynchronize() != hipSuccess) return -1;  // batches still running first
+  return view_push(*m) < 0 || view_pull(*m) < 0 ? -1 : 0;
+}
+
+// ---- tracepoint perf events + BPF_PROG_ATTACH (bpftime_shm.cpp:249-253,
+// bpftime_shm_internal.cpp:282-314) -----------------------------------------
+int bpftime_amd_perf_event_syscall(int fd, int64_t sys_nr) {
+  Runtime &r = rt();
+  std::lock_guard<std::mutex> g(r.mu);
+  if (sys_nr < -1) {
+    errno = EINVAL;
+    return -1;
+  }
+  fd = alloc_fd(fd);
+  if (fd < 0) return -1;
+  r.perfs[fd].sys_nr = sys_nr;
+  r.kind[fd] = HKind::PERF;
+  return fd;
+}
+
+int bpftime_is_perf_event_fd(int fd) { return fd >= 0 && fd < (int)kMaxFds && rt().kind[fd] == HKind::PERF; }
+
+int bpftime_attach_perf_to_bpf(int perf_fd, int bpf_fd) {
+  Runtime &r = rt();
+  int64_t nr;
+  {
+    std::lock_guard<std::mutex> g(r.mu);
+    if (!bpftime_is_perf_event_fd(perf_fd)) {  // "Fd is not a perf fd"
+      errno = ENOENT;
+      return -1;
+    }
+    if (bpf_fd < 0 || bpf_fd >= (int)kMaxFds || r.kind[bpf_fd] != HKind::PROG) {
+      errno = ENOENT;
+      return -1;
+    }
+    nr = r.perfs[perf_fd].sys_nr;
+  }
+  const int id = bpftime_amd_syscall_attach(bpf_fd, nr);  // instantiates the program (outside the lock)
+  if (id < 0) return -1;
+  std::lock_guard<std::mutex> g(r.mu);
+  const int fd = alloc_fd(-1);
+  if (fd < 0) {
+    bpftime_amd_syscall_detach(id);
+    return -1;
+  }
+  LinkRec l;
+  l.prog_fd = (uint32_t)bpf_fd;
+  l.target = (uint32_t)perf_fd;
+  l.attach_id = id;
+  r.links[fd] = l;
+  r.kind[fd] = HKind::LINK;
+  return fd;
 }
 
 // ---- host merge ------------------------------------------------------------

@@ -24,6 +24,21 @@ struct MapRec {
   uint64_t ix_addr = 0;    // hash lookup index storage (common.hpp ix_pos), 0 = none
   bool ix_valid = false;   // d.ix = ix_addr while the index holds exactly the reachable keys
   std::shared_ptr<struct LpmTrie> lpm;  // LPM_TRIE: the authoritative host trie
+  // BPF_MAP_CREATE attributes as given (BPF_OBJ_GET_INFO_BY_FD reports them)
+  uint32_t ifindex = 0, btf_vmlinux_value_type_id = 0, btf_id = 0, btf_key_type_id = 0, btf_value_type_id = 0;
+  uint64_t map_extra = 0;
+  // host view of an ARRAY map (bpftime_get_array_map_raw_data, the mmap a
+  // libbpf loader makes of .bss / .data): page-aligned host bytes kept
+  // coherent with the device copy at batch boundaries (maps.cpp host_view_*)
+  uint8_t *host_view = nullptr;
+  uint64_t host_view_bytes = 0;
+  std::vector<uint8_t> host_shadow;  // the bytes last exchanged with the device
+};
+
+// A tracepoint perf event (perf_event_open of a syscall sys_enter
+// tracepoint, the target BPF_PROG_ATTACH links a program to)
+struct PerfRec {
+  int64_t sys_nr = -1;  // -1: every syscall (raw_syscalls:sys_enter)
 };
 
 struct ProgRec {
@@ -34,9 +49,10 @@ struct ProgRec {
 
 struct LinkRec {
   uint32_t prog_fd = 0, target = 0, attach_type = 0, flags = 0;
+  int attach_id = 0;  // a perf link: its syscall attachment (syscall_dispatch.cpp)
 };
 
-enum class HKind : uint8_t { NONE, MAP, PROG, LINK };
+enum class HKind : uint8_t { NONE, MAP, PROG, LINK, PERF };
 
 struct Runtime {
   std::mutex mu;
@@ -44,6 +60,12 @@ struct Runtime {
   std::vector<MapRec> maps = std::vector<MapRec>(kMaxFds);
   std::vector<ProgRec> progs = std::vector<ProgRec>(kMaxFds);
   std::vector<LinkRec> links = std::vector<LinkRec>(kMaxFds);
+  std::vector<PerfRec> perfs = std::vector<PerfRec>(kMaxFds);
+  std::set<int> host_views;     // ARRAY maps with a host view
+  // before a launch: host writes to host views reach the device; after a
+  // synchronous batch (or bpftime_amd_map_msync): device bytes reach them
+  int host_views_push();
+  int host_views_pull();
   int device = -1;
   DMap *d_maptab = nullptr;     // device table indexed by fd
   uint8_t *arena = nullptr;     // device map arena

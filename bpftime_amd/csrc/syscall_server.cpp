@@ -5,9 +5,12 @@
 // over this runtime's records: an unmodified libbpf loader whose bpf()
 // calls an LD_PRELOAD shim forwards here creates its maps in HBM, its
 // programs and its BPF_XDP links at fds this runtime allocates, and reads
-// maps back with the syscall-side semantics (from_syscall = true).
+// maps back with the syscall-side semantics (from_syscall = true), and links
+// programs to syscall tracepoint perf events (BPF_PROG_ATTACH).
 #include <errno.h>
 #include <linux/bpf.h>
+#include <stddef.h>
+#include <stdint.h>
 #include <string.h>
 
 #include "../../include/bpftime_amd.h"
@@ -73,6 +76,44 @@ extern "C" long bpftime_amd_handle_sysbpf(int cmd, void *attr_, uint32_t size) {
     }
     case BPF_MAP_FREEZE:  // :669-678: accepted, not implemented
       return 0;
+    case BPF_MAP_LOOKUP_AND_DELETE_ELEM:  // :540-551 -> bpf_map_handler::map_pop_elem
+      // (map_handler.cpp:1411-1434): queue / stack maps only, -ENOTSUP for
+      // every other map type; -1 for an fd without a map handler
+      if (!bpftime_is_map_fd((int)attr->map_fd)) return -1;
+      return -ENOTSUP;
+    case BPF_OBJ_GET_INFO_BY_FD: {  // :679-722
+      const int fd = (int)attr->info.bpf_fd;
+      if (bpftime_is_map_fd(fd)) {
+        struct bpf_map_attr a;
+        const char *name = nullptr;
+        int type = 0;
+        if (bpftime_map_get_info(fd, &a, &name, &type) < 0) return -1;
+        struct bpf_map_info *p = (struct bpf_map_info *)(uintptr_t)attr->info.info;
+        p->btf_id = a.btf_id;
+        p->btf_key_type_id = a.btf_key_type_id;
+        p->btf_value_type_id = a.btf_value_type_id;
+        p->type = (uint32_t)type;
+        p->value_size = a.value_size;
+        p->btf_vmlinux_value_type_id = a.btf_vmlinux_value_type_id;
+        p->key_size = a.key_size;
+        p->id = (uint32_t)fd;
+        p->ifindex = a.ifindex;
+        // map_extra follows btf_value_type_id and a pad word in the kernel
+        // ABI (newer than this image's linux/bpf.h): written when the
+        // caller's buffer has room for it
+        const size_t xoff = (offsetof(struct bpf_map_info, btf_value_type_id) + 4 + 7) & ~(size_t)7;
+        if (attr->info.info_len >= xoff + 8) memcpy((uint8_t *)p + xoff, &a.map_extra, 8);
+        p->max_entries = a.max_ents;
+        p->map_flags = (uint32_t)a.flags;
+        strncpy(p->name, name ? name : "", sizeof(p->name) - 1);
+      } else if (bpftime_is_prog_fd(fd)) {
+        struct bpf_prog_info *p = (struct bpf_prog_info *)(uintptr_t)attr->info.info;
+        p->id = (uint32_t)fd;
+      }
+      return 0;
+    }
+    case BPF_PROG_ATTACH:  // :723-735 -> bpftime_attach_perf_to_bpf(target perf fd, prog fd)
+      return bpftime_attach_perf_to_bpf((int)attr->target_fd, (int)attr->attach_bpf_fd);
   }
   errno = ENOTSUP;  // commands the data path does not serve
   return -1;

@@ -511,6 +511,10 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       return -1;
     }
   }
+  if (r.host_views_push() < 0) {  // host writes to mmap'd array maps first
+    error = "host view upload failed";
+    return -1;
+  }
   hipError_t e = bpftime_amd_launch_interp(&p, b->ctx_kind, prog.big_stack, grid, ordered ? 1 : 0, s);
   if (e == hipSuccess && p.flush_log) e = bpftime_amd_launch_merge(p.flush_log, p.log_words, grid, s);
   if (e != hipSuccess) {
@@ -520,7 +524,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   if (b->flags & EBPF_BATCH_SYNC) {
     uint32_t failed = 0;
     if (hipMemcpyAsync(&failed, err, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess) {
+        hipStreamSynchronize(s) != hipSuccess || r.host_views_pull() < 0) {
       error = "batch sync failed";
       return -1;
     }

@@ -67,10 +67,32 @@ int bpftime_is_array_map(int fd);
 int bpftime_is_prog_fd(int fd);
 int bpftime_find_minimal_unused_fd(void);
 void bpftime_close(int fd);
+/* bpftime_shm.cpp:287-306: a map's creation attributes and name; -1 +
+ * ENOENT for a non-map fd */
+int bpftime_map_get_info(int fd, struct bpf_map_attr *out_attr, const char **out_name, int *type);
+/* bpftime_shm.cpp:347-353 (what the syscall server's mmap64 of an array map
+ * fd returns, syscall_context.cpp:915-920): a host view of an ARRAY map's
+ * bytes, page aligned, stable until the map is closed.  The device holds the
+ * map: host writes to the view reach it before the next launch; the view
+ * receives the device bytes when a synchronous batch (EBPF_BATCH_SYNC,
+ * ebpf_exec) returns and on bpftime_amd_map_msync.  NULL + EINVAL for other
+ * maps. */
+void *bpftime_get_array_map_raw_data(int fd);
+int bpftime_amd_map_msync(int fd); /* push host writes, wait for the device, pull; 0 / -1 */
 
 /* ---- progs / links (bpftime_shm.hpp:303-309) ---- */
 int bpftime_progs_create(int fd, const void *insns, size_t insn_cnt, const char *prog_name, int prog_type);
 int bpftime_link_create(int fd, struct bpf_link_create_args *args);
+/* A syscall sys_enter tracepoint perf event (what perf_event_open of
+ * syscalls:sys_enter_<nr>, or raw_syscalls:sys_enter for sys_nr = -1,
+ * creates in the reference's syscall server): a new fd, or `fd` when >= 0. */
+int bpftime_amd_perf_event_syscall(int fd, int64_t sys_nr);
+int bpftime_is_perf_event_fd(int fd);
+/* bpftime_shm.cpp:249-253 (BPF_PROG_ATTACH): link prog bpf_fd to the perf
+ * event: a link fd whose close detaches it; the program then runs in
+ * bpftime_amd_syscall_dispatch.  -1 + ENOENT when perf_fd is not a perf
+ * event or bpf_fd not a program. */
+int bpftime_attach_perf_to_bpf(int perf_fd, int bpf_fd);
 
 /* ---- bpf(2) commands from an interposed loader ----
  * syscall_context::handle_sysbpf's userspace branch
