@@ -122,6 +122,15 @@ SIGNATURES = [
     ("bpftime_amd_perf_event_syscall", C.c_int, [C.c_int, C.c_int64]),
     ("bpftime_is_perf_event_fd", C.c_int, [C.c_int]),
     ("bpftime_attach_perf_to_bpf", C.c_int, [C.c_int, C.c_int]),
+    ("bpftime_amd_attach_create", C.c_void_p, [C.c_int, C.c_int]),
+    ("bpftime_amd_attach_run", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint64)]),
+    ("bpftime_amd_attach_run_batch", C.c_int, [C.c_void_p, C.POINTER(EbpfBatch)]),
+    ("bpftime_amd_attach_destroy", None, [C.c_void_p]),
+    ("bpftime_amd_simple_attach_impl_create", C.c_int, [C.c_int, C.c_void_p]),
+    ("bpftime_amd_simple_attach", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_int]),
+    ("bpftime_amd_simple_detach", C.c_int, [C.c_int, C.c_int]),
+    ("bpftime_amd_simple_trigger", C.c_int, [C.c_int, C.c_void_p]),
+    ("bpftime_amd_simple_attach_impl_destroy", C.c_int, [C.c_int]),
     ("bpftime_amd_merge_delta_u64", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     ("bpftime_amd_merge_delta", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32]),
     ("bpftime_amd_device_count", C.c_int, []),

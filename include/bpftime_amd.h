@@ -209,6 +209,32 @@ int bpftime_amd_syscall_attach(int prog_fd, int64_t sys_nr);   /* attach id or -
 int bpftime_amd_syscall_detach(int id);
 int64_t bpftime_amd_syscall_dispatch(const void *records, uint64_t n, uint32_t flags, void *stream);
 
+/* ---- attach plugins (attach/base_attach_impl/base_attach_impl.hpp:24-71,
+ * attach/simple_attach_impl/simple_attach_impl.cpp:7-55; csrc/attach.cpp) ----
+ * An attach entry is a program loaded on the device.  bpftime_amd_attach_run
+ * has the shape of ebpf_run_callback, int(void *memory, size_t memory_size,
+ * uint64_t *return_value), with the entry as a leading context argument, so a
+ * base_attach_impl can bind it as its callback: one unit,
+ * bpftime_prog_exec's contract.  bpftime_amd_attach_run_batch runs the entry
+ * over a device batch (ebpf_exec_batch's contract). */
+struct bpftime_amd_attach;
+struct bpftime_amd_attach *bpftime_amd_attach_create(int prog_fd, int ctx_kind); /* ctx_kind -1: from the prog type */
+int bpftime_amd_attach_run(void *attach, void *memory, size_t memory_size, uint64_t *return_value);
+int bpftime_amd_attach_run_batch(struct bpftime_amd_attach *attach, const struct ebpf_batch *batch);
+void bpftime_amd_attach_destroy(struct bpftime_amd_attach *attach);
+/* simple_attach_impl over device batches: create an impl for one attach
+ * type with a callback; attach one program (a second attach, or a mismatched
+ * type, fails: -1); trigger calls cb(attach-time argument, trigger argument,
+ * the attach entry) and returns its result, or 1 when nothing is attached;
+ * detach by the id attach returned. */
+typedef int (*bpftime_amd_simple_callback)(const char *argument, void *trigger_argument,
+                                           struct bpftime_amd_attach *attach);
+int bpftime_amd_simple_attach_impl_create(int attach_type, bpftime_amd_simple_callback cb);
+int bpftime_amd_simple_attach(int impl, int prog_fd, int ctx_kind, const char *argument, int attach_type);
+int bpftime_amd_simple_detach(int impl, int id);
+int bpftime_amd_simple_trigger(int impl, void *trigger_argument);
+int bpftime_amd_simple_attach_impl_destroy(int impl);
+
 /* ---- host merge of per-GPU map shards ---- */
 /* acc += shard - init over u64 words (array counters, additive rule) */
 int bpftime_amd_merge_delta_u64(void *acc, const void *init, const void *shard, uint64_t bytes);
