@@ -75,6 +75,7 @@ constexpr uint32_t MT_ARRAY = 2;
 constexpr uint32_t MT_PROG_ARRAY = 3;
 constexpr uint32_t MT_PERCPU_HASH = 5;
 constexpr uint32_t MT_PERCPU_ARRAY = 6;
+constexpr uint32_t MT_LRU_HASH = 9;
 constexpr uint32_t MT_LPM_TRIE = 11;
 constexpr uint32_t MT_RINGBUF = 27;
 
@@ -85,6 +86,12 @@ constexpr uint32_t MT_RINGBUF = 27;
 //                  [u32 state][u32 pad][key, padded to 8][value(s), padded to 8]
 //                  state 0 = empty, 1 = filled, 2 = being written
 //                  ix: lookup index beside that layout (see ix_pos), 0 = none
+//   LRU_HASH       the HASH slot layout over nbuckets = next_prime(2 x
+//                  max_entries + 1), state 3 = tombstone (deleted / evicted;
+//                  probes go past it, inserts reuse it); at count_addr the u64
+//                  element count and (+8) the u64 tombstone count, at
+//                  count_addr + 128 a u64 last-use stamp per bucket (see
+//                  lru_stamp); no lookup index
 //   RINGBUF        u64 consumer position at data, u64 producer position at
 //                  data + 128 (own cache lines), 2 x max_entries record bytes
 //                  at data + 256 (ringbuf_map.cpp layout and record format)
@@ -126,6 +133,20 @@ inline BA_HD uint32_t ix_pos(uint64_t h, uint32_t mask) {
   return (g ^ (g >> 16)) & mask;
 }
 constexpr uint32_t kIxProbes = 8;  // index probes before the reference probe
+
+// LRU_HASH recency (lru_var_hash_map.cpp keeps a doubly linked list, head =
+// most recently used).  Here every element carries the stamp of its last
+// use, and the list order is the stamp order: move_to_head = a larger stamp,
+// the tail = the smallest.  A stamp is {sequence:24 | unit:32 | op:8}: the
+// sequence counts launches and host-side operations (Runtime::lru_seq), the
+// unit is the unit's index in its batch, the op counts the unit's LRU
+// operations.  Units of a parallel batch raise a stamp with an atomic max, so
+// after the batch every element holds the stamp of its last use in unit
+// order -- the order a serial run of the batch leaves.
+constexpr uint32_t kLruUnitShift = 8;
+constexpr uint32_t kLruSeqShift = 40;
+constexpr uint64_t kLruSeqLimit = 1ull << 23;  // renumber the stamps before the sequence gets here
+constexpr uint32_t kLruScan = 256;             // parallel batches: buckets examined per eviction
 
 // bpf_tail_call (helper 12, bpf_helper.cpp:568-650).  The reference runs the
 // target as a nested exec over a 64-B copy of the ctx and returns its r0 to
@@ -189,6 +210,7 @@ struct KParams {
   uint32_t log_words;     // u64 words per block: count, then {tag, delta} pairs
   uint64_t *lane_scratch; // a u64 per lane of the grid (PROG_ARRAY lookups hand out a copy there), or nullptr
   uint32_t dbg;           // BPFTIME_AMD_DBG experiment bits (0 in production)
+  uint64_t lru_seq;       // this launch's LRU stamp sequence (common.hpp kLruSeqShift)
 };
 
 // Block-end counter deltas.  Every block holds its counter deltas (the wave

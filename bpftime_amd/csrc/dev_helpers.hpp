@@ -226,6 +226,194 @@ __device__ uint64_t hash_find(const DMap &m, uint64_t key, bool insert, uint64_t
   }
 }
 
+// ---------------------------------------------------------------------------
+// LRU hash (runtime/src/bpf_map/userspace/lru_var_hash_map.cpp) over the
+// HASH slot layout with tombstones and per-bucket last-use stamps (common.hpp
+// DMap, kLruSeqShift).  Every state and key read is made at the coherence
+// point: slots change owner within a launch (evictions, deletions, reuse).
+//   lookup  (:27-41)  a hit raises the element's stamp (move_to_head)
+//   update  (:43-90)  exact flags 0/1/2; an existing key: value + stamp; a new
+//                     key claims the first tombstone / empty bucket of its
+//                     probe, and past max_entries evicts the smallest stamp:
+//                     over every bucket when the batch is ORDERED (the
+//                     reference's list tail), over kLruScan buckets from a
+//                     hashed start in parallel batches
+//   delete  (:92-103) the element becomes a tombstone, ENOENT when absent
+// Two parallel inserts of one key converge on one bucket (the first free
+// bucket of the same probe), except when a deletion or eviction frees an
+// earlier bucket between their probes; the later-probing copy then folds
+// itself into the earlier one after publishing (lru_dedup).
+// ---------------------------------------------------------------------------
+constexpr uint32_t ST_TOMB = 3;
+
+__device__ __forceinline__ uint64_t lru_stamp_at(const DMap &m, uint64_t idx) { return m.count_addr + 128 + 8 * idx; }
+
+__device__ __forceinline__ void lru_touch(const DMap &m, uint64_t idx, uint64_t stamp) {
+  __hip_atomic_fetch_max(G64(lru_stamp_at(m, idx)), (unsigned long long)stamp, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the FILLED bucket holding key (-1 absent, -2 gave up on a BUSY bucket);
+// *free_idx = the first tombstone or empty bucket of the probe (-1 none)
+__device__ int64_t lru_probe(const DMap &m, uint64_t key, int64_t *free_idx, uint32_t *free_st) {
+  const uint64_t nb = m.nbuckets;
+  uint64_t idx = key_hash(key, m.key_size) % nb;
+  const uint64_t start = idx;
+  *free_idx = -1;
+  *free_st = ST_EMPTY;
+  uint32_t spins = 0;
+  for (;;) {
+    const uint64_t s = m.data + idx * (uint64_t)m.slot_size;
+    const uint32_t st = acoh32(s);
+    if (st == ST_BUSY) {
+      if (++spins > (1u << 22)) return -2;  // bounded: never hang the GPU
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    if (st == ST_EMPTY || st == ST_TOMB) {
+      if (*free_idx < 0) {
+        *free_idx = (int64_t)idx;
+        *free_st = st;
+      }
+      if (st == ST_EMPTY) return -1;
+    } else if (key_eq(s + m.key_off, key, m.key_size, true)) {
+      return (int64_t)idx;
+    }
+    idx = idx + 1 == nb ? 0 : idx + 1;
+    if (idx == start) return -1;
+  }
+}
+
+__device__ __forceinline__ bool lru_kill(const DMap &m, uint64_t idx) {
+  uint32_t prev = ST_FILLED;
+  if (!__hip_atomic_compare_exchange_strong(G32(m.data + idx * (uint64_t)m.slot_size), &prev, ST_TOMB,
+                                            __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    return false;
+  __hip_atomic_fetch_add(G64(m.count_addr), ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(G64(m.count_addr + 8), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+// evict one element: the smallest stamp among the FILLED buckets examined
+__device__ bool lru_evict(const DMap &m, uint64_t h, uint64_t stamp, bool exact) {
+  const uint64_t nb = m.nbuckets;
+  const uint64_t span = exact || nb <= kLruScan ? nb : kLruScan;
+  for (uint32_t attempt = 0; attempt < 16; attempt++) {
+    const uint64_t start = span == nb ? 0 : ((h ^ (stamp * 0x9E3779B97F4A7C15ull)) + attempt * span) % nb;
+    int64_t best = -1;
+    uint64_t bs = ~0ull;
+    for (uint64_t k = 0, i = start; k < span; k++, i = i + 1 == nb ? 0 : i + 1) {
+      if (acoh32(m.data + i * (uint64_t)m.slot_size) != ST_FILLED) continue;
+      const uint64_t t = __hip_atomic_load(G64(lru_stamp_at(m, i)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t < bs) {
+        bs = t;
+        best = (int64_t)i;
+      }
+    }
+    if (best >= 0 && lru_kill(m, (uint64_t)best)) return true;
+  }
+  return false;
+}
+
+// After publishing bucket f for key: another copy of key on the probe
+// (possible only when a deletion or eviction freed an earlier bucket between
+// two inserts' probes) is resolved by probe position, the earlier copy
+// staying.  Each insert scans the whole probe once its own copy is visible,
+// so of two copies at least the later-scanning insert sees the other one.
+// The dropped copy's value is dropped with it, as if its insert had come
+// first and the other one had overwritten it.
+__device__ void lru_dedup(const DMap &m, uint64_t key, uint64_t f, uint64_t stamp) {
+  const uint64_t nb = m.nbuckets;
+  const uint64_t home = key_hash(key, m.key_size) % nb;
+  const uint64_t fdist = (f + nb - home) % nb;
+  uint64_t idx = home;
+  uint32_t spins = 0;
+  for (uint64_t k = 0; k < nb;) {
+    const uint64_t s = m.data + idx * (uint64_t)m.slot_size;
+    const uint32_t st = acoh32(s);
+    if (st == ST_BUSY && idx != f) {
+      if (++spins > (1u << 22)) return;
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    if (st == ST_EMPTY) return;
+    if (idx != f && st == ST_FILLED && key_eq(s + m.key_off, key, m.key_size, true)) {
+      if (k < fdist) {  // an earlier copy: this one goes
+        if (lru_kill(m, f)) lru_touch(m, idx, stamp);
+        return;
+      }
+      lru_kill(m, idx);  // a later copy goes
+    }
+    idx = idx + 1 == nb ? 0 : idx + 1;
+    k++;
+  }
+}
+
+__device__ uint64_t lru_lookup(const DMap &m, uint64_t key, uint64_t stamp) {
+  int64_t fi;
+  uint32_t fst;
+  const int64_t idx = lru_probe(m, key, &fi, &fst);
+  if (idx < 0) return 0;
+  lru_touch(m, (uint64_t)idx, stamp);
+  return m.data + (uint64_t)idx * m.slot_size + m.val_off;
+}
+
+__device__ uint64_t lru_update(const DMap &m, uint64_t key, uint64_t val, uint64_t flags, uint64_t stamp, bool exact,
+                               bool keep_existing) {
+  if (flags > 2) return (uint64_t)-1;  // is_good_update_flag (:8-11): EINVAL
+  for (uint32_t tries = 0; tries < 64; tries++) {
+    int64_t fi;
+    uint32_t fst;
+    const int64_t idx = lru_probe(m, key, &fi, &fst);
+    if (idx == -2) return (uint64_t)-1;
+    if (idx >= 0) {
+      if (flags == 1) return (uint64_t)-1;  // BPF_NOEXIST: EEXIST
+      if (!keep_existing) copy_bytes_publish(m.data + (uint64_t)idx * m.slot_size + m.val_off, val, m.value_size);
+      lru_touch(m, (uint64_t)idx, stamp);
+      return 0;
+    }
+    if (flags == 2) return (uint64_t)-1;  // BPF_EXIST: ENOENT
+    if (fi < 0) return (uint64_t)-1;      // no free bucket on the probe
+    const uint64_t s = m.data + (uint64_t)fi * m.slot_size;
+    uint32_t prev = fst;
+    if (!__hip_atomic_compare_exchange_strong(G32(s), &prev, ST_BUSY, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT))
+      continue;  // the bucket changed under the probe: probe again
+    if (fst == ST_TOMB)
+      __hip_atomic_fetch_add(G64(m.count_addr + 8), ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long c =
+        __hip_atomic_fetch_add(G64(m.count_addr), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c >= m.max_entries && !lru_evict(m, key_hash(key, m.key_size), stamp, exact)) {
+      // nothing evictable (every element in flight): give the bucket back
+      __hip_atomic_fetch_add(G64(m.count_addr), ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(G64(m.count_addr + 8), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(G32(s), ST_TOMB, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      return (uint64_t)-1;
+    }
+    copy_bytes_publish(s + m.key_off, key, m.key_size);
+    copy_bytes_publish(s + m.val_off, val, m.value_size);
+    __hip_atomic_store(G64(lru_stamp_at(m, (uint64_t)fi)), (unsigned long long)stamp, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // key / value / stamp before the state
+    __hip_atomic_store(G32(s), ST_FILLED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (!exact) lru_dedup(m, key, (uint64_t)fi, stamp);
+    return 0;
+  }
+  return (uint64_t)-1;
+}
+
+__device__ uint64_t lru_delete(const DMap &m, uint64_t key) {
+  int64_t fi;
+  uint32_t fst;
+  for (uint32_t tries = 0; tries < 64; tries++) {
+    const int64_t idx = lru_probe(m, key, &fi, &fst);
+    if (idx < 0) return (uint64_t)-1;  // ENOENT
+    if (lru_kill(m, (uint64_t)idx)) return 0;
+  }
+  return (uint64_t)-1;
+}
+
 // LPM trie lookup on the device replica: the walk of lpm_trie_map.cpp:
 // 192-264 (longest prefix match down the trie, the last non-intermediate
 // node on the path wins; an exact full-length match ends the walk).  The
@@ -366,11 +554,20 @@ __device__ uint64_t rb_output(const DMap *maps, uint64_t fd, uint64_t data, uint
 
 struct LaneEnv {
   uint64_t vcpu;
+  uint64_t lru_stamp;  // this unit's LRU stamp base (common.hpp kLruSeqShift)
+  uint32_t lru_ops;    // LRU operations the unit has made (the stamp's low byte)
+  bool exact;          // ORDERED batch: LRU evictions scan every bucket
   uint64_t scratch;  // this lane's scratch word (KParams::lane_scratch), 0 = none
   // last lookup miss (map fd, key hash) for the lookup_or_try_init race rule
   int32_t miss_fd;
   uint64_t miss_hash;
 };
+
+__device__ __forceinline__ uint64_t lru_next_stamp(LaneEnv &env) {
+  const uint32_t op = env.lru_ops < 255 ? env.lru_ops : 255;
+  env.lru_ops++;
+  return env.lru_stamp | op;
+}
 
 __device__ uint64_t helper_lookup(const DMap *maps, uint64_t fd, uint64_t key, LaneEnv &env) {
   if (fd >= kMaxFds) return 0;
@@ -401,6 +598,14 @@ __device__ uint64_t helper_lookup(const DMap *maps, uint64_t fd, uint64_t key, L
     }
     case MT_LPM_TRIE:
       return lpm_lookup(m, key);
+    case MT_LRU_HASH: {
+      const uint64_t v = lru_lookup(m, key, lru_next_stamp(env));
+      if (!v) {
+        env.miss_fd = (int32_t)fd;
+        env.miss_hash = key_hash(key, m.key_size);
+      }
+      return v;
+    }
     case MT_PROG_ARRAY: {  // prog_array.cpp:113-143: a copy of the slot's prog fd
       const int32_t k = (int32_t)*(const u32u *)key;
       if (k < 0 || (uint32_t)k >= m.max_entries) return 0;
@@ -464,6 +669,13 @@ __device__ uint64_t helper_update(const DMap *maps, uint64_t fd, uint64_t key, u
       env.miss_fd = -1;
       return 0;
     }
+    case MT_LRU_HASH: {
+      // the lookup-miss race of MT_HASH above: an existing element is not
+      // overwritten by the lane whose lookup of the key just missed
+      const bool race = env.miss_fd == (int32_t)fd && env.miss_hash == key_hash(key, m.key_size);
+      env.miss_fd = -1;
+      return lru_update(m, key, val, flags, lru_next_stamp(env), env.exact, race);
+    }
   }
   return (uint64_t)-1;
 }
@@ -496,6 +708,8 @@ __device__ uint64_t helper_delete(const DMap *maps, uint64_t fd, uint64_t key, L
       }
       return 0;
     }
+    case MT_LRU_HASH:
+      return lru_delete(m, key);
   }
   return (uint64_t)-1;
 }

@@ -556,6 +556,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
   SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(flush_log); SRV(log_words); SRP(lane_scratch);
+  SRV(lru_seq);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
 #undef SRP
 #undef SRV
@@ -644,6 +645,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const uint64_t vcpu = (p.first_unit + unit) / 64;
     int32_t miss_fd = -1;
     uint64_t miss_hash = 0;
+    uint32_t lru_ops = 0;
     uint32_t tdepth = 0;  // tail-call frames this lane has pushed
 
     // ---- per-unit setup: r1, r2, r10 (other registers zero) are set by the
@@ -812,6 +814,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         env.scratch = p.lane_scratch ? (uint64_t)(uintptr_t)(p.lane_scratch + (uint64_t)blockIdx.x * kBlock + tid) : 0;
         env.miss_fd = miss_fd;
         env.miss_hash = miss_hash;
+        env.lru_stamp = (p.lru_seq << kLruSeqShift) | ((unit & 0xffffffffull) << kLruUnitShift);
+        env.lru_ops = lru_ops;
+        env.exact = ordered;
         uint32_t cerr = E_OK;
         uint64_t *R = &Rf[tid];
         const uint64_t rv = call_helper(c.call_id, R[1 * kBlock], R[2 * kBlock], R[3 * kBlock], R[4 * kBlock],
@@ -820,6 +825,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         R[0] = rv;
         miss_fd = env.miss_fd;
         miss_hash = env.miss_hash;
+        lru_ops = env.lru_ops;
         if (cerr != E_OK) {
           c.err = cerr;
           c.alive = false;

@@ -1012,6 +1012,26 @@ static std::vector<bool> counter_nodefer(const std::vector<DInsn> &p, const std:
   return nodefer;
 }
 
+// A hash element's bucket can change owner while a launch runs: LRU inserts
+// evict, and a deleted key's bucket is reused.  A counter add held until its
+// block ends could then land in another key's value, so adds into such maps
+// go to memory at once.
+static bool rebinds(const std::vector<DInsn> &p, const PVal &b, bool may_delete) {
+  auto moves = [&](const MapRec *m) {
+    return m && (m->type == MT_LRU_HASH || (may_delete && (m->type == MT_HASH || m->type == MT_PERCPU_HASH)));
+  };
+  if (b.kind == P_MAPVAL) return moves(map_rec(b.id));
+  if (b.kind != P_CONST) return false;
+  const Loc l = loc_of(p, b, 0, 8);
+  Runtime &r = rt();
+  for (uint32_t fd = 0; fd < kMaxFds; fd++) {
+    if (r.kind[fd] != HKind::MAP || !moves(&r.maps[fd])) continue;
+    const MapRec &m = r.maps[fd];
+    if (l.lo < (int64_t)(m.d.data + m.bytes) && (int64_t)m.d.data < l.hi) return true;
+  }
+  return false;
+}
+
 static uint32_t direct_add_handler(const DInsn &d) {
   const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
   if (sz != 4 && sz != 8) return F_SLOW;
@@ -1076,7 +1096,8 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
   }
   const std::vector<bool> nodefer = counter_nodefer(prog, in);
   for (size_t i = 0; i < prog.size(); i++)
-    if (out.add_site[i] && (nodefer[i] || (prog[i].aux & A_FETCH))) make_direct(i);
+    if (out.add_site[i] && (nodefer[i] || (prog[i].aux & A_FETCH) || rebinds(prog, in[i][prog[i].dst], lo.may_delete)))
+      make_direct(i);
   // per-lane counter adds (fused counters, atomic adds without fetch) whose
   // target is not a wave-uniform constant use the LDS combining table
   bool comb = false;

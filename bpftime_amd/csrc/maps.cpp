@@ -150,6 +150,229 @@ static int64_t host_hash_find(const MapRec &m, const void *key, std::vector<uint
 }
 
 
+// ---- LRU hash (runtime/src/bpf_map/userspace/lru_var_hash_map.cpp) ---------
+// Host-side operations on the device table (common.hpp DMap LRU_HASH,
+// dev_helpers.hpp lru_*): the same probe, tombstones and stamps, with the
+// exact eviction of the reference (the smallest stamp over every bucket).
+static constexpr uint32_t kStTomb = 3;
+
+static uint64_t lru_host_stamp() { return (rt().lru_seq.fetch_add(1) + 1) << kLruSeqShift; }
+static uint64_t lru_stamp_addr(const MapRec &m, uint64_t i) { return m.d.count_addr + 128 + 8 * i; }
+static bool lru_write_stamp(const MapRec &m, uint64_t i, uint64_t st) {
+  return hipMemcpy((void *)lru_stamp_addr(m, i), &st, 8, hipMemcpyHostToDevice) == hipSuccess;
+}
+static uint64_t read_word(const MapRec &m, uint64_t off) {
+  uint64_t c = 0;
+  hipMemcpy(&c, (void *)(m.d.count_addr + off), 8, hipMemcpyDeviceToHost);
+  return c;
+}
+static void write_word(const MapRec &m, uint64_t off, uint64_t c) {
+  hipMemcpy((void *)(m.d.count_addr + off), &c, 8, hipMemcpyHostToDevice);
+}
+
+// the FILLED bucket holding key or -1; *free_idx = first tombstone / empty
+static int64_t lru_host_probe(const MapRec &m, const void *key, std::vector<uint8_t> &slot, int64_t *free_idx) {
+  const uint64_t nb = m.d.nbuckets;
+  uint64_t idx = hash_bytes(key, m.key_size) % nb, start = idx;
+  *free_idx = -1;
+  do {
+    if (!read_slot(m, idx, slot)) return -1;
+    uint32_t st;
+    memcpy(&st, slot.data(), 4);
+    if (st == 0 || st == kStTomb) {
+      if (*free_idx < 0) *free_idx = (int64_t)idx;
+      if (st == 0) return -1;
+    } else if (st == 1 && memcmp(slot.data() + m.d.key_off, key, m.key_size) == 0) {
+      return (int64_t)idx;
+    }
+    idx = (idx + 1) % nb;
+  } while (idx != start);
+  return -1;
+}
+
+static bool lru_download(const MapRec &m, std::vector<uint8_t> &tab, std::vector<uint64_t> &stamps) {
+  tab.resize(m.bytes);
+  stamps.resize(m.d.nbuckets);
+  return hipMemcpy(tab.data(), (void *)m.d.data, m.bytes, hipMemcpyDeviceToHost) == hipSuccess &&
+         hipMemcpy(stamps.data(), (void *)lru_stamp_addr(m, 0), 8 * m.d.nbuckets, hipMemcpyDeviceToHost) ==
+             hipSuccess;
+}
+static uint32_t tab_state(const MapRec &m, const std::vector<uint8_t> &tab, uint64_t i) {
+  uint32_t st;
+  memcpy(&st, tab.data() + i * m.d.slot_size, 4);
+  return st;
+}
+
+// evict the list tail (lru_var_hash_map.cpp:66-71): the smallest stamp
+static bool lru_host_evict(const MapRec &m) {
+  std::vector<uint8_t> tab;
+  std::vector<uint64_t> stamps;
+  if (!lru_download(m, tab, stamps)) return false;
+  int64_t best = -1;
+  for (uint64_t i = 0; i < m.d.nbuckets; i++)
+    if (tab_state(m, tab, i) == 1 && (best < 0 || stamps[i] < stamps[(uint64_t)best])) best = (int64_t)i;
+  if (best < 0) return false;
+  const uint32_t t = kStTomb;
+  if (hipMemcpy((void *)(m.d.data + (uint64_t)best * m.d.slot_size), &t, 4, hipMemcpyHostToDevice) != hipSuccess)
+    return false;
+  write_word(m, 0, read_word(m, 0) - 1);
+  write_word(m, 8, read_word(m, 8) + 1);
+  return true;
+}
+
+// rebuild the table without tombstones (elements keep their stamps); with
+// `renumber`, the stamps become their ranks (the recency order, below every
+// sequence-stamped use)
+static int lru_rebuild(const MapRec &m, bool renumber) {
+  std::vector<uint8_t> tab, out(m.bytes, 0);
+  std::vector<uint64_t> stamps, os(m.d.nbuckets, 0);
+  if (!lru_download(m, tab, stamps)) return -1;
+  const uint64_t nb = m.d.nbuckets, ss = m.d.slot_size;
+  std::vector<uint64_t> live;
+  for (uint64_t i = 0; i < nb; i++)
+    if (tab_state(m, tab, i) == 1) live.push_back(i);
+  if (renumber) {
+    std::vector<uint64_t> ord = live;
+    std::sort(ord.begin(), ord.end(), [&](uint64_t a, uint64_t b) { return stamps[a] < stamps[b]; });
+    for (uint64_t r = 0; r < ord.size(); r++) stamps[ord[r]] = r + 1;
+  }
+  for (uint64_t i : live) {
+    uint64_t j = hash_bytes(tab.data() + i * ss + m.d.key_off, m.key_size) % nb;
+    while (tab_state(m, out, j) != 0) j = (j + 1) % nb;
+    memcpy(out.data() + j * ss, tab.data() + i * ss, ss);
+    os[j] = stamps[i];
+  }
+  if (hipMemcpy((void *)m.d.data, out.data(), m.bytes, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy((void *)lru_stamp_addr(m, 0), os.data(), 8 * nb, hipMemcpyHostToDevice) != hipSuccess)
+    return -1;
+  write_word(m, 0, live.size());
+  write_word(m, 8, 0);
+  return 0;
+}
+
+static const void *lru_host_lookup(MapRec &m, const void *key) {  // :27-41
+  std::vector<uint8_t> slot;
+  int64_t fi;
+  const int64_t idx = key ? lru_host_probe(m, key, slot, &fi) : -1;
+  if (idx < 0) {
+    errno = ENOENT;
+    return nullptr;
+  }
+  if (!lru_write_stamp(m, (uint64_t)idx, lru_host_stamp())) return nullptr;  // move_to_head
+  tl_lookup_buf.assign(slot.begin() + m.d.val_off, slot.begin() + m.d.val_off + m.value_size);
+  return tl_lookup_buf.data();
+}
+
+static long lru_host_update(MapRec &m, const void *key, const void *value, uint64_t flags) {  // :43-90
+  if (flags > 2) {  // is_good_update_flag (:8-11): exactly BPF_ANY / BPF_NOEXIST / BPF_EXIST
+    errno = EINVAL;
+    return -1;
+  }
+  std::vector<uint8_t> slot;
+  int64_t fi;
+  int64_t idx = lru_host_probe(m, key, slot, &fi);
+  if (flags == 1 && idx >= 0) {
+    errno = EEXIST;
+    return -1;
+  }
+  if (flags == 2 && idx < 0) {
+    errno = ENOENT;
+    return -1;
+  }
+  if (idx >= 0) {  // a new value, moved to the head
+    memcpy(slot.data() + m.d.val_off, value, m.value_size);
+    if (!write_slot(m, (uint64_t)idx, slot) || !lru_write_stamp(m, (uint64_t)idx, lru_host_stamp())) return -1;
+    return 0;
+  }
+  if (read_word(m, 0) >= m.max_entries && !lru_host_evict(m)) {
+    errno = ENOMEM;
+    return -1;
+  }
+  if (fi < 0) {  // every bucket on the probe is taken: drop the tombstones
+    if (lru_rebuild(m, false) < 0) return -1;
+    lru_host_probe(m, key, slot, &fi);
+    if (fi < 0) {
+      errno = ENOMEM;
+      return -1;
+    }
+  }
+  std::vector<uint8_t> s(m.d.slot_size, 0);
+  read_slot(m, (uint64_t)fi, slot);
+  uint32_t was;
+  memcpy(&was, slot.data(), 4);
+  const uint32_t st = 1;
+  memcpy(s.data(), &st, 4);
+  memcpy(s.data() + m.d.key_off, key, m.key_size);
+  memcpy(s.data() + m.d.val_off, value, m.value_size);
+  if (!lru_write_stamp(m, (uint64_t)fi, lru_host_stamp()) || !write_slot(m, (uint64_t)fi, s)) return -1;
+  write_word(m, 0, read_word(m, 0) + 1);
+  if (was == kStTomb) write_word(m, 8, read_word(m, 8) - 1);
+  return 0;
+}
+
+static long lru_host_delete(MapRec &m, const void *key) {  // :92-103
+  std::vector<uint8_t> slot;
+  int64_t fi;
+  const int64_t idx = lru_host_probe(m, key, slot, &fi);
+  if (idx < 0) {
+    errno = ENOENT;
+    return -1;
+  }
+  const uint32_t t = kStTomb;
+  memcpy(slot.data(), &t, 4);
+  if (!write_slot(m, (uint64_t)idx, slot)) return -1;
+  write_word(m, 0, read_word(m, 0) - 1);
+  write_word(m, 8, read_word(m, 8) + 1);
+  return 0;
+}
+
+// :105-135 walks the unordered_map's order (not part of its contract: the
+// reference's tests compare visited sets); this walks buckets.  A key that
+// is not present restarts at the first key.
+static int lru_host_next_key(const MapRec &m, const void *key, void *next_key) {
+  std::vector<uint8_t> tab;
+  std::vector<uint64_t> stamps;
+  if (!next_key) {
+    errno = EINVAL;
+    return -1;
+  }
+  if (!lru_download(m, tab, stamps)) return -1;
+  uint64_t from = 0;
+  if (key) {
+    std::vector<uint8_t> slot;
+    int64_t fi;
+    const int64_t idx = lru_host_probe(m, key, slot, &fi);
+    if (idx >= 0) from = (uint64_t)idx + 1;
+  }
+  for (uint64_t i = from; i < m.d.nbuckets; i++)
+    if (tab_state(m, tab, i) == 1) {
+      memcpy(next_key, tab.data() + i * m.d.slot_size + m.d.key_off, m.key_size);
+      return 0;
+    }
+  errno = ENOENT;
+  return -1;
+}
+
+uint64_t Runtime::prepare_lru() {
+  std::lock_guard<std::mutex> g(mu);
+  if (!lru_maps.empty()) {
+    const bool renumber = lru_seq.load() >= kLruSeqLimit;
+    const bool check = renumber || ++lru_launches >= 16;
+    if (check) {
+      lru_launches = 0;
+      // no launch may run while tables move
+      if (hipDeviceSynchronize() != hipSuccess) return 0;
+      for (int fd : lru_maps) {
+        const MapRec &m = maps[fd];
+        if (renumber || read_word(m, 8) > (m.d.nbuckets - m.max_entries) / 2)
+          if (lru_rebuild(m, renumber) < 0) return 0;
+      }
+      if (renumber) lru_seq = 1;
+    }
+  }
+  return lru_seq.fetch_add(1) + 1;
+}
+
 // ---- LPM trie (runtime/src/bpf_map/userspace/lpm_trie_map.cpp) -------------
 // The host keeps the authoritative trie (same node structure and update /
 // logical-delete rules as the reference); the device holds a read-only
@@ -536,13 +759,15 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
       m.bytes = (uint64_t)m.value_size * m.max_entries * d.ncpu;
       break;
     case MT_HASH:
-    case MT_PERCPU_HASH: {
+    case MT_PERCPU_HASH:
+    case MT_LRU_HASH: {
       if (m.key_size == 0 || m.value_size == 0 || m.max_entries == 0) {
         errno = EINVAL;
         set_error("hash map needs key/value size and max_entries");
         return -1;
       }
-      d.nbuckets = next_prime(m.max_entries);
+      // LRU: room for the tombstones that evictions and deletions leave
+      d.nbuckets = next_prime(m.type == MT_LRU_HASH ? 2ull * m.max_entries + 1 : m.max_entries);
       d.key_off = 8;
       d.val_off = 8 + ((m.key_size + 7) & ~7u);
       uint64_t vbytes = (uint64_t)m.value_size * (m.type == MT_PERCPU_HASH ? d.ncpu : 1);
@@ -602,7 +827,10 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
       set_error("unsupported map type " + std::to_string(m.type));
       return -1;
   }
-  uint64_t extra = (m.type == MT_HASH || m.type == MT_PERCPU_HASH) ? 128 : 0;
+  // hash maps: a 128-B counter line; LRU maps: + a u64 stamp per bucket
+  uint64_t extra = (m.type == MT_HASH || m.type == MT_PERCPU_HASH) ? 128
+                   : m.type == MT_LRU_HASH                          ? 128 + 8ull * d.nbuckets
+                                                                    : 0;
   // PROG_ARRAY: a second copy of the slots after them, where device-side
   // map_lookup_elem hands out the looked-up fd (the reference returns a
   // thread-local copy, prog_array.cpp:113-143: a write through the pointer
@@ -625,7 +853,7 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
     const int32_t none = -1;
     if (hipMemcpy((void *)base, &none, 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
   }
-  if (extra && !getenv("BPFTIME_AMD_NO_HASH_INDEX")) {
+  if (extra && m.type != MT_LRU_HASH && !getenv("BPFTIME_AMD_NO_HASH_INDEX")) {
     // lookup index (common.hpp ix_pos): a power of two >= 2 x buckets, so
     // it is at most half full; an empty table's index is empty and valid
     uint64_t isz = 64;
@@ -640,6 +868,7 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
   }
   r.maps[fd] = m;
   r.kind[fd] = HKind::MAP;
+  if (m.type == MT_LRU_HASH) r.lru_maps.insert(fd);
   if (r.push_map(fd) < 0) return -1;
   return fd;
 }
@@ -747,6 +976,7 @@ const void *bpftime_map_lookup_elem(int fd, const void *key) {
     return nullptr;
   }
   if (m->type == MT_PROG_ARRAY) return prog_array_lookup(*m, key);
+  if (m->type == MT_LRU_HASH) return lru_host_lookup(*m, key);
   std::vector<uint8_t> &buf = tl_lookup_buf;
   switch (m->type) {
     case MT_ARRAY:
@@ -797,6 +1027,7 @@ long bpftime_map_update_elem(int fd, const void *key, const void *value, uint64_
     return -1;
   }
   if (m->type == MT_PROG_ARRAY) return prog_array_update(*m, key, value);
+  if (m->type == MT_LRU_HASH) return lru_host_update(*m, key, value, flags);
   uint64_t b = flags & 0xffffffffull;
   bool flags_ok = b == 0 || b == 1 || b == 2;  // map_common_def.hpp:83-94
   if (m->type == MT_LPM_TRIE) {
@@ -897,6 +1128,7 @@ long bpftime_map_delete_elem(int fd, const void *key) {
   MapRec *m = map_of(fd);
   if (!m) return -1;
   if (m->type == MT_PROG_ARRAY) return prog_array_delete(*m, key);
+  if (m->type == MT_LRU_HASH) return lru_host_delete(*m, key);
   if (m->type == MT_RINGBUF) {
     errno = ENOTSUP;
     return -1;
@@ -952,6 +1184,7 @@ int bpftime_map_get_next_key(int fd, const void *key, void *next_key) {
     return m->lpm->first_key((uint8_t *)next_key);
   }
   if (m->type == MT_PROG_ARRAY) return prog_array_next_key(*m, key, next_key);
+  if (m->type == MT_LRU_HASH) return lru_host_next_key(*m, key, next_key);
   switch (m->type) {
     case MT_ARRAY:
     case MT_PERCPU_ARRAY: {  // array_map.cpp:66-81
@@ -1018,6 +1251,7 @@ void bpftime_close(int fd) {
     r.prog_gen++;
     if (r.kind[fd] == HKind::MAP) {
       drop_host_view(r, fd);
+      r.lru_maps.erase(fd);
       r.maps[fd] = MapRec();
       r.push_map(fd);
     } else if (r.kind[fd] == HKind::PROG) {
@@ -1042,6 +1276,7 @@ void bpftime_amd_reset(void) {
     if (r.kind[i] == HKind::LINK && r.links[i].attach_id) detach.push_back(r.links[i].attach_id);
     r.kind[i] = HKind::NONE;
     r.maps[i] = MapRec();
+    r.lru_maps.erase((int)i);
     r.progs[i] = ProgRec();
     r.links[i] = LinkRec();
     r.perfs[i] = PerfRec();

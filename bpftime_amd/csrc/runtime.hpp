@@ -5,6 +5,7 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <set>
@@ -82,6 +83,13 @@ struct Runtime {
   // before a launch: a program that can delete invalidates every hash
   // lookup index; any other rebuilds the stale ones
   int prepare_ix(bool may_delete);
+  std::set<int> lru_maps;                // LRU_HASH maps
+  std::atomic<uint64_t> lru_seq{1};      // LRU stamp sequence: launches and host-side ops (common.hpp)
+  uint32_t lru_launches = 0;             // launches since the last tombstone check
+  // before a launch: renumbers the LRU stamps before the sequence runs out,
+  // compacts tombstone-heavy LRU tables now and then; returns the launch's
+  // stamp sequence (0 on failure)
+  uint64_t prepare_lru();
 };
 
 // hash lookup index upkeep for host-side writes (maps.cpp)

@@ -450,6 +450,11 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     error = "hash lookup index rebuild failed";
     return -1;
   }
+  p.lru_seq = r.prepare_lru();
+  if (!p.lru_seq) {
+    error = "LRU table upkeep failed";
+    return -1;
+  }
   const bool ordered = (b->flags & EBPF_BATCH_ORDERED) != 0;
   uint32_t grid = 1;
   if (!ordered) {

@@ -74,6 +74,7 @@ BPF_MAP_TYPE_ARRAY = 2
 BPF_MAP_TYPE_PROG_ARRAY = 3
 BPF_MAP_TYPE_PERCPU_HASH = 5
 BPF_MAP_TYPE_PERCPU_ARRAY = 6
+BPF_MAP_TYPE_LRU_HASH = 9
 BPF_MAP_TYPE_LPM_TRIE = 11
 BPF_MAP_TYPE_RINGBUF = 27
 BPF_ANY, BPF_NOEXIST, BPF_EXIST = 0, 1, 2

@@ -232,6 +232,81 @@ def ringbuf_sampler(rb_fd: int, every_log2: int = 4) -> bytes:
 # Interpreter known-answer programs (analytic expectations).
 # ---------------------------------------------------------------------------
 
+def lru_track(lru_fd: int) -> bytes:
+    """Connection-tracking style use of an LRU hash (key u32, value 16 B {u64
+    hits, u64 tag}) over 16-B raw units {u32 key, u32 op, u64 tag}:
+      op 0: lookup; a hit adds 1 to hits and returns the element's tag, a
+            miss inserts {0, tag} with BPF_ANY, looks up again, adds 1 to
+            hits and returns 100 + the insert's result
+      op 1: update {0, tag} with BPF_NOEXIST, returns 200 + its result
+      op 2: delete, returns 300 + its result
+      op 3: update {0, tag} with BPF_EXIST, returns 400 + its result"""
+    a = Asm()
+    a.mov64(6, "r1")
+    a.ldx(4, 2, 6, 0)
+    a.stx(4, 10, -4, "r2")                # key at fp-4
+    a.ldx(4, 7, 6, 4)                     # r7 = op
+    a.ldx(8, 8, 6, 8)                     # r8 = tag
+    a.st(8, 10, -24, 0)                   # value {0, tag} at fp-24
+    a.stx(8, 10, -16, "r8")
+    a.jmp("jeq", 7, 1, "noexist")
+    a.jmp("jeq", 7, 2, "delete")
+    a.jmp("jeq", 7, 3, "exist")
+    a.ld_map_fd(1, lru_fd)
+    a.mov64(2, "r10")
+    a.add64(2, -4)
+    a.call(BPF_FUNC_map_lookup_elem)
+    a.jmp("jeq", 0, 0, "miss")
+    a.mov64(1, 1)
+    a.atomic(8, ATOMIC_ADD, 0, 0, "r1")   # __sync_fetch_and_add(&v->hits, 1)
+    a.ldx(8, 0, 0, 8)                     # return v->tag
+    a.exit()
+    a.label("miss")                       # bpf_map_lookup_or_try_init (BPF_ANY), then count
+    a.ld_map_fd(1, lru_fd)
+    a.mov64(2, "r10")
+    a.add64(2, -4)
+    a.mov64(3, "r10")
+    a.add64(3, -24)
+    a.mov64(4, BPF_ANY)
+    a.call(BPF_FUNC_map_update_elem)
+    a.mov64(9, "r0")
+    a.add64(9, 100)
+    a.ld_map_fd(1, lru_fd)
+    a.mov64(2, "r10")
+    a.add64(2, -4)
+    a.call(BPF_FUNC_map_lookup_elem)
+    a.jmp("jeq", 0, 0, "ret9")
+    a.mov64(1, 1)
+    a.atomic(8, ATOMIC_ADD, 0, 0, "r1")
+    a.label("ret9")
+    a.mov64(0, "r9")
+    a.exit()
+    a.label("noexist")
+    a.mov64(9, 200)
+    a.mov64(4, BPF_NOEXIST)
+    a.ja("upd")
+    a.label("exist")
+    a.mov64(9, 400)
+    a.mov64(4, 2)                         # BPF_EXIST
+    a.label("upd")
+    a.ld_map_fd(1, lru_fd)
+    a.mov64(2, "r10")
+    a.add64(2, -4)
+    a.mov64(3, "r10")
+    a.add64(3, -24)
+    a.call(BPF_FUNC_map_update_elem)
+    a.add64(0, "r9")
+    a.exit()
+    a.label("delete")
+    a.ld_map_fd(1, lru_fd)
+    a.mov64(2, "r10")
+    a.add64(2, -4)
+    a.call(3)                             # bpf_map_delete_elem
+    a.add64(0, 300)
+    a.exit()
+    return a.assemble()
+
+
 def kat_add_mem() -> bytes:
     """vm/example/bpf_progs.h:6-11 ``bpf_add_mem_64_bit_minimal``: return
     ``(u32)mem[0..4) + (u32)mem[4..8)`` (64-bit add of two zero-extended words)."""

@@ -19,7 +19,8 @@
 #include <stdlib.h>
 #include <string.h>
 
-enum { T_HASH = 1, T_ARRAY = 2, T_PROG_ARRAY = 3, T_PERCPU_HASH = 5, T_PERCPU_ARRAY = 6, T_LPM_TRIE = 11, T_RINGBUF = 27 };
+enum { T_HASH = 1, T_ARRAY = 2, T_PROG_ARRAY = 3, T_PERCPU_HASH = 5, T_PERCPU_ARRAY = 6, T_LRU_HASH = 9, T_LPM_TRIE = 11,
+       T_RINGBUF = 27 };
 
 struct orc_map {
 	int used;
@@ -37,6 +38,11 @@ struct orc_map {
 	int64_t nnodes, ncap, root;
 	uint64_t lpm_entries;
 	uint8_t *tl_value; /* the reference returns a thread-local copy */
+	/* LRU_HASH (lru_var_hash_map.cpp): keys[i], vals[i], last-use stamps; the
+	 * reference's recency list is the stamp order (head = largest stamp) */
+	uint8_t *lkeys, *lvals;
+	uint64_t *lstamp;
+	uint64_t lcount, lclock;
 	/* RINGBUF (ringbuf_map.cpp): consumer / producer positions, 2 x max_ent data */
 	uint64_t rb_cons, rb_prod;
 };
@@ -88,6 +94,9 @@ static void free_map(struct orc_map *m)
 	free(m->data);
 	free(m->pkeys);
 	free(m->pvals);
+	free(m->lkeys);
+	free(m->lvals);
+	free(m->lstamp);
 	memset(m, 0, sizeof(*m));
 }
 
@@ -169,6 +178,15 @@ int orc_map_create(int fd, uint32_t type, uint32_t ksize, uint32_t vsize, uint32
 		break;
 	case T_PERCPU_HASH:
 		m->ncpu = (uint32_t)g_ncpu;
+		break;
+	case T_LRU_HASH: /* lru_var_hash_map.cpp:13-25 (max_entries 0 would evict from an empty list) */
+		if (ksize == 0 || vsize == 0 || max_entries == 0) {
+			g_errno = EINVAL;
+			return -1;
+		}
+		m->lkeys = malloc((size_t)max_entries * ksize);
+		m->lvals = malloc((size_t)max_entries * vsize);
+		m->lstamp = malloc((size_t)max_entries * 8);
 		break;
 	case T_PROG_ARRAY: /* prog_array.cpp:101-110: every slot INVALID_ENTRY (-1) */
 		if (ksize != 4 || vsize != 4) {
@@ -298,6 +316,99 @@ static void phash_erase(struct orc_map *m, uint64_t i)
 	memmove(m->pkeys + i * m->ksize, m->pkeys + (i + 1) * m->ksize, (m->pcount - i - 1) * m->ksize);
 	memmove(m->pvals + i * vs, m->pvals + (i + 1) * vs, (m->pcount - i - 1) * vs);
 	m->pcount--;
+}
+
+/* ---- LRU hash (runtime/src/bpf_map/userspace/lru_var_hash_map.cpp) ----
+ * The reference keeps a boost unordered_map plus a doubly linked recency list
+ * (head = most recent).  Here each element carries the clock value of its
+ * last use: move_to_head (:137-161) = a new, largest stamp, the list tail =
+ * the smallest stamp, evict_entry (:189-221) = removal.  Same observable
+ * contents and eviction victims. */
+static int64_t lru_find(struct orc_map *m, const void *key)
+{
+	for (uint64_t i = 0; i < m->lcount; i++)
+		if (memcmp(m->lkeys + i * m->ksize, key, m->ksize) == 0)
+			return (int64_t)i;
+	return -1;
+}
+
+static void lru_erase(struct orc_map *m, uint64_t i)
+{
+	uint64_t last = m->lcount - 1;
+	if (i != last) {
+		memcpy(m->lkeys + i * m->ksize, m->lkeys + last * m->ksize, m->ksize);
+		memcpy(m->lvals + i * m->vsize, m->lvals + last * m->vsize, m->vsize);
+		m->lstamp[i] = m->lstamp[last];
+	}
+	m->lcount--;
+}
+
+static void *lru_lookup(struct orc_map *m, const void *key) /* :27-41 */
+{
+	int64_t i = key ? lru_find(m, key) : -1;
+	if (i < 0) {
+		g_errno = ENOENT;
+		return NULL;
+	}
+	m->lstamp[i] = ++m->lclock; /* move_to_head */
+	return m->lvals + (size_t)i * m->vsize;
+}
+
+static long lru_update(struct orc_map *m, const void *key, const void *value, uint64_t flags) /* :43-90 */
+{
+	if (flags != 0 && flags != 1 && flags != 2) { /* is_good_update_flag (:8-11): exact values */
+		g_errno = EINVAL;
+		return -1;
+	}
+	int64_t i = lru_find(m, key);
+	if (flags == 1 /*BPF_NOEXIST*/ && i >= 0) {
+		g_errno = EEXIST;
+		return -1;
+	}
+	if (flags == 2 /*BPF_EXIST*/ && i < 0) {
+		g_errno = ENOENT;
+		return -1;
+	}
+	if (i < 0 && m->lcount == m->max_entries) { /* evict the list tail */
+		uint64_t t = 0;
+		for (uint64_t j = 1; j < m->lcount; j++)
+			if (m->lstamp[j] < m->lstamp[t])
+				t = j;
+		lru_erase(m, t);
+	}
+	if (i < 0) { /* insert_new_entry (:163-187): at the head */
+		i = (int64_t)m->lcount++;
+		memcpy(m->lkeys + (size_t)i * m->ksize, key, m->ksize);
+	}
+	memcpy(m->lvals + (size_t)i * m->vsize, value, m->vsize);
+	m->lstamp[i] = ++m->lclock;
+	return 0;
+}
+
+static long lru_delete(struct orc_map *m, const void *key) /* :92-103 */
+{
+	int64_t i = lru_find(m, key);
+	if (i < 0) {
+		g_errno = ENOENT;
+		return -1;
+	}
+	lru_erase(m, (uint64_t)i);
+	return 0;
+}
+
+/* :105-135.  The reference walks its unordered_map's order, which is not
+ * part of its contract (its tests compare visited sets); this walks element
+ * slots.  A key that is not present restarts at the first key. */
+static int lru_next_key(struct orc_map *m, const void *key, void *next)
+{
+	int64_t i = key ? lru_find(m, key) : -1;
+	uint64_t nx = i < 0 ? 0 : (uint64_t)i + 1;
+	if (nx >= m->lcount) {
+		g_errno = ENOENT;
+		return -1;
+	}
+	memcpy(next, m->lkeys + nx * m->ksize, m->ksize);
+	return 0;
 }
 
 /* ---- helper-side ops (bpf_map_handler::map_*_elem, from_syscall=false) ---- */
@@ -723,6 +834,8 @@ void *orc_map_lookup(int fd, const void *key)
 	}
 	case T_HASH:
 		return hash_lookup(m, key);
+	case T_LRU_HASH:
+		return lru_lookup(m, key);
 	case T_LPM_TRIE:
 		return key ? lpm_lookup(m, key) : NULL;
 	case T_RINGBUF:
@@ -772,6 +885,8 @@ long orc_map_update(int fd, const void *key, const void *value, uint64_t flags)
 	}
 	case T_LPM_TRIE:
 		return lpm_update(m, key, value, flags);
+	case T_LRU_HASH:
+		return lru_update(m, key, value, flags);
 	case T_HASH: /* fix_hash_map.cpp:34-39: flags ignored, always 0 */
 		hash_update(m, key, value);
 		return 0;
@@ -805,6 +920,8 @@ long orc_map_delete(int fd, const void *key)
 		return 0;
 	case T_LPM_TRIE:
 		return lpm_delete(m, key);
+	case T_LRU_HASH:
+		return lru_delete(m, key);
 	case T_PERCPU_HASH: { /* per_cpu_hash_map.cpp:96-107: zeroes [0, cpu*vsize) */
 		int64_t i = phash_find(m, key);
 		if (i >= 0)
@@ -940,6 +1057,8 @@ int orc_map_get_next_key(int fd, const void *key, void *next_key)
 	}
 	case T_LPM_TRIE:
 		return lpm_next_key(m, key, next_key);
+	case T_LRU_HASH:
+		return lru_next_key(m, key, next_key);
 	case T_PERCPU_HASH: {
 		int64_t i = key ? phash_find(m, key) : -1;
 		uint64_t nx = i < 0 ? 0 : (uint64_t)i + 1;
@@ -997,7 +1116,10 @@ uint64_t orc_map_count(int fd)
 	struct orc_map *m = get(fd);
 	if (!m)
 		return 0;
-	return m->type == T_PERCPU_HASH ? m->pcount : m->type == T_LPM_TRIE ? m->lpm_entries : m->count;
+	return m->type == T_PERCPU_HASH ? m->pcount
+	       : m->type == T_LPM_TRIE	 ? m->lpm_entries
+	       : m->type == T_LRU_HASH	 ? m->lcount
+					 : m->count;
 }
 
 /* bpftime_shm.cpp:637-652: the map "pointer" is the fd itself */
