@@ -225,6 +225,16 @@ constexpr uint32_t kMergeGroup = 16;
 constexpr uint32_t kMergeEntries = 4096;  // merge table entries (64 KiB of LDS)
 inline uint32_t log_words_for(uint32_t comb_entries) { return 1 + 2 * (kWaveCacheEntries + comb_entries); }
 
+// Dynamic LDS of an interpreter block: the lanes' XDP ctx (48 B each), their
+// stacks (LDS-stack programs), 32 B of tail-call launch constants (interp.hip
+// tenv; the asm finds them 32 B before the combining table), the combining
+// table (u32 tags + u64 deltas per entry).
+constexpr uint32_t kTenvBytes = 32;
+inline size_t dyn_lds_for(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries) {
+  return (size_t)kBlock * ((kind == CTX_XDP ? 48 : 0) + (big_stack ? 0 : stack_size)) + kTenvBytes +
+         12 * (size_t)comb_entries;
+}
+
 // Error codes recorded per unit (err_count counts units with any error)
 constexpr uint32_t E_OK = 0;
 constexpr uint32_t E_OOB = 1;

@@ -141,6 +141,7 @@ def handler_ids():
         for cc in JCC:
             for k in ("R", "I"):
                 ids.append(f"J{w}_{cc}_{k}")
+    ids += ["TAIL", "TRET"]  # rare: after the hot handlers
     return ids
 
 
@@ -1125,6 +1126,208 @@ class Gen:
         self.dispatch()
         self.e(f"{last}:", "s_mov_b32 s84, 0", "s_mov_b64 exec, 0", "s_mov_b32 s68, 2", f"s_branch {L('done')}")
 
+    # ---- bpf_tail_call in a linked image (XDP entry form) ----
+    # The C++ path (interp.hip, kTailHelper / kRetHelper) restated for the
+    # common case: every lane's ctx argument is its own LDS ctx (48 bytes
+    # copied).  Frames have the C++ layout ([depth][word][lane] u64: r1..r10,
+    # ctx address, return pc | ctx bytes << 32, ctx bytes from word 12, stack
+    # bytes from word 20), so either tier pops what the other pushed.  The
+    # launch constants sit in LDS 32 bytes below the combining table
+    # (common.hpp dyn_lds_for; frames 0: tail calls in C++): frames
+    # base, entry table, word stride, depth stride, stack words; a lane's depth
+    # and grid lane index in its R[12] slot (v40 + 12 * 2048).
+    def tail_env(self):
+        self.e(f"s_sub_u32 s69, %[comb], {32}", "v_mov_b32 v41, s69",
+               "ds_read_b128 v[42:45], v41", "ds_read_b128 v[46:49], v41 offset:16",
+               "ds_read_b64 v[54:55], v40 offset:24576",                      # depth, grid lane
+               "s_waitcnt lgkmcnt(0)",
+               "v_readfirstlane_b32 s72, v42", "v_readfirstlane_b32 s73, v43",  # frames
+               "v_readfirstlane_b32 s74, v44", "v_readfirstlane_b32 s75, v45",  # entry table
+               "v_readfirstlane_b32 s76, v46", "v_readfirstlane_b32 s77, v47",  # word / depth stride
+               "v_readfirstlane_b32 s85, v48",                                  # stack words
+               "s_cmp_eq_u64 s[72:73], 0", f"s_cbranch_scc1 {L('slow')}")
+
+    def frame_ptr(self):
+        """v[56:57] = this lane's word 0 at depth v54."""
+        self.e("v_mad_u64_u32 v[56:57], s[62:63], v55, 8, s[72:73]",
+               "v_mad_u64_u32 v[56:57], s[62:63], v54, s77, v[56:57]")
+
+    def fnext(self, n=1):
+        for _ in range(n):
+            self.e("v_add_co_u32 v56, vcc, s76, v56", "v_addc_co_u32 v57, vcc, 0, v57, vcc")
+
+    def go_groups(self):
+        """Every running lane continues at its own IP (v50, bytes): the
+        first group runs, up to two more are parked as pending groups; more
+        groups than that hand every lane's pc to the C++ scheduler."""
+        single, multi, over = self.label("g1"), self.label("gm"), self.label("gov")
+        self.e("s_mov_b64 s[60:61], exec",
+               "v_readfirstlane_b32 s69, v50",
+               "v_cmp_eq_u32 s[62:63], s69, v50",
+               "s_andn2_b64 s[64:65], s[60:61], s[62:63]",
+               f"s_cbranch_scc1 {multi}",
+               "s_mov_b32 s48, s69")
+        self.dispatch()
+        self.e(f"{multi}:",
+               "s_mov_b64 exec, s[64:65]",                                   # the second group
+               "v_readfirstlane_b32 s70, v50",
+               "v_cmp_eq_u32 s[66:67], s70, v50",
+               "s_andn2_b64 exec, exec, s[66:67]",                            # a third?
+               f"s_cbranch_scc0 {single}",
+               "v_readfirstlane_b32 s71, v50",                               # (s71 = its IP)
+               "v_cmp_eq_u32 s[64:65], s71, v50",
+               "s_andn2_b64 exec, exec, s[64:65]",
+               f"s_cbranch_scc1 {over}",                                     # a fourth group
+               "s_add_u32 s49, s92, 2", "s_cmp_gt_u32 s49, 2", f"s_cbranch_scc1 {over}",
+               "s_mov_b64 exec, s[62:63]", "s_mov_b32 s48, s69",            # the first runs
+               "s_mov_b32 s69, s70", "s_mov_b64 s[62:63], s[66:67]")
+        self.push()
+        self.e("s_mov_b32 s69, s71", "s_mov_b64 s[62:63], s[64:65]")
+        self.push()
+        self.dispatch()
+        self.e(f"{single}:",                                                   # two groups
+               "s_add_u32 s49, s92, 1", "s_cmp_gt_u32 s49, 2", f"s_cbranch_scc1 {over}",
+               "s_mov_b64 exec, s[62:63]", "s_mov_b32 s48, s69",
+               "s_mov_b32 s69, s70", "s_mov_b64 s[62:63], s[66:67]")
+        self.push()
+        self.dispatch()
+        # too many groups: every running lane's pc from v50, the pending
+        # groups' from their IPs; exit reason 3
+        self.e(f"{over}:",
+               "s_mov_b64 exec, s[60:61]",
+               "v_lshrrev_b32 %[lpc], 5, v50")
+        for i, (pc, m) in enumerate((("s86", "s[88:89]"), ("s87", "s[90:91]"))):
+            skip = self.label("gz")
+            self.e(f"s_cmp_ge_u32 s92, {i + 1}", f"s_cbranch_scc0 {skip}",
+                   f"s_mov_b64 exec, {m}", f"s_lshr_b32 s52, {pc}, 5",
+                   "v_mov_b32 %[lpc], s52", "s_or_b64 s[60:61], s[60:61], exec", f"{skip}:")
+        self.e("s_mov_b64 exec, s[60:61]", "s_mov_b32 s92, 0", "s_mov_b32 s68, 3", f"s_branch {L('spill')}")
+
+    def tail_call(self):
+        """bpf_tail_call(ctx, prog_array, index) (bpf_helper.cpp:568-650):
+        index in range, a prog fd in the slot that is linked into the image,
+        depth below 32 -> push a frame, r0 = r3..r9 = 0, r2 = 64, enter the
+        target; else r0 = -1 and go on.  The map must be wave-uniform and a
+        PROG_ARRAY, and every lane that can call must pass its own ctx;
+        anything else leaves for C++ before changing state."""
+        noval, ni = self.label("tnv"), self.label("tni")
+        self.tail_env()
+        self.rd_fixed(2, 44)
+        self.uniform64((44, 45), (62, 63))
+        self.e("s_cmp_lg_u32 s63, 0", f"s_cbranch_scc1 {L('slow')}",
+               "s_cmpk_ge_u32 s62, 0x400", f"s_cbranch_scc1 {L('slow')}",
+               "s_lshl_b32 s69, s62, 6",
+               "s_load_dwordx4 s[64:67], %[maps], s69",                       # type, ksz, vsz, max
+               "s_add_u32 s69, s69, 16",
+               "s_load_dwordx2 s[70:71], %[maps], s69",                       # slots
+               "s_waitcnt lgkmcnt(0)",
+               "s_cmp_lg_u32 s64, 3", f"s_cbranch_scc1 {L('slow')}",         # BPF_MAP_TYPE_PROG_ARRAY
+               f"v_mov_b32 v46, v{R0 + 6}",                                  # `int idx = index`
+               "v_cmp_gt_u32 s[54:55], s67, v46",                            # 0 <= idx < max_entries
+               "v_cndmask_b32 v46, 0, v46, s[54:55]",
+               "v_mad_u64_u32 v[48:49], s[56:57], v46, 4, s[70:71]",
+               "global_load_dword v47, v[48:49], off",
+               "s_waitcnt vmcnt(0)",
+               "v_cmp_gt_u32 vcc, 0x400, v47", "s_and_b64 s[54:55], s[54:55], vcc",
+               "v_cndmask_b32 v47, 0, v47, s[54:55]",
+               "v_mad_u64_u32 v[48:49], s[56:57], v47, 4, s[74:75]",
+               "global_load_dword v50, v[48:49], off",
+               "s_waitcnt vmcnt(0)",
+               "v_cmp_le_i32 s[56:57], 0, v50", "s_and_b64 s[54:55], s[54:55], s[56:57]",
+               "v_cmp_gt_u32 s[56:57], 32, v54", "s_and_b64 s[54:55], s[54:55], s[56:57]",   # depth
+               "s_and_b64 s[54:55], s[54:55], exec",
+               # callers passing anything but their own ctx go to C++
+               f"v_cmp_eq_u32 s[56:57], %[r1lo], v{R0 + 2}",
+               f"v_cmp_eq_u32 vcc, %[r1hi], v{R0 + 3}", "s_and_b64 s[56:57], s[56:57], vcc",
+               "s_andn2_b64 s[56:57], s[54:55], s[56:57]", f"s_cbranch_scc1 {L('slow')}",
+               "s_lshr_b32 s49, s48, 5", "s_add_u32 s49, s49, 1",           # return pc
+               "s_mov_b64 s[60:61], exec",
+               "s_and_b64 exec, exec, s[54:55]", f"s_cbranch_execz {noval}")
+        # ---- push: r1..r10, ctx address, return pc | 48 << 32, ctx, stack ----
+        self.frame_ptr()
+        for r in range(1, 11):
+            self.e(f"global_store_dwordx2 v[56:57], v[{R0 + 2 * r}:{R0 + 2 * r + 1}], off")
+            self.fnext()
+        self.e(f"global_store_dwordx2 v[56:57], v[{R0 + 2}:{R0 + 3}], off")
+        self.fnext()
+        self.e("v_mov_b32 v44, s49", "v_mov_b32 v45, 48",
+               "global_store_dwordx2 v[56:57], v[44:45], off")
+        self.fnext()
+        for half in (0, 24):
+            self.e(f"ds_read_b64 v[42:43], v{R0 + 2} offset:{half}",
+                   f"ds_read_b64 v[44:45], v{R0 + 2} offset:{half + 8}",
+                   f"ds_read_b64 v[46:47], v{R0 + 2} offset:{half + 16}",
+                   "s_waitcnt lgkmcnt(0)")
+            for v in (42, 44, 46):
+                self.e(f"global_store_dwordx2 v[56:57], v[{v}:{v + 1}], off")
+                self.fnext()
+        self.fnext(2)                                                        # ctx words 18, 19
+        loop, done = self.label("tsl"), self.label("tsd")
+        self.e("s_lshl_b32 s69, s85, 3", "v_subrev_u32 v41, s69, %[stklo]",   # stack base
+               "s_mov_b32 s69, s85",
+               f"{loop}:", "s_cmp_eq_u32 s69, 0", f"s_cbranch_scc1 {done}",
+               "ds_read_b64 v[42:43], v41", "s_waitcnt lgkmcnt(0)",
+               "global_store_dwordx2 v[56:57], v[42:43], off",
+               "v_add_u32 v41, 8, v41", "s_sub_u32 s69, s69, 1")
+        self.fnext()
+        self.e(f"s_branch {loop}", f"{done}:",
+               "v_add_u32 v54, 1, v54", "ds_write_b32 v40, v54 offset:24576",
+               f"v_mov_b32 v{R0}, 0", f"v_mov_b32 v{R0 + 1}, 0",
+               f"v_mov_b32 v{R0 + 4}, 64", f"v_mov_b32 v{R0 + 5}, 0",
+               f"v_mov_b32 v{R0 + 20}, %[r10lo]", f"v_mov_b32 v{R0 + 21}, %[r10hi]")
+        for r in range(3, 10):
+            self.e(f"v_mov_b32 v{R0 + 2 * r}, 0", f"v_mov_b32 v{R0 + 2 * r + 1}, 0")
+        self.e("v_lshlrev_b32 v50, 5, v50",                                 # target IP
+               f"{noval}:",
+               "s_andn2_b64 exec, s[60:61], s[54:55]", f"s_cbranch_execz {ni}",
+               f"v_mov_b32 v{R0}, -1", f"v_mov_b32 v{R0 + 1}, -1",
+               "s_lshl_b32 s69, s49, 5", "v_mov_b32 v50, s69",
+               f"{ni}:", "s_mov_b64 exec, s[60:61]")
+        self.go_groups()
+
+    def tail_ret(self):
+        """A linked target's exit (kRetHelper): pop the frame, r0 stays the
+        target's result, continue after the tail call."""
+        self.tail_env()
+        self.e("v_cmp_eq_u32 s[54:55], 0, v54", "s_and_b64 s[54:55], s[54:55], exec",
+               f"s_cbranch_scc1 {L('slow')}",                                # no frame: C++ fails the lane
+               "v_add_u32 v54, -1, v54",
+               "s_waitcnt vmcnt(0)")
+        self.frame_ptr()
+        self.e("v_mad_u64_u32 v[44:45], s[62:63], 10, s76, v[56:57]",
+               "global_load_dwordx2 v[46:47], v[44:45], off",               # ctx address
+               "v_add_co_u32 v44, vcc, s76, v44", "v_addc_co_u32 v45, vcc, 0, v45, vcc",
+               "global_load_dwordx2 v[48:49], v[44:45], off",               # return pc | ctx bytes
+               "s_waitcnt vmcnt(0)",
+               "v_cmp_eq_u32 s[54:55], %[r1lo], v46", "v_cmp_eq_u32 vcc, %[r1hi], v47",
+               "s_and_b64 s[54:55], s[54:55], vcc",
+               "v_cmp_eq_u32 vcc, 48, v49", "s_and_b64 s[54:55], s[54:55], vcc",
+               "s_andn2_b64 s[54:55], exec, s[54:55]", f"s_cbranch_scc1 {L('slow')}",
+               "ds_write_b32 v40, v54 offset:24576",
+               "v_lshlrev_b32 v50, 5, v48")                                  # return IP
+        for r in range(1, 11):
+            self.e(f"global_load_dwordx2 v[{R0 + 2 * r}:{R0 + 2 * r + 1}], v[56:57], off")
+            self.fnext()
+        self.fnext(2)
+        ctxv = [(42, 43), (44, 45), (46, 47), (48, 49), (54, 55), (58, 59)]
+        for a, b in ctxv:
+            self.e(f"global_load_dwordx2 v[{a}:{b}], v[56:57], off")
+            self.fnext()
+        self.fnext(2)
+        self.e("s_waitcnt vmcnt(0)")
+        for k, (a, b) in enumerate(ctxv):
+            self.e(f"ds_write_b64 %[r1lo], v[{a}:{b}] offset:{8 * k}")
+        loop, done = self.label("trl"), self.label("trd")
+        self.e("s_lshl_b32 s69, s85, 3", "v_subrev_u32 v41, s69, %[stklo]",
+               "s_mov_b32 s69, s85",
+               f"{loop}:", "s_cmp_eq_u32 s69, 0", f"s_cbranch_scc1 {done}",
+               "global_load_dwordx2 v[42:43], v[56:57], off", "s_waitcnt vmcnt(0)",
+               "ds_write_b64 v41, v[42:43]",
+               "v_add_u32 v41, 8, v41", "s_sub_u32 s69, s69, 1")
+        self.fnext()
+        self.e(f"s_branch {loop}", f"{done}:", "s_waitcnt lgkmcnt(0)")
+        self.go_groups()
+
     # ---- divergence: min-pc scheduling of lane groups ----
     # A split branch leaves the wave as the running group (IP, exec) plus up
     # to two pending groups (s86/s87 = IPs, s[88:89] / s[90:91] = lane masks,
@@ -1328,6 +1531,10 @@ class Gen:
                 self.call_lookup_ak()
             elif name == "EXIT":
                 self.exit_()
+            elif name == "TAIL":
+                self.tail_call()
+            elif name == "TRET":
+                self.tail_ret()
             elif name.startswith("RMWD"):
                 self.rmwd(int(name[4]), name[6])
             elif name.startswith("RMWMV"):

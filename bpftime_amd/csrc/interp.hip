@@ -141,8 +141,9 @@ __device__ __forceinline__ uint32_t run_loop(Ctx &c) {
     const uint64_t mask = w32 ? 0xffffffffull : ~0ull;
     uint32_t npc = cur + 1;
 
-// write a register (only selected lanes in the divergent loop)
-#define WRO(r, val, old) RG(r) = (UNI || sel) ? (uint64_t)(val) : (uint64_t)(old)
+// write a register: selected lanes only (in the uniform loop the other
+// lanes may be parked lane groups, interp kernel loop)
+#define WRO(r, val, old) RG(r) = sel ? (uint64_t)(val) : (uint64_t)(old)
 #define OPB(rv) (srcreg ? (rv) : (uint64_t)(int64_t)d.imm)
 #define ALU(expr)                              \
   {                                            \
@@ -191,8 +192,7 @@ __device__ __forceinline__ uint32_t run_loop(Ctx &c) {
                           : a)
       case X_LDDW: {
         const uint64_t v = (uint64_t)(uint32_t)d.imm | ((uint64_t)(uint32_t)d.hi << 32);
-        if (UNI) RG(d.dst) = v;
-        else WRO(d.dst, v, RG(d.dst));
+        WRO(d.dst, v, RG(d.dst));
         npc = cur + 2;
         break;
       }
@@ -201,8 +201,7 @@ __device__ __forceinline__ uint32_t run_loop(Ctx &c) {
         const uint64_t a = RG(d.src) + (int64_t)d.off;
         const bool ok = c.win.ok(a, sz);
         const uint64_t v = mem_load(sel && ok ? a : c.dummy, sz);
-        if (UNI) RG(d.dst) = v;
-        else WRO(d.dst, v, RG(d.dst));
+        WRO(d.dst, v, RG(d.dst));
         if (__ballot(sel && !ok) != 0) {
           c.err = (sel && !ok) ? E_OOB : c.err;
           c.alive = c.alive && !(sel && !ok);
@@ -444,7 +443,7 @@ __device__ __forceinline__ uint32_t run_loop(Ctx &c) {
         } else if (tm == __ballot(sel)) {
           c.pc = d.tgt;
         } else {
-          c.lpc = taken ? (uint32_t)d.tgt : npc;
+          c.lpc = sel ? (taken ? (uint32_t)d.tgt : npc) : c.lpc;
           return R_DIVERGE;
         }
       } else {
@@ -497,9 +496,13 @@ __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const Fas
   const uint64_t alive = __ballot(c.alive);
   const uint32_t limit = __builtin_amdgcn_readfirstlane(c.step_limit);
   const uint32_t entry = __builtin_amdgcn_readfirstlane(u.entry);
-  uint64_t c0a = c.c0a, c1a = c.c1a;
-  uint32_t c0dl = (uint32_t)c.c0d, c0dh = (uint32_t)(c.c0d >> 32), c1dl = (uint32_t)c.c1d,
-           c1dh = (uint32_t)(c.c1d >> 32), c0s = c.c0s, c1s = c.c1s;
+  // (the wave's counter cache: uniform by construction, but the compiler
+  // cannot prove it across the lane-group scheduling loop)
+  auto u32 = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); };
+  auto u64 = [&](uint64_t v) { return (uint64_t)u32((uint32_t)v) | ((uint64_t)u32((uint32_t)(v >> 32)) << 32); };
+  uint64_t c0a = u64(c.c0a), c1a = u64(c.c1a);
+  uint32_t c0dl = u32((uint32_t)c.c0d), c0dh = u32((uint32_t)(c.c0d >> 32)), c1dl = u32((uint32_t)c.c1d),
+           c1dh = u32((uint32_t)(c.c1d >> 32)), c0s = u32(c.c0s), c1s = u32(c.c1s);
   const uint64_t vaddr = c.verdicts ? (uint64_t)(uintptr_t)(c.verdicts + c.unit) : 0;
   const uint64_t raddr = c.rets ? (uint64_t)(uintptr_t)(c.rets + c.unit) : 0;
   asm volatile(BPFTIME_AMD_FAST_ASM
@@ -526,7 +529,7 @@ __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const Fas
   c.c1s = c1s;
   // lanes that ran exit inside the block are done (verdict stored)
   c.alive = c.alive && ((alive_out >> __lane_id()) & 1);
-  if (why == FAST_SPLIT) c.lpc = lpc;
+  if (why == FAST_SPLIT && c.alive) c.lpc = lpc;  // (parked lane groups keep theirs)
   return why;
 }
 
@@ -543,7 +546,8 @@ __device__ __forceinline__ void write_xdp_ctx(XdpCtx *x, uint64_t slot, uint32_t
   x->buffer_end = chunk + (p.descs && !p.stride ? len : p.stride);
 }
 
-template <uint32_t KIND, bool BIGSTACK>
+// IMAGE: a linked tail-call image (lane groups scheduled through the asm tier)
+template <uint32_t KIND, bool BIGSTACK, bool IMAGE>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_interp(KParams pin) {
   // Copy every kernel argument through an SGPR barrier: without it the
   // compiler keeps the argument block as one 16-dword tuple that it spills
@@ -560,7 +564,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
 #undef SRP
 #undef SRV
-  __shared__ uint64_t Rf[12 * kBlock];  // r0..r10 + a dummy slot per lane
+  // r0..r10, a dummy slot, and (images) the lane's tail-call depth | its
+  // grid lane index << 32 (gen_fast.py tail_env).  (2 KiB of LDS decide
+  // between 3 and 4 resident blocks of the headline program: images only.)
+  __shared__ uint64_t Rf[(IMAGE ? 13 : 12) * kBlock];
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
   constexpr uint32_t CTXB = KIND == CTX_XDP ? 48 : 0;
   const uint32_t tid = threadIdx.x;
@@ -570,11 +577,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   // the ctx and stack areas: comb_entries u32 tags {arena offset | 2 |
   // (4-byte ? 1 : 0)} (8-way sets), then comb_entries u64 deltas, flushed
   // when the block ends; sized 0 for programs that never need it
-  uint32_t *comb = (uint32_t *)(dyn + kBlock * (CTXB + (BIGSTACK ? 0 : p.stack_size)));
+  uint64_t *tenv = (uint64_t *)(dyn + kBlock * (CTXB + (BIGSTACK ? 0 : p.stack_size)));
+  uint32_t *comb = (uint32_t *)((uint8_t *)tenv + kTenvBytes);
   uint64_t *comb_d = (uint64_t *)(comb + p.comb_entries);
   for (uint32_t i = tid; i < 3 * p.comb_entries; i += kBlock) comb[i] = 0;
   // a table tag as a flush tag {address | (4-byte ? 1 : 0)}
   auto comb_tag = [&](uint32_t t) -> uint64_t { return t ? (p.arena_lo + (t & ~3u)) | (t & 1u) : 0; };
+  // tail-call launch constants for the asm tier (XDP images: the frames'
+  // ctx copy is the lane's LDS ctx): frames (0: tail calls in C++), entry
+  // table, word stride | depth stride << 32, stack words
+  if (tid == 0) {
+    const bool on = IMAGE && KIND == CTX_XDP && p.frames && p.tail_entry;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock * 8;
+    tenv[0] = on ? (uint64_t)(uintptr_t)p.frames : 0;
+    tenv[1] = (uint64_t)(uintptr_t)p.tail_entry;
+    tenv[2] = stride | ((stride * p.frame_words) << 32);
+    tenv[3] = p.stack_size / 8;
+  }
   __syncthreads();
   uint64_t big_stack[BIGSTACK ? kStackSize / 8 : 1];
   const uint64_t stack_top = BIGSTACK ? (uint64_t)(uintptr_t)(big_stack + kStackSize / 8)
@@ -646,7 +665,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     int32_t miss_fd = -1;
     uint64_t miss_hash = 0;
     uint32_t lru_ops = 0;
-    uint32_t tdepth = 0;  // tail-call frames this lane has pushed
+    // tail-call frames this lane has pushed (images: in LDS, the asm tier
+    // pushes too)
+    uint32_t tdepth_reg = 0;
+    uint32_t *const tdep = IMAGE ? (uint32_t *)&Rf[(IMAGE ? 12 : 0) * kBlock + tid] : &tdepth_reg;
+    if (IMAGE) Rf[(IMAGE ? 12 : 0) * kBlock + tid] = (uint64_t)(blockIdx.x * kBlock + tid) << 32;
 
     // ---- per-unit setup: r1, r2, r10 (other registers zero) are set by the
     // fast path's fresh entry, which every unit starts with ----
@@ -686,6 +709,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     c.steps = 0;
 
     bool uni = true;
+    // Divergent waves run one lane group at a time in the asm tier: the
+    // group at the lowest pc runs as a uniform wave while the other lanes
+    // are parked at their pcs (c.lpc), until the group exits, splits or
+    // reaches a tail call / return; then the lowest group runs next, and
+    // groups that meet at one pc run together again.  (BPFTIME_AMD_DBG bit 2:
+    // the C++ divergent loop instead.)
+    const bool groups = IMAGE && p.fast_div && !(p.dbg & 4);
+    bool parked = false;
+    auto unpark = [&]() {
+      c.alive = c.alive || parked;
+      parked = false;
+      uni = false;
+    };
     // the asm tier computes specialised ctx->data / data_end loads from the
     // slot; the C++ tier reads the ctx, so it is written before the C++ tier
     // first runs an instruction of this unit
@@ -696,22 +732,38 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         ctx_ready = true;
       }
     };
-    while (__ballot(c.alive) != 0) {
+    while (__ballot(c.alive || parked) != 0) {
       uint32_t r;
+      if (IMAGE && uni && __ballot(c.alive) == 0) {  // the running group died (a helper error): the parked lanes go on
+        unpark();
+        continue;
+      }
+      if (!uni && groups) {
+        const uint32_t m = c.alive ? c.lpc : 0xffffffffu;
+        const uint32_t cur = __builtin_amdgcn_readfirstlane(__reduce_min_sync(~0ull, m));
+        parked = c.alive && c.lpc != cur;
+        c.alive = c.alive && !parked;
+        c.pc = cur;
+        uni = true;
+        continue;
+      }
       if (uni) {
         const uint32_t why = run_fast(c, fe, fu);
         fu.entry &= 4u;
-        if (why == FAST_EXIT) {  // every live lane ran exit; r0 already stored
+        if (why == FAST_EXIT) {  // every running lane ran exit; r0 already stored
           c.alive = false;
-          break;
+          if (__ballot(parked) == 0) break;
+          unpark();
+          continue;
         }
-        if (why == FAST_SPLIT) {  // lane groups at different pcs: C++ divergent loop
+        if (why == FAST_SPLIT) {  // lane groups at different pcs (c.lpc)
           uni = false;
+          unpark();
           continue;
         }
         if (why == FAST_STEPS) {
-          c.err = c.alive ? E_STEPS : c.err;
-          c.alive = false;
+          c.err = c.alive || parked ? E_STEPS : c.err;
+          c.alive = parked = false;
           break;
         }
         ctx_for_cpp();
@@ -721,9 +773,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         r = run_loop<false>(c);
       }
       if (r == R_STEP) continue;
-      if (r == R_DONE) break;
+      if (r == R_DONE) {
+        if (__ballot(parked) == 0) break;
+        unpark();
+        continue;
+      }
       if (r == R_DIVERGE) {
-        uni = false;
+        unpark();
         continue;
       }
       if (r == R_RECONV) {
@@ -767,8 +823,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
               for (cb = 0; cb < kFrameCtx && c.win.ok(a1 + cb, 8); cb += 8) {
               }
             const bool in_stack = a1 + 64 > stack_top - sbytes && a1 < stack_top;
-            if (entry >= 0 && tdepth < kTailDepth && a1 != 0 && !in_stack) {
-              const uint32_t d = tdepth;
+            if (entry >= 0 && tdep[0] < kTailDepth && a1 != 0 && !in_stack) {
+              const uint32_t d = tdep[0];
               for (int r = 1; r <= 10; r++) FW(d, r - 1) = R[r * kBlock];
               FW(d, 10) = a1;
               FW(d, 11) = (uint64_t)next | ((uint64_t)cb << 32);
@@ -780,17 +836,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
               R[1 * kBlock] = a1;
               R[2 * kBlock] = 64;  // bpftime_prog_exec(context, sizeof(context), ...)
               R[10 * kBlock] = stack_top;
-              tdepth++;
+              tdep[0] = d + 1;
               next = (uint32_t)entry;
             } else {
               R[0] = (uint64_t)-1;
             }
-          } else if (tdepth == 0) {
+          } else if (tdep[0] == 0) {
             c.err = E_BADOP;
             c.alive = false;
           } else {
-            tdepth--;
-            const uint32_t d = tdepth;
+            const uint32_t d = tdep[0] - 1;
+            tdep[0] = d;
             const uint64_t rv = R[0];
             for (int r = 1; r <= 10; r++) R[r * kBlock] = FW(d, r - 1);
             const uint64_t a1 = FW(d, 10);
@@ -805,7 +861,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
           }
         }
         c.lpc = csel ? next : c.lpc;
-        uni = false;
+        unpark();
         continue;
       }
       if (csel) {
@@ -991,7 +1047,7 @@ static_assert(kMergeEntries == 4u << 10, "k_comb_merge hashes into 2^10 sets of 
 // Host-side launch wrappers
 // ---------------------------------------------------------------------------
 static size_t dyn_lds_bytes(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries) {
-  return kBlock * ((kind == CTX_XDP ? 48 : 0) + (big_stack ? 0 : stack_size)) + 12 * (size_t)comb_entries;
+  return dyn_lds_for(kind, big_stack, stack_size, comb_entries);
 }
 
 extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind, bool big_stack, uint32_t grid,
@@ -1000,13 +1056,14 @@ extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind,
   q.ordered = ordered;
   const size_t dyn = dyn_lds_bytes(kind, big_stack, p->stack_size, p->comb_entries);
   dim3 g(grid), b(kBlock);
-#define L(K, B) hipLaunchKernelGGL((k_interp<K, B>), g, b, dyn, stream, q)
+  const bool image = q.tail_entry && !big_stack;
+#define L(K, B, I) hipLaunchKernelGGL((k_interp<K, B, I>), g, b, dyn, stream, q)
   if (kind == CTX_XDP) {
-    if (big_stack) L(CTX_XDP, true); else L(CTX_XDP, false);
+    if (big_stack) L(CTX_XDP, true, false); else if (image) L(CTX_XDP, false, true); else L(CTX_XDP, false, false);
   } else if (kind == CTX_SYSCALL) {
-    if (big_stack) L(CTX_SYSCALL, true); else L(CTX_SYSCALL, false);
+    if (big_stack) L(CTX_SYSCALL, true, false); else if (image) L(CTX_SYSCALL, false, true); else L(CTX_SYSCALL, false, false);
   } else {
-    if (big_stack) L(CTX_RAW, true); else L(CTX_RAW, false);
+    if (big_stack) L(CTX_RAW, true, false); else if (image) L(CTX_RAW, false, true); else L(CTX_RAW, false, false);
   }
 #undef L
   return hipGetLastError();
@@ -1023,7 +1080,7 @@ extern "C" hipError_t bpftime_amd_launch_merge(const uint64_t *log, uint32_t log
 extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds) {
   int n = 0;
   hipError_t e;
-#define O(K, B) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_interp<K, B>, kBlock, dyn_lds)
+#define O(K, B) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_interp<K, B, false>, kBlock, dyn_lds)
   if (kind == CTX_XDP) {
     if (big_stack) O(CTX_XDP, true); else O(CTX_XDP, false);
   } else if (kind == CTX_SYSCALL) {

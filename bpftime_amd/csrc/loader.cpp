@@ -627,6 +627,7 @@ int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &
 
   int depth = entries.empty() ? stack_depth(p, reach) : -1;  // an image: every program on a 512-B stack
   out.multi_entry = !entries.empty();
+  out.entries = entries;
   if (depth < 0 || depth > (int)kLdsStackMax) {
     out.big_stack = true;
     out.stack_size = kStackSize;
@@ -769,18 +770,39 @@ static bool is_cond_jump(uint8_t op) { return op >= X_JEQ && op <= X_JSLE; }
 
 // in[i][r]: kind of register r before instruction i; returns false when the
 // program may rewrite its ctx (then no ctx / packet kinds are trusted).
+//
+// A linked tail-call image (vm_api.cpp) also enters at every target: with r1
+// = the ctx the caller passed (`ctx_entries`: the caller's own ctx / slot at
+// every tail-call site, checked by the caller of this function), r2 = 64, r10
+// = the same stack top.  Only stores that can move the packet pointers (ctx
+// data / data_end / buffer_start / buffer_end) make the ctx untrusted; a
+// target that rewrites other fields of its ctx copy gets them back restored.
 static bool pointer_kinds(const std::vector<DInsn> &p, const std::vector<uint8_t> &lddw_src, bool xdp,
-                          bool pkt_ok, std::vector<std::vector<PVal>> &in) {
+                          bool pkt_ok, std::vector<std::vector<PVal>> &in,
+                          const std::vector<uint32_t> &entries = {}, bool ctx_entries = false) {
   const uint32_t n = (uint32_t)p.size();
   in.assign(n, std::vector<PVal>(11, PVal{P_UNDEF, 0, 0}));
   std::vector<bool> queued(n, false);
   std::vector<uint32_t> work;
-  for (int r = 0; r < 11; r++) in[0][r] = kOther;
-  in[0][1] = xdp ? PVal{P_CTX, 0, 0} : PVal{P_SLOT, 0, 0};
-  in[0][10] = PVal{P_STK, 0, 0};
-  work.push_back(0);
-  queued[0] = true;
+  const PVal ctx0 = xdp ? PVal{P_CTX, 0, 0} : PVal{P_SLOT, 0, 0};
+  auto seed = [&](uint32_t e, bool ctx) {
+    for (int r = 0; r < 11; r++) in[e][r] = kOther;
+    in[e][1] = ctx ? ctx0 : kOther;
+    in[e][10] = PVal{P_STK, 0, 0};
+    work.push_back(e);
+    queued[e] = true;
+  };
+  seed(0, true);
+  for (uint32_t e : entries)
+    if (e < n && !queued[e]) seed(e, ctx_entries);
   bool ctx_written = false;
+  // a store to [at, at + sz) of the ctx: does it reach a packet pointer field?
+  auto moves_pkt = [&](const PVal &b, int64_t off, uint32_t sz) {
+    if (b.kind != P_CTX) return false;
+    const int64_t at = (int64_t)b.k + off;
+    auto hit = [&](int64_t lo, int64_t hi) { return at < hi && lo < at + (int64_t)sz; };
+    return hit(0, 16) || hit(32, 48);
+  };
   auto ptr = [](uint8_t k) {
     return k == P_CTX || k == P_PKT || k == P_SLOT || k == P_STK || k == P_CONST || k == P_MAPVAL;
   };
@@ -818,14 +840,14 @@ static bool pointer_kinds(const std::vector<DInsn> &p, const std::vector<uint8_t
       }
       case X_ST:
       case X_STX:
-        if (st[d.dst].kind == P_CTX) ctx_written = true;
+        if (moves_pkt(st[d.dst], d.off, 1u << ((d.aux >> A_SIZE_SHIFT) & 3))) ctx_written = true;
         break;
       case X_RMW_ADD:
-        if (st[d.dst].kind == P_CTX) ctx_written = true;
+        if (moves_pkt(st[d.dst], d.off, 1u << ((d.aux >> A_SIZE_SHIFT) & 3))) ctx_written = true;
         if (d.aux & A_FETCH) st[d.hi] = kOther;
         break;
       case X_ATOMIC:
-        if (st[d.dst].kind == P_CTX) ctx_written = true;
+        if (moves_pkt(st[d.dst], d.off, 1u << ((d.aux >> A_SIZE_SHIFT) & 3))) ctx_written = true;
         if (d.hi == 0xf1) st[0] = kOther;
         else if (d.hi & 1) st[d.src] = kOther;
         break;
@@ -981,6 +1003,20 @@ static std::vector<bool> counter_nodefer(const std::vector<DInsn> &p, const std:
     if (reached(i)) accesses(p, i, in[i], acc[i]);
   std::vector<bool> nodefer(n, false);
   std::vector<uint32_t> seen(n, UINT32_MAX), work;
+  // a linked target's exit continues after every tail-call site
+  std::vector<uint32_t> ret_points;
+  for (uint32_t i = 0; i + 1 < n; i++)
+    if (p[i].op == X_CALL && p[i].hi == (int32_t)kTailHelper && reached(i)) ret_points.push_back(i + 1);
+  auto next_of = [&](uint32_t k, std::vector<uint32_t> &w) {
+    if (p[k].op == X_CALL && p[k].hi == kRetHelper) {
+      for (uint32_t r : ret_points) w.push_back(r);
+      return;
+    }
+    uint32_t s[2];
+    int ns;
+    successors(p, k, s, ns);
+    for (int j = 0; j < ns; j++) w.push_back(s[j]);
+  };
   for (uint32_t i = 0; i < n; i++) {
     const DInsn &d = p[i];
     const bool add = (d.op == X_RMW_ADD && !(d.aux & A_FETCH)) || (d.op == X_ATOMIC && d.hi == 0x00);
@@ -993,10 +1029,7 @@ static std::vector<bool> counter_nodefer(const std::vector<DInsn> &p, const std:
     }
     bool hit = false;
     work.clear();
-    uint32_t s[2];
-    int ns;
-    successors(p, i, s, ns);
-    for (int j = 0; j < ns; j++) work.push_back(s[j]);
+    next_of(i, work);
     while (!work.empty() && !hit) {
       const uint32_t k = work.back();
       work.pop_back();
@@ -1004,8 +1037,7 @@ static std::vector<bool> counter_nodefer(const std::vector<DInsn> &p, const std:
       seen[k] = i;
       for (const Loc &l : acc[k])
         if (may_alias(me, l)) hit = true;
-      successors(p, k, s, ns);
-      for (int j = 0; j < ns; j++) work.push_back(s[j]);
+      next_of(k, work);
     }
     nodefer[i] = hit;
   }
@@ -1067,26 +1099,35 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
                            : (int64_t)d.imm;
     f.target = (uint32_t)d.tgt * kFastInsnBytes;
     f.aux = d.imm;
+    // tail calls / a linked target's exit: asm frames in the XDP form
+    // (gen_fast.py tail_call; the raw form's ctx copy is left to C++)
+    if (xdp && d.op == X_CALL && d.hi == (int32_t)kTailHelper) f.hoff = 4 + 4 * F_TAIL;
+    if (xdp && d.op == X_CALL && d.hi == kRetHelper) f.hoff = 4 + 4 * F_TRET;
   }
   // helpers that move ctx->data / data_end invalidate packet pointers
   bool pkt_ok = true;
   for (const DInsn &d : prog)
     if (d.op == X_CALL && (d.hi == 44 || d.hi == 65)) pkt_ok = false;
   std::vector<std::vector<PVal>> in;
-  // a linked tail-call image has entries the pointer kinds do not start from:
-  // generic handlers, and adds without fetch in the C++ tier, which sums a
-  // wave's adds to one address (the combining table needs the kinds)
   auto make_direct = [&](size_t i) {
     out.fast[i].hoff = 4 + 4 * direct_add_handler(prog[i]);
     out.fast[i].w1 |= FW_NODEFER;
   };
+  bool kinds_ok;
   if (lo.multi_entry) {
+    // targets enter with the caller's ctx when every tail-call site passes it
+    kinds_ok = pointer_kinds(prog, lo.lddw_src, xdp, pkt_ok, in, lo.entries, true);
+    const PVal ctx0 = xdp ? PVal{P_CTX, 0, 0} : PVal{P_SLOT, 0, 0};
+    bool passes = true;
     for (size_t i = 0; i < prog.size(); i++)
-      if (out.add_site[i]) make_direct(i);
-    out.needs_comb = false;
-    return;
+      if (prog[i].op == X_CALL && prog[i].hi == (int32_t)kTailHelper && in[i][1].kind != P_UNDEF &&
+          !(in[i][1] == ctx0))
+        passes = false;
+    if (kinds_ok && !passes) kinds_ok = pointer_kinds(prog, lo.lddw_src, xdp, pkt_ok, in, lo.entries, false);
+  } else {
+    kinds_ok = pointer_kinds(prog, lo.lddw_src, xdp, pkt_ok, in);
   }
-  if (!pointer_kinds(prog, lo.lddw_src, xdp, pkt_ok, in)) {
+  if (!kinds_ok) {
     // ctx rewritten: generic handlers only, no pointer kinds to prove a
     // counter unobserved
     for (size_t i = 0; i < prog.size(); i++)

@@ -58,6 +58,7 @@ struct LoadOut {
   bool may_delete = false;    // calls map_delete_elem: hash lookup indexes stop being valid
   bool tail_call = false;     // calls bpf_tail_call: linked with the prog arrays' targets at launch
   bool multi_entry = false;   // a linked image (tail-call targets are extra entries)
+  std::vector<uint32_t> entries;  // the linked targets' entry pcs
 };
 
 // Helper ids the device implements (interp.hip helper switch).

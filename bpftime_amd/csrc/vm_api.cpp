@@ -425,9 +425,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     const uint64_t key = ((uint64_t)b->ctx_kind << 40) | ((uint64_t)prog.big_stack << 32) | prog.stack_size;
     auto it = best.find(key);
     if (it == best.end()) {
-      auto dyn = [&](uint32_t e) {
-        return kBlock * ((b->ctx_kind == CTX_XDP ? 48 : 0) + (prog.big_stack ? 0 : prog.stack_size)) + 12 * (size_t)e;
-      };
+      auto dyn = [&](uint32_t e) { return dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, e); };
       const int base = std::min(2, bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn(kComb)));
       uint32_t e = kComb;
       while (e < kCombMax && bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn(2 * e)) >= base) e *= 2;
@@ -466,8 +464,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       hipGetDeviceProperties(&prop, dev);
       cus = prop.multiProcessorCount;
     }
-    const size_t dyn = kBlock * ((b->ctx_kind == CTX_XDP ? 48 : 0) + (prog.big_stack ? 0 : prog.stack_size)) +
-                       12 * (size_t)prog.comb_entries;
+    const size_t dyn = dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, prog.comb_entries);
     int occ = bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn);
     if (occ < 1) occ = 1;
     uint64_t want = (b->count + kBlock - 1) / kBlock;

@@ -1,31 +1,6 @@
-#!/bin/bash
-# GPU-box check: parity tests, smoke, bench, rocprofv3 kernel-trace summary.
-# Every GPU step has its own time limit; a crash / fault / timeout ends the
-# script (exit codes other than 0 and pytest's 1 = "tests failed").
-set -u
+set -o pipefail
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-step() {  # name, timeout, cmd...
-  local name=$1 t=$2; shift 2
-  echo "== $name"
-  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
-  local rc=$?
-  echo "== $name rc=$rc"
-  tail -n 25 "gpurun_out/$name.log"
-  return $rc
-}
-MODE=${1:-all}
-if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
-  step pytest_gpu 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider
-  rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
-fi
-if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
-  step bench 600 python bench.py --steps 10 --warmup 2 --cpu-seconds 8 || exit $?
-fi
-if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
-  step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- \
-      python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline || exit $?
-  find gpurun_out/prof -name "*stats*" | head -20
-fi
-exit 0
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/gpu_all.log 2>&1 || { tail -30 gpurun_out/gpu_all.log; exit 1; }
+tail -3 gpurun_out/gpu_all.log
+for w in tail-call flow-hash syscall-agg; do timeout -k 10 300 python bench.py --workload $w --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/b_$w.json 2> gpurun_out/b_$w.err || { tail gpurun_out/b_$w.err; exit 1; }; python -c "import json;d=json.load(open('gpurun_out/b_$w.json'));print('$w',d['value'],d['ms_per_step'],d.get('parity'))"; done
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/b_main.json 2> gpurun_out/b_main.err && python -c "import json;d=json.load(open('gpurun_out/b_main.json'));print('main',d['value'],d['ms_per_step'])"
