@@ -76,8 +76,8 @@ budget (v40..v101 -> v66..v127):
   s[76:77] DMap data pointer                     s[78:79] PROG (FInsn base)
   s80 S (staged bytes; 0 = staging off)  s81 0   s[82:83] O (uniform offset)
   s84 dirty 16-B chunk mask                      s85 scratch
-  s86/s87, s[88:89]/s[90:91], s92  pending lane groups (divergence): IPs,
-               lane masks, count
+  s86/s87/s93, s[88:89]/s[90:91]/s[94:95], s92  pending lane groups
+               (divergence): IPs, lane masks, count
   v40 lane's R[0] LDS address  v41, v[42:43] scratch
   v[44:45] X  v[46:47] Y  v[48:49] Z (address)  v[50:51] E (address end)
   v[52:53] slot address (staging base)           v[54:55] O (per-lane offset)
@@ -106,6 +106,10 @@ R0 = 60        # first VGPR of the eBPF register file
 STG = 84       # first VGPR of the staged bytes
 NREG = 11
 INSN = 32      # FInsn bytes
+# pending lane groups (divergence): IPs, lane masks, capacity
+PIP = ["s86", "s87", "s93"]
+PM = ["s[88:89]", "s[90:91]", "s[94:95]"]
+KP = 3
 
 # staged (link-resolved) packet / slot accesses
 STAGED_LD = ["LDXS1", "LDXS2", "LDXS4", "LDXS2X", "LDXS4X", "LDXS8A", "LDXS8U"]
@@ -387,8 +391,9 @@ class Gen:
 
     def union_exec(self):
         """exec |= the masks of the pending lane groups (divergence)."""
-        self.e("s_cmp_ge_u32 s92, 1", "s_cselect_b64 s[56:57], s[88:89], 0", "s_or_b64 exec, exec, s[56:57]",
-               "s_cmp_ge_u32 s92, 2", "s_cselect_b64 s[56:57], s[90:91], 0", "s_or_b64 exec, exec, s[56:57]")
+        for i in range(KP):
+            self.e(f"s_cmp_ge_u32 s92, {i + 1}", f"s_cselect_b64 s[56:57], {PM[i]}, 0",
+                   "s_or_b64 exec, exec, s[56:57]")
 
     def flush_all(self):
         """Write back the dirty chunks of every live lane, pending groups
@@ -812,7 +817,22 @@ class Gen:
         if stack_key:
             hsh = self.label("hash")
             self.e("s_cmp_eq_u32 s72, 1", f"s_cbranch_scc1 {hsh}")          # BPF_MAP_TYPE_HASH
-        self.e("s_cmp_lg_u32 s72, 2", f"s_cbranch_scc1 {L('slow')}")        # not BPF_MAP_TYPE_ARRAY
+        # ARRAY: element key; PERCPU_ARRAY (per_cpu_array_map.cpp:34-48):
+        # element key * ncpu + this wave's virtual cpu (%[vcpu] = cpu | ncpu
+        # << 16 when the wave's lanes share one, else ~0: C++)
+        parr, arr = self.label("lpc"), self.label("lar")
+        self.e("s_mov_b32 s70, 1", "s_mov_b32 s71, 0",
+               "s_cmp_eq_u32 s72, 6", f"s_cbranch_scc1 {parr}",
+               "s_cmp_lg_u32 s72, 2", f"s_cbranch_scc1 {L('slow')}",        # not BPF_MAP_TYPE_ARRAY
+               f"s_branch {arr}",
+               f"{parr}:",
+               "s_add_u32 s85, s85, 28",
+               "s_load_dword s70, %[maps], s85",                             # DMap ncpu
+               "s_lshr_b32 s69, %[vcpu], 16",
+               "s_waitcnt lgkmcnt(0)",
+               "s_cmp_lg_u32 s69, s70", f"s_cbranch_scc1 {L('slow')}",
+               "s_and_b32 s71, %[vcpu], 0xffff",
+               f"{arr}:")
         if stack_key:
             self.e("v_add_u32 v41, s46, %[stklo]", "ds_read_b32 v46, v41", "s_waitcnt lgkmcnt(0)",
                    f"s_branch {got}")
@@ -827,6 +847,7 @@ class Gen:
         self.e(f"{got}:",
                "v_cmp_gt_u32 s[54:55], s75, v46",                            # key < max_entries
                "v_mov_b32 v47, s74",
+               "v_mul_lo_u32 v46, v46, s70", "v_add_u32 v46, s71, v46",
                "v_mad_u64_u32 v[50:51], s[56:57], v46, v47, s[76:77]",
                f"v_cndmask_b32 v{R0}, 0, v50, s[54:55]",
                f"v_cndmask_b32 v{R0 + 1}, 0, v51, s[54:55]")
@@ -1157,50 +1178,32 @@ class Gen:
             self.e("v_add_co_u32 v56, vcc, s76, v56", "v_addc_co_u32 v57, vcc, 0, v57, vcc")
 
     def go_groups(self):
-        """Every running lane continues at its own IP (v50, bytes): the
-        first group runs, up to two more are parked as pending groups; more
-        groups than that hand every lane's pc to the C++ scheduler."""
-        single, multi, over = self.label("g1"), self.label("gm"), self.label("gov")
+        """Every running lane continues at its own IP (v50, bytes): the first
+        lane's group runs, the others are parked as pending groups; more
+        groups than the list holds hand every lane's pc to the C++ side."""
+        single, over = self.label("g1"), self.label("gov")
         self.e("s_mov_b64 s[60:61], exec",
                "v_readfirstlane_b32 s69, v50",
                "v_cmp_eq_u32 s[62:63], s69, v50",
-               "s_andn2_b64 s[64:65], s[60:61], s[62:63]",
-               f"s_cbranch_scc1 {multi}",
-               "s_mov_b32 s48, s69")
+               "s_mov_b32 s48, s69", "s_mov_b64 s[72:73], s[62:63]",           # the running group
+               "s_andn2_b64 s[74:75], s[60:61], s[62:63]")                     # lanes left
+        for _ in range(KP):
+            self.e("s_cmp_eq_u64 s[74:75], 0", f"s_cbranch_scc1 {single}",
+                   f"s_cmp_ge_u32 s92, {KP}", f"s_cbranch_scc1 {over}",
+                   "s_mov_b64 exec, s[74:75]",
+                   "v_readfirstlane_b32 s69, v50",
+                   "v_cmp_eq_u32 s[62:63], s69, v50",
+                   "s_andn2_b64 s[74:75], s[74:75], s[62:63]")
+            self.push()
+        self.e("s_cmp_eq_u64 s[74:75], 0", f"s_cbranch_scc0 {over}",
+               f"{single}:", "s_mov_b64 exec, s[72:73]")
         self.dispatch()
-        self.e(f"{multi}:",
-               "s_mov_b64 exec, s[64:65]",                                   # the second group
-               "v_readfirstlane_b32 s70, v50",
-               "v_cmp_eq_u32 s[66:67], s70, v50",
-               "s_andn2_b64 exec, exec, s[66:67]",                            # a third?
-               f"s_cbranch_scc0 {single}",
-               "v_readfirstlane_b32 s71, v50",                               # (s71 = its IP)
-               "v_cmp_eq_u32 s[64:65], s71, v50",
-               "s_andn2_b64 exec, exec, s[64:65]",
-               f"s_cbranch_scc1 {over}",                                     # a fourth group
-               "s_add_u32 s49, s92, 2", "s_cmp_gt_u32 s49, 2", f"s_cbranch_scc1 {over}",
-               "s_mov_b64 exec, s[62:63]", "s_mov_b32 s48, s69",            # the first runs
-               "s_mov_b32 s69, s70", "s_mov_b64 s[62:63], s[66:67]")
-        self.push()
-        self.e("s_mov_b32 s69, s71", "s_mov_b64 s[62:63], s[64:65]")
-        self.push()
-        self.dispatch()
-        self.e(f"{single}:",                                                   # two groups
-               "s_add_u32 s49, s92, 1", "s_cmp_gt_u32 s49, 2", f"s_cbranch_scc1 {over}",
-               "s_mov_b64 exec, s[62:63]", "s_mov_b32 s48, s69",
-               "s_mov_b32 s69, s70", "s_mov_b64 s[62:63], s[66:67]")
-        self.push()
-        self.dispatch()
-        # too many groups: every running lane's pc from v50, the pending
-        # groups' from their IPs; exit reason 3
+        # too many groups: every lane of this instruction takes its pc from
+        # v50, the pending groups theirs (some may be this instruction's)
         self.e(f"{over}:",
                "s_mov_b64 exec, s[60:61]",
                "v_lshrrev_b32 %[lpc], 5, v50")
-        for i, (pc, m) in enumerate((("s86", "s[88:89]"), ("s87", "s[90:91]"))):
-            skip = self.label("gz")
-            self.e(f"s_cmp_ge_u32 s92, {i + 1}", f"s_cbranch_scc0 {skip}",
-                   f"s_mov_b64 exec, {m}", f"s_lshr_b32 s52, {pc}, 5",
-                   "v_mov_b32 %[lpc], s52", "s_or_b64 s[60:61], s[60:61], exec", f"{skip}:")
+        self.materialize_pending()
         self.e("s_mov_b64 exec, s[60:61]", "s_mov_b32 s92, 0", "s_mov_b32 s68, 3", f"s_branch {L('spill')}")
 
     def tail_call(self):
@@ -1330,12 +1333,12 @@ class Gen:
 
     # ---- divergence: min-pc scheduling of lane groups ----
     # A split branch leaves the wave as the running group (IP, exec) plus up
-    # to two pending groups (s86/s87 = IPs, s[88:89] / s[90:91] = lane masks,
-    # s92 = count), sorted by IP.  The running group always has the lowest
+    # to three pending groups (PIP = IPs, PM = lane masks, s92 = count),
+    # sorted by IP.  The running group always has the lowest
     # pc; while any group is pending, dispatch goes through the divergent
     # table, whose entries compare IP with the first pending IP: equal -> the
     # groups merge (reconvergence), greater -> the running group is parked
-    # and the pending one runs.  A third pending group, or any instruction
+    # and the pending one runs.  A fourth pending group, or any instruction
     # the asm does not run, hands every group's pc to the C++ divergent loop
     # (exit reason 3).
     def set_table(self, divergent):
@@ -1347,32 +1350,38 @@ class Gen:
 
     def pop0(self):
         keep = self.label("keep")
-        self.e("s_mov_b32 s86, s87", "s_mov_b64 s[88:89], s[90:91]", "s_mov_b32 s87, -1",
+        for i in range(KP - 1):
+            self.e(f"s_mov_b32 {PIP[i]}, {PIP[i + 1]}", f"s_mov_b64 {PM[i]}, {PM[i + 1]}")
+        self.e(f"s_mov_b32 {PIP[KP - 1]}, -1",
                "s_sub_u32 s92, s92, 1", "s_cmp_eq_u32 s92, 0", f"s_cbranch_scc0 {keep}")
         self.set_table(False)
         self.e(f"{keep}:")
 
     def push(self):
-        """Park group (s69 = IP, s[62:63] = lanes)."""
-        nonempty, ne0, after0, two, done = (self.label(x) for x in ("pne", "pn0", "pa0", "p2", "pd"))
-        self.e("s_cmp_eq_u32 s92, 0", f"s_cbranch_scc0 {nonempty}",
-               "s_mov_b32 s86, s69", "s_mov_b64 s[88:89], s[62:63]", "s_mov_b32 s92, 1")
+        """Park group (s69 = IP, s[62:63] = lanes): merged into a pending
+        group at the same IP, else inserted in IP order (s49 / s[56:57]
+        scratch); a full list leaves for C++ (overflow)."""
+        done, ins, first = self.label("pd"), self.label("pi"), self.label("pf")
+        for i in range(KP):
+            nx = self.label("pm")
+            self.e(f"s_cmp_gt_u32 s92, {i}", f"s_cbranch_scc0 {ins}",
+                   f"s_cmp_eq_u32 s69, {PIP[i]}", f"s_cbranch_scc0 {nx}",
+                   f"s_or_b64 {PM[i]}, {PM[i]}, s[62:63]", f"s_branch {done}", f"{nx}:")
+        self.e(f"{ins}:", f"s_cmp_ge_u32 s92, {KP}", f"s_cbranch_scc1 {L('overflow')}",
+               "s_cmp_eq_u32 s92, 0", f"s_cbranch_scc0 {first}")
         self.set_table(True)
-        self.e(f"s_branch {done}",
-               f"{nonempty}:",
-               "s_cmp_eq_u32 s69, s86", f"s_cbranch_scc0 {ne0}",
-               "s_or_b64 s[88:89], s[88:89], s[62:63]", f"s_branch {done}",
-               f"{ne0}:",
-               "s_cmp_eq_u32 s92, 1", f"s_cbranch_scc0 {two}",
-               "s_cmp_lt_u32 s69, s86", f"s_cbranch_scc0 {after0}",
-               "s_mov_b32 s87, s86", "s_mov_b64 s[90:91], s[88:89]",
-               "s_mov_b32 s86, s69", "s_mov_b64 s[88:89], s[62:63]", "s_mov_b32 s92, 2", f"s_branch {done}",
-               f"{after0}:",
-               "s_mov_b32 s87, s69", "s_mov_b64 s[90:91], s[62:63]", "s_mov_b32 s92, 2", f"s_branch {done}",
-               f"{two}:",
-               "s_cmp_eq_u32 s69, s87", f"s_cbranch_scc0 {L('overflow')}",
-               "s_or_b64 s[90:91], s[90:91], s[62:63]",
-               f"{done}:")
+        self.e(f"{first}:")
+        for n in range(KP):  # append at index n = count, then bubble towards the front
+            nx = self.label("pa")
+            self.e(f"s_cmp_eq_u32 s92, {n}", f"s_cbranch_scc0 {nx}",
+                   f"s_mov_b32 {PIP[n]}, s69", f"s_mov_b64 {PM[n]}, s[62:63]", f"s_add_u32 s92, s92, 1")
+            for j in range(n, 0, -1):
+                self.e(f"s_cmp_lt_u32 {PIP[j]}, {PIP[j - 1]}", f"s_cbranch_scc0 {done}",
+                       f"s_mov_b32 s49, {PIP[j]}", f"s_mov_b32 {PIP[j]}, {PIP[j - 1]}", f"s_mov_b32 {PIP[j - 1]}, s49",
+                       f"s_mov_b64 s[56:57], {PM[j]}", f"s_mov_b64 {PM[j]}, {PM[j - 1]}",
+                       f"s_mov_b64 {PM[j - 1]}, s[56:57]")
+            self.e(f"s_branch {done}", f"{nx}:")
+        self.e(f"{done}:")
 
     def materialize(self, extra):
         """Every group's pc (FInsn index) into the lpc output of its lanes,
@@ -1382,12 +1391,16 @@ class Gen:
         if extra:
             self.e("s_mov_b64 exec, s[62:63]", "s_lshr_b32 s52, s69, 5",
                    "v_mov_b32 %[lpc], s52", "s_or_b64 s[60:61], s[60:61], exec")
-        for i, (pc, m) in enumerate((("s86", "s[88:89]"), ("s87", "s[90:91]"))):
+        self.materialize_pending()
+        self.e("s_mov_b64 exec, s[60:61]", "s_mov_b32 s68, 3", f"s_branch {L('spill')}")
+
+    def materialize_pending(self):
+        """lpc of the pending groups' lanes; s[60:61] |= their masks."""
+        for i in range(KP):
             skip = self.label("mz")
             self.e(f"s_cmp_ge_u32 s92, {i + 1}", f"s_cbranch_scc0 {skip}",
-                   f"s_mov_b64 exec, {m}", f"s_lshr_b32 s52, {pc}, 5",
+                   f"s_mov_b64 exec, {PM[i]}", f"s_lshr_b32 s52, {PIP[i]}, 5",
                    "v_mov_b32 %[lpc], s52", "s_or_b64 s[60:61], s[60:61], exec", f"{skip}:")
-        self.e("s_mov_b64 exec, s[60:61]", "s_mov_b32 s68, 3", f"s_branch {L('spill')}")
 
     def divergence_routines(self):
         n4 = 4 * len(handler_ids())
@@ -1439,7 +1452,7 @@ class Gen:
           "s_lshl_b32 s48, %[pc], 5",
           "s_mov_b64 s[58:59], exec", "s_mov_b64 exec, %[alive]",
           "s_mov_b32 s80, 0", "s_mov_b32 s81, 0", "s_mov_b32 s84, 0", "s_mov_b32 s92, 0",
-          "s_mov_b32 s86, -1", "s_mov_b32 s87, -1",
+          "s_mov_b32 s86, -1", "s_mov_b32 s87, -1", "s_mov_b32 s93, -1",
           "v_mov_b32 v52, %[slotlo]", "v_mov_b32 v53, %[slothi]",
           "s_bitcmp1_b32 %[entry], 0", f"s_cbranch_scc1 {fresh}")
         # re-entry: registers from the C++ side's LDS copy, no staging
@@ -1590,7 +1603,7 @@ def main():
     g.out = [relocate(x) for x in g.out]
     # v126/v127 (v100/v101 before relocation) are read, never written, by
     # staged loads near the window end
-    clob = [f"s{i}" for i in range(40, 93)] + [f"v{vmap(i)}" for i in range(40, 102)]
+    clob = [f"s{i}" for i in range(40, 96)] + [f"v{vmap(i)}" for i in range(40, 102)]
     with open(os.path.join(HERE, "fast_asm.inc"), "w") as f:
         f.write("// Generated by gen_fast.py; do not edit.\n")
         f.write("#define BPFTIME_AMD_FAST_ASM \\\n")

@@ -474,6 +474,7 @@ struct FastEnv {
   uint32_t combn;   // its entries (0: add straight to memory)
   uint32_t rb;      // LDS byte address of this lane's R[0]
   uint32_t stage;   // staged bytes per unit (0: no staging)
+  uint32_t ncpu;    // virtual CPUs (per-CPU maps)
 };
 
 constexpr uint32_t FAST_SLOW = 0, FAST_STEPS = 1, FAST_EXIT = 2, FAST_SPLIT = 3;
@@ -485,6 +486,7 @@ struct FastUnit {
   uint32_t r2;
   uint32_t len;    // unit length (ctx->data_end - ctx->data)
   uint32_t entry;  // bit 0: fresh unit, bit 1: stage the slot, bit 2: lane groups in asm
+  uint64_t vcpu;   // the unit's virtual CPU (helper 8, per-CPU maps)
 };
 
 __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const FastUnit &u) {
@@ -503,6 +505,10 @@ __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const Fas
   uint64_t c0a = u64(c.c0a), c1a = u64(c.c1a);
   uint32_t c0dl = u32((uint32_t)c.c0d), c0dh = u32((uint32_t)(c.c0d >> 32)), c1dl = u32((uint32_t)c.c1d),
            c1dh = u32((uint32_t)(c.c1d >> 32)), c0s = u32(c.c0s), c1s = u32(c.c1s);
+  // the wave's virtual cpu for per-CPU array lookups: cpu | ncpu << 16 when
+  // every lane shares it (consecutive units), else ~0
+  const uint32_t vm = (uint32_t)(u.vcpu % f.ncpu), vm0 = __builtin_amdgcn_readfirstlane(vm);
+  const uint32_t vcpu = __ballot(c.alive && vm != vm0) == 0 && f.ncpu <= 0xffff ? vm0 | (f.ncpu << 16) : ~0u;
   const uint64_t vaddr = c.verdicts ? (uint64_t)(uintptr_t)(c.verdicts + c.unit) : 0;
   const uint64_t raddr = c.rets ? (uint64_t)(uintptr_t)(c.rets + c.unit) : 0;
   asm volatile(BPFTIME_AMD_FAST_ASM
@@ -517,7 +523,7 @@ __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const Fas
                  [r2lo] "v"(u.r2), [r10lo] "v"((uint32_t)u.r10), [r10hi] "v"((uint32_t)(u.r10 >> 32)),
                  [slotlo] "v"((uint32_t)u.slot), [slothi] "v"((uint32_t)(u.slot >> 32)),
                  [head] "s"(f.head), [ulen] "v"(u.len), [stklo] "v"((uint32_t)u.r10), [comb] "s"(f.comb), [combn] "s"(f.combn),
-                 [stage] "s"(f.stage)
+                 [stage] "s"(f.stage), [vcpu] "s"(vcpu)
                : BPFTIME_AMD_FAST_CLOBBERS);
   c.pc = pc;
   c.steps = steps;
@@ -635,6 +641,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   // the host sized the staged window (gen_fast.py, unit staging) from the
   // program's static packet / slot accesses, 16-B aligned slots only
   fe.stage = p.stage;
+  fe.ncpu = p.ncpu ? p.ncpu : 1;
 
   const bool ordered = p.ordered != 0;
   const uint64_t ustep = ordered ? 1 : (uint64_t)gridDim.x * kBlock;
@@ -674,6 +681,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     // ---- per-unit setup: r1, r2, r10 (other registers zero) are set by the
     // fast path's fresh entry, which every unit starts with ----
     FastUnit fu;
+    fu.vcpu = vcpu;
     fu.slot = slot;
     fu.r10 = stack_top;
     fu.len = len;

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -258,33 +259,57 @@ class Mi355xVm {
           i++;
         }
     };
-    std::set<int32_t> arrays, seen_arrays, targets;
-    arrays_of(raw.data(), raw.size(), arrays);
+    // the prog arrays each program loads, and the targets each array names
+    std::map<int32_t, std::set<int32_t>> arrays_of_prog;  // target prog fd -> arrays
+    std::map<int32_t, std::vector<int32_t>> slots_of;     // array fd -> target prog fds
+    std::set<int32_t> root_arrays, pending;
+    arrays_of(raw.data(), raw.size(), root_arrays);
+    pending = root_arrays;
     link_note.clear();
-    while (!arrays.empty()) {
-      const int32_t fd = *arrays.begin();
-      arrays.erase(arrays.begin());
-      if (!seen_arrays.insert(fd).second) continue;
+    while (!pending.empty()) {
+      const int32_t fd = *pending.begin();
+      pending.erase(pending.begin());
+      if (slots_of.count(fd)) continue;
       std::vector<int32_t> slots(r.maps[fd].max_entries);
       if (!slots.empty() &&
           hipMemcpy(slots.data(), (const void *)r.maps[fd].d.data, 4 * slots.size(), hipMemcpyDeviceToHost) != hipSuccess) {
         error = "prog array read failed";
         return -1;
       }
+      std::vector<int32_t> &ts = slots_of[fd];
       for (int32_t v : slots)
-        if (v >= 0 && v < (int32_t)kMaxFds && r.kind[v] == HKind::PROG && targets.insert(v).second) {
-          const std::vector<uint8_t> &b = r.progs[v].insns;
-          arrays_of((const RawInsn *)b.data(), b.size() / 8, arrays);
+        if (v >= 0 && v < (int32_t)kMaxFds && r.kind[v] == HKind::PROG) {
+          ts.push_back(v);
+          if (!arrays_of_prog.count(v)) {
+            const std::vector<uint8_t> &b = r.progs[v].insns;
+            arrays_of((const RawInsn *)b.data(), b.size() / 8, arrays_of_prog[v]);
+            for (int32_t a : arrays_of_prog[v]) pending.insert(a);
+          }
         }
     }
-    std::vector<RawInsn> code(raw);
+    // Callees before callers (post-order from the loaded program, which
+    // goes last behind a jump at pc 0): lane groups run lowest pc first, so
+    // targets run before the code they return to, and lanes returning from
+    // different targets (or failing the call) meet at the return point.
+    std::vector<int32_t> order;
+    std::set<int32_t> visited;
+    std::function<void(int32_t)> visit = [&](int32_t t) {
+      if (!visited.insert(t).second) return;
+      for (int32_t a : arrays_of_prog[t])
+        for (int32_t u : slots_of[a]) visit(u);
+      order.push_back(t);
+    };
+    for (int32_t a : root_arrays)
+      for (int32_t u : slots_of[a]) visit(u);
+    std::vector<RawInsn> code;
     std::vector<uint32_t> entries;
     std::vector<int32_t> entry(kMaxFds, -1);
     uint32_t stack_need = base_stack;  // the deepest program of the image
-    for (int32_t t : targets) {
+    if (!order.empty()) code.push_back(RawInsn{});  // pc 0: ja to the loaded program
+    for (int32_t t : order) {
       const std::vector<uint8_t> &bytes = r.progs[t].insns;
       const size_t n = bytes.size() / 8;
-      if (code.size() + n + 1 > kMaxInsts) {
+      if (code.size() + n + raw.size() + 1 > kMaxInsts || code.size() + n > 0x7fff) {
         link_note += "prog " + std::to_string(t) + ": image would exceed " + std::to_string(kMaxInsts) + " insns; ";
         continue;
       }
@@ -309,6 +334,13 @@ class Mi355xVm {
         if (c[i].code == 0x18 && i + 1 < n) code.push_back(c[++i]);
       }
     }
+    if (entries.empty()) {
+      code.clear();  // nothing linked: the program alone
+    } else {
+      code[0].code = 0x05;  // ja +off
+      code[0].off = (int16_t)(code.size() - 1);
+    }
+    code.insert(code.end(), raw.begin(), raw.end());
     if (!entries.empty()) {
       RawInsn ex{};
       ex.code = 0x95;
