@@ -163,6 +163,14 @@ constexpr uint32_t kTailGrid = 1024;         // blocks per launch of an image wi
 constexpr uint32_t kFrameCtx = 64;
 constexpr uint32_t kFrameHdr = 96;           // r1..r10, ctx address, ret pc, ctx bytes
 constexpr uint32_t kFrameBytes = kFrameHdr + kFrameCtx + kStackSize;
+// Frame header word 11: return pc | ctx bytes << 32 (a full frame: r1..r10,
+// the ctx address and cb ctx bytes from it, the whole stack), or with
+// kFrameMasked: the lane's own LDS ctx, and only the registers of the live
+// mask (bit r: r1..r9, header bits 41..), the ctx / stack words of the
+// image's save masks (KParams tail_ctx_mask / tail_stack_mask); r10 is the
+// stack top again after the return
+constexpr uint64_t kFrameMasked = 1ull << 40;
+constexpr uint32_t kFrameLiveShift = 40;  // + r: the bit of register r (1..9)
 
 // Context kinds for a batch
 constexpr uint32_t CTX_RAW = 0;      // r1 = unit memory, r2 = length
@@ -211,6 +219,8 @@ struct KParams {
   uint64_t *lane_scratch; // a u64 per lane of the grid (PROG_ARRAY lookups hand out a copy there), or nullptr
   uint32_t dbg;           // BPFTIME_AMD_DBG experiment bits (0 in production)
   uint64_t lru_seq;       // this launch's LRU stamp sequence (common.hpp kLruSeqShift)
+  uint32_t tail_ctx_mask;    // XDP images: ctx words / stack words a frame keeps (loader.cpp tail_save_masks)
+  uint32_t tail_stack_mask;
 };
 
 // Block-end counter deltas.  Every block holds its counter deltas (the wave

@@ -1165,7 +1165,8 @@ class Gen:
                "v_readfirstlane_b32 s72, v42", "v_readfirstlane_b32 s73, v43",  # frames
                "v_readfirstlane_b32 s74, v44", "v_readfirstlane_b32 s75, v45",  # entry table
                "v_readfirstlane_b32 s76, v46", "v_readfirstlane_b32 s77, v47",  # word / depth stride
-               "v_readfirstlane_b32 s85, v48",                                  # stack words
+               "v_readfirstlane_b32 s85, v48",                 # stack save mask | stack bytes << 16
+               "v_readfirstlane_b32 s68, v49",                 # ctx save mask (s68: free until an exit)
                "s_cmp_eq_u64 s[72:73], 0", f"s_cbranch_scc1 {L('slow')}")
 
     def frame_ptr(self):
@@ -1176,6 +1177,32 @@ class Gen:
     def fnext(self, n=1):
         for _ in range(n):
             self.e("v_add_co_u32 v56, vcc, s76, v56", "v_addc_co_u32 v57, vcc, 0, v57, vcc")
+
+    def word_addr(self, w):
+        """v[58:59] = the address of frame word w of this lane's frame."""
+        if w == 0:
+            self.e("v_mov_b32 v58, v56", "v_mov_b32 v59, v57")
+        else:
+            self.e(f"v_mad_u64_u32 v[58:59], s[62:63], {w}, s76, v[56:57]")
+
+    def stack_words(self, store):
+        """The stack words of the save mask (s85 & 0xffff; stack bytes
+        s85 >> 16) to (store) or from the frame (words 20..)."""
+        loop, done = self.label("tsl"), self.label("tsd")
+        self.e("s_lshr_b32 s69, s85, 16", "v_subrev_u32 v41, s69, %[stklo]",   # the stack bottom
+               "s_and_b32 s70, s85, 0xffff",
+               f"{loop}:", "s_cmp_eq_u32 s70, 0", f"s_cbranch_scc1 {done}",
+               "s_ff1_i32_b32 s69, s70", "s_bitset0_b32 s70, s69",
+               "s_lshl_b32 s71, s69, 3", "v_add_u32 v43, s71, v41",
+               "s_add_u32 s71, s69, 20", "s_mul_i32 s71, s71, s76",
+               "v_add_co_u32 v58, vcc, s71, v56", "v_addc_co_u32 v59, vcc, 0, v57, vcc")
+        if store:
+            self.e("ds_read_b64 v[44:45], v43", "s_waitcnt lgkmcnt(0)",
+                   "global_store_dwordx2 v[58:59], v[44:45], off")
+        else:
+            self.e("global_load_dwordx2 v[44:45], v[58:59], off", "s_waitcnt vmcnt(0)",
+                   "ds_write_b64 v43, v[44:45]")
+        self.e(f"s_branch {loop}", f"{done}:")
 
     def go_groups(self):
         """Every running lane continues at its own IP (v50, bytes): the first
@@ -1246,35 +1273,27 @@ class Gen:
                "s_lshr_b32 s49, s48, 5", "s_add_u32 s49, s49, 1",           # return pc
                "s_mov_b64 s[60:61], exec",
                "s_and_b64 exec, exec, s[54:55]", f"s_cbranch_execz {noval}")
-        # ---- push: r1..r10, ctx address, return pc | 48 << 32, ctx, stack ----
+        # ---- push (a masked frame, common.hpp kFrameMasked): the caller's
+        # live registers (FInsn imm), the header, the ctx / stack words the
+        # image's targets may write (tenv masks) ----
         self.frame_ptr()
-        for r in range(1, 11):
-            self.e(f"global_store_dwordx2 v[56:57], v[{R0 + 2 * r}:{R0 + 2 * r + 1}], off")
-            self.fnext()
-        self.e(f"global_store_dwordx2 v[56:57], v[{R0 + 2}:{R0 + 3}], off")
-        self.fnext()
-        self.e("v_mov_b32 v44, s49", "v_mov_b32 v45, 48",
-               "global_store_dwordx2 v[56:57], v[44:45], off")
-        self.fnext()
-        for half in (0, 24):
-            self.e(f"ds_read_b64 v[42:43], v{R0 + 2} offset:{half}",
-                   f"ds_read_b64 v[44:45], v{R0 + 2} offset:{half + 8}",
-                   f"ds_read_b64 v[46:47], v{R0 + 2} offset:{half + 16}",
-                   "s_waitcnt lgkmcnt(0)")
-            for v in (42, 44, 46):
-                self.e(f"global_store_dwordx2 v[56:57], v[{v}:{v + 1}], off")
-                self.fnext()
-        self.fnext(2)                                                        # ctx words 18, 19
-        loop, done = self.label("tsl"), self.label("tsd")
-        self.e("s_lshl_b32 s69, s85, 3", "v_subrev_u32 v41, s69, %[stklo]",   # stack base
-               "s_mov_b32 s69, s85",
-               f"{loop}:", "s_cmp_eq_u32 s69, 0", f"s_cbranch_scc1 {done}",
-               "ds_read_b64 v[42:43], v41", "s_waitcnt lgkmcnt(0)",
-               "global_store_dwordx2 v[56:57], v[42:43], off",
-               "v_add_u32 v41, 8, v41", "s_sub_u32 s69, s69, 1")
-        self.fnext()
-        self.e(f"s_branch {loop}", f"{done}:",
-               "v_add_u32 v54, 1, v54", "ds_write_b32 v40, v54 offset:24576",
+        for r in range(1, 10):
+            skip = self.label("tpr")
+            self.e(f"s_bitcmp1_b32 s42, {r}", f"s_cbranch_scc0 {skip}")
+            self.word_addr(r - 1)
+            self.e(f"global_store_dwordx2 v[58:59], v[{R0 + 2 * r}:{R0 + 2 * r + 1}], off", f"{skip}:")
+        self.word_addr(11)
+        self.e("s_lshl_b32 s69, s42, 8", "s_or_b32 s69, s69, 0x100",              # masked | live << 8
+               "v_mov_b32 v44, s49", "v_mov_b32 v45, s69",
+               "global_store_dwordx2 v[58:59], v[44:45], off")
+        for k in range(6):
+            skip = self.label("tpc")
+            self.e(f"s_bitcmp1_b32 s68, {k}", f"s_cbranch_scc0 {skip}",
+                   f"ds_read_b64 v[42:43], v{R0 + 2} offset:{8 * k}", "s_waitcnt lgkmcnt(0)")
+            self.word_addr(12 + k)
+            self.e("global_store_dwordx2 v[58:59], v[42:43], off", f"{skip}:")
+        self.stack_words(store=True)
+        self.e("v_add_u32 v54, 1, v54", "ds_write_b32 v40, v54 offset:24576",
                f"v_mov_b32 v{R0}, 0", f"v_mov_b32 v{R0 + 1}, 0",
                f"v_mov_b32 v{R0 + 4}, 64", f"v_mov_b32 v{R0 + 5}, 0",
                f"v_mov_b32 v{R0 + 20}, %[r10lo]", f"v_mov_b32 v{R0 + 21}, %[r10hi]")
@@ -1289,46 +1308,42 @@ class Gen:
         self.go_groups()
 
     def tail_ret(self):
-        """A linked target's exit (kRetHelper): pop the frame, r0 stays the
-        target's result, continue after the tail call."""
+        """A linked target's exit (kRetHelper): pop a masked frame (the live
+        registers its header names, the image's ctx / stack words), r10 =
+        the stack top, r0 stays the target's result, continue after the
+        tail call.  Full frames (pushed by C++) leave for C++."""
         self.tail_env()
-        self.e("v_cmp_eq_u32 s[54:55], 0, v54", "s_and_b64 s[54:55], s[54:55], exec",
+        self.e("s_bitcmp1_b32 s68, 31", f"s_cbranch_scc1 {L('slow')}",
+               "v_cmp_eq_u32 s[54:55], 0, v54", "s_and_b64 s[54:55], s[54:55], exec",
                f"s_cbranch_scc1 {L('slow')}",                                # no frame: C++ fails the lane
                "v_add_u32 v54, -1, v54",
                "s_waitcnt vmcnt(0)")
         self.frame_ptr()
-        self.e("v_mad_u64_u32 v[44:45], s[62:63], 10, s76, v[56:57]",
-               "global_load_dwordx2 v[46:47], v[44:45], off",               # ctx address
-               "v_add_co_u32 v44, vcc, s76, v44", "v_addc_co_u32 v45, vcc, 0, v45, vcc",
-               "global_load_dwordx2 v[48:49], v[44:45], off",               # return pc | ctx bytes
+        self.word_addr(11)
+        self.e("global_load_dwordx2 v[46:47], v[58:59], off",                 # return pc | flags
                "s_waitcnt vmcnt(0)",
-               "v_cmp_eq_u32 s[54:55], %[r1lo], v46", "v_cmp_eq_u32 vcc, %[r1hi], v47",
-               "s_and_b64 s[54:55], s[54:55], vcc",
-               "v_cmp_eq_u32 vcc, 48, v49", "s_and_b64 s[54:55], s[54:55], vcc",
-               "s_andn2_b64 s[54:55], exec, s[54:55]", f"s_cbranch_scc1 {L('slow')}",
+               "v_and_b32 v41, 0x100, v47", "v_cmp_ne_u32 vcc, 0, v41",
+               "s_andn2_b64 s[54:55], exec, vcc", f"s_cbranch_scc1 {L('slow')}",
                "ds_write_b32 v40, v54 offset:24576",
-               "v_lshlrev_b32 v50, 5, v48")                                  # return IP
-        for r in range(1, 11):
-            self.e(f"global_load_dwordx2 v[{R0 + 2 * r}:{R0 + 2 * r + 1}], v[56:57], off")
-            self.fnext()
-        self.fnext(2)
-        ctxv = [(42, 43), (44, 45), (46, 47), (48, 49), (54, 55), (58, 59)]
-        for a, b in ctxv:
-            self.e(f"global_load_dwordx2 v[{a}:{b}], v[56:57], off")
-            self.fnext()
-        self.fnext(2)
-        self.e("s_waitcnt vmcnt(0)")
-        for k, (a, b) in enumerate(ctxv):
-            self.e(f"ds_write_b64 %[r1lo], v[{a}:{b}] offset:{8 * k}")
-        loop, done = self.label("trl"), self.label("trd")
-        self.e("s_lshl_b32 s69, s85, 3", "v_subrev_u32 v41, s69, %[stklo]",
-               "s_mov_b32 s69, s85",
-               f"{loop}:", "s_cmp_eq_u32 s69, 0", f"s_cbranch_scc1 {done}",
-               "global_load_dwordx2 v[42:43], v[56:57], off", "s_waitcnt vmcnt(0)",
-               "ds_write_b64 v41, v[42:43]",
-               "v_add_u32 v41, 8, v41", "s_sub_u32 s69, s69, 1")
-        self.fnext()
-        self.e(f"s_branch {loop}", f"{done}:", "s_waitcnt lgkmcnt(0)")
+               "v_lshlrev_b32 v50, 5, v46",                                  # return IP
+               "s_mov_b64 s[60:61], exec")
+        for r in range(1, 10):
+            skip = self.label("trr")
+            self.e("s_mov_b64 exec, s[60:61]",
+                   f"v_and_b32 v41, {1 << (8 + r)}, v47", "v_cmp_ne_u32 vcc, 0, v41",
+                   "s_and_b64 exec, s[60:61], vcc", f"s_cbranch_execz {skip}")
+            self.word_addr(r - 1)
+            self.e(f"global_load_dwordx2 v[{R0 + 2 * r}:{R0 + 2 * r + 1}], v[58:59], off", f"{skip}:")
+        self.e("s_mov_b64 exec, s[60:61]",
+               f"v_mov_b32 v{R0 + 20}, %[r10lo]", f"v_mov_b32 v{R0 + 21}, %[r10hi]")
+        for k in range(6):
+            skip = self.label("trc")
+            self.e(f"s_bitcmp1_b32 s68, {k}", f"s_cbranch_scc0 {skip}")
+            self.word_addr(12 + k)
+            self.e("global_load_dwordx2 v[42:43], v[58:59], off", "s_waitcnt vmcnt(0)",
+                   f"ds_write_b64 %[r1lo], v[42:43] offset:{8 * k}", f"{skip}:")
+        self.stack_words(store=False)
+        self.e("s_waitcnt vmcnt(0) lgkmcnt(0)")
         self.go_groups()
 
     # ---- divergence: min-pc scheduling of lane groups ----

@@ -566,7 +566,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
   SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(flush_log); SRV(log_words); SRP(lane_scratch);
-  SRV(lru_seq);
+  SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
 #undef SRP
 #undef SRV
@@ -591,14 +591,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   auto comb_tag = [&](uint32_t t) -> uint64_t { return t ? (p.arena_lo + (t & ~3u)) | (t & 1u) : 0; };
   // tail-call launch constants for the asm tier (XDP images: the frames'
   // ctx copy is the lane's LDS ctx): frames (0: tail calls in C++), entry
-  // table, word stride | depth stride << 32, stack words
+  // table, word stride | depth stride << 32, stack / ctx save masks
   if (tid == 0) {
-    const bool on = IMAGE && KIND == CTX_XDP && p.frames && p.tail_entry;
+    const bool on = IMAGE && KIND == CTX_XDP && p.frames && p.tail_entry && !(p.dbg & 8);  // dbg 8: C++ frames
     const uint64_t stride = (uint64_t)gridDim.x * kBlock * 8;
     tenv[0] = on ? (uint64_t)(uintptr_t)p.frames : 0;
     tenv[1] = (uint64_t)(uintptr_t)p.tail_entry;
     tenv[2] = stride | ((stride * p.frame_words) << 32);
-    tenv[3] = p.stack_size / 8;
+    const uint32_t sw = p.stack_size / 8;  // (images in the asm tier: <= kLdsStackMax bytes)
+    const uint32_t smask = p.tail_stack_mask & (sw >= 16 ? 0xffffu : (1u << sw) - 1);
+    tenv[3] = (uint64_t)smask | ((uint64_t)p.stack_size << 16) | ((uint64_t)(p.tail_ctx_mask & 0x3f) << 32) |
+              ((p.dbg & 16) ? 1ull << 63 : 0);  // dbg 16: frames popped in C++
   }
   __syncthreads();
   uint64_t big_stack[BIGSTACK ? kStackSize / 8 : 1];
@@ -856,15 +859,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             const uint32_t d = tdep[0] - 1;
             tdep[0] = d;
             const uint64_t rv = R[0];
-            for (int r = 1; r <= 10; r++) R[r * kBlock] = FW(d, r - 1);
-            const uint64_t a1 = FW(d, 10);
             const uint64_t w11 = FW(d, 11);
             next = (uint32_t)w11;
-            const uint32_t cb = (uint32_t)(w11 >> 32);
-            for (uint32_t i = 0; i < cb; i += 8) mem_store(a1 + i, 8, FW(d, kFrameHdr / 8 + i / 8));
             const uint64_t sb = stack_top - sbytes;
-            for (uint32_t i = 0; i < sbytes; i += 8)
-              *(uint64_t *)(sb + i) = FW(d, (kFrameHdr + kFrameCtx) / 8 + i / 8);
+            if (w11 & kFrameMasked) {  // pushed by the asm tier (common.hpp kFrameMasked)
+              for (int r = 1; r <= 9; r++)
+                if ((w11 >> (kFrameLiveShift + r)) & 1) R[r * kBlock] = FW(d, r - 1);
+              R[10 * kBlock] = stack_top;
+              for (uint32_t k = 0; k < 6; k++)
+                if ((p.tail_ctx_mask >> k) & 1) mem_store((uint64_t)(uintptr_t)my_ctx + 8 * k, 8, FW(d, kFrameHdr / 8 + k));
+              for (uint32_t j = 0; 8 * j < sbytes; j++)
+                if ((p.tail_stack_mask >> j) & 1) *(uint64_t *)(sb + 8 * j) = FW(d, (kFrameHdr + kFrameCtx) / 8 + j);
+            } else {
+              for (int r = 1; r <= 10; r++) R[r * kBlock] = FW(d, r - 1);
+              const uint64_t a1 = FW(d, 10);
+              const uint32_t cb = (uint32_t)(w11 >> 32) & 0xff;
+              for (uint32_t i = 0; i < cb; i += 8) mem_store(a1 + i, 8, FW(d, kFrameHdr / 8 + i / 8));
+              for (uint32_t i = 0; i < sbytes; i += 8)
+                *(uint64_t *)(sb + i) = FW(d, (kFrameHdr + kFrameCtx) / 8 + i / 8);
+            }
             R[0] = rv;
           }
         }
@@ -905,7 +918,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       if (c.err != E_OK) {
         // bpftime_prog.cpp:250-257: a failed exec reports 0
         if (p.verdicts) p.verdicts[unit] = 0;
-        if (p.rets) p.rets[unit] = 0;
+        if (p.rets) p.rets[unit] = (p.dbg & 32) ? (0xE0000000ull | c.err | ((uint64_t)c.pc << 8) | ((uint64_t)c.lpc << 36)) : 0;
         atomicAdd(p.err_count, 1u);
       } else if (KIND == CTX_SYSCALL) {
         const int64_t nr = *(const int64_t *)(slot + 8);

@@ -593,6 +593,12 @@ int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &
     }
   }
 
+  // what a tail-call frame must keep of its caller's registers
+  out.tail_live.assign(n, 0);
+  for (uint32_t i = 0; i + 1 < n; i++)
+    if (reach[i] && p[i].op == X_CALL && p[i].hi == (int32_t)kTailHelper)
+      out.tail_live[i] = (uint16_t)(live_in[i + 1] & 0x3fe);
+
   // RMW fusion: ldx r,[b+o]; add r,v; stx [b+o],r is one atomic add (the
   // reference's ld/add/st is not atomic, but it runs one unit at a time: a
   // parallel batch needs the add to be indivisible to give the same total).
@@ -1064,6 +1070,61 @@ static bool rebinds(const std::vector<DInsn> &p, const PVal &b, bool may_delete)
   return false;
 }
 
+// The ctx and stack words a linked target may write (FastForm
+// tail_ctx_mask / tail_stack_mask): its stores through ctx / stack pointers
+// of known offset, and the helpers that write ctx fields or stack buffers.
+// Targets are the pcs before the loaded program (vm_api.cpp links them first,
+// behind a jump at pc 0); anything not understood saves everything.
+static void tail_save_masks(const std::vector<DInsn> &p, const std::vector<std::vector<PVal>> &in,
+                            uint32_t stack_size, FastForm &out) {
+  uint32_t cm = 0, sm = 0;
+  const uint32_t all_s = stack_size >= 256 ? 0xffffffffu : (1u << ((stack_size + 7) / 8)) - 1;
+  auto ctx_bytes = [&](int64_t at, int64_t len) {
+    for (int64_t k = 0; k < 6; k++)
+      if (at < 8 * k + 8 && 8 * k < at + len) cm |= 1u << k;
+  };
+  auto stk_bytes = [&](int64_t at, int64_t len) {  // at: offset from the stack top (< 0)
+    const int64_t lo = (int64_t)stack_size + at, hi = lo + len;
+    if (lo < 0 || hi > (int64_t)stack_size) {
+      sm = all_s;
+      return;
+    }
+    for (int64_t j = 0; 8 * j < (int64_t)stack_size; j++)
+      if (lo < 8 * j + 8 && 8 * j < hi) sm |= 1u << j;
+  };
+  auto write = [&](const PVal &b, int64_t off, int64_t len) {
+    switch (b.kind) {
+      case P_CTX: ctx_bytes((int64_t)b.k + off, len); break;
+      case P_STK: stk_bytes((int64_t)b.k + off, len); break;
+      case P_PKT: case P_SLOT: case P_MAPVAL: case P_CONST: break;
+      default: cm = 0x3f; sm = all_s;
+    }
+  };
+  uint32_t end = (uint32_t)p.size();
+  if (!p.empty() && p[0].op == X_JA) end = p[0].tgt;  // the loaded program starts there
+  for (uint32_t i = 1; i < end; i++) {
+    const std::vector<PVal> &st = in[i];
+    if (st[0].kind == P_UNDEF && st[1].kind == P_UNDEF) continue;  // unreached
+    const DInsn &d = p[i];
+    const int64_t sz = 1 << ((d.aux >> A_SIZE_SHIFT) & 3);
+    if (d.op == X_ST || d.op == X_STX || d.op == X_ATOMIC || d.op == X_RMW_ADD) write(st[d.dst], d.off, sz);
+    if (d.op != X_CALL) continue;
+    switch ((uint32_t)d.hi) {
+      case 1: case 2: case 3: case 5: case 7: case 8: case 12: case 28: case 130: case 131: case 132: case 133:
+        break;
+      case 44: case 65: ctx_bytes(0, 16); break;  // adjust_head / adjust_tail: data, data_end
+      case 189: write(st[3], 0, 1 << 16); break;  // xdp_load_bytes(ctx, off, to, len)
+      default:
+        if (d.hi != kRetHelper) {
+          cm = 0x3f;
+          sm = all_s;
+        }
+    }
+  }
+  out.tail_ctx_mask = cm;
+  out.tail_stack_mask = sm & all_s;
+}
+
 static uint32_t direct_add_handler(const DInsn &d) {
   const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
   if (sz != 4 && sz != 8) return F_SLOW;
@@ -1101,7 +1162,10 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
     f.aux = d.imm;
     // tail calls / a linked target's exit: asm frames in the XDP form
     // (gen_fast.py tail_call; the raw form's ctx copy is left to C++)
-    if (xdp && d.op == X_CALL && d.hi == (int32_t)kTailHelper) f.hoff = 4 + 4 * F_TAIL;
+    if (xdp && d.op == X_CALL && d.hi == (int32_t)kTailHelper) {
+      f.hoff = 4 + 4 * F_TAIL;
+      f.imm = i < lo.tail_live.size() ? lo.tail_live[i] : 0x3fe;  // registers the frame keeps
+    }
     if (xdp && d.op == X_CALL && d.hi == kRetHelper) f.hoff = 4 + 4 * F_TRET;
   }
   // helpers that move ctx->data / data_end invalidate packet pointers
@@ -1149,6 +1213,7 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
       comb = true;
   }
   out.needs_comb = comb;
+  if (lo.multi_entry && xdp) tail_save_masks(prog, in, lo.stack_size, out);
   uint32_t nspec = 0;
   bool ctx_escapes = false;
   const bool big_stack = lo.big_stack;

@@ -46,6 +46,10 @@ struct FastForm {
   bool needs_comb = true;      // per-lane counter adds (LDS combining table)
   bool needs_ctx = true;       // XDP: the ctx must exist in LDS
   std::vector<uint8_t> add_site;  // per insn: a counter add (fused RMW, atomic add without fetch)
+  // linked images, XDP form: the ctx words (bit k = bytes [8k, 8k+8)) and
+  // LDS stack words (bit j = the j-th 8 bytes from the stack bottom) that a
+  // tail-call target may write -- what a frame must save for its caller
+  uint32_t tail_ctx_mask = 0x3f, tail_stack_mask = 0xffffffffu;
 };
 
 struct LoadOut {
@@ -59,6 +63,7 @@ struct LoadOut {
   bool tail_call = false;     // calls bpf_tail_call: linked with the prog arrays' targets at launch
   bool multi_entry = false;   // a linked image (tail-call targets are extra entries)
   std::vector<uint32_t> entries;  // the linked targets' entry pcs
+  std::vector<uint16_t> tail_live;  // per pc: registers r1..r9 live after a bpf_tail_call (bit r)
 };
 
 // Helper ids the device implements (interp.hip helper switch).

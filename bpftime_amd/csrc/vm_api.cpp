@@ -517,6 +517,8 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     // one buffer per stream: concurrent batches never share frames
     p.tail_entry = im.d_tail_entry;
     p.frame_words = im.frame_words;
+    p.tail_ctx_mask = im.fx.tail_ctx_mask;
+    p.tail_stack_mask = im.fx.tail_stack_mask;
     const uint64_t fbytes = (uint64_t)grid * kBlock * kTailDepth * im.frame_words * 8;
     p.frames = (uint8_t *)frames.get(s, fbytes);
     if (!p.frames) {
