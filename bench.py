@@ -151,15 +151,17 @@ def main():
     tmax = max(times)
     value = world * n * args.steps / tmax / 1e6
     achieved_gbs = ALGO_BYTES_PER_PKT * n / kern_avg_s / 1e9
+    # HBM bytes per launch from the committed PMC pass of this command
+    # (tools/prof_workload.sh xdp-counter + tools/pmc_table.py: FETCH_SIZE x2 +
+    # WRITE_SIZE), when it was taken at this launch size
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            if pmc.get("packets") == n and pmc.get("program") == "xdp-counter":
-                traffic = pmc.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_xdp-counter.json")) as f:
+            pmc = json.load(f)
+        if pmc.get("units") == n:
+            traffic = pmc.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        traffic = None
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:

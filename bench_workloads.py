@@ -18,6 +18,19 @@ import time
 import numpy as np
 
 HBM_PEAK_GBS = 8000.0
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def pmc_traffic(workload, units):
+    """HBM bytes per launch from the committed PMC pass of this workload
+    (profiles/pmc_<workload>.json, tools/prof_workload.sh + tools/pmc_table.py:
+    FETCH_SIZE x2 + WRITE_SIZE), when it was taken at this launch size."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_%s.json" % workload)) as f:
+            pmc = json.load(f)
+        return pmc.get("hbm_bytes_per_launch") if pmc.get("units") == units else None
+    except (OSError, ValueError):
+        return None
 
 
 def _timed(dev, step, steps, warmup):
@@ -108,7 +121,7 @@ def flow_hash(args, dev, gen, isa, programs):
         "parity": {"per_flow_totals_exact": ok_map, "verdict_classes": ok_verd, "flows": len(got),
                    "ok": ok_map and ok_verd},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic("flow-hash", n),
                      "kernel_avg_ms": round(kern_s * 1e3, 4), "algo_bytes_per_pkt": round(algo, 2)},
         "cpu_baseline": cpu,
     }
@@ -178,7 +191,7 @@ def syscall_agg(args, dev, gen, isa, programs):
         "parity": {"per_id_totals_exact": ok_map, "r0_all_zero": ok_ret, "keys": len(got),
                    "ok": ok_map and ok_ret},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic("syscall-agg", n),
                      "kernel_avg_ms": round(kern_s * 1e3, 4), "algo_bytes_per_rec": round(algo, 2)},
         "cpu_baseline": cpu,
     }
@@ -247,7 +260,7 @@ def lpm_route(args, dev, gen, isa, programs):
         "parity": {"sample_verdicts_exact": ok, "sample": sn, "ok": ok,
                    "verdicts": {str(k): int((verd == k).sum()) for k in (1, 2, 3)}},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic("lpm-route", n),
                      "kernel_avg_ms": round(kern_s * 1e3, 4), "algo_bytes_per_pkt": algo},
         "cpu_baseline": cpu,
     }
@@ -310,7 +323,7 @@ def ringbuf_sample(args, dev, gen, isa, programs):
                                % int(np.log2(n)), "packets": n, "records_per_run": picked},
         "parity": {"records": len(recs), "expected_records": fits, "ok": ok},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic("ringbuf-sample", n),
                      "kernel_avg_ms": round(kern_s * 1e3, 4), "algo_bytes_per_pkt": algo},
         "cpu_baseline": cpu,
     }
@@ -385,7 +398,7 @@ def tail_call(args, dev, gen, isa, programs):
                    "packets": n, "slots": 4},
         "parity": {"verdicts_exact": ok, "counters": got, "ok": ok},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic("tail-call", n),
                      "kernel_avg_ms": round(kern_s * 1e3, 4), "algo_bytes_per_pkt": algo},
         "cpu_baseline": cpu,
     }

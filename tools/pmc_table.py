@@ -1,4 +1,4 @@
-"""Per-launch PMC means of the interpreter kernel for one tools/prof_workload.sh
+"""Per-launch PMC medians of the interpreter kernel for one tools/prof_workload.sh
 run, as a table and as JSON (the `traffic` figure bench_workloads.py reads).
 
     python tools/pmc_table.py gpurun_out/prof_<tag>_<workload> <units per launch> [out.json]
@@ -29,18 +29,20 @@ def means(d):
     for r, f in rows:
         if int(r["Grid_Size"]) == big:
             per[r["Counter_Name"]][(r["Dispatch_Id"], f)] += float(r["Counter_Value"])
-    return {c: statistics.mean(v.values()) for c, v in per.items()}
+    # the median launch: a bench's first launch can differ (e.g. flow-hash
+    # inserts its 65536 flows there), the timed ones are alike
+    return {c: statistics.median(v.values()) for c, v in per.items()}
 
 
 def kernel_ms(d):
-    f = os.path.join(d, "kt_kernel_stats.csv")
+    """(median launch ms, launches) of the hot kernel from the kernel trace."""
+    f = os.path.join(d, "kt_kernel_trace.csv")
     if not os.path.exists(f):
         return None
     with open(f) as fh:
-        for r in csv.DictReader(fh):
-            if HOT in r["Name"]:
-                return float(r["AverageNs"]) / 1e6, int(r["Calls"])
-    return None
+        ds = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in csv.DictReader(fh)
+              if HOT in r["Kernel_Name"]]
+    return (statistics.median(ds), len(ds)) if ds else None
 
 
 def main():

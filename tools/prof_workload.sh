@@ -10,7 +10,11 @@ EXTRA="$*"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 D=gpurun_out/prof_${TAG}_${W}
-ARGS="--workload $W --steps 3 --warmup 1 --no-cpu-baseline $EXTRA"
+if [ "$W" = xdp-counter ]; then  # the headline bench line
+  ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-e2e $EXTRA"
+else
+  ARGS="--workload $W --steps 3 --warmup 1 --no-cpu-baseline $EXTRA"
+fi
 run() {  # name, counters...
   local name=$1; shift
   if [ "$name" = kt ]; then
