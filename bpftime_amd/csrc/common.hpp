@@ -52,6 +52,7 @@ constexpr uint8_t A_FETCH = 0x08;   // X_RMW_ADD: the loaded register stays live
                                     // r = fetch_add(addr, v) + v, the ldx/add/stx in one atomic
 
 // FInsn::w1 flags (per entry form and launch, loader.cpp build_fast / link_fast)
+constexpr uint32_t FW_LCACHE = 2;   // hash lookup: probe / fill the block's LDS lookup cache (gen_fast.py)
 constexpr uint32_t FW_NODEFER = 1;  // counter add: apply it to memory now (a later access of
                                     // the same unit may read or overwrite it, or the batch is
                                     // ORDERED): no per-wave delta cache, no LDS combining table
@@ -221,6 +222,7 @@ struct KParams {
   uint64_t lru_seq;       // this launch's LRU stamp sequence (common.hpp kLruSeqShift)
   uint32_t tail_ctx_mask;    // XDP images: ctx words / stack words a frame keeps (loader.cpp tail_save_masks)
   uint32_t tail_stack_mask;
+  uint32_t lcache;           // 1 = the block's hash-lookup cache exists (common.hpp kLcacheEntries)
 };
 
 // Block-end counter deltas.  Every block holds its counter deltas (the wave
@@ -240,9 +242,16 @@ inline uint32_t log_words_for(uint32_t comb_entries) { return 1 + 2 * (kWaveCach
 // tenv; the asm finds them 32 B before the combining table), the combining
 // table (u32 tags + u64 deltas per entry).
 constexpr uint32_t kTenvBytes = 32;
-inline size_t dyn_lds_for(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries) {
-  return (size_t)kBlock * ((kind == CTX_XDP ? 48 : 0) + (big_stack ? 0 : stack_size)) + kTenvBytes +
-         12 * (size_t)comb_entries;
+// Hash-lookup cache of a block (programs whose hash lookups the loader marks
+// FW_LCACHE: no deletions): kLcacheEntries {u32 tag, u32 (slot + 1) | fd << 22}
+// entries, 2-way sets, right below the tail-call constants.  A slot found for
+// a key stays that key's slot for the rest of a launch when nothing deletes.
+constexpr uint32_t kLcacheEntries = 1024;
+constexpr uint32_t kLcacheBytes = 8 * kLcacheEntries;
+inline size_t dyn_lds_for(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
+                          bool lcache = false) {
+  return (size_t)kBlock * ((kind == CTX_XDP ? 48 : 0) + (big_stack ? 0 : stack_size)) + (lcache ? kLcacheBytes : 0) +
+         kTenvBytes + 12 * (size_t)comb_entries;
 }
 
 // Error codes recorded per unit (err_count counts units with any error)

@@ -883,6 +883,66 @@ class Gen:
                "v_cndmask_b32 v50, v50, v42, vcc", "v_cndmask_b32 v51, v51, v43, vcc",
                "v_cvt_u32_f64 v56, v[50:51]")
 
+    # ---- the block's hash-lookup cache (common.hpp kLcacheEntries) ----
+    # 512 two-way sets of {u32 tag, u32 (slot + 1) | fd << 22} right below
+    # the tail-call constants (%[comb] - 32 - kLcacheBytes).  The tag is the
+    # key itself for 4-byte keys (a hit needs no memory access) and the low
+    # word of the h*31 hash otherwise (a hit re-reads the slot's key once,
+    # instead of the index entry and then the slot).  Only hash lookups the
+    # loader marked FW_LCACHE use it: nothing deletes during their launch, so
+    # a slot found for a key stays that key's slot.  v82 = the set's address,
+    # v83 = the tag, s49 = the map fd, kept until the lookup ends.
+    def lcache_on(self, skip):
+        self.e("s_bitcmp1_b32 s41, 1", f"s_cbranch_scc0 {skip}",
+               "s_cmp_gt_u32 s66, 0x3ffffe", f"s_cbranch_scc1 {skip}")      # slot + 1 in 22 bits
+
+    def lcache_probe(self, kd, done):
+        """Lanes whose key the cache holds get r0 and leave s[60:61]."""
+        skip = self.label("lcs")
+        self.lcache_on(skip)
+        self.e("v_xor_b32 v41, v48, v49",
+               "s_mul_i32 s69, s49, 0x9e3779b1", "v_xor_b32 v41, s69, v41",
+               "s_mov_b32 s69, 0x85ebca6b", "v_mul_lo_u32 v41, v41, s69",
+               "v_lshrrev_b32 v41, 23, v41", "v_lshlrev_b32 v41, 4, v41",          # set * 16 (512 sets)
+               f"s_sub_u32 s69, %[comb], {32 + 8 * 1024}", "v_add_u32 v82, s69, v41",
+               f"v_mov_b32 v83, v{44 if kd == 1 else 48}",
+               "ds_read_b128 v[54:57], v82", "s_waitcnt lgkmcnt(0)",
+               "s_lshl_b32 s69, s49, 22")
+        for way, (t, v, m) in enumerate(((54, 55, "s[56:57]"), (56, 57, "s[54:55]"))):
+            self.e(f"v_cmp_eq_u32 vcc, v{t}, v83",
+                   f"v_and_b32 v58, 0xffc00000, v{v}", f"v_cmp_eq_u32 {m}, s69, v58", f"s_and_b64 {m}, {m}, vcc",
+                   f"v_cmp_ne_u32 vcc, 0, v{v}", f"s_and_b64 {m}, {m}, vcc")
+        self.e("v_cndmask_b32 v58, v57, v55, s[56:57]",
+               "v_and_b32 v58, 0x3fffff, v58", "v_add_u32 v58, -1, v58",          # the slot
+               "s_or_b64 s[56:57], s[56:57], s[54:55]", "s_and_b64 s[56:57], s[56:57], exec",
+               f"s_cbranch_scc0 {skip}",
+               "v_mov_b32 v59, s68",
+               "v_mad_u64_u32 v[42:43], s[54:55], v58, v59, s[64:65]")
+        if kd > 1:  # a hash tag: compare the slot's key
+            self.e("s_mov_b64 exec, s[56:57]",
+                   "global_load_dwordx4 v[54:57], v[42:43], off offset:8 sc1",
+                   "s_waitcnt vmcnt(0)",
+                   "v_cmp_eq_u32 s[54:55], v54, v44")
+            for j in range(1, kd):
+                self.e(f"v_cmp_eq_u32 vcc, v{54 + j}, v{44 + j}", "s_and_b64 s[54:55], s[54:55], vcc")
+            self.e("s_and_b64 s[56:57], s[56:57], s[54:55]",
+                   "s_mov_b64 exec, s[60:61]")
+        self.e("s_mov_b64 s[54:55], exec", "s_mov_b64 exec, s[56:57]",            # exec = hits
+               f"v_add_co_u32 v{R0}, vcc, s70, v42", f"v_addc_co_u32 v{R0 + 1}, vcc, 0, v43, vcc",
+               "s_andn2_b64 s[60:61], s[54:55], s[56:57]", "s_mov_b64 exec, s[60:61]",
+               f"s_cbranch_execz {done}",
+               f"{skip}:")
+
+    def lcache_fill(self, vslot):
+        """exec = lanes that found their key in slot v<vslot>: remember it
+        (the way picked by a tag bit; a racing lane of the same set may win)."""
+        skip = self.label("lcf")
+        self.lcache_on(skip)
+        self.e(f"v_add_u32 v59, 1, v{vslot}", "s_lshl_b32 s69, s49, 22", "v_or_b32 v59, s69, v59",
+               "v_bfe_u32 v58, v83, 3, 1", "v_lshlrev_b32 v58, 3, v58", "v_add_u32 v58, v82, v58",
+               "ds_write2_b32 v58, v83, v59 offset1:1",
+               f"{skip}:")
+
     def index_probe(self, kd, done):
         """The map's lookup index (common.hpp ix_pos), if it has one: up to
         kIxProbes entries from ix_pos(h) until every lane has found its key
@@ -911,8 +971,9 @@ class Gen:
         for j in range(kd):
             self.e(f"v_cmp_eq_u32 vcc, v{56 + j}, v{44 + j}", "s_and_b64 s[56:57], s[56:57], vcc")
         self.e("s_and_saveexec_b64 s[62:63], s[56:57]",                         # exec = hits
-               f"v_add_co_u32 v{R0}, vcc, s70, v54", f"v_addc_co_u32 v{R0 + 1}, vcc, 0, v55, vcc",
-               "s_andn2_b64 exec, s[62:63], s[56:57]",                          # exec = other keys
+               f"v_add_co_u32 v{R0}, vcc, s70, v54", f"v_addc_co_u32 v{R0 + 1}, vcc, 0, v55, vcc")
+        self.lcache_fill(50)
+        self.e("s_andn2_b64 exec, s[62:63], s[56:57]",                          # exec = other keys
                f"s_cbranch_execz {done}",
                "v_add_u32 v41, 1, v41", "v_and_b32 v41, s67, v41",
                "s_add_u32 s85, s85, 1", "s_cmp_ge_u32 s85, 8", f"s_cbranch_scc1 {fail}",
@@ -931,7 +992,8 @@ class Gen:
                "v_add_u32 v41, s46, %[stklo]",
                "ds_read_b32 v44, v41", "ds_read_b32 v45, v41 offset:4",
                "ds_read_b32 v46, v41 offset:8", "ds_read_b32 v47, v41 offset:12",
-               "s_mov_b64 s[60:61], exec",
+               "s_mov_b64 s[60:61], exec", "s_mov_b64 s[76:77], exec",     # lanes still looking / all of them
+               "s_mov_b32 s49, s62",                                          # the map fd
                "s_waitcnt lgkmcnt(0)")
         for kd in (1, 2, 3, 4):
             nxt = self.label("kdn")
@@ -943,6 +1005,7 @@ class Gen:
                        "v_sub_co_u32 v48, vcc, v50, v48", "v_subb_co_u32 v49, vcc, v51, v49, vcc",
                        f"v_bfe_u32 v50, v{44 + i // 4}, {8 * (i % 4)}, 8",
                        "v_add_co_u32 v48, vcc, v48, v50", "v_addc_co_u32 v49, vcc, 0, v49, vcc")
+            self.lcache_probe(kd, done)
             self.index_probe(kd, done)
             # idx = h % nbuckets: h = ((hi * 2^16 + lo >> 16) * 2^16 + lo & 0xffff)
             self.e("v_cvt_f64_u32 v[58:59], s66", "v_rcp_f64 v[54:55], v[58:59]",
@@ -966,8 +1029,9 @@ class Gen:
             for j in range(1, kd):
                 self.e(f"v_cmp_eq_u32 vcc, v{48 + j}, v{44 + j}", "s_and_b64 s[56:57], s[56:57], vcc")
             self.e("s_and_saveexec_b64 s[62:63], s[56:57]",                   # exec = hits
-                   f"v_add_co_u32 v{R0}, vcc, s70, v54", f"v_addc_co_u32 v{R0 + 1}, vcc, 0, v55, vcc",
-                   "s_andn2_b64 exec, s[62:63], s[56:57]",                    # exec = other keys
+                   f"v_add_co_u32 v{R0}, vcc, s70, v54", f"v_addc_co_u32 v{R0 + 1}, vcc, 0, v55, vcc")
+            self.lcache_fill(56)
+            self.e("s_andn2_b64 exec, s[62:63], s[56:57]",                    # exec = other keys
                    f"s_cbranch_execz {done}",
                    "v_add_u32 v56, 1, v56",
                    "v_cmp_eq_u32 vcc, s66, v56", "v_cndmask_b32 v56, v56, 0, vcc",
@@ -977,8 +1041,8 @@ class Gen:
                    f"s_branch {loop}",
                    f"{nxt}:")
         self.e(f"s_branch {L('slow')}",
-               f"{bail}:", "s_mov_b64 exec, s[60:61]", f"s_branch {L('slow')}",
-               f"{done}:", "s_mov_b64 exec, s[60:61]")
+               f"{bail}:", "s_mov_b64 exec, s[76:77]", f"s_branch {L('slow')}",
+               f"{done}:", "s_mov_b64 exec, s[76:77]")
         self.next_seq()
 
     def counter_cache(self, sz, done):

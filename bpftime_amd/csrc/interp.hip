@@ -566,7 +566,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
   SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(flush_log); SRV(log_words); SRP(lane_scratch);
-  SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask);
+  SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask); SRV(lcache);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
 #undef SRP
 #undef SRV
@@ -583,10 +583,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   // the ctx and stack areas: comb_entries u32 tags {arena offset | 2 |
   // (4-byte ? 1 : 0)} (8-way sets), then comb_entries u64 deltas, flushed
   // when the block ends; sized 0 for programs that never need it
-  uint64_t *tenv = (uint64_t *)(dyn + kBlock * (CTXB + (BIGSTACK ? 0 : p.stack_size)));
+  uint32_t *lcache = (uint32_t *)(dyn + kBlock * (CTXB + (BIGSTACK ? 0 : p.stack_size)));
+  uint64_t *tenv = (uint64_t *)((uint8_t *)lcache + (p.lcache ? kLcacheBytes : 0));
   uint32_t *comb = (uint32_t *)((uint8_t *)tenv + kTenvBytes);
   uint64_t *comb_d = (uint64_t *)(comb + p.comb_entries);
   for (uint32_t i = tid; i < 3 * p.comb_entries; i += kBlock) comb[i] = 0;
+  if (p.lcache)
+    for (uint32_t i = tid; i < 2 * kLcacheEntries; i += kBlock) lcache[i] = 0;
   // a table tag as a flush tag {address | (4-byte ? 1 : 0)}
   auto comb_tag = [&](uint32_t t) -> uint64_t { return t ? (p.arena_lo + (t & ~3u)) | (t & 1u) : 0; };
   // tail-call launch constants for the asm tier (XDP images: the frames'
@@ -1067,15 +1070,16 @@ static_assert(kMergeEntries == 4u << 10, "k_comb_merge hashes into 2^10 sets of 
 // ---------------------------------------------------------------------------
 // Host-side launch wrappers
 // ---------------------------------------------------------------------------
-static size_t dyn_lds_bytes(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries) {
-  return dyn_lds_for(kind, big_stack, stack_size, comb_entries);
+static size_t dyn_lds_bytes(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
+                            bool lcache) {
+  return dyn_lds_for(kind, big_stack, stack_size, comb_entries, lcache);
 }
 
 extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind, bool big_stack, uint32_t grid,
                                                 uint32_t ordered, hipStream_t stream) {
   KParams q = *p;
   q.ordered = ordered;
-  const size_t dyn = dyn_lds_bytes(kind, big_stack, p->stack_size, p->comb_entries);
+  const size_t dyn = dyn_lds_bytes(kind, big_stack, p->stack_size, p->comb_entries, p->lcache != 0);
   dim3 g(grid), b(kBlock);
   const bool image = q.tail_entry && !big_stack;
 #define L(K, B, I) hipLaunchKernelGGL((k_interp<K, B, I>), g, b, dyn, stream, q)

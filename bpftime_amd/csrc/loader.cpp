@@ -1261,6 +1261,13 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
           f.src_x2 = m->value_size;
         } else {
           f.hoff = 4 + 4 * F_CALL_LOOKUP_STK;
+          // a HASH map nothing deletes from during the launch: found slots
+          // can be remembered in the block's LDS lookup cache
+          if (m && m->type == MT_HASH && !lo.may_delete && m->key_size % 4 == 0 && m->key_size <= 16 &&
+              !getenv("BPFTIME_AMD_NO_LCACHE")) {
+            f.w1 |= FW_LCACHE;
+            out.needs_lcache = true;
+          }
         }
         f.target = (uint32_t)(int32_t)at;
         nspec++;

@@ -45,6 +45,7 @@ struct FastForm {
   uint32_t specialized = 0;    // accesses / calls with statically typed bases
   bool needs_comb = true;      // per-lane counter adds (LDS combining table)
   bool needs_ctx = true;       // XDP: the ctx must exist in LDS
+  bool needs_lcache = false;   // a hash lookup uses the block's LDS lookup cache (FW_LCACHE)
   std::vector<uint8_t> add_site;  // per insn: a counter add (fused RMW, atomic add without fetch)
   // linked images, XDP form: the ctx words (bit k = bytes [8k, 8k+8)) and
   // LDS stack words (bit j = the j-th 8 bytes from the stack bottom) that a

@@ -421,6 +421,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       return -1;
     }
     p.needs_ctx = xdp && im.fx.needs_ctx ? 1 : 0;
+    p.lcache = (xdp ? im.fx : im.fr).needs_lcache ? 1 : 0;
     p.fast_div = getenv("BPFTIME_AMD_NO_ASM_DIVERGENCE") ? 0 : 1;
   }
   p.maps = r.d_maptab;
@@ -454,10 +455,11 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     // table reach beats occupancy (r01c sweep: flow-hash 256 -> 2048
     // entries 2.1 -> 0.6 ms per 2^22 packets)
     static std::map<uint64_t, uint32_t> best;  // (kind, big stack, stack bytes) -> entries
-    const uint64_t key = ((uint64_t)b->ctx_kind << 40) | ((uint64_t)prog.big_stack << 32) | prog.stack_size;
+    const uint64_t key = ((uint64_t)p.lcache << 48) | ((uint64_t)b->ctx_kind << 40) |
+                         ((uint64_t)prog.big_stack << 32) | prog.stack_size;
     auto it = best.find(key);
     if (it == best.end()) {
-      auto dyn = [&](uint32_t e) { return dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, e); };
+      auto dyn = [&](uint32_t e) { return dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, e, p.lcache); };
       const int base = std::min(2, bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn(kComb)));
       uint32_t e = kComb;
       while (e < kCombMax && bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn(2 * e)) >= base) e *= 2;
@@ -496,7 +498,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       hipGetDeviceProperties(&prop, dev);
       cus = prop.multiProcessorCount;
     }
-    const size_t dyn = dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, prog.comb_entries);
+    const size_t dyn = dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, p.comb_entries, p.lcache);
     int occ = bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn);
     if (occ < 1) occ = 1;
     uint64_t want = (b->count + kBlock - 1) / kBlock;
