@@ -1213,6 +1213,26 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
       comb = true;
   }
   out.needs_comb = comb;
+  // how many counter addresses the table can be asked to hold per block: an
+  // element per (map, site) -- per-CPU elements for the few virtual CPUs a
+  // block's consecutive units span (kBlock / 64 waves)
+  {
+    uint64_t hint = 0;
+    for (size_t i = 0; i < prog.size() && hint < ~0u; i++) {
+      const DInsn &d = prog[i];
+      if (!out.add_site[i] || (out.fast[i].w1 & FW_NODEFER)) continue;
+      const PVal b = in[i][d.dst];
+      if (b.kind == P_CONST || b.kind == P_UNDEF) continue;
+      const MapRec *m = b.kind == P_MAPVAL ? map_rec(b.id) : nullptr;
+      if (!m) {
+        hint = ~0u;
+        break;
+      }
+      const bool percpu = m->type == MT_PERCPU_ARRAY || m->type == MT_PERCPU_HASH;
+      hint += (uint64_t)m->max_entries * (percpu ? kBlock / 64 : 1);
+    }
+    out.comb_hint = hint >= ~0u ? ~0u : (uint32_t)hint;
+  }
   if (lo.multi_entry && xdp) tail_save_masks(prog, in, lo.stack_size, out);
   uint32_t nspec = 0;
   bool ctx_escapes = false;

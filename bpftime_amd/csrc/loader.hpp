@@ -46,6 +46,9 @@ struct FastForm {
   bool needs_comb = true;      // per-lane counter adds (LDS combining table)
   bool needs_ctx = true;       // XDP: the ctx must exist in LDS
   bool needs_lcache = false;   // a hash lookup uses the block's LDS lookup cache (FW_LCACHE)
+  // counter addresses a block's deferred per-lane adds can reach (an upper
+  // bound from the maps they target; ~0u: unknown): sizes the combining table
+  uint32_t comb_hint = ~0u;
   std::vector<uint8_t> add_site;  // per insn: a counter add (fused RMW, atomic add without fetch)
   // linked images, XDP form: the ctx words (bit k = bytes [8k, 8k+8)) and
   // LDS stack words (bit j = the j-th 8 bytes from the stack bottom) that a

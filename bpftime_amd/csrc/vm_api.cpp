@@ -455,14 +455,22 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     // table reach beats occupancy (r01c sweep: flow-hash 256 -> 2048
     // entries 2.1 -> 0.6 ms per 2^22 packets)
     static std::map<uint64_t, uint32_t> best;  // (kind, big stack, stack bytes) -> entries
-    const uint64_t key = ((uint64_t)p.lcache << 48) | ((uint64_t)b->ctx_kind << 40) |
-                         ((uint64_t)prog.big_stack << 32) | prog.stack_size;
+    const bool xdp_form = b->ctx_kind == CTX_XDP;
+    const uint32_t hint_key = (xdp_form ? im.fx : im.fr).comb_hint;
+    const uint64_t key = ((uint64_t)(hint_key >= 4096 ? 4096 : hint_key) << 50) | ((uint64_t)p.lcache << 48) |
+                         ((uint64_t)b->ctx_kind << 40) | ((uint64_t)prog.big_stack << 32) | prog.stack_size;
     auto it = best.find(key);
     if (it == best.end()) {
       auto dyn = [&](uint32_t e) { return dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, e, p.lcache); };
       const int base = std::min(2, bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn(kComb)));
+      // ... but no larger than twice the counter addresses a block can reach
+      // (per-CPU counters: a few; flow keys: the table's whole reach), since
+      // LDS it does not need is occupancy lost (tail-call 2.68 -> 2.07 ms)
+      const uint32_t hint = (xdp_form ? im.fx : im.fr).comb_hint;
       uint32_t e = kComb;
-      while (e < kCombMax && bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn(2 * e)) >= base) e *= 2;
+      while (e < kCombMax && (uint64_t)e < 2ull * hint &&
+             bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn(2 * e)) >= base)
+        e *= 2;
       if (getenv("BPFTIME_AMD_COMB_ENTRIES")) e = (uint32_t)atoi(getenv("BPFTIME_AMD_COMB_ENTRIES"));
       it = best.emplace(key, e).first;
     }
