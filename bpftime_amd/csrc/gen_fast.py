@@ -61,7 +61,7 @@ Fixed registers (declared as clobbers; the compiler keeps nothing live in
 them across the block).  The handlers are written against the numbering
 below; main() relocates every VGPR by +26 to the top of a 128-register
 budget (v40..v101 -> v66..v127):
-  s[40:47] W   current FInsn: w0 handler offset, w1 0, w[2:3] imm64 or off64
+  s[40:47] W   current FInsn: w0 handler offset, w1 flags | next handler offset << 8, w[2:3] imm64 or off64
                (staged: w2 dword index, w3 bit shift), w4 dst*2 (staged
                stores: dirty-chunk bits; lookups: max_entries), w5 src*2
                (staged imm stores: the imm; lookups: value size), w6 jump
@@ -176,8 +176,16 @@ class Gen:
                "s_setpc_b64 s[52:53]")
 
     def next_seq(self, slots=1):
-        self.e(f"s_add_u32 s48, s48, {INSN * slots}")
-        self.dispatch()
+        """Fall through: the handler offset of the next FInsn is w1 >> 8 of
+        this one (link_fast), so the jump does not wait for the fetch; the
+        handler waits for it on entry (lgkmcnt), overlapping the scalar load
+        with the two control transfers."""
+        self.e(f"s_add_u32 s48, s48, {INSN * slots}",
+               "s_lshr_b32 s52, s41, 8",
+               "s_load_dwordx8 s[40:47], s[78:79], s48",
+               "s_add_u32 s52, s50, s52",
+               "s_addc_u32 s53, s51, 0",
+               "s_setpc_b64 s[52:53]")
 
     def jump_taken(self):
         """IP = target; a taken jump is the only way back, so the step limit
@@ -1209,7 +1217,85 @@ class Gen:
                "s_mov_b32 s48, s86", "s_mov_b64 exec, s[88:89]")
         self.pop0()
         self.dispatch()
-        self.e(f"{last}:", "s_mov_b32 s84, 0", "s_mov_b64 exec, 0", "s_mov_b32 s68, 2", f"s_branch {L('done')}")
+        self.e(f"{last}:", "s_mov_b32 s84, 0", f"s_branch {L('chain')}")
+
+    # ---- unit chaining: the next unit starts inside the block ----
+    # After a unit every lane of the wave has exited, the wave's next unit
+    # (unit + ustep: %[sstep] bytes further on) runs without leaving the
+    # block, while %[chain] (full iterations left, counted down here) allows:
+    # the C++ side's per-unit setup and the block's entry / exit cost once
+    # per chain instead of once per unit.  entry bits: 3 r1 = the slot,
+    # 4 r2 = the unit length, 5 lengths from %[laddr], 6 the syscall-record
+    # filter (exit / exit_group records are skipped with r0 = 0,
+    # syscall_trace_attach_impl.cpp:25), 7 reset the lane's tail-call depth
+    # (images), 16.. the per-unit step of the
+    # virtual cpu (%[vcpu] = cpu | ncpu << 16, or ~0).
+    def chain_routine(self):
+        nxt, nov, nol, nos, sv, sr, nod = (self.label(x) for x in ("cnext", "cnv", "cnl", "cns", "csv", "csr", "cnd"))
+        e = self.e
+        e(f"{L('chain')}:",
+          "s_cmp_eq_u32 %[chain], 0", f"s_cbranch_scc1 {L('cend')}",
+          f"{nxt}:",
+          "s_sub_u32 %[chain], %[chain], 1",
+          "s_mov_b64 exec, s[58:59]",
+          "s_mov_b32 s71, 0",
+          "s_mov_b32 s70, %[sstep]",
+          "v_lshl_add_u64 v[52:53], v[52:53], 0, s[70:71]",
+          "s_lshl_b32 s70, %[ustep], 2",
+          "v_lshl_add_u64 %[vaddr], %[vaddr], 0, s[70:71]",
+          "v_lshl_add_u64 %[laddr], %[laddr], 0, s[70:71]",
+          "s_lshl_b32 s70, %[ustep], 3",
+          "v_lshl_add_u64 %[raddr], %[raddr], 0, s[70:71]",
+          # virtual cpu: + step, mod ncpu
+          "s_cmp_eq_u32 %[vcpu], -1", f"s_cbranch_scc1 {nov}",
+          "s_lshr_b32 s69, %[vcpu], 16",
+          "s_and_b32 s70, %[vcpu], 0xffff",
+          "s_lshr_b32 s71, %[entry], 16",
+          "s_add_u32 s70, s70, s71",
+          "s_sub_u32 s71, s70, s69",
+          "s_cmp_ge_u32 s70, s69",
+          "s_cselect_b32 s70, s71, s70",
+          "s_lshl_b32 s69, s69, 16",
+          "s_or_b32 %[vcpu], s70, s69",
+          f"{nov}:",
+          "s_bitcmp1_b32 %[entry], 5", f"s_cbranch_scc0 {nol}",
+          "global_load_dword %[ulen], %[laddr], off",
+          "s_waitcnt vmcnt(0)",
+          f"{nol}:",
+          "s_bitcmp1_b32 %[entry], 6", f"s_cbranch_scc0 {nos}",
+          # syscall filter: nr = *(u64 *)(slot + 8) in {60, 231} -> r0 = 0
+          "global_load_dwordx2 v[56:57], v[52:53], off offset:8",
+          "s_movk_i32 s70, 0xe7", "s_mov_b32 s71, 0",
+          "s_waitcnt vmcnt(0)",
+          "v_cmp_eq_u64 s[54:55], 60, v[56:57]",
+          "v_cmp_eq_u64 s[56:57], s[70:71], v[56:57]",
+          "s_or_b64 s[54:55], s[54:55], s[56:57]",
+          "s_and_b64 s[54:55], s[54:55], exec",
+          f"s_cbranch_scc0 {nos}",
+          "s_andn2_b64 s[60:61], exec, s[54:55]",
+          "s_mov_b64 exec, s[54:55]",
+          "v_mov_b32 v56, 0", "v_mov_b32 v57, 0",
+          "s_bitcmp1_b32 %[oflags], 0", f"s_cbranch_scc0 {sv}",
+          "global_store_dword %[vaddr], v56, off",
+          f"{sv}:",
+          "s_bitcmp1_b32 %[oflags], 1", f"s_cbranch_scc0 {sr}",
+          "global_store_dwordx2 %[raddr], v[56:57], off",
+          f"{sr}:",
+          "s_mov_b64 exec, s[60:61]",
+          f"s_cbranch_execnz {nos}",
+          "s_cmp_eq_u32 %[chain], 0", f"s_cbranch_scc0 {nxt}",
+          f"s_branch {L('cend')}",
+          f"{nos}:",
+          # images: the lane's tail-call depth back to 0 (R slot 12, lo word)
+          "s_bitcmp1_b32 %[entry], 7", f"s_cbranch_scc0 {nod}",
+          "v_mov_b32 v56, 0",
+          f"ds_write_b32 v40, v56 offset:{12 * 2048}",
+          f"{nod}:",
+          "s_mov_b32 %[steps], 0",
+          "s_mov_b32 s48, 0",
+          f"s_branch {L('fresh')}",
+          f"{L('cend')}:",
+          "s_mov_b64 exec, 0", "s_mov_b32 s68, 2", f"s_branch {L('done')}")
 
     # ---- bpf_tail_call in a linked image (XDP entry form) ----
     # The C++ path (interp.hip, kTailHelper / kRetHelper) restated for the
@@ -1508,6 +1594,7 @@ class Gen:
                f"s_sub_u32 s52, s52, {n4}", "s_subb_u32 s53, s53, 0",
                "s_setpc_b64 s[52:53]",
                f"{L('dswitch')}:",
+               "s_waitcnt lgkmcnt(0)",       # the fall-through fetch lands before another
                "s_cmp_eq_u32 s48, s86", f"s_cbranch_scc0 {ahead}",
                "s_or_b64 exec, exec, s[88:89]")                # reconvergence
         self.pop0()
@@ -1524,7 +1611,7 @@ class Gen:
     def build(self):
         ids = handler_ids()
         e = self.e
-        fresh, loaded = self.label("fresh"), self.label("loaded")
+        fresh, loaded = L("fresh"), self.label("loaded")
         # ---- entry ----
         e("s_mov_b64 s[78:79], %[prog]",
           "v_mov_b32 v40, %[rb]",
@@ -1549,6 +1636,14 @@ class Gen:
                 e(f"v_mov_b32 v{R0 + 20}, %[r10lo]", f"v_mov_b32 v{R0 + 21}, %[r10hi]")
             else:
                 e(f"v_mov_b32 v{R0 + 2 * r}, 0", f"v_mov_b32 v{R0 + 2 * r + 1}, 0")
+        # raw / syscall units: r1 = the slot, r2 = the length (chained units)
+        n1, n2 = self.label("nr1"), self.label("nr2")
+        e("s_bitcmp1_b32 %[entry], 3", f"s_cbranch_scc0 {n1}",
+          f"v_mov_b32 v{R0 + 2}, v52", f"v_mov_b32 v{R0 + 3}, v53",
+          f"{n1}:",
+          "s_bitcmp1_b32 %[entry], 4", f"s_cbranch_scc0 {n2}",
+          f"v_mov_b32 v{R0 + 4}, %[ulen]",
+          f"{n2}:")
         e("s_bitcmp1_b32 %[entry], 1", f"s_cbranch_scc0 {loaded}",
           "s_mov_b32 s80, %[stage]",
           f"global_load_dwordx4 v[{STG}:{STG + 3}], v[52:53], off")
@@ -1566,7 +1661,7 @@ class Gen:
         self.dispatch()
         # ---- handlers ----
         for name in ids:
-            e(f"{L('h_' + name)}:")
+            e(f"{L('h_' + name)}:", "s_waitcnt lgkmcnt(0)")  # W of a fall-through fetch
             if name == "SLOW":
                 e(f"s_branch {L('slow')}")
             elif name.startswith("ATOMD"):
@@ -1641,6 +1736,7 @@ class Gen:
             else:
                 raise ValueError(name)
         self.divergence_routines()
+        self.chain_routine()
         # ---- exits: the instruction at pc was not executed; write back
         # staging, spill registers
         e(f"{L('steps')}:", "s_mov_b32 s68, 1")

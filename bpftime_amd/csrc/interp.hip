@@ -475,6 +475,8 @@ struct FastEnv {
   uint32_t rb;      // LDS byte address of this lane's R[0]
   uint32_t stage;   // staged bytes per unit (0: no staging)
   uint32_t ncpu;    // virtual CPUs (per-CPU maps)
+  uint32_t sstep;   // chained units: slot bytes from one unit of a lane to its next
+  uint32_t ustep;   // ... and units (verdict / ret / length array steps)
 };
 
 constexpr uint32_t FAST_SLOW = 0, FAST_STEPS = 1, FAST_EXIT = 2, FAST_SPLIT = 3;
@@ -485,11 +487,19 @@ struct FastUnit {
   uint64_t r1, r10, slot;
   uint32_t r2;
   uint32_t len;    // unit length (ctx->data_end - ctx->data)
-  uint32_t entry;  // bit 0: fresh unit, bit 1: stage the slot, bit 2: lane groups in asm
-  uint64_t vcpu;   // the unit's virtual CPU (helper 8, per-CPU maps)
+  // bit 0: fresh unit, 1: stage the slot, 2: lane groups in asm; chained
+  // units (gen_fast.py chain_routine): 3 r1 = slot, 4 r2 = length, 5 lengths
+  // from laddr, 6 syscall-record filter, 16.. virtual-cpu step
+  uint32_t entry;
+  uint32_t vm;     // the unit's virtual CPU mod ncpu (per-CPU array lookups)
+  uint64_t vaddr, raddr, laddr;  // the unit's verdict / ret / length addresses (0: none)
+  uint32_t chain;  // further units the asm may run for this wave (every lane's unit < n)
 };
 
-__device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const FastUnit &u) {
+// adv: units the asm tier finished and moved past (chained); the lanes are
+// then in the wave's unit `adv` iterations further on, at c.pc
+__device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const FastUnit &u, uint32_t chain_in,
+                                             uint32_t &adv) {
   // every "s" operand must be provably uniform: readfirstlane what the
   // compiler cannot prove (the values are uniform by construction)
   uint32_t pc = __builtin_amdgcn_readfirstlane(c.pc), steps = __builtin_amdgcn_readfirstlane(c.steps), why;
@@ -507,24 +517,26 @@ __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const Fas
            c1dh = u32((uint32_t)(c.c1d >> 32)), c0s = u32(c.c0s), c1s = u32(c.c1s);
   // the wave's virtual cpu for per-CPU array lookups: cpu | ncpu << 16 when
   // every lane shares it (consecutive units), else ~0
-  const uint32_t vm = (uint32_t)(u.vcpu % f.ncpu), vm0 = __builtin_amdgcn_readfirstlane(vm);
-  const uint32_t vcpu = __ballot(c.alive && vm != vm0) == 0 && f.ncpu <= 0xffff ? vm0 | (f.ncpu << 16) : ~0u;
-  const uint64_t vaddr = c.verdicts ? (uint64_t)(uintptr_t)(c.verdicts + c.unit) : 0;
-  const uint64_t raddr = c.rets ? (uint64_t)(uintptr_t)(c.rets + c.unit) : 0;
+  const uint32_t vm0 = __builtin_amdgcn_readfirstlane(u.vm);
+  uint32_t vcpu = __ballot(c.alive && u.vm != vm0) == 0 && f.ncpu <= 0xffff ? vm0 | (f.ncpu << 16) : ~0u;
+  uint64_t vaddr = u.vaddr, raddr = u.raddr, laddr = u.laddr;
+  uint32_t ulen = u.len, chain = __builtin_amdgcn_readfirstlane(chain_in);
   asm volatile(BPFTIME_AMD_FAST_ASM
                : [pc] "+s"(pc), [steps] "+s"(steps), [why] "=s"(why), [aliveout] "=s"(alive_out),
                  [lpc] "=v"(lpc), [c0a] "+s"(c0a), [c1a] "+s"(c1a),
                  [c0dl] "+s"(c0dl), [c0dh] "+s"(c0dh), [c1dl] "+s"(c1dl), [c1dh] "+s"(c1dh), [c0s] "+s"(c0s),
-                 [c1s] "+s"(c1s)
+                 [c1s] "+s"(c1s), [vaddr] "+v"(vaddr), [raddr] "+v"(raddr), [laddr] "+v"(laddr), [ulen] "+v"(ulen),
+                 [chain] "+s"(chain), [vcpu] "+s"(vcpu)
                : [prog] "s"(f.fast), [maps] "s"(f.maps), [dlo] "s"(f.dlo), [dhi] "s"(f.dhi), [alo] "s"(f.alo),
                  [ahi] "s"(f.ahi), [shi] "s"(f.shi), [phi] "s"(f.phi), [limit] "s"(limit), [rb] "v"(f.rb),
-                 [alive] "s"(alive), [oflags] "s"(f.oflags), [vaddr] "v"(vaddr), [raddr] "v"(raddr),
+                 [alive] "s"(alive), [oflags] "s"(f.oflags),
                  [entry] "s"(entry), [r1lo] "v"((uint32_t)u.r1), [r1hi] "v"((uint32_t)(u.r1 >> 32)),
                  [r2lo] "v"(u.r2), [r10lo] "v"((uint32_t)u.r10), [r10hi] "v"((uint32_t)(u.r10 >> 32)),
                  [slotlo] "v"((uint32_t)u.slot), [slothi] "v"((uint32_t)(u.slot >> 32)),
-                 [head] "s"(f.head), [ulen] "v"(u.len), [stklo] "v"((uint32_t)u.r10), [comb] "s"(f.comb), [combn] "s"(f.combn),
-                 [stage] "s"(f.stage), [vcpu] "s"(vcpu)
+                 [head] "s"(f.head), [stklo] "v"((uint32_t)u.r10), [comb] "s"(f.comb), [combn] "s"(f.combn),
+                 [stage] "s"(f.stage), [sstep] "s"(f.sstep), [ustep] "s"(f.ustep)
                : BPFTIME_AMD_FAST_CLOBBERS);
+  adv = __builtin_amdgcn_readfirstlane(chain_in) - chain;
   c.pc = pc;
   c.steps = steps;
   c.c0a = c0a;
@@ -533,8 +545,9 @@ __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const Fas
   c.c1d = (uint64_t)c1dl | ((uint64_t)c1dh << 32);
   c.c0s = c0s;
   c.c1s = c1s;
-  // lanes that ran exit inside the block are done (verdict stored)
-  c.alive = c.alive && ((alive_out >> __lane_id()) & 1);
+  // lanes that ran exit inside the block are done (verdict stored); after
+  // chaining every lane is in a later unit, alive as the asm left it
+  c.alive = (adv ? true : c.alive) && ((alive_out >> __lane_id()) & 1);
   if (why == FAST_SPLIT && c.alive) c.lpc = lpc;  // (parked lane groups keep theirs)
   return why;
 }
@@ -651,33 +664,78 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
 
   const bool ordered = p.ordered != 0;
   const uint64_t ustep = ordered ? 1 : (uint64_t)gridDim.x * kBlock;
-  for (uint64_t u0 = ordered ? 0 : (uint64_t)blockIdx.x * kBlock; u0 < p.n; u0 += ustep) {
-    const uint64_t unit = ordered ? u0 : u0 + tid;
-    const bool active = ordered ? (tid == 0 && blockIdx.x == 0) : unit < p.n;
-    uint64_t slot = (uint64_t)(uintptr_t)p.data + unit * p.stride;
-    uint64_t chunk = slot;  // XDP ctx buffer_start
-    uint32_t len = p.fixed_len;
-    bool desc_ok = true;
-    if (p.descs) {
-      // AF_XDP descriptor ring: the frame at umem + addr; its chunk bounds
-      // the ctx buffer (aligned-chunk umem)
-      uint64_t addr = 0;
-      len = 0;
-      if (active) {
-        addr = p.descs[2 * unit];
-        len = (uint32_t)p.descs[2 * unit + 1];
+  // Chained units (gen_fast.py chain_routine): while every lane of the wave
+  // has a unit, the asm tier starts the wave's next unit itself.  Plain
+  // strided batches only: no descriptors, no per-unit ctx in LDS or ctx
+  // outputs, no syscall-number filter; dbg 64 turns it off.  (Images: only
+  // from a unit no lane group is parked in, and the depth is reset.)
+  const bool chain_ok = !ordered && !p.descs && p.stride && !p.out_data_off && !p.out_len &&
+                        !(KIND == CTX_XDP && p.needs_ctx) && !(KIND == CTX_SYSCALL && p.sys_nr >= 0) &&
+                        ustep * p.stride < (1ull << 32) && !(p.dbg & 64);
+  uint64_t full = 0;  // iterations in which every lane of this wave has a unit
+  if (chain_ok) {
+    const uint64_t wb = (uint64_t)blockIdx.x * kBlock + (tid & ~63u);
+    full = p.n >= wb + 64 ? (p.n - 64 - wb) / ustep + 1 : 0;
+  }
+  fe.sstep = (uint32_t)(ustep * p.stride);
+  fe.ustep = (uint32_t)ustep;
+  const uint32_t ncpu = fe.ncpu;
+  const bool ncpu_pow2 = (ncpu & (ncpu - 1)) == 0;
+  const uint32_t chain_bits = (KIND != CTX_XDP ? 8u : 0u) | (KIND == CTX_RAW ? 16u : 0u) | (p.lens ? 32u : 0u) |
+                              (KIND == CTX_SYSCALL ? 64u : 0u) | (IMAGE ? 128u : 0u) |
+                              ((uint32_t)((ustep / 64) % ncpu) << 16);
+  uint64_t it = 0;
+  for (uint64_t u0 = ordered ? 0 : (uint64_t)blockIdx.x * kBlock; u0 < p.n; u0 += ustep, it++) {
+    uint64_t unit, slot, chunk, vcpu;
+    bool active, desc_ok;
+    uint32_t len;
+    int32_t miss_fd;
+    uint64_t miss_hash;
+    uint32_t lru_ops;
+    bool ctx_ready;
+    FastUnit fu;
+    // the unit's addresses and per-unit helper state (also after the asm
+    // tier chained into a later unit: `chained`)
+    auto begin = [&](bool chained) {
+      unit = ordered ? u0 : u0 + tid;
+      active = ordered ? (tid == 0 && blockIdx.x == 0) : unit < p.n;
+      slot = (uint64_t)(uintptr_t)p.data + unit * p.stride;
+      chunk = slot;  // XDP ctx buffer_start
+      len = p.fixed_len;
+      desc_ok = true;
+      if (p.descs) {
+        // AF_XDP descriptor ring: the frame at umem + addr; its chunk bounds
+        // the ctx buffer (aligned-chunk umem)
+        uint64_t addr = 0;
+        len = 0;
+        if (active) {
+          addr = p.descs[2 * unit];
+          len = (uint32_t)p.descs[2 * unit + 1];
+        }
+        desc_ok = addr < p.umem_bytes && len <= p.umem_bytes - addr;
+        if (!desc_ok) addr = len = 0;
+        slot = (uint64_t)(uintptr_t)p.data + addr;
+        chunk = (uint64_t)(uintptr_t)p.data + (p.stride ? addr - addr % p.stride : addr);
+      } else if (active && p.lens) {
+        len = p.lens[unit];
       }
-      desc_ok = addr < p.umem_bytes && len <= p.umem_bytes - addr;
-      if (!desc_ok) addr = len = 0;
-      slot = (uint64_t)(uintptr_t)p.data + addr;
-      chunk = (uint64_t)(uintptr_t)p.data + (p.stride ? addr - addr % p.stride : addr);
-    } else if (active && p.lens) {
-      len = p.lens[unit];
-    }
-    const uint64_t vcpu = (p.first_unit + unit) / 64;
-    int32_t miss_fd = -1;
-    uint64_t miss_hash = 0;
-    uint32_t lru_ops = 0;
+      vcpu = (p.first_unit + unit) / 64;
+      miss_fd = -1;
+      miss_hash = 0;
+      lru_ops = 0;
+      fu.vm = ncpu_pow2 ? (uint32_t)vcpu & (ncpu - 1) : (uint32_t)(vcpu % ncpu);
+      fu.slot = slot;
+      fu.len = len;
+      fu.vaddr = p.verdicts ? (uint64_t)(uintptr_t)(p.verdicts + unit) : 0;
+      fu.raddr = p.rets ? (uint64_t)(uintptr_t)(p.rets + unit) : 0;
+      fu.laddr = p.lens ? (uint64_t)(uintptr_t)(p.lens + unit) : 0;
+      fu.chain = it + 1 < full ? (full - 1 - it > 0x7fffffffull ? 0x7fffffffu : (uint32_t)(full - 1 - it)) : 0;
+      c.unit = unit;
+      c.err = active && !desc_ok ? E_OOB : E_OK;
+      ctx_ready = KIND != CTX_XDP || p.needs_ctx;
+      (void)chained;
+    };
+    begin(false);
     // tail-call frames this lane has pushed (images: in LDS, the asm tier
     // pushes too)
     uint32_t tdepth_reg = 0;
@@ -686,12 +744,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
 
     // ---- per-unit setup: r1, r2, r10 (other registers zero) are set by the
     // fast path's fresh entry, which every unit starts with ----
-    FastUnit fu;
-    fu.vcpu = vcpu;
-    fu.slot = slot;
     fu.r10 = stack_top;
-    fu.len = len;
-    fu.entry = 1u | (p.stage ? 2u : 0u) | (p.fast_div ? 4u : 0u);
+    fu.entry = 1u | (p.stage ? 2u : 0u) | (p.fast_div ? 4u : 0u) | chain_bits;
     if (p.descs && p.stage) {
       // staging needs every lane's window 16-B aligned inside the umem
       const bool bad = active && ((slot & 15) != 0 || slot + p.stage > (uint64_t)(uintptr_t)p.data + p.umem_bytes);
@@ -715,9 +769,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       const int64_t nr = *(const int64_t *)(slot + 8);
       if (nr == 60 || nr == 231 || (p.sys_nr >= 0 && nr != p.sys_nr)) alive = false;
     }
-    c.unit = unit;
     c.alive = alive && desc_ok;
-    c.err = active && !desc_ok ? E_OOB : E_OK;
     c.pc = 0;
     c.lpc = 0;
     c.steps = 0;
@@ -738,8 +790,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     };
     // the asm tier computes specialised ctx->data / data_end loads from the
     // slot; the C++ tier reads the ctx, so it is written before the C++ tier
-    // first runs an instruction of this unit
-    bool ctx_ready = KIND != CTX_XDP || p.needs_ctx;
+    // first runs an instruction of this unit (ctx_ready: begin)
     auto ctx_for_cpp = [&]() {
       if (KIND == CTX_XDP && !ctx_ready) {
         write_xdp_ctx((XdpCtx *)my_ctx, slot, len, chunk, p);
@@ -762,8 +813,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         continue;
       }
       if (uni) {
-        const uint32_t why = run_fast(c, fe, fu);
-        fu.entry &= 4u;
+        // chain only from a unit every lane of the wave runs without a failure
+        const bool whole = __ballot(c.alive) == ~0ull && __ballot(c.err != E_OK) == 0 && __ballot(parked) == 0;
+        uint32_t adv = 0;
+        const uint32_t why = run_fast(c, fe, fu, whole ? fu.chain : 0u, adv);
+        fu.entry &= ~1u;
+        if (adv) {  // the asm tier finished `adv` units of this wave and is in the next
+          it += adv;
+          u0 += adv * ustep;
+          begin(true);
+        }
         if (why == FAST_EXIT) {  // every running lane ran exit; r0 already stored
           c.alive = false;
           if (__ballot(parked) == 0) break;

@@ -1374,8 +1374,28 @@ uint32_t stage_need(const FastForm &f, uint32_t head) {
   return (uint32_t)((ext + 15) & ~15);
 }
 
+// w1 bits 8+: the handler offset of the FInsn sequential flow reaches next
+// (gen_fast.py next_seq jumps on it before the fetch lands); the SLOW handler
+// past the end
+static void link_next(const std::vector<DInsn> &prog, std::vector<FInsn> &out) {
+  for (size_t i = 0; i < out.size(); i++) {
+    const size_t nx = i + (i < prog.size() && prog[i].op == X_LDDW ? 2 : 1);
+    const uint32_t h = nx < out.size() ? out[nx].hoff : 4 + 4 * F_SLOW;
+    out[i].w1 = (out[i].w1 & 0xffu) | (h << 8);
+  }
+}
+
+static void link_staged(const FastForm &f, uint32_t head, uint32_t stage, bool ordered,
+                        const std::vector<DInsn> &prog, std::vector<FInsn> &out);
+
 void link_fast(const FastForm &f, uint32_t head, uint32_t stage, bool ordered, const std::vector<DInsn> &prog,
                std::vector<FInsn> &out) {
+  link_staged(f, head, stage, ordered, prog, out);
+  link_next(prog, out);
+}
+
+static void link_staged(const FastForm &f, uint32_t head, uint32_t stage, bool ordered,
+                        const std::vector<DInsn> &prog, std::vector<FInsn> &out) {
   out = f.fast;
   if (ordered)  // the reference's sequential order: every counter add reaches memory at once
     for (size_t i = 0; i < out.size(); i++)

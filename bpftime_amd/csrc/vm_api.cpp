@@ -520,6 +520,9 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       if (atoi(g) > 0) mult = (uint32_t)atoi(g);
     uint64_t cap = (uint64_t)cus * (uint64_t)occ * mult;
     grid = (uint32_t)(want < cap ? want : cap);
+    // (tests: few blocks, so that small batches take many units per lane)
+    if (const char *g = getenv("BPFTIME_AMD_MAX_GRID"))
+      if (atoi(g) > 0 && grid > (uint32_t)atoi(g)) grid = (uint32_t)atoi(g);
     if (im.d_tail_entry && grid > kTailGrid) grid = kTailGrid;  // one frame stack per lane of the grid
   }
   if (im.d_tail_entry) {

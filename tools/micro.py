@@ -1,0 +1,95 @@
+"""Interpreter cost model on the GPU: kernel time of tiny XDP programs over
+2^24 64-B frames (fixed per-unit cost, cost per dispatched instruction of a
+few handler classes).  python tools/micro.py [log2n]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench_workloads as bw  # noqa: E402
+from bpftime_amd import gen, isa, programs  # noqa: E402
+from bpftime_amd import vm as dev  # noqa: E402
+
+PKT = 64
+
+
+def ret_only():
+    a = isa.Asm()
+    a.mov64(0, isa.XDP_PASS)
+    a.exit()
+    return a.assemble()
+
+
+def alu(n):
+    a = isa.Asm()
+    for i in range(n):
+        a.add64(3, i + 1)
+    a.mov64(0, isa.XDP_PASS)
+    a.exit()
+    return a.assemble()
+
+
+def alu_rr(n):
+    a = isa.Asm()
+    a.mov64(4, 7)
+    for i in range(n):
+        a.add64(3, "r4")
+    a.mov64(0, isa.XDP_PASS)
+    a.exit()
+    return a.assemble()
+
+
+def staged_loads(n):
+    a = isa.Asm()
+    a.ldx(8, 2, 1, 0)
+    a.ldx(8, 3, 1, 8)
+    a.mov64(4, "r2")
+    a.add64(4, 32)
+    a.mov64(0, isa.XDP_DROP)
+    a.jmp("jgt", 4, "r3", "out")
+    for i in range(n):
+        a.ldx(2, 5, 2, 2 * (i % 16))
+    a.mov64(0, isa.XDP_PASS)
+    a.label("out")
+    a.exit()
+    return a.assemble()
+
+
+def jumps(n):
+    a = isa.Asm()
+    for i in range(n):
+        a.jmp("jeq", 3, 12345, "out")
+    a.mov64(0, isa.XDP_PASS)
+    a.label("out")
+    a.exit()
+    return a.assemble()
+
+
+def main():
+    log2n = int(sys.argv[1]) if len(sys.argv) > 1 else 24
+    n = 1 << log2n
+    ngpu = dev.lib().bpftime_amd_device_count()
+    if ngpu <= 0 or dev.lib().bpftime_amd_set_device(0) != 0:
+        raise SystemExit("no GPU")
+    dev.reset_runtime()
+    ctl = dev.Map(isa.BPF_MAP_TYPE_ARRAY, 4, 4, 2, name="ctl_array")
+    bss = dev.Map(isa.BPF_MAP_TYPE_ARRAY, 4, 4096, 1, flags=isa.BPF_F_MMAPABLE, name=".bss")
+    pkts = dev.DeviceBuffer(n * PKT)
+    if dev.lib().bpftime_amd_gen_xdp(pkts.ptr, n, PKT, PKT, gen.SEED_CFG2, 0, None) != 0:
+        raise SystemExit("generator failed")
+    verd = dev.DeviceBuffer(4 * n)
+    cases = [("ret", ret_only(), 2), ("alu8", alu(8), 10), ("alu32", alu(32), 34), ("alurr32", alu_rr(32), 35),
+             ("ld8", staged_loads(8), 15), ("ld32", staged_loads(32), 39), ("jmp32", jumps(32), 34),
+             ("xdp-counter", programs.xdp_counter(ctl.fd, bss.fd), 37)]
+    for name, code, ninsn in cases:
+        vm = dev.VM()
+        vm.load(code)
+
+        def step():
+            vm.exec_batch(dev.CTX_XDP, pkts, n, PKT, fixed_len=PKT, verdicts=verd, flags=0)
+        _, k = bw._timed(dev, step, 10, 3)
+        print("%-12s insns %3d  kernel %.4f ms  %.2f ps/pkt  %.3f ps/pkt/insn" %
+              (name, ninsn, k * 1e3, k / n * 1e12, k / n / ninsn * 1e12), flush=True)
+
+
+if __name__ == "__main__":
+    main()
