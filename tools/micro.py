@@ -64,6 +64,75 @@ def jumps(n):
     return a.assemble()
 
 
+def xc(ctl_fd, bss_fd, lookup=True, counter=True, loads=True, stores=True):
+    """xdp-counter (programs.xdp_counter) with parts left out."""
+    a = isa.Asm()
+    a.mov64(6, "r1")
+    if lookup:
+        a.mov64(1, 0)
+        a.stx(4, 10, -4, "r1")
+        a.mov64(2, "r10")
+        a.add64(2, -4)
+        a.ld_map_fd(1, ctl_fd)
+        a.call(1)
+        a.mov64(1, "r0")
+        a.mov64(0, isa.XDP_PASS)
+        a.jmp("jeq", 1, 0, "out")
+        a.ldx(4, 1, 1, 0)
+        a.jmp("jne", 1, 0, "out")
+    if counter:
+        a.ld_map_value(1, bss_fd, 0)
+        a.ldx(8, 2, 1, 0)
+        a.add64(2, 1)
+        a.stx(8, 1, 0, "r2")
+    a.ldx(8, 1, 6, 8)
+    a.ldx(8, 2, 6, 0)
+    a.mov64(3, "r2")
+    a.add64(3, 14)
+    a.mov64(0, isa.XDP_DROP)
+    a.jmp("jgt", 3, "r1", "out")
+    if loads:
+        a.ldx(2, 1, 2, 0)
+        a.ldx(2, 3, 2, 6)
+    if stores:
+        a.stx(2, 2, 0, "r3")
+    if loads:
+        a.ldx(2, 3, 2, 2)
+        a.ldx(2, 4, 2, 8)
+    if stores:
+        a.stx(2, 2, 2, "r4")
+    if loads:
+        a.ldx(2, 4, 2, 4)
+        a.ldx(2, 5, 2, 10)
+    if stores:
+        a.stx(2, 2, 4, "r5")
+        a.stx(2, 2, 6, "r1")
+        a.stx(2, 2, 8, "r3")
+        a.stx(2, 2, 10, "r4")
+    a.mov64(0, isa.XDP_TX)
+    a.label("out")
+    a.exit()
+    return a.assemble()
+
+
+def stores(load_at, store_ats):
+    """Staged window sized by a load at load_at; 2-byte stores at store_ats."""
+    a = isa.Asm()
+    a.ldx(8, 2, 1, 0)
+    a.ldx(8, 3, 1, 8)
+    a.mov64(4, "r2")
+    a.add64(4, 64)
+    a.mov64(0, isa.XDP_DROP)
+    a.jmp("jgt", 4, "r3", "out")
+    a.ldx(2, 5, 2, load_at)
+    for at in store_ats:
+        a.stx(2, 2, at, "r5")
+    a.mov64(0, isa.XDP_PASS)
+    a.label("out")
+    a.exit()
+    return a.assemble()
+
+
 def main():
     log2n = int(sys.argv[1]) if len(sys.argv) > 1 else 24
     n = 1 << log2n
@@ -79,7 +148,16 @@ def main():
     verd = dev.DeviceBuffer(4 * n)
     cases = [("ret", ret_only(), 2), ("alu8", alu(8), 10), ("alu32", alu(32), 34), ("alurr32", alu_rr(32), 35),
              ("ld8", staged_loads(8), 15), ("ld32", staged_loads(32), 39), ("jmp32", jumps(32), 34),
-             ("xdp-counter", programs.xdp_counter(ctl.fd, bss.fd), 37)]
+             ("xdp-counter", programs.xdp_counter(ctl.fd, bss.fd), 37),
+             ("xc-nolookup", xc(ctl.fd, bss.fd, lookup=False), 26),
+             ("xc-nocounter", xc(ctl.fd, bss.fd, counter=False), 33),
+             ("xc-nostores", xc(ctl.fd, bss.fd, stores=False), 31),
+             ("xc-noswap", xc(ctl.fd, bss.fd, loads=False, stores=False), 25),
+             ("xc-bare", xc(ctl.fd, bss.fd, lookup=False, counter=False, loads=False, stores=False), 8),
+             ("st-none16", stores(0, []), 9), ("st-none64", stores(60, []), 9),
+             ("st-1of16", stores(0, [0]), 10), ("st-1of64", stores(60, [0]), 10),
+             ("st-2of64", stores(60, [0, 16]), 11), ("st-4of64", stores(60, [0, 16, 32, 48]), 13),
+             ("st-6of16", stores(0, [0, 2, 4, 6, 8, 10]), 15)]
     for name, code, ninsn in cases:
         vm = dev.VM()
         vm.load(code)
