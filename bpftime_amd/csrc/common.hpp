@@ -235,12 +235,13 @@ struct KParams {
 constexpr uint32_t kWaveCacheEntries = (kBlock / 64) * 2;
 constexpr uint32_t kMergeGroup = 16;
 constexpr uint32_t kMergeEntries = 4096;  // merge table entries (64 KiB of LDS)
-inline uint32_t log_words_for(uint32_t comb_entries) { return 1 + 2 * (kWaveCacheEntries + comb_entries); }
+// (a combining-table entry flushes up to four counters: gen_fast.py comb_add)
+inline uint32_t log_words_for(uint32_t comb_entries) { return 1 + 2 * (kWaveCacheEntries + 4 * comb_entries); }
 
 // Dynamic LDS of an interpreter block: the lanes' XDP ctx (48 B each), their
 // stacks (LDS-stack programs), 32 B of tail-call launch constants (interp.hip
 // tenv; the asm finds them 32 B before the combining table), the combining
-// table (u32 tags + u64 deltas per entry).
+// table (a u32 tag + a 16-byte delta granule per entry).
 constexpr uint32_t kTenvBytes = 32;
 // Hash-lookup cache of a block (programs whose hash lookups the loader marks
 // FW_LCACHE: no deletions): kLcacheEntries {u32 tag, u32 (slot + 1) | fd << 22}
@@ -251,7 +252,7 @@ constexpr uint32_t kLcacheBytes = 8 * kLcacheEntries;
 inline size_t dyn_lds_for(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
                           bool lcache = false) {
   return (size_t)kBlock * ((kind == CTX_XDP ? 48 : 0) + (big_stack ? 0 : stack_size)) + (lcache ? kLcacheBytes : 0) +
-         kTenvBytes + 12 * (size_t)comb_entries;
+         kTenvBytes + 20 * (size_t)comb_entries;
 }
 
 // Error codes recorded per unit (err_count counts units with any error)

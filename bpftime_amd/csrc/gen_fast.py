@@ -110,6 +110,7 @@ INSN = 32      # FInsn bytes
 PIP = ["s86", "s87", "s93"]
 PM = ["s[88:89]", "s[90:91]", "s[94:95]"]
 KP = 3
+WAYS = 8  # combining-table associativity
 
 # staged (link-resolved) packet / slot accesses
 STAGED_LD = ["LDXS1", "LDXS2", "LDXS4", "LDXS2X", "LDXS4X", "LDXS8A", "LDXS8U"]
@@ -136,6 +137,7 @@ def handler_ids():
         for op in ("ADD", "OR", "AND", "XOR"):
             ids += [f"ATOM{sz}_{op}", f"ATOM{sz}_{op}_F"]
         ids += [f"ATOMMV{sz}_ADD"]
+    ids += ["ATOMMV8_ADD2"]
     ids += ["LDDW", "JA", "CALL_LOOKUP", "CALL_LOOKUP_STK", "CALL_LOOKUP_AK", "EXIT"]
     for sz in (4, 8):
         for k in ("R", "I"):
@@ -268,88 +270,121 @@ class Gen:
                "s_andn2_b64 s[54:55], exec, s[54:55]",
                f"s_cbranch_scc1 {L('slow')}")
 
-    def comb_add(self, sz, direct_only=False):
+    def comb_add(self, sz, direct_only=False, pair=False):
         """Per-lane add of Y (v46, v[46:47] for 8 B) at the global address Z
         through the workgroup's LDS combining table (interp.hip: %[combn] u32
-        tags, then %[combn] u64 deltas, flushed when the block ends): Zipf-hot
-        counters cost an LDS add instead of a same-address device atomic per
-        lane (those serialize at the memory side, ~12 ns each).  A tag is the
-        counter's offset in the map arena | 2 | (4-byte ? 1 : 0).  The table
-        is 8-way set associative: a lane reads the eight tags of its set (two
-        ds_read_b128, one wait), adds to the way holding its counter (a tag
-        never changes once set: no atomic claim), else claims an empty way
-        with a compare-and-swap (a lane that loses the race to another
-        counter re-reads its set once), else adds to memory directly; so do
-        misaligned lanes and counters outside the arena.  Lanes sharing a
-        counter are serialized by the LDS itself.  direct_only: every lane
-        adds to memory now (FW_NODEFER counters)."""
-        glob_add = ("global_atomic_add_x2 v[48:49], v[46:47], off" if sz == 8
-                    else "global_atomic_add v[48:49], v46, off")
+        tags, then %[combn] 16-byte delta granules, flushed when the block
+        ends): Zipf-hot counters cost an LDS add instead of a same-address
+        device atomic per lane (those serialize at the memory side, ~12 ns
+        each).  An entry stands for the 16-byte granule of the map arena
+        holding the counter (for fused pairs: the 16 bytes at the pair's
+        8-byte aligned address): tag = the granule's arena offset | 2 |
+        (4-byte ? 1 : 0); its deltas are two u64 (8-byte counters at +0 / +8)
+        or four u32 (4-byte counters), so the {packets, bytes} pair of a flow
+        value shares one entry.  (A counter may have deltas in two entries;
+        both reach it at the flush.)  The table is 4-way set associative: a lane reads
+        its set's four tags (one ds_read_b128), adds to the way holding its
+        granule (a tag never changes once set: no atomic claim), else claims
+        an empty way with a compare-and-swap (a lane that loses the race to
+        another granule re-reads its set once), else adds to memory directly;
+        so do misaligned lanes and counters outside the arena.  Lanes sharing
+        a counter are serialized by the LDS itself.  pair: also Y2 (v[44:45])
+        at Z + 8 (fused atomic pairs).  direct_only: every
+        lane adds to memory now (FW_NODEFER counters)."""
+        glob_add = ["global_atomic_add_x2 v[48:49], v[46:47], off" if sz == 8
+                    else "global_atomic_add v[48:49], v46, off"]
+        if pair:
+            glob_add.append("global_atomic_add_x2 v[48:49], v[44:45], off offset:8")
         if direct_only:
-            self.e(glob_add)
+            self.e(*glob_add)
             return
         done, direct, retry = self.label("cd"), self.label("cx"), self.label("cr")
-        nohit, noclaim = self.label("cnh"), self.label("cnc")
+        miss, lost, noclaim = self.label("cm"), self.label("cl"), self.label("cnc")
+
+        def add(va):
+            if sz == 8:
+                self.e(f"ds_add_u64 {va}, v[46:47]")
+                if pair:
+                    self.e(f"ds_add_u64 {va}, v[44:45] offset:8")
+            else:
+                self.e(f"ds_add_u32 {va}, v46")
         self.e("s_mov_b64 s[60:61], exec", "s_mov_b64 s[54:55], 0",
                "s_cmp_eq_u32 %[combn], 0", f"s_cbranch_scc1 {direct}",
-               f"v_and_b32 v41, {sz - 1}, v48", "v_cmp_eq_u32 vcc, 0, v41",            # aligned lanes
+               f"v_and_b32 v41, {sz - 1}, v48", "v_cmp_eq_u32 vcc, 0, v41",   # aligned lanes
                "s_and_b64 exec, exec, vcc", f"s_cbranch_execz {direct}",
                "s_mov_b64 s[72:73], %[alo]",
                "v_mov_b32 v55, s73",
                "v_subrev_co_u32 v54, vcc, s72, v48", "v_subb_co_u32 v55, vcc, v49, v55, vcc",
                "v_cmp_eq_u32 vcc, 0, v55",                                       # inside the arena's 4 GiB
                "s_and_b64 exec, exec, vcc", f"s_cbranch_execz {direct}",
-               f"v_or_b32 v54, {3 if sz == 4 else 2}, v54")
-        if sz == 4:
-            self.e("v_mov_b32 v47, 0")
-        self.e("v_lshrrev_b32 v41, 3, v48", "s_mov_b32 s69, 0x9e3779b1", "v_mul_lo_u32 v41, v41, s69",
+               # the granule: 16-byte aligned for single counters (byte offset
+               # v43), the pair's own 8-byte aligned address for pairs
+               "v_mov_b32 v43, 0" if pair else "v_and_b32 v43, 15, v54",
+               f"v_and_b32 v54, {-8 if pair else -16}, v54",
+               f"v_or_b32 v54, {3 if sz == 4 else 2}, v54",                      # tag
+               "v_lshrrev_b32 v41, 4, v54", "s_mov_b32 s69, 0x9e3779b1", "v_mul_lo_u32 v41, v41, s69",
                "s_ff1_i32_b32 s69, %[combn]", "s_sub_u32 s69, 32, s69",          # 32 - log2(entries)
-               "v_lshrrev_b32 v41, s69, v41", "v_and_b32 v41, -8, v41",          # first way of the set
-               "v_lshlrev_b32 v55, 3, v41", "v_lshlrev_b32 v41, 2, v41",
+               "v_lshrrev_b32 v41, s69, v41", f"v_and_b32 v41, -{WAYS}, v41",    # first way of the set
+               "v_lshlrev_b32 v55, 4, v41", "v_lshlrev_b32 v41, 2, v41",
                "v_add_u32 v41, %[comb], v41",                                   # the set's tags
                "s_lshl_b32 s70, %[combn], 2", "s_add_u32 s70, s70, %[comb]",
-               "v_add_u32 v55, s70, v55",                                       # ... and its deltas
+               "v_add3_u32 v55, s70, v55, v43",                                 # way 0's delta + byte
                "s_mov_b32 s85, 0",
                f"{retry}:",
                "s_mov_b64 s[62:63], exec",                                       # lanes of this pass
-               "ds_read_b128 v[56:59], v41", "ds_read_b128 v[42:45], v41 offset:16",
+               "ds_read_b128 v[56:59], v41",
+               "ds_read_b64 v[82:83], v41 offset:16",
+               "ds_read_b64 v[50:51], v41 offset:24",
                "s_waitcnt lgkmcnt(0)",
-               "v_mov_b32 v50, -1", "v_mov_b32 v51, 0")
-        tags = ["v56", "v57", "v58", "v59", "v42", "v43", "v44", "v45"]
-        for k in range(7, -1, -1):                                               # first empty way
-            self.e(f"v_cmp_eq_u32 vcc, 0, {tags[k]}", f"v_cndmask_b32_e64 v50, v50, {k}, vcc")
-        for k in range(7, -1, -1):                                               # the counter's way wins
-            self.e(f"v_cmp_eq_u32 vcc, v54, {tags[k]}", f"v_cndmask_b32_e64 v50, v50, {k}, vcc",
-                   "v_cndmask_b32_e64 v51, v51, 1, vcc")
-        self.e("v_lshlrev_b32 v56, 2, v50", "v_add_u32 v56, v41, v56",           # the way's tag
-               "v_lshlrev_b32 v57, 3, v50", "v_add_u32 v57, v55, v57",           # ... and its delta
-               "v_cmp_eq_u32 s[56:57], 1, v51", "s_and_b64 exec, s[62:63], s[56:57]",
-               f"s_cbranch_execz {nohit}",
-               "ds_add_u64 v57, v[46:47]",
-               f"{nohit}:",
-               "s_or_b64 s[54:55], s[54:55], exec",
-               "s_mov_b64 exec, s[62:63]",                                      # compares write only exec lanes
-               "v_cmp_ne_u32 s[56:57], -1, v50", "s_andn2_b64 s[56:57], s[56:57], s[54:55]",
-               "s_and_b64 exec, s[62:63], s[56:57]",                            # lanes claiming an empty way
-               f"s_cbranch_execz {noclaim}",
-               "v_mov_b32 v42, 0",
-               "ds_cmpst_rtn_b32 v50, v56, v42, v54",
+               "v_mov_b32 v42, -1")
+        tags = ["v56", "v57", "v58", "v59", "v82", "v83", "v50", "v51"]
+        for k in range(WAYS - 1, -1, -1):                                        # the granule's way
+            self.e(f"v_cmp_eq_u32 vcc, v54, {tags[k]}", f"v_cndmask_b32_e64 v42, v42, {k}, vcc")
+        self.e("v_cmp_ne_u32 s[56:57], -1, v42", "s_and_b64 exec, s[62:63], s[56:57]",
+               f"s_cbranch_execz {miss}",
+               "v_lshl_add_u32 v43, v42, 4, v55")
+        add("v43")
+        self.e("s_or_b64 s[54:55], s[54:55], exec",
+               f"{miss}:",
+               "s_andn2_b64 exec, s[62:63], s[54:55]", f"s_cbranch_execz {noclaim}",
+               "v_mov_b32 v42, -1")
+        for k in range(WAYS - 1, -1, -1):                                        # first empty way
+            self.e(f"v_cmp_eq_u32 vcc, 0, {tags[k]}", f"v_cndmask_b32_e64 v42, v42, {k}, vcc")
+        self.e("v_cmp_ne_u32 s[56:57], -1, v42", "s_and_b64 exec, exec, s[56:57]",
+               f"s_cbranch_execz {noclaim}",                                    # a full set: direct
+               "v_lshl_add_u32 v43, v42, 2, v41",
+               "v_mov_b32 v50, 0",
+               "ds_cmpst_rtn_b32 v51, v43, v50, v54",
                "s_waitcnt lgkmcnt(0)",
-               "v_cmp_eq_u32 s[56:57], 0, v50", "v_cmp_eq_u32 vcc, v54, v50",
+               "v_cmp_eq_u32 s[56:57], 0, v51", "v_cmp_eq_u32 vcc, v54, v51",
                "s_or_b64 s[56:57], s[56:57], vcc",                              # claimed (or claimed for us)
                "s_and_b64 s[64:65], exec, s[56:57]",
-               "s_andn2_b64 s[66:67], exec, s[56:57]",                           # lost to another counter
-               "s_mov_b64 exec, s[64:65]", f"s_cbranch_execz {noclaim}",
-               "ds_add_u64 v57, v[46:47]",
-               "s_or_b64 s[54:55], s[54:55], exec",
+               "s_andn2_b64 s[66:67], exec, s[56:57]",                           # lost to another granule
+               "s_mov_b64 exec, s[64:65]", f"s_cbranch_execz {lost}",
+               "v_lshl_add_u32 v43, v42, 4, v55")
+        add("v43")
+        self.e("s_or_b64 s[54:55], s[54:55], exec",
+               f"{lost}:",
                "s_cmp_eq_u64 s[66:67], 0", f"s_cbranch_scc1 {noclaim}",
                "s_add_u32 s85, s85, 1", "s_cmp_gt_u32 s85, 1", f"s_cbranch_scc1 {noclaim}",
                "s_mov_b64 exec, s[66:67]", f"s_branch {retry}",
                f"{noclaim}:")
         self.e(f"{direct}:",
                "s_andn2_b64 exec, s[60:61], s[54:55]", f"s_cbranch_execz {done}",
-               glob_add,
-               f"{done}:", "s_mov_b64 exec, s[60:61]")
+               *glob_add)
+        self.e(f"{done}:", "s_mov_b64 exec, s[60:61]")
+
+    def atomic_pair(self):
+        """Two fused BPF_ATOMIC adds without fetch (loader: same map-value
+        base, 8-byte counters at off and off + 8, the second FInsn skipped):
+        one combining-table probe for both (w5 / w7 = the two value
+        registers times two)."""
+        self.rd("s44", 48)
+        self.rd("s45", 46)
+        self.rd("s47", 44)
+        self.e("v_lshl_add_u64 v[48:49], v[48:49], 0, s[42:43]")
+        self.comb_add(8, pair=True)
+        self.next_seq(2)
 
     def comb_peel(self, sz, direct_only=False):
         """Per-lane adds of Y to addresses Z (exec = the adding lanes).  When
@@ -1664,6 +1699,8 @@ class Gen:
             e(f"{L('h_' + name)}:", "s_waitcnt lgkmcnt(0)")  # W of a fall-through fetch
             if name == "SLOW":
                 e(f"s_branch {L('slow')}")
+            elif name == "ATOMMV8_ADD2":
+                self.atomic_pair()
             elif name.startswith("ATOMD"):
                 self.atomd(int(name[5]))
             elif name.startswith("ATOMMV"):

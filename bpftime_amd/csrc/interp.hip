@@ -593,18 +593,34 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   uint8_t *my_ctx = dyn + tid * CTXB;
   uint8_t *my_stack = dyn + kBlock * CTXB + tid * p.stack_size;
   // combining table for per-lane counter adds (gen_fast.py comb_add), after
-  // the ctx and stack areas: comb_entries u32 tags {arena offset | 2 |
-  // (4-byte ? 1 : 0)} (8-way sets), then comb_entries u64 deltas, flushed
-  // when the block ends; sized 0 for programs that never need it
+  // the ctx and stack areas: comb_entries u32 tags {16-byte granule's arena
+  // offset (8-byte aligned for 8-byte counters) | 2 | (4-byte ? 1 : 0)}
+  // (4-way sets), then comb_entries 16-byte
+  // delta granules (2 x u64 or 4 x u32), flushed when the block ends; sized 0
+  // for programs that never need it
   uint32_t *lcache = (uint32_t *)(dyn + kBlock * (CTXB + (BIGSTACK ? 0 : p.stack_size)));
   uint64_t *tenv = (uint64_t *)((uint8_t *)lcache + (p.lcache ? kLcacheBytes : 0));
   uint32_t *comb = (uint32_t *)((uint8_t *)tenv + kTenvBytes);
   uint64_t *comb_d = (uint64_t *)(comb + p.comb_entries);
-  for (uint32_t i = tid; i < 3 * p.comb_entries; i += kBlock) comb[i] = 0;
+  for (uint32_t i = tid; i < 5 * p.comb_entries; i += kBlock) comb[i] = 0;
   if (p.lcache)
     for (uint32_t i = tid; i < 2 * kLcacheEntries; i += kBlock) lcache[i] = 0;
-  // a table tag as a flush tag {address | (4-byte ? 1 : 0)}
-  auto comb_tag = [&](uint32_t t) -> uint64_t { return t ? (p.arena_lo + (t & ~3u)) | (t & 1u) : 0; };
+  // counter v of the table (entry v / 4, counter v % 4 of its granule) as a
+  // flush tag {address | (4-byte ? 1 : 0)} and delta
+  auto comb_counter = [&](uint32_t v, uint64_t &tag, uint64_t &delta) {
+    const uint32_t e = v >> 2, j = v & 3, t = comb[e];
+    tag = delta = 0;
+    if (!t) return;
+    // 4-byte granules are 16-byte aligned; 8-byte ones 8-byte aligned (pairs)
+    const uint64_t g = p.arena_lo + (t & ((t & 1) ? ~15u : ~7u));
+    if (t & 1) {
+      delta = ((const uint32_t *)comb_d)[4 * e + j];
+      tag = (g + 4 * j) | 1;
+    } else if (j < 2) {
+      delta = comb_d[2 * e + j];
+      tag = g + 8 * j;
+    }
+  };
   // tail-call launch constants for the asm tier (XDP images: the frames'
   // ctx copy is the lane's LDS ctx): frames (0: tail calls in C++), entry
   // table, word stride | depth stride << 32, stack / ctx save masks
@@ -1027,7 +1043,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   }
   if (!p.flush_log) {
     if (!(p.dbg & 1))
-      for (uint32_t i = tid; i < p.comb_entries; i += kBlock) flush_delta_tag(comb_tag(comb[i]), comb_d[i]);
+      for (uint32_t i = tid; i < 4 * p.comb_entries; i += kBlock) {
+        uint64_t tag, delta;
+        comb_counter(i, tag, delta);
+        flush_delta_tag(tag, delta);
+      }
     return;
   }
   // append the nonzero deltas (wave caches, then the table) to this block's
@@ -1036,15 +1056,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   // so its atomics do not queue on a few words, and merging would not fold them
   __syncthreads();
   uint64_t *reg = p.flush_log + (uint64_t)blockIdx.x * p.log_words;
-  const uint32_t total = NE + p.comb_entries;
+  const uint32_t total = NE + 4 * p.comb_entries;
   auto entry = [&](uint32_t i, uint64_t &tag, uint64_t &delta) {
     tag = delta = 0;
     if (i < NE) {
       tag = e[2 * i];
       delta = e[2 * i + 1];
     } else if (i < total) {
-      tag = comb_tag(comb[i - NE]);
-      delta = comb_d[i - NE];
+      comb_counter(i - NE, tag, delta);
     }
   };
   for (uint32_t r0 = 0; r0 < total; r0 += kBlock) {

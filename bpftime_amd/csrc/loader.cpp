@@ -1356,6 +1356,24 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
       }
     }
   }
+  // adjacent 8-byte atomic adds through one map-value base at off / off + 8
+  // (the {packets, bytes} idiom) share one combining-table probe
+  // (gen_fast.py atomic_pair); the second must not be a jump target or entry
+  {
+    std::vector<uint8_t> target(prog.size() + 1, 0);
+    for (const DInsn &d : prog)
+      if ((d.op == X_JA || is_cond_jump(d.op)) && d.tgt >= 0 && (size_t)d.tgt < prog.size()) target[d.tgt] = 1;
+    for (uint32_t e : lo.entries)
+      if (e < prog.size()) target[e] = 1;
+    for (size_t i = 0; i + 1 < prog.size() && !getenv("BPFTIME_AMD_NO_PAIR"); i++) {
+      const DInsn &a = prog[i], &b = prog[i + 1];
+      if (out.fast[i].hoff != 4 + 4 * F_ATOMMV8_ADD || out.fast[i + 1].hoff != 4 + 4 * F_ATOMMV8_ADD) continue;
+      if (target[i + 1] || a.dst != b.dst || b.off != a.off + 8 || !(in[i][a.dst] == in[i + 1][b.dst])) continue;
+      out.fast[i].hoff = 4 + 4 * F_ATOMMV8_ADD2;
+      out.fast[i].aux = (int32_t)b.src * 2;
+      i++;
+    }
+  }
   out.specialized = nspec;
   out.needs_ctx = xdp && ctx_escapes;
 }
@@ -1379,7 +1397,7 @@ uint32_t stage_need(const FastForm &f, uint32_t head) {
 // past the end
 static void link_next(const std::vector<DInsn> &prog, std::vector<FInsn> &out) {
   for (size_t i = 0; i < out.size(); i++) {
-    const size_t nx = i + (i < prog.size() && prog[i].op == X_LDDW ? 2 : 1);
+    const size_t nx = i + ((i < prog.size() && prog[i].op == X_LDDW) || out[i].hoff == 4 + 4 * F_ATOMMV8_ADD2 ? 2 : 1);
     const uint32_t h = nx < out.size() ? out[nx].hoff : 4 + 4 * F_SLOW;
     out[i].w1 = (out[i].w1 & 0xffu) | (h << 8);
   }

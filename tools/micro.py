@@ -133,6 +133,105 @@ def stores(load_at, store_ats):
     return a.assemble()
 
 
+def flow(flows_fd, lookup=True, adds=True, split=True):
+    """programs.flow_hash with parts left out (split=False: no TCP/UDP
+    divergence)."""
+    from bpftime_amd.isa import BPF_NOEXIST
+    a = isa.Asm()
+    a.ldx(8, 2, 1, 0)
+    a.ldx(8, 3, 1, 8)
+    a.mov64(6, "r3")
+    a.alu64("sub", 6, "r2")
+    a.mov64(4, "r2")
+    a.add64(4, 14)
+    a.mov64(0, isa.XDP_DROP)
+    a.jmp("jgt", 4, "r3", "out")
+    a.ldx(2, 4, 2, 12)
+    a.mov64(0, isa.XDP_PASS)
+    a.jmp("jne", 4, 0x0008, "out")
+    a.mov64(4, "r2")
+    a.add64(4, 34)
+    a.mov64(0, isa.XDP_DROP)
+    a.jmp("jgt", 4, "r3", "out")
+    a.ldx(1, 4, 2, 14)
+    a.mov64(0, isa.XDP_PASS)
+    a.jmp("jne", 4, 0x45, "out")
+    a.ldx(1, 7, 2, 23)
+    if split:
+        a.jmp("jeq", 7, 6, "l4")
+        a.jmp("jne", 7, 17, "out")
+    a.label("l4")
+    a.mov64(4, "r2")
+    a.add64(4, 38)
+    a.mov64(0, isa.XDP_DROP)
+    a.jmp("jgt", 4, "r3", "out")
+    a.ldx(4, 4, 2, 26)
+    a.stx(4, 10, -16, "r4")
+    a.ldx(4, 4, 2, 30)
+    a.stx(4, 10, -12, "r4")
+    a.ldx(4, 4, 2, 34)
+    a.stx(4, 10, -8, "r4")
+    a.stx(4, 10, -4, "r7")
+    a.st(8, 10, -32, 0)
+    a.st(8, 10, -24, 0)
+    if lookup:
+        a.ld_map_fd(1, flows_fd)
+        a.mov64(2, "r10")
+        a.add64(2, -16)
+        a.call(1)
+        a.jmp("jne", 0, 0, "have")
+        a.ld_map_fd(1, flows_fd)
+        a.mov64(2, "r10")
+        a.add64(2, -16)
+        a.mov64(3, "r10")
+        a.add64(3, -32)
+        a.mov64(4, BPF_NOEXIST)
+        a.call(2)
+        a.ld_map_fd(1, flows_fd)
+        a.mov64(2, "r10")
+        a.add64(2, -16)
+        a.call(1)
+        a.mov64(1, "r0")
+        a.mov64(0, isa.XDP_ABORTED)
+        a.jmp("jeq", 1, 0, "out")
+        a.mov64(0, "r1")
+        a.label("have")
+        if adds:
+            a.mov64(1, 1)
+            a.atomic(8, isa.ATOMIC_ADD, 0, 0, "r1")
+            a.atomic(8, isa.ATOMIC_ADD, 0, 8, "r6")
+    a.mov64(0, isa.XDP_TX)
+    if split:
+        a.jmp("jeq", 7, 6, "out")
+        a.mov64(0, isa.XDP_PASS)
+    a.label("out")
+    a.exit()
+    return a.assemble()
+
+
+def flow_cases(n, zipf_s=1.1, only=None):
+    """flow-hash variants over the bench's frames (2048-B slots)."""
+    nflows, stride = 65536, 2048
+    cdf = dev.DeviceBuffer.from_array(gen.zipf_cdf(nflows, zipf_s))
+    pk = dev.DeviceBuffer(n * stride)
+    dl = dev.DeviceBuffer(4 * n)
+    if dev.lib().bpftime_amd_gen_flow(pk.ptr, dl.ptr, n, stride, gen.SEED_CFG3, 0, cdf.ptr, nflows, None):
+        raise SystemExit("flow generator failed")
+    dv = dev.DeviceBuffer(4 * n)
+    for name, kw in [("flow", {}), ("flow-noadds", {"adds": False}), ("flow-nolookup", {"lookup": False}),
+                     ("flow-nosplit", {"split": False}), ("flow-nosplit-nolk", {"split": False, "lookup": False})]:
+        if only and name not in only:
+            continue
+        flows = dev.Map(isa.BPF_MAP_TYPE_HASH, 16, 16, nflows, name="flows")
+        vm = dev.VM()
+        vm.load(flow(flows.fd, **kw))
+
+        def step():
+            vm.exec_batch(dev.CTX_XDP, pk, n, stride, lens=dl, verdicts=dv, flags=0)
+        _, k = bw._timed(dev, step, 10, 3)
+        print("%-18s kernel %.4f ms  %.2f ps/pkt" % (name, k * 1e3, k / n * 1e12), flush=True)
+
+
 def main():
     log2n = int(sys.argv[1]) if len(sys.argv) > 1 else 24
     n = 1 << log2n
@@ -158,6 +257,11 @@ def main():
              ("st-1of16", stores(0, [0]), 10), ("st-1of64", stores(60, [0]), 10),
              ("st-2of64", stores(60, [0, 16]), 11), ("st-4of64", stores(60, [0, 16, 32, 48]), 13),
              ("st-6of16", stores(0, [0, 2, 4, 6, 8, 10]), 15)]
+    if os.environ.get("MICRO_FLOW"):
+        del pkts
+        s = float(os.environ.get("MICRO_ZIPF", "1.1"))
+        flow_cases(n, s, os.environ.get("MICRO_ONLY", "").split(",") if os.environ.get("MICRO_ONLY") else None)
+        return
     for name, code, ninsn in cases:
         vm = dev.VM()
         vm.load(code)
