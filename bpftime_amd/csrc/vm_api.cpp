@@ -449,11 +449,12 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   // ORDERED: every counter add goes straight to memory (link_fast), no table
   p.comb_entries = (b->flags & EBPF_BATCH_ORDERED) ? 0 : prog.comb_entries;
   if (p.comb_entries) {
-    // the largest combining table (256 .. kCombMax entries) that keeps two
-    // blocks (8 waves) resident per CU: a counter that finds no entry is a
-    // device atomic, serialized with every other add to its address, so
-    // table reach beats occupancy (r01c sweep: flow-hash 256 -> 2048
-    // entries 2.1 -> 0.6 ms per 2^22 packets)
+    // the largest combining table (256 .. kCombMax entries) that keeps the
+    // residency the smallest table allows: a counter that finds no entry is a
+    // device atomic (memory-side, ~10 G/s chip-wide for scattered 8-byte
+    // adds), so table reach matters, but a block fewer per CU costs more
+    // (flow-hash 1024 entries at 2 blocks / CU 1.61 ms, 2048 at 1 2.04;
+    // syscall-agg 512 at 3 blocks 0.73 ms, 1024 at 2 0.94)
     static std::map<uint64_t, uint32_t> best;  // (kind, big stack, stack bytes) -> entries
     const bool xdp_form = b->ctx_kind == CTX_XDP;
     const uint32_t hint_key = (xdp_form ? im.fx : im.fr).comb_hint;
@@ -462,7 +463,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     auto it = best.find(key);
     if (it == best.end()) {
       auto dyn = [&](uint32_t e) { return dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, e, p.lcache); };
-      const int base = std::min(2, bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn(kComb)));
+      const int base = bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn(kComb));
       // ... but no larger than twice the counter addresses a block can reach
       // (per-CPU counters: a few; flow keys: the table's whole reach), since
       // LDS it does not need is occupancy lost (tail-call 2.68 -> 2.07 ms)
