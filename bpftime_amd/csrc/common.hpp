@@ -223,6 +223,7 @@ struct KParams {
   uint32_t tail_ctx_mask;    // XDP images: ctx words / stack words a frame keeps (loader.cpp tail_save_masks)
   uint32_t tail_stack_mask;
   uint32_t lcache;           // 1 = the block's hash-lookup cache exists (common.hpp kLcacheEntries)
+  uint64_t *gregs;           // r0..r10 copies for the C++ tier: [grid][11][kBlock] u64 (k_interp G), or nullptr (LDS)
 };
 
 // Block-end counter deltas.  Every block holds its counter deltas (the wave
@@ -239,10 +240,10 @@ constexpr uint32_t kMergeEntries = 4096;  // merge table entries (64 KiB of LDS)
 inline uint32_t log_words_for(uint32_t comb_entries) { return 1 + 2 * (kWaveCacheEntries + 4 * comb_entries); }
 
 // Dynamic LDS of an interpreter block: the lanes' XDP ctx (48 B each), their
-// stacks (LDS-stack programs), 32 B of tail-call launch constants (interp.hip
-// tenv; the asm finds them 32 B before the combining table), the combining
+// stacks (LDS-stack programs), 48 B of launch constants (interp.hip
+// tenv; the asm finds them 48 B before the combining table), the combining
 // table (a u32 tag + a 16-byte delta granule per entry).
-constexpr uint32_t kTenvBytes = 32;
+constexpr uint32_t kTenvBytes = 48;  // gen_fast.py TENV: tail-call constants, the register copy base
 // Hash-lookup cache of a block (programs whose hash lookups the loader marks
 // FW_LCACHE: no deletions): kLcacheEntries {u32 tag, u32 (slot + 1) | fd << 22}
 // entries, 2-way sets, right below the tail-call constants.  A slot found for

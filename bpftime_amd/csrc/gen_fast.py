@@ -111,6 +111,7 @@ PIP = ["s86", "s87", "s93"]
 PM = ["s[88:89]", "s[90:91]", "s[94:95]"]
 KP = 3
 WAYS = 8  # combining-table associativity
+TENV = 48  # launch constants below the combining table (common.hpp kTenvBytes)
 
 # staged (link-resolved) packet / slot accesses
 STAGED_LD = ["LDXS1", "LDXS2", "LDXS4", "LDXS2X", "LDXS4X", "LDXS8A", "LDXS8U"]
@@ -156,9 +157,14 @@ def L(name):
 
 
 class Gen:
-    def __init__(self):
+    def __init__(self, greg=False):
+        """greg: r0..r10's spill copy lives in global memory (%[rgb] + v40 +
+        r * 2048, interp.hip k_interp<.., G = true>) and the lane's LDS column
+        holds only its dummy and tail-call depth slots."""
         self.out = []
         self.uid = 0
+        self.greg = greg
+        self.depth_off = 2048 if greg else 12 * 2048  # the lane's tail-call depth slot
 
     def e(self, *lines):
         self.out.extend(lines)
@@ -928,7 +934,7 @@ class Gen:
 
     # ---- the block's hash-lookup cache (common.hpp kLcacheEntries) ----
     # 512 two-way sets of {u32 tag, u32 (slot + 1) | fd << 22} right below
-    # the tail-call constants (%[comb] - 32 - kLcacheBytes).  The tag is the
+    # the launch constants (%[comb] - TENV - kLcacheBytes).  The tag is the
     # key itself for 4-byte keys (a hit needs no memory access) and the low
     # word of the h*31 hash otherwise (a hit re-reads the slot's key once,
     # instead of the index entry and then the slot).  Only hash lookups the
@@ -947,7 +953,7 @@ class Gen:
                "s_mul_i32 s69, s49, 0x9e3779b1", "v_xor_b32 v41, s69, v41",
                "s_mov_b32 s69, 0x85ebca6b", "v_mul_lo_u32 v41, v41, s69",
                "v_lshrrev_b32 v41, 23, v41", "v_lshlrev_b32 v41, 4, v41",          # set * 16 (512 sets)
-               f"s_sub_u32 s69, %[comb], {32 + 8 * 1024}", "v_add_u32 v82, s69, v41",
+               f"s_sub_u32 s69, %[comb], {TENV + 8 * 1024}", "v_add_u32 v82, s69, v41",
                f"v_mov_b32 v83, v{44 if kd == 1 else 48}",
                "ds_read_b128 v[54:57], v82", "s_waitcnt lgkmcnt(0)",
                "s_lshl_b32 s69, s49, 22")
@@ -1324,7 +1330,7 @@ class Gen:
           # images: the lane's tail-call depth back to 0 (R slot 12, lo word)
           "s_bitcmp1_b32 %[entry], 7", f"s_cbranch_scc0 {nod}",
           "v_mov_b32 v56, 0",
-          f"ds_write_b32 v40, v56 offset:{12 * 2048}",
+          f"ds_write_b32 v40, v56 offset:{self.depth_off}",
           f"{nod}:",
           "s_mov_b32 %[steps], 0",
           "s_mov_b32 s48, 0",
@@ -1342,10 +1348,20 @@ class Gen:
     # (common.hpp dyn_lds_for; frames 0: tail calls in C++): frames
     # base, entry table, word stride, depth stride, stack words; a lane's depth
     # and grid lane index in its R[12] slot (v40 + 12 * 2048).
+    def rgb(self):
+        """s[52:53] = the launch constant tenv[4] (greg: the block's global
+        r0 column minus the LDS address of the lane columns, so that v40 +
+        r * 2048 addresses r's copy).  With no lane in exec nothing is
+        stored or loaded through it.  (A VALU write of an SGPR that a VMEM
+        instruction reads as its address needs 5 wait states: s_nop 4.)"""
+        self.e(f"s_sub_u32 s52, %[comb], {TENV - 32}", "v_mov_b32 v41, s52",
+               "ds_read_b64 v[42:43], v41", "s_waitcnt lgkmcnt(0)",
+               "v_readfirstlane_b32 s52, v42", "v_readfirstlane_b32 s53, v43", "s_nop 4")
+
     def tail_env(self):
-        self.e(f"s_sub_u32 s69, %[comb], {32}", "v_mov_b32 v41, s69",
+        self.e(f"s_sub_u32 s69, %[comb], {TENV}", "v_mov_b32 v41, s69",
                "ds_read_b128 v[42:45], v41", "ds_read_b128 v[46:49], v41 offset:16",
-               "ds_read_b64 v[54:55], v40 offset:24576",                      # depth, grid lane
+               f"ds_read_b64 v[54:55], v40 offset:{self.depth_off}",          # depth, grid lane
                "s_waitcnt lgkmcnt(0)",
                "v_readfirstlane_b32 s72, v42", "v_readfirstlane_b32 s73, v43",  # frames
                "v_readfirstlane_b32 s74, v44", "v_readfirstlane_b32 s75, v45",  # entry table
@@ -1478,7 +1494,7 @@ class Gen:
             self.word_addr(12 + k)
             self.e("global_store_dwordx2 v[58:59], v[42:43], off", f"{skip}:")
         self.stack_words(store=True)
-        self.e("v_add_u32 v54, 1, v54", "ds_write_b32 v40, v54 offset:24576",
+        self.e("v_add_u32 v54, 1, v54", f"ds_write_b32 v40, v54 offset:{self.depth_off}",
                f"v_mov_b32 v{R0}, 0", f"v_mov_b32 v{R0 + 1}, 0",
                f"v_mov_b32 v{R0 + 4}, 64", f"v_mov_b32 v{R0 + 5}, 0",
                f"v_mov_b32 v{R0 + 20}, %[r10lo]", f"v_mov_b32 v{R0 + 21}, %[r10hi]")
@@ -1509,7 +1525,7 @@ class Gen:
                "s_waitcnt vmcnt(0)",
                "v_and_b32 v41, 0x100, v47", "v_cmp_ne_u32 vcc, 0, v41",
                "s_andn2_b64 s[54:55], exec, vcc", f"s_cbranch_scc1 {L('slow')}",
-               "ds_write_b32 v40, v54 offset:24576",
+               f"ds_write_b32 v40, v54 offset:{self.depth_off}",
                "v_lshlrev_b32 v50, 5, v46",                                  # return IP
                "s_mov_b64 s[60:61], exec")
         for r in range(1, 10):
@@ -1657,9 +1673,15 @@ class Gen:
           "v_mov_b32 v52, %[slotlo]", "v_mov_b32 v53, %[slothi]",
           "s_bitcmp1_b32 %[entry], 0", f"s_cbranch_scc1 {fresh}")
         # re-entry: registers from the C++ side's LDS copy, no staging
+        if self.greg:
+            self.rgb()
         for r in range(NREG):
-            e(f"ds_read_b64 v[{R0 + 2 * r}:{R0 + 2 * r + 1}], v40 offset:{r * 2048}")
-        e("s_waitcnt lgkmcnt(0)", f"s_branch {loaded}")
+            if self.greg:
+                e(f"v_add_u32 v41, {r * 2048}, v40",
+                  f"global_load_dwordx2 v[{R0 + 2 * r}:{R0 + 2 * r + 1}], v41, s[52:53]")
+            else:
+                e(f"ds_read_b64 v[{R0 + 2 * r}:{R0 + 2 * r + 1}], v40 offset:{r * 2048}")
+        e("s_waitcnt vmcnt(0) lgkmcnt(0)", f"s_branch {loaded}")
         # fresh unit: r1, r2, r10 from operands, the rest zero; stage the slot
         e(f"{fresh}:")
         for r in range(NREG):
@@ -1784,8 +1806,14 @@ class Gen:
         self.materialize(extra=False)
         e(f"{L('spill')}:")
         self.flush()
+        if self.greg:
+            self.rgb()
         for r in range(NREG):
-            e(f"ds_write_b64 v40, v[{R0 + 2 * r}:{R0 + 2 * r + 1}] offset:{r * 2048}")
+            if self.greg:
+                e(f"v_add_u32 v41, {r * 2048}, v40",
+                  f"global_store_dwordx2 v41, v[{R0 + 2 * r}:{R0 + 2 * r + 1}], s[52:53]")
+            else:
+                e(f"ds_write_b64 v40, v[{R0 + 2 * r}:{R0 + 2 * r + 1}] offset:{r * 2048}")
         e(f"{L('done')}:",
           "s_waitcnt vmcnt(0) lgkmcnt(0)",
           "s_mov_b64 %[aliveout], exec",
@@ -1810,18 +1838,20 @@ def relocate(line):
 
 
 def main():
-    g = Gen()
-    ids = g.build()
-    g.out = [relocate(x) for x in g.out]
     # v126/v127 (v100/v101 before relocation) are read, never written, by
     # staged loads near the window end
     clob = [f"s{i}" for i in range(40, 96)] + [f"v{vmap(i)}" for i in range(40, 102)]
     with open(os.path.join(HERE, "fast_asm.inc"), "w") as f:
         f.write("// Generated by gen_fast.py; do not edit.\n")
-        f.write("#define BPFTIME_AMD_FAST_ASM \\\n")
-        for line in g.out:
-            f.write('  "%s\\n" \\\n' % line)
-        f.write('  ""\n')
+        # register spill copy in LDS, and (_G) in global memory
+        for suffix, greg in (("", False), ("_G", True)):
+            g = Gen(greg)
+            ids = g.build()
+            g.out = [relocate(x) for x in g.out]
+            f.write("#define BPFTIME_AMD_FAST_ASM%s \\\n" % suffix)
+            for line in g.out:
+                f.write('  "%s\\n" \\\n' % line)
+            f.write('  ""\n')
         f.write("#define BPFTIME_AMD_FAST_CLOBBERS %s\n" %
                 ", ".join('"%s"' % c for c in clob + ["vcc", "scc", "m0", "memory"]))
     with open(os.path.join(HERE, "fast_ops.hpp"), "w") as f:

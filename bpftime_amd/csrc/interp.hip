@@ -472,7 +472,7 @@ struct FastEnv {
   uint32_t head;    // batch head: ctx->data = slot + head
   uint32_t comb;    // LDS address of the block's combining table
   uint32_t combn;   // its entries (0: add straight to memory)
-  uint32_t rb;      // LDS byte address of this lane's R[0]
+  uint32_t rb;      // LDS byte address of this lane's R[0] (G: of its dummy slot)
   uint32_t stage;   // staged bytes per unit (0: no staging)
   uint32_t ncpu;    // virtual CPUs (per-CPU maps)
   uint32_t sstep;   // chained units: slot bytes from one unit of a lane to its next
@@ -498,6 +498,7 @@ struct FastUnit {
 
 // adv: units the asm tier finished and moved past (chained); the lanes are
 // then in the wave's unit `adv` iterations further on, at c.pc
+template <bool G>
 __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const FastUnit &u, uint32_t chain_in,
                                              uint32_t &adv) {
   // every "s" operand must be provably uniform: readfirstlane what the
@@ -521,21 +522,25 @@ __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const Fas
   uint32_t vcpu = __ballot(c.alive && u.vm != vm0) == 0 && f.ncpu <= 0xffff ? vm0 | (f.ncpu << 16) : ~0u;
   uint64_t vaddr = u.vaddr, raddr = u.raddr, laddr = u.laddr;
   uint32_t ulen = u.len, chain = __builtin_amdgcn_readfirstlane(chain_in);
-  asm volatile(BPFTIME_AMD_FAST_ASM
-               : [pc] "+s"(pc), [steps] "+s"(steps), [why] "=s"(why), [aliveout] "=s"(alive_out),
-                 [lpc] "=v"(lpc), [c0a] "+s"(c0a), [c1a] "+s"(c1a),
-                 [c0dl] "+s"(c0dl), [c0dh] "+s"(c0dh), [c1dl] "+s"(c1dl), [c1dh] "+s"(c1dh), [c0s] "+s"(c0s),
-                 [c1s] "+s"(c1s), [vaddr] "+v"(vaddr), [raddr] "+v"(raddr), [laddr] "+v"(laddr), [ulen] "+v"(ulen),
-                 [chain] "+s"(chain), [vcpu] "+s"(vcpu)
-               : [prog] "s"(f.fast), [maps] "s"(f.maps), [dlo] "s"(f.dlo), [dhi] "s"(f.dhi), [alo] "s"(f.alo),
-                 [ahi] "s"(f.ahi), [shi] "s"(f.shi), [phi] "s"(f.phi), [limit] "s"(limit), [rb] "v"(f.rb),
-                 [alive] "s"(alive), [oflags] "s"(f.oflags),
-                 [entry] "s"(entry), [r1lo] "v"((uint32_t)u.r1), [r1hi] "v"((uint32_t)(u.r1 >> 32)),
-                 [r2lo] "v"(u.r2), [r10lo] "v"((uint32_t)u.r10), [r10hi] "v"((uint32_t)(u.r10 >> 32)),
-                 [slotlo] "v"((uint32_t)u.slot), [slothi] "v"((uint32_t)(u.slot >> 32)),
-                 [head] "s"(f.head), [stklo] "v"((uint32_t)u.r10), [comb] "s"(f.comb), [combn] "s"(f.combn),
-                 [stage] "s"(f.stage), [sstep] "s"(f.sstep), [ustep] "s"(f.ustep)
-               : BPFTIME_AMD_FAST_CLOBBERS);
+#define FAST_OUTS                                                                                             \
+  [pc] "+s"(pc), [steps] "+s"(steps), [why] "=s"(why), [aliveout] "=s"(alive_out), [lpc] "=v"(lpc),            \
+      [c0a] "+s"(c0a), [c1a] "+s"(c1a), [c0dl] "+s"(c0dl), [c0dh] "+s"(c0dh), [c1dl] "+s"(c1dl),                \
+      [c1dh] "+s"(c1dh), [c0s] "+s"(c0s), [c1s] "+s"(c1s), [vaddr] "+v"(vaddr), [raddr] "+v"(raddr),            \
+      [laddr] "+v"(laddr), [ulen] "+v"(ulen), [chain] "+s"(chain), [vcpu] "+s"(vcpu)
+#define FAST_INS                                                                                              \
+  [prog] "s"(f.fast), [maps] "s"(f.maps), [dlo] "s"(f.dlo), [dhi] "s"(f.dhi), [alo] "s"(f.alo),               \
+      [ahi] "s"(f.ahi), [shi] "s"(f.shi), [phi] "s"(f.phi), [limit] "s"(limit), [rb] "v"(f.rb),               \
+      [alive] "s"(alive), [oflags] "s"(f.oflags), [entry] "s"(entry), [r1lo] "v"((uint32_t)u.r1),               \
+      [r1hi] "v"((uint32_t)(u.r1 >> 32)), [r2lo] "v"(u.r2), [r10lo] "v"((uint32_t)u.r10),                       \
+      [r10hi] "v"((uint32_t)(u.r10 >> 32)), [slotlo] "v"((uint32_t)u.slot),                                    \
+      [slothi] "v"((uint32_t)(u.slot >> 32)), [head] "s"(f.head), [stklo] "v"((uint32_t)u.r10),                 \
+      [comb] "s"(f.comb), [combn] "s"(f.combn), [stage] "s"(f.stage), [sstep] "s"(f.sstep), [ustep] "s"(f.ustep)
+  if constexpr (G)
+    asm volatile(BPFTIME_AMD_FAST_ASM_G : FAST_OUTS : FAST_INS : BPFTIME_AMD_FAST_CLOBBERS);
+  else
+    asm volatile(BPFTIME_AMD_FAST_ASM : FAST_OUTS : FAST_INS : BPFTIME_AMD_FAST_CLOBBERS);
+#undef FAST_OUTS
+#undef FAST_INS
   adv = __builtin_amdgcn_readfirstlane(chain_in) - chain;
   c.pc = pc;
   c.steps = steps;
@@ -566,7 +571,11 @@ __device__ __forceinline__ void write_xdp_ctx(XdpCtx *x, uint64_t slot, uint32_t
 }
 
 // IMAGE: a linked tail-call image (lane groups scheduled through the asm tier)
-template <uint32_t KIND, bool BIGSTACK, bool IMAGE>
+// G: r0..r10's copy for the C++ tier lives in global memory (p.gregs, the
+// block's [register][lane] columns) instead of LDS: 22 KiB of LDS per block
+// go to residency (launches with a combining table or lookup cache, whose
+// units stay in the asm tier)
+template <uint32_t KIND, bool BIGSTACK, bool IMAGE, bool G>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_interp(KParams pin) {
   // Copy every kernel argument through an SGPR barrier: without it the
   // compiler keeps the argument block as one 16-dword tuple that it spills
@@ -579,14 +588,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
   SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(flush_log); SRV(log_words); SRP(lane_scratch);
-  SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask); SRV(lcache);
+  SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask); SRV(lcache); SRP(gregs);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
 #undef SRP
 #undef SRV
   // r0..r10, a dummy slot, and (images) the lane's tail-call depth | its
   // grid lane index << 32 (gen_fast.py tail_env).  (2 KiB of LDS decide
   // between 3 and 4 resident blocks of the headline program: images only.)
-  __shared__ uint64_t Rf[(IMAGE ? 13 : 12) * kBlock];
+  // (G: the dummy and depth slots only)
+  constexpr uint32_t kDummy = G ? 0 : 11, kDepth = G ? 1 : 12;
+  __shared__ uint64_t Rf[(IMAGE ? kDepth + 1 : kDummy + 1) * kBlock];
+  uint64_t *const Rg = G ? p.gregs + (uint64_t)blockIdx.x * 11 * kBlock : Rf;  // r0..r10 columns
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
   constexpr uint32_t CTXB = KIND == CTX_XDP ? 48 : 0;
   const uint32_t tid = threadIdx.x;
@@ -634,6 +646,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const uint32_t smask = p.tail_stack_mask & (sw >= 16 ? 0xffffu : (1u << sw) - 1);
     tenv[3] = (uint64_t)smask | ((uint64_t)p.stack_size << 16) | ((uint64_t)(p.tail_ctx_mask & 0x3f) << 32) |
               ((p.dbg & 16) ? 1ull << 63 : 0);  // dbg 16: frames popped in C++
+    // G: the block's global r0 column minus the LDS address of the lane
+    // columns (gen_fast.py rgb: v40 + r * 2048 + this addresses r's copy)
+    tenv[4] = G ? (uint64_t)(uintptr_t)Rg - (uint32_t)(uintptr_t)&Rf[0] : 0;
   }
   __syncthreads();
   uint64_t big_stack[BIGSTACK ? kStackSize / 8 : 1];
@@ -641,7 +656,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                                       : (uint64_t)(uintptr_t)(my_stack + p.stack_size);
 
   Ctx c;
-  c.R = &Rf[tid];
+  c.R = &Rg[tid];
   c.prog = (prog_ptr)p.prog;
   c.fast = p.fast;
   {
@@ -649,7 +664,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     c.win = Win{p.data_lo, p.data_hi, p.arena_lo, p.arena_hi, sl, sl ? sl + 8ull * gridDim.x * kBlock : 0,
                 p.checked != 0};
   }
-  c.dummy = (uint64_t)(uintptr_t)&Rf[11 * kBlock + tid];
+  c.dummy = (uint64_t)(uintptr_t)&Rf[kDummy * kBlock + tid];
   c.verdicts = p.verdicts;
   c.rets = p.rets;
   c.step_limit = p.step_limit > 0xffffffffull ? 0xffffffffu : (uint32_t)p.step_limit;
@@ -673,6 +688,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                           (uint32_t)((uint64_t)(uintptr_t)&big_stack[0] >> 32)))
                     : fe.shi;
   fe.rb = (uint32_t)(uintptr_t)&Rf[tid];
+
   // the host sized the staged window (gen_fast.py, unit staging) from the
   // program's static packet / slot accesses, 16-B aligned slots only
   fe.stage = p.stage;
@@ -755,8 +771,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     // tail-call frames this lane has pushed (images: in LDS, the asm tier
     // pushes too)
     uint32_t tdepth_reg = 0;
-    uint32_t *const tdep = IMAGE ? (uint32_t *)&Rf[(IMAGE ? 12 : 0) * kBlock + tid] : &tdepth_reg;
-    if (IMAGE) Rf[(IMAGE ? 12 : 0) * kBlock + tid] = (uint64_t)(blockIdx.x * kBlock + tid) << 32;
+    uint32_t *const tdep = IMAGE ? (uint32_t *)&Rf[(IMAGE ? kDepth : 0) * kBlock + tid] : &tdepth_reg;
+    if (IMAGE) Rf[(IMAGE ? kDepth : 0) * kBlock + tid] = (uint64_t)(blockIdx.x * kBlock + tid) << 32;
 
     // ---- per-unit setup: r1, r2, r10 (other registers zero) are set by the
     // fast path's fresh entry, which every unit starts with ----
@@ -832,7 +848,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         // chain only from a unit every lane of the wave runs without a failure
         const bool whole = __ballot(c.alive) == ~0ull && __ballot(c.err != E_OK) == 0 && __ballot(parked) == 0;
         uint32_t adv = 0;
-        const uint32_t why = run_fast(c, fe, fu, whole ? fu.chain : 0u, adv);
+        const uint32_t why = run_fast<G>(c, fe, fu, whole ? fu.chain : 0u, adv);
         fu.entry &= ~1u;
         if (adv) {  // the asm tier finished `adv` units of this wave and is in the next
           it += adv;
@@ -885,7 +901,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         uint32_t next = c.lpc;
         if (csel) {
           ctx_for_cpp();
-          uint64_t *R = &Rf[tid];
+          uint64_t *R = &Rg[tid];
           // frames word-interleaved across the grid's lanes ([depth][word][lane]):
           // a wave's save of one word is one coalesced 512-B store
           uint64_t *const fbase = (uint64_t *)p.frames + (blockIdx.x * kBlock + tid);
@@ -973,7 +989,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         env.lru_ops = lru_ops;
         env.exact = ordered;
         uint32_t cerr = E_OK;
-        uint64_t *R = &Rf[tid];
+        uint64_t *R = &Rg[tid];
         const uint64_t rv = call_helper(c.call_id, R[1 * kBlock], R[2 * kBlock], R[3 * kBlock], R[4 * kBlock],
                                         R[5 * kBlock], p.maps, p.ncpu,
                                         (p.first_unit + unit) ^ ((uint64_t)c.steps << 40), env, &cerr);
@@ -1160,14 +1176,20 @@ extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind,
   const size_t dyn = dyn_lds_bytes(kind, big_stack, p->stack_size, p->comb_entries, p->lcache != 0);
   dim3 g(grid), b(kBlock);
   const bool image = q.tail_entry && !big_stack;
-#define L(K, B, I) hipLaunchKernelGGL((k_interp<K, B, I>), g, b, dyn, stream, q)
+  const bool g_regs = q.gregs && !big_stack;
+#define L(K, B, I, G) hipLaunchKernelGGL((k_interp<K, B, I, G>), g, b, dyn, stream, q)
+#define LK(K)                                                          \
+  if (big_stack) L(K, true, false, false);                             \
+  else if (image) { if (g_regs) L(K, false, true, true); else L(K, false, true, false); } \
+  else { if (g_regs) L(K, false, false, true); else L(K, false, false, false); }
   if (kind == CTX_XDP) {
-    if (big_stack) L(CTX_XDP, true, false); else if (image) L(CTX_XDP, false, true); else L(CTX_XDP, false, false);
+    LK(CTX_XDP)
   } else if (kind == CTX_SYSCALL) {
-    if (big_stack) L(CTX_SYSCALL, true, false); else if (image) L(CTX_SYSCALL, false, true); else L(CTX_SYSCALL, false, false);
+    LK(CTX_SYSCALL)
   } else {
-    if (big_stack) L(CTX_RAW, true, false); else if (image) L(CTX_RAW, false, true); else L(CTX_RAW, false, false);
+    LK(CTX_RAW)
   }
+#undef LK
 #undef L
   return hipGetLastError();
 }
@@ -1180,17 +1202,22 @@ extern "C" hipError_t bpftime_amd_launch_merge(const uint64_t *log, uint32_t log
   return hipGetLastError();
 }
 
-extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds) {
+extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds, bool gregs) {
   int n = 0;
   hipError_t e;
-#define O(K, B) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_interp<K, B, false>, kBlock, dyn_lds)
+#define O(K, B, G) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_interp<K, B, false, G>, kBlock, dyn_lds)
+#define OK(K)                         \
+  if (big_stack) O(K, true, false);   \
+  else if (gregs) O(K, false, true);  \
+  else O(K, false, false);
   if (kind == CTX_XDP) {
-    if (big_stack) O(CTX_XDP, true); else O(CTX_XDP, false);
+    OK(CTX_XDP)
   } else if (kind == CTX_SYSCALL) {
-    if (big_stack) O(CTX_SYSCALL, true); else O(CTX_SYSCALL, false);
+    OK(CTX_SYSCALL)
   } else {
-    if (big_stack) O(CTX_RAW, true); else O(CTX_RAW, false);
+    OK(CTX_RAW)
   }
+#undef OK
 #undef O
   return e == hipSuccess ? n : 1;
 }

@@ -1213,11 +1213,13 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
       comb = true;
   }
   out.needs_comb = comb;
-  // how many counter addresses the table can be asked to hold per block: an
-  // element per (map, site) -- per-CPU elements for the few virtual CPUs a
+  // how many counter granules the table can be asked to hold per block: the
+  // elements of every map a deferred add reaches (the sites adding to one
+  // value share its granules) -- per-CPU elements for the few virtual CPUs a
   // block's consecutive units span (kBlock / 64 waves)
   {
     uint64_t hint = 0;
+    std::vector<uint32_t> seen;
     for (size_t i = 0; i < prog.size() && hint < ~0u; i++) {
       const DInsn &d = prog[i];
       if (!out.add_site[i] || (out.fast[i].w1 & FW_NODEFER)) continue;
@@ -1228,6 +1230,8 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
         hint = ~0u;
         break;
       }
+      if (std::find(seen.begin(), seen.end(), (uint32_t)b.id) != seen.end()) continue;
+      seen.push_back((uint32_t)b.id);
       const bool percpu = m->type == MT_PERCPU_ARRAY || m->type == MT_PERCPU_HASH;
       hint += (uint64_t)m->max_entries * (percpu ? kBlock / 64 : 1);
     }

@@ -27,7 +27,7 @@
 namespace bpftime_amd {
 extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind, bool big_stack, uint32_t grid,
                                                 uint32_t ordered, hipStream_t stream);
-extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds);
+extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds, bool gregs);
 extern "C" hipError_t bpftime_amd_launch_merge(const uint64_t *log, uint32_t log_words, uint32_t nblocks,
                                                 hipStream_t stream);
 
@@ -159,7 +159,7 @@ class Mi355xVm {
   uint32_t base_stack = 0;  // the loaded program's own stack need (kStackSize + 1: unknown)
   std::string link_note;    // targets left out of the last image, and why
   // block-end flush logs (common.hpp kMergeGroup) and tail-call frames
-  StreamBufs logs, frames, scratch;
+  StreamBufs logs, frames, scratch, regs;
 
   Mi355xVm() {
     // bpftime_prog.cpp:126-127 defaults, pointed at the device registry
@@ -448,34 +448,36 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   p.stack_size = prog.stack_size;
   // ORDERED: every counter add goes straight to memory (link_fast), no table
   p.comb_entries = (b->flags & EBPF_BATCH_ORDERED) ? 0 : prog.comb_entries;
+  // launches holding a combining table or lookup cache keep the C++ tier's
+  // register copy in global memory (k_interp G): their units stay in the asm
+  // tier, and the LDS goes to resident blocks (latency-bound: more waves
+  // hide the packet and probe loads)
+  const bool greg = !(b->flags & EBPF_BATCH_ORDERED) && !prog.big_stack && (p.comb_entries || p.lcache) &&
+                    !getenv("BPFTIME_AMD_LDS_REGS");
   if (p.comb_entries) {
-    // the largest combining table (256 .. kCombMax entries) that keeps the
-    // residency the smallest table allows: a counter that finds no entry is a
-    // device atomic (memory-side, ~10 G/s chip-wide for scattered 8-byte
-    // adds), so table reach matters, but a block fewer per CU costs more
-    // (flow-hash 1024 entries at 2 blocks / CU 1.61 ms, 2048 at 1 2.04;
-    // syscall-agg 512 at 3 blocks 0.73 ms, 1024 at 2 0.94)
-    static std::map<uint64_t, uint32_t> best;  // (kind, big stack, stack bytes) -> entries
-    const bool xdp_form = b->ctx_kind == CTX_XDP;
-    const uint32_t hint_key = (xdp_form ? im.fx : im.fr).comb_hint;
-    const uint64_t key = ((uint64_t)(hint_key >= 4096 ? 4096 : hint_key) << 50) | ((uint64_t)p.lcache << 48) |
-                         ((uint64_t)b->ctx_kind << 40) | ((uint64_t)prog.big_stack << 32) | prog.stack_size;
-    auto it = best.find(key);
-    if (it == best.end()) {
-      auto dyn = [&](uint32_t e) { return dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, e, p.lcache); };
-      const int base = bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn(kComb));
-      // ... but no larger than twice the counter addresses a block can reach
-      // (per-CPU counters: a few; flow keys: the table's whole reach), since
-      // LDS it does not need is occupancy lost (tail-call 2.68 -> 2.07 ms)
-      const uint32_t hint = (xdp_form ? im.fx : im.fr).comb_hint;
-      uint32_t e = kComb;
-      while (e < kCombMax && (uint64_t)e < 2ull * hint &&
-             bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn(2 * e)) >= base)
-        e *= 2;
-      if (getenv("BPFTIME_AMD_COMB_ENTRIES")) e = (uint32_t)atoi(getenv("BPFTIME_AMD_COMB_ENTRIES"));
-      it = best.emplace(key, e).first;
-    }
-    p.comb_entries = it->second;
+    // the table's reach: a counter that finds no entry is a device atomic
+    // (memory-side, ~10 G/s chip-wide for scattered 8-byte adds), so the
+    // table should hold the hot part of the counter granules a block's adds
+    // can reach (the loader's hint), even at a block fewer per CU.  Measured
+    // with the register copy in global memory (k_interp G, one MI355X):
+    // flow-hash (65536 flows) 512 entries at 3 blocks / CU 2.71 ms, 1024 at
+    // 3 1.71, 2048 at 2 1.34; syscall-agg (8192 ids) 256 at 4 1.40, 512 at
+    // 4 0.68, 1024 at 3 0.74; tail-call (per-CPU counters) 256 and 512 at 4
+    // 1.63, 1024 2.41.  So: hint / 32 granules, a power of two in
+    // [512, kCombMax] (1024 when the loader cannot bound the addresses)
+    const uint32_t hint = (b->ctx_kind == CTX_XDP ? im.fx : im.fr).comb_hint;
+    uint32_t e = 2 * kComb;
+    if (hint == ~0u)
+      e = 1024;
+    else
+      while (e < kCombMax && 32ull * e < hint) e *= 2;
+    if (const char *ce = getenv("BPFTIME_AMD_COMB_ENTRIES")) e = (uint32_t)atoi(ce);
+    // (a block must still fit the CU's LDS beside the lanes' ctx and stacks)
+    while (e > kComb && bpftime_amd_occupancy(b->ctx_kind, prog.big_stack,
+                                              dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, e, p.lcache),
+                                              greg) < 1)
+      e /= 2;
+    p.comb_entries = e;
   }
   p.ncpu = r.ncpu;
   p.ifindex = b->ingress_ifindex;
@@ -508,7 +510,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       cus = prop.multiProcessorCount;
     }
     const size_t dyn = dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, p.comb_entries, p.lcache);
-    int occ = bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn);
+    int occ = bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn, greg);
     if (occ < 1) occ = 1;
     uint64_t want = (b->count + kBlock - 1) / kBlock;
     // resident blocks x 4 when the program has no combining table: more,
@@ -525,6 +527,13 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     if (const char *g = getenv("BPFTIME_AMD_MAX_GRID"))
       if (atoi(g) > 0 && grid > (uint32_t)atoi(g)) grid = (uint32_t)atoi(g);
     if (im.d_tail_entry && grid > kTailGrid) grid = kTailGrid;  // one frame stack per lane of the grid
+  }
+  if (greg) {
+    p.gregs = (uint64_t *)regs.get(s, (uint64_t)grid * 11 * kBlock * 8);
+    if (!p.gregs) {
+      error = "register copy allocation failed";
+      return -1;
+    }
   }
   if (im.d_tail_entry) {
     // tail-call frames for the lanes of this launch ([depth][word][lane]),
@@ -566,8 +575,9 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     return -1;
   }
   if (getenv("BPFTIME_AMD_VERBOSE"))
-    fprintf(stderr, "bpftime_amd: launch units %llu grid %u comb %u lcache %u stage %u stack %u\n",
-            (unsigned long long)b->count, grid, p.comb_entries, p.lcache, p.stage, (unsigned)prog.stack_size);
+    fprintf(stderr, "bpftime_amd: launch units %llu grid %u comb %u lcache %u stage %u stack %u gregs %d\n",
+            (unsigned long long)b->count, grid, p.comb_entries, p.lcache, p.stage, (unsigned)prog.stack_size,
+            p.gregs ? 1 : 0);
   hipError_t e = bpftime_amd_launch_interp(&p, b->ctx_kind, prog.big_stack, grid, ordered ? 1 : 0, s);
   if (e == hipSuccess && p.flush_log) e = bpftime_amd_launch_merge(p.flush_log, p.log_words, grid, s);
   if (e != hipSuccess) {
