@@ -115,7 +115,7 @@ struct DMap {
   uint32_t val_off;     // = 8 + round8(key_size)
   uint32_t ncpu;        // per-CPU slot count
   uint64_t count_addr;  // device address of the u64 element counter (hash)
-  uint64_t ix;          // device address of the u32 lookup index, 0 = not valid
+  uint64_t ix;          // device address of the u32 lookup index, 0 = not valid (LPM_TRIE: its flat table)
 };
 static_assert(sizeof(DMap) == 64, "DMap must be 64 bytes");
 

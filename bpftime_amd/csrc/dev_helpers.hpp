@@ -426,6 +426,13 @@ __device__ uint64_t lpm_lookup(const DMap &m, uint64_t key) {
   const uint32_t kp = *(const u32u *)key;
   if (kp > maxp) return 0;
   const uint8_t *kd = (const uint8_t *)(uintptr_t)(key + 4);
+  if (m.ix && kp == 32 && dsz == 4) {
+    // IPv4 full-length key: the flat table (maps.cpp LpmTrie::flat)
+    const uint32_t *t = (const uint32_t *)(uintptr_t)m.ix;
+    uint32_t e = t[((uint32_t)kd[0] << 16) | ((uint32_t)kd[1] << 8) | kd[2]];
+    if (e & 0x80000000u) e = t[(1u << 24) + 256u * (e & 0x7fffffffu) + kd[3]];
+    return e ? m.data + 16 + (uint64_t)(e - 1) * m.slot_size + m.val_off : 0;
+  }
   int32_t node = *(const int32_t *)(uintptr_t)m.data;
   uint64_t found = 0;
   for (uint32_t guard = 0; node >= 0 && guard <= maxp + 1; guard++) {

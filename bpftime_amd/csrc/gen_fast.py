@@ -864,8 +864,9 @@ class Gen:
                "s_load_dwordx2 s[76:77], %[maps], s85",                     # data
                "s_waitcnt lgkmcnt(0)")
         if stack_key:
-            hsh = self.label("hash")
-            self.e("s_cmp_eq_u32 s72, 1", f"s_cbranch_scc1 {hsh}")          # BPF_MAP_TYPE_HASH
+            hsh, lpm = self.label("hash"), self.label("lpm")
+            self.e("s_cmp_eq_u32 s72, 1", f"s_cbranch_scc1 {hsh}",          # BPF_MAP_TYPE_HASH
+                   "s_cmp_eq_u32 s72, 11", f"s_cbranch_scc1 {lpm}")         # BPF_MAP_TYPE_LPM_TRIE
         # ARRAY: element key; PERCPU_ARRAY (per_cpu_array_map.cpp:34-48):
         # element key * ncpu + this wave's virtual cpu (%[vcpu] = cpu | ncpu
         # << 16 when the wave's lanes share one, else ~0: C++)
@@ -904,6 +905,52 @@ class Gen:
         if stack_key:
             self.e(f"{hsh}:")
             self.hash_lookup()
+            self.e(f"{lpm}:")
+            self.lpm_lookup()
+
+    def lpm_lookup(self):
+        """LPM_TRIE with a 4-byte (IPv4) key on the stack whose prefixlen is
+        32 in every lane: the flat table (maps.cpp LpmTrie::flat, DMap.ix):
+        e = t[top 24 address bits], e = group[e][low byte] when bit 31 is
+        set; r0 = e ? &value of node e - 1 in the replica : 0 -- the node the
+        trie walk (dev_helpers.hpp lpm_lookup) returns.  Other keys, and
+        tries without the table, leave for C++.  s85 = fd * 64 + 16."""
+        grp = self.label("lg")
+        self.e("s_cmp_lg_u32 s73, 8", f"s_cbranch_scc1 {L('slow')}",        # key_size 4 + 4
+               "s_add_u32 s69, s85, 16",
+               "s_load_dwordx4 s[64:67], %[maps], s69",                      # slot_size, key_off, val_off, ncpu
+               "s_add_u32 s69, s85, 40",
+               "s_load_dwordx2 s[70:71], %[maps], s69",                      # ix = the flat table
+               "v_add_u32 v41, s46, %[stklo]",
+               "ds_read_b32 v44, v41", "ds_read_b32 v45, v41 offset:4",     # prefixlen, address bytes
+               "s_waitcnt lgkmcnt(0)",
+               "s_cmp_eq_u64 s[70:71], 0", f"s_cbranch_scc1 {L('slow')}",
+               "v_cmp_ne_u32 s[54:55], 32, v44", "s_and_b64 s[54:55], s[54:55], exec",
+               f"s_cbranch_scc1 {L('slow')}",                                # a lane's prefixlen != 32
+               "s_mov_b32 s69, 0x10203",
+               "v_perm_b32 v46, v45, v45, s69",                              # the address, big endian
+               "v_lshrrev_b32 v47, 8, v46", "v_lshlrev_b32 v47, 2, v47",
+               "global_load_dword v50, v47, s[70:71]",
+               "s_waitcnt vmcnt(0)",
+               "v_cmp_gt_i32 vcc, 0, v50", "s_and_b64 vcc, vcc, exec",       # bit 31: a /24 group
+               f"s_cbranch_vccz {grp}",
+               "s_mov_b64 s[56:57], exec", "s_mov_b64 exec, vcc",
+               "v_and_b32 v51, 0x7fffffff, v50", "v_lshlrev_b32 v51, 8, v51",
+               "v_and_b32 v42, 0xff, v46", "s_mov_b32 s69, 0x1000000", "v_add3_u32 v51, v51, v42, s69",
+               "v_lshlrev_b32 v51, 2, v51",
+               "global_load_dword v50, v51, s[70:71]",
+               "s_waitcnt vmcnt(0)",
+               "s_mov_b64 exec, s[56:57]",
+               f"{grp}:",
+               "v_cmp_ne_u32 s[54:55], 0, v50",
+               "v_add_u32 v50, -1, v50",
+               "v_mov_b32 v47, s64",
+               "v_mad_u64_u32 v[42:43], s[56:57], v50, v47, s[76:77]",      # data + node * slot_size
+               "s_add_u32 s69, s66, 16",                                     # + 16 + val_off
+               "v_add_co_u32 v42, vcc, s69, v42", "v_addc_co_u32 v43, vcc, 0, v43, vcc",
+               f"v_cndmask_b32 v{R0}, 0, v42, s[54:55]",
+               f"v_cndmask_b32 v{R0 + 1}, 0, v43, s[54:55]")
+        self.next_seq()
 
     def call_lookup_ak(self):
         """ARRAY lookup, map bound at load (w[2:3] = value base, w4 =

@@ -16,6 +16,7 @@
 #include <set>
 
 #include <algorithm>
+#include <functional>
 #include <vector>
 
 #include "../../include/bpftime_amd.h"
@@ -389,6 +390,87 @@ struct LpmTrie {
   std::vector<Node> nodes;
   int32_t root = -1;
   uint64_t entries = 0;
+  // device flat table of a 4-byte-key trie (flat(); DMap.ix), 0 = none
+  void *flat_dev = nullptr;
+  uint64_t flat_bytes = 0;
+  ~LpmTrie() {
+    if (flat_dev) (void)hipFree(flat_dev);
+  }
+
+  // DIR-24-8 form of a trie with 4-byte keys (IPv4 routing), for device
+  // lookups of full-length keys (prefixlen 32): t[a >> 8] for the top 24
+  // address bits holds node + 1 of the node lookup() returns for every
+  // address of that /24 (0: none), or 0x80000000 | g when the result
+  // depends on the low byte, whose 256 results then sit in group g at
+  // t[2^24 + 256 g].  Built by partitioning the address space the way the
+  // walk does (lpm_trie_map.cpp:192-264, restated in lookup()): the
+  // addresses reaching a node form one prefix block; those its prefix does
+  // not match keep the result found above it, the matching ones continue to
+  // its children, and a matching 32-bit node ends the walk (a deleted, i.e.
+  // intermediate, one with no result: the reference's ENOENT, not the
+  // covering prefix).  The blocks are disjoint and cover every address, so
+  // each table entry is written by exactly one of them.  False when more
+  // than max_groups /24s need a group.
+  bool flat(std::vector<uint32_t> &t, uint32_t max_groups) const {
+    t.assign(1u << 24, 0);
+    uint32_t ng = 0;
+    bool ok = true;
+    auto top = [](uint32_t a, uint32_t len) { return len ? a & (~0u << (32 - len)) : 0u; };
+    auto paint = [&](uint32_t a, uint32_t len, uint32_t v) {
+      a = top(a, len);
+      if (len <= 24) {
+        const uint32_t j = a >> 8;
+        std::fill(t.begin() + j, t.begin() + j + (1u << (24 - len)), v);
+        return;
+      }
+      const uint32_t j = a >> 8;
+      if (!(t[j] & 0x80000000u)) {
+        if (ng >= max_groups) {
+          ok = false;
+          return;
+        }
+        t.resize(t.size() + 256, 0);
+        t[j] = 0x80000000u | ng++;
+      }
+      const uint64_t g = (1u << 24) + 256ull * (t[j] & 0x7fffffffu) + (a & 0xff);
+      std::fill(t.begin() + g, t.begin() + g + (1u << (32 - len)), v);
+    };
+    // (node, arrival block (a, len), result found above it)
+    std::function<void(int32_t, uint32_t, uint32_t, uint32_t)> visit = [&](int32_t ni, uint32_t a, uint32_t len,
+                                                                           uint32_t f) {
+      if (!ok) return;
+      if (ni < 0) {
+        paint(a, len, f);
+        return;
+      }
+      const Node &n = nodes[ni];
+      const uint32_t np = n.plen;
+      const uint32_t nd = top(((uint32_t)n.data[0] << 24) | ((uint32_t)n.data[1] << 16) |
+                                  ((uint32_t)n.data[2] << 8) | n.data[3], np);
+      const uint32_t c = std::min(len, np);
+      if (top(a, c) != top(nd, c)) {  // no address of the block matches the node
+        paint(a, len, f);
+        return;
+      }
+      for (uint32_t i = len; i < np; i++)  // first mismatch at bit i
+        paint(top(nd, i) | ((~nd) & (0x80000000u >> i)), i + 1, f);
+      const uint32_t ml = std::max(len, np);
+      const uint32_t m = len > np ? a : (top(a, len) | nd);  // the matching block (m, ml)
+      if (np == 32) {
+        paint(m, 32, n.inter ? 0 : (uint32_t)ni + 1);
+        return;
+      }
+      const uint32_t f2 = n.inter ? f : (uint32_t)ni + 1;
+      for (uint32_t b = 0; b < 2; b++) {
+        const uint32_t bitv = b ? (0x80000000u >> np) : 0;
+        if (ml > np && (m & (0x80000000u >> np)) != bitv) continue;
+        const uint32_t nl = std::max(ml, np + 1);
+        visit(n.child[b], top(top(m, np) | bitv | (m & ~top(~0u, np + 1)), nl), nl, f2);
+      }
+    };
+    visit(root, 0, 0, 0);
+    return ok;
+  }
 
   int bit(const uint8_t *d, size_t i) const {  // :88-98
     if (i >= (size_t)dsz * 8) return 0;
@@ -619,7 +701,24 @@ static int lpm_upload(int fd) {
   if (hipDeviceSynchronize() != hipSuccess) return -1;  // no batch still reading the replica
   if (hipMemcpy((void *)m.d.data, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) return -1;
   r.lpm_stale.erase(fd);
-  return 0;
+  // IPv4 tries also get the flat table (LpmTrie::flat) device lookups of
+  // full-length keys take in one or two loads instead of the trie walk
+  uint64_t flat = 0;
+  std::vector<uint32_t> t;
+  if (m.lpm->dsz == 4 && !getenv("BPFTIME_AMD_NO_LPM_FLAT") && m.lpm->flat(t, 1u << 16)) {
+    LpmTrie &lt = *m.lpm;
+    const uint64_t bytes = 4ull * t.size();
+    if (lt.flat_bytes < bytes) {
+      if (lt.flat_dev) (void)hipFree(lt.flat_dev);
+      lt.flat_dev = nullptr;
+      lt.flat_bytes = 0;
+      if (hipMalloc(&lt.flat_dev, bytes) == hipSuccess) lt.flat_bytes = bytes;
+    }
+    if (lt.flat_dev && hipMemcpy(lt.flat_dev, t.data(), bytes, hipMemcpyHostToDevice) == hipSuccess)
+      flat = (uint64_t)(uintptr_t)lt.flat_dev;
+  }
+  m.d.ix = flat;
+  return r.push_map(fd);
 }
 
 void ix_invalidate(int fd) {
