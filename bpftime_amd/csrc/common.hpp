@@ -178,6 +178,11 @@ constexpr uint32_t CTX_RAW = 0;      // r1 = unit memory, r2 = length
 constexpr uint32_t CTX_XDP = 1;      // r1 = xdp_md_userspace (48 B, LDS)
 constexpr uint32_t CTX_SYSCALL = 2;  // r1 = 64-B trace_event_raw_sys_enter record
 
+// Ring-buffer staging per block (dev_helpers.hpp RbStage)
+constexpr uint32_t kRbStageRec = 2048;                                // record bytes (a ring chunk) per block
+constexpr uint32_t kRbStageMaxRec = kRbStageRec / 8;                  // records per block (>= 8 B each)
+constexpr uint32_t kRbStageBytes = kRbStageRec + 4 * kRbStageMaxRec;  // + u32 record offsets
+
 // Kernel launch parameters (passed by value).
 struct FInsn;
 struct KParams {
@@ -224,6 +229,7 @@ struct KParams {
   uint32_t tail_stack_mask;
   uint32_t lcache;           // 1 = the block's hash-lookup cache exists (common.hpp kLcacheEntries)
   uint64_t *gregs;           // r0..r10 copies for the C++ tier: [grid][11][kBlock] u64 (k_interp G), or nullptr (LDS)
+  uint8_t *rb_stage;         // ring-buffer staging: [grid][kRbStageBytes] right after lane_scratch's words, or nullptr
 };
 
 // Block-end counter deltas.  Every block holds its counter deltas (the wave

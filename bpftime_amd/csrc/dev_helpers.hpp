@@ -472,6 +472,31 @@ constexpr uint64_t kRbMaxWaves = 256 * 32;                 // CUs x resident wav
 constexpr uint64_t kRbWaveMax = 4096;                      // largest wave reservation on the fast path
 constexpr uint64_t kRbSlack = kRbMaxWaves * kRbWaveMax;    // 32 MiB
 
+// Block staging of ring-buffer records.  A block does not move the ring's
+// producer position per record (a same-address atomic at the memory side,
+// ~40 ns each under the whole chip's contention: it bounded the sampler at
+// 1.5 Gpps): its first reservation, when the ring has ample room (the fast
+// path's condition), reserves a chunk of kRbStageRec bytes of the ring with
+// one fetch-and-add, and the block's waves then claim records inside the
+// chunk with an LDS add, writing them to a per-block staging area.  When the
+// block ends it copies its records to their places in the chunk (with the
+// flags submit / discard gave them) and fills the chunk's unused tail with
+// one DISCARD record, which a consumer skips.  Every byte is reserved in the
+// ring before it is handed out, so no reservation of any other block or
+// path can overrun (the exact path below is unchanged); the difference to
+// the reference is the discarded tail, up to one chunk per block and launch
+// of ring space that a ring going from ample room to full inside one launch
+// can no longer give to records.  A wave whose records do not fit the chunk
+// reserves directly.  A host consumer reads the ring after the batch, so it
+// sees the same records in another parallel order.
+// (sizes: common.hpp kRbStage*)
+struct RbStage {
+  uint8_t *buf = nullptr;  // this block's area: records, then u32 offsets (nullptr: no staging)
+  uint32_t *used = nullptr, *end = nullptr, *nrec = nullptr;  // LDS: bytes claimed, staged end, records
+  int32_t *fd = nullptr;   // LDS: the ring of the block's chunk (-1 undecided, -3 deciding, -2 none)
+  uint64_t *base = nullptr;  // LDS: the chunk's ring position
+};
+
 __device__ __forceinline__ uint64_t rb_cas_reserve(const DMap &m, uint64_t total) {
   // returns the old producer position, or ~0 if total does not fit
   const uint64_t cons = __hip_atomic_load(G64(m.data), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -489,7 +514,7 @@ __device__ __forceinline__ uint64_t rb_cas_reserve(const DMap &m, uint64_t total
   return ~0ull;
 }
 
-__device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size) {
+__device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size, const RbStage &st) {
   const bool ok = fd < kMaxFds && maps[fd < kMaxFds ? fd : 0].type == MT_RINGBUF &&
                   !(size & (RB_BUSY | RB_DISCARD));
   const DMap m = maps[ok ? fd : 0];
@@ -507,6 +532,56 @@ __device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size) {
       const uint64_t t = __shfl(total, l);
       if (l < me) before += t;
       sum += t;
+    }
+    if (st.buf) {
+      // block staging (RbStage): the block's first reservation reserves
+      // its chunk (a wave arriving while another decides reserves directly)
+      int32_t sfd = __shfl(__hip_atomic_load(st.fd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), leader);
+      if (sfd == -1) {
+        if (me == leader) {
+          int32_t cur = -1;
+          if (__hip_atomic_compare_exchange_strong(st.fd, &cur, -3, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            const uint64_t cons = __hip_atomic_load(G64(m.data), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t prod = __hip_atomic_load(G64(m.data + 128), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int32_t got = -2;
+            // the fast path's condition (below), for a chunk
+            if (m.max_entries >= 2 * kRbSlack && (uint64_t)m.max_entries - (prod - cons) >= kRbStageRec + kRbSlack) {
+              *st.base = __hip_atomic_fetch_add(G64(m.data + 128), (uint64_t)kRbStageRec, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+              got = (int32_t)fd;
+            }
+            __hip_atomic_store(st.fd, got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            cur = got;
+          }
+          sfd = cur;
+        }
+        sfd = __shfl(sfd, leader);
+      }
+      if (sfd == (int32_t)fd) {
+        uint32_t base = ~0u, rbase = 0;
+        const uint32_t cnt = (uint32_t)__builtin_popcountll(active);
+        if (me == leader) {
+          base = __hip_atomic_fetch_add(st.used, (uint32_t)sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if ((uint64_t)base + sum <= kRbStageRec) {  // (then the record slots fit too: >= 8 B each)
+            rbase = __hip_atomic_fetch_add(st.nrec, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_max(st.end, base + (uint32_t)sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          } else {
+            base = ~0u;  // staging full: direct (the staged end stays below every later claim)
+          }
+        }
+        base = __shfl(base, leader);
+        rbase = __shfl(rbase, leader);
+        if (base != ~0u) {
+          const uint32_t off = base + (uint32_t)before;
+          const uint32_t rank = (uint32_t)__builtin_popcountll(active & ((1ull << me) - 1));
+          uint8_t *rec = st.buf + off;
+          *(uint32_t *)rec = (uint32_t)size | RB_BUSY;
+          *(int32_t *)(rec + 4) = (int32_t)fd;
+          ((uint32_t *)(st.buf + kRbStageRec))[rbase + rank] = off;
+          return (uint64_t)(uintptr_t)(rec + RB_HDR);
+        }
+      }
     }
     uint64_t base = ~0ull;
     if (me == leader) {
@@ -537,7 +612,13 @@ __device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size) {
   return d + ((pos + RB_HDR) & mask);
 }
 
-__device__ void rb_submit(const DMap *maps, uint64_t sample, bool discard) {
+__device__ void rb_submit(const DMap *maps, uint64_t sample, bool discard, const RbStage &st) {
+  if (st.buf && sample >= (uint64_t)(uintptr_t)st.buf + RB_HDR &&
+      sample < (uint64_t)(uintptr_t)st.buf + kRbStageRec) {  // a staged record: published at block end
+    uint32_t *h = (uint32_t *)(uintptr_t)(sample - RB_HDR);
+    *h = (*h & ~RB_BUSY) | (discard ? RB_DISCARD : 0u);
+    return;
+  }
   const int32_t fd = *(const int32_t *)(uintptr_t)(sample - 4);  // the header's fd (bpf_helper.cpp:484)
   if (fd < 0 || fd >= (int32_t)kMaxFds) return;
   const DMap m = maps[fd];
@@ -551,12 +632,37 @@ __device__ void rb_submit(const DMap *maps, uint64_t sample, bool discard) {
                         __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ uint64_t rb_output(const DMap *maps, uint64_t fd, uint64_t data, uint64_t size) {
-  const uint64_t buf = rb_reserve(maps, fd, size);
+__device__ uint64_t rb_output(const DMap *maps, uint64_t fd, uint64_t data, uint64_t size, const RbStage &st) {
+  const uint64_t buf = rb_reserve(maps, fd, size, st);
   if (!buf) return (uint64_t)-1;
   copy_bytes(buf, data, (uint32_t)size);
-  rb_submit(maps, buf, false);
+  rb_submit(maps, buf, false, st);
   return 0;
+}
+
+// The block's staged records into its chunk of the ring (every wave of the
+// block is done), one thread per record, and the chunk's unused tail as one
+// DISCARD record.
+__device__ void rb_publish(const DMap *maps, const RbStage &st, uint32_t tid, uint32_t nthreads) {
+  const int32_t fd = *st.fd;
+  if (!st.buf || fd < 0) return;
+  const DMap m = maps[fd];
+  const uint64_t base = *st.base, mask = m.max_entries - 1, d = m.data + 256;
+  const uint32_t end = *st.end, n = min(*st.nrec, kRbStageMaxRec);
+  const uint32_t *offs = (const uint32_t *)(st.buf + kRbStageRec);
+  for (uint32_t i = tid; i < n; i += nthreads) {
+    const uint32_t off = offs[i];
+    const uint32_t h = *(const uint32_t *)(st.buf + off);
+    const uint32_t total = ((h & ~(RB_BUSY | RB_DISCARD)) + RB_HDR + 7) / 8 * 8;
+    const uint64_t *src = (const uint64_t *)(st.buf + off);
+    uint64_t *dst = (uint64_t *)(uintptr_t)(d + ((base + off) & mask));
+    for (uint32_t w = 0; w < total / 8; w++) dst[w] = src[w];
+  }
+  if (tid == 0 && end < kRbStageRec) {
+    const uint64_t h = d + ((base + end) & mask);
+    *(uint32_t *)(uintptr_t)h = (kRbStageRec - end - RB_HDR) | RB_DISCARD;
+    *(int32_t *)(uintptr_t)(h + 4) = fd;
+  }
 }
 
 struct LaneEnv {
@@ -568,6 +674,7 @@ struct LaneEnv {
   // last lookup miss (map fd, key hash) for the lookup_or_try_init race rule
   int32_t miss_fd;
   uint64_t miss_hash;
+  RbStage rb;        // the block's ring-buffer staging (RbStage)
 };
 
 __device__ __forceinline__ uint64_t lru_next_stamp(LaneEnv &env) {

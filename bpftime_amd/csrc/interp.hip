@@ -53,10 +53,10 @@ __device__ __forceinline__ uint64_t call_helper(uint32_t id, uint64_t a1, uint64
     case 44: return helper_adjust_head(a1, a2);
     case 65: return helper_adjust_tail(a1, a2);
     case 189: return helper_xdp_load_bytes(a1, a2, a3, a4);
-    case 130: return rb_output(maps, a1, a2, a3);
-    case 131: return rb_reserve(maps, a1, a2);
-    case 132: rb_submit(maps, a1, false); return 0;
-    case 133: rb_submit(maps, a1, true); return 0;
+    case 130: return rb_output(maps, a1, a2, a3, env.rb);
+    case 131: return rb_reserve(maps, a1, a2, env.rb);
+    case 132: rb_submit(maps, a1, false, env.rb); return 0;
+    case 133: rb_submit(maps, a1, true, env.rb); return 0;
   }
   *err = E_BADOP;
   return 0;
@@ -588,7 +588,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
   SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(flush_log); SRV(log_words); SRP(lane_scratch);
-  SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask); SRV(lcache); SRP(gregs);
+  SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask); SRV(lcache); SRP(gregs); SRP(rb_stage);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
 #undef SRP
 #undef SRV
@@ -617,6 +617,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   for (uint32_t i = tid; i < 5 * p.comb_entries; i += kBlock) comb[i] = 0;
   if (p.lcache)
     for (uint32_t i = tid; i < 2 * kLcacheEntries; i += kBlock) lcache[i] = 0;
+  // ring-buffer staging (dev_helpers.hpp RbStage): LDS counters of the block
+  __shared__ uint32_t rb_used, rb_end, rb_nrec;
+  __shared__ int32_t rb_fd;
+  __shared__ uint64_t rb_base;
+  if (tid == 0) {
+    rb_used = rb_end = rb_nrec = 0;
+    rb_fd = -1;
+  }
+  RbStage rbs;
+  if (p.rb_stage) {
+    rbs.buf = p.rb_stage + (uint64_t)blockIdx.x * kRbStageBytes;
+    rbs.used = &rb_used;
+    rbs.end = &rb_end;
+    rbs.nrec = &rb_nrec;
+    rbs.fd = &rb_fd;
+    rbs.base = &rb_base;
+  }
   // counter v of the table (entry v / 4, counter v % 4 of its granule) as a
   // flush tag {address | (4-byte ? 1 : 0)} and delta
   auto comb_counter = [&](uint32_t v, uint64_t &tag, uint64_t &delta) {
@@ -661,7 +678,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   c.fast = p.fast;
   {
     const uint64_t sl = (uint64_t)(uintptr_t)p.lane_scratch;
-    c.win = Win{p.data_lo, p.data_hi, p.arena_lo, p.arena_hi, sl, sl ? sl + 8ull * gridDim.x * kBlock : 0,
+    // (the lane scratch words, then the blocks' ring-buffer staging areas:
+    // a program writes a record it reserved there)
+    c.win = Win{p.data_lo, p.data_hi, p.arena_lo, p.arena_hi, sl,
+                sl ? sl + 8ull * gridDim.x * kBlock + (p.rb_stage ? (uint64_t)gridDim.x * kRbStageBytes : 0) : 0,
                 p.checked != 0};
   }
   c.dummy = (uint64_t)(uintptr_t)&Rf[kDummy * kBlock + tid];
@@ -988,6 +1008,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         env.lru_stamp = (p.lru_seq << kLruSeqShift) | ((unit & 0xffffffffull) << kLruUnitShift);
         env.lru_ops = lru_ops;
         env.exact = ordered;
+        env.rb = rbs;
         uint32_t cerr = E_OK;
         uint64_t *R = &Rg[tid];
         const uint64_t rv = call_helper(c.call_id, R[1 * kBlock], R[2 * kBlock], R[3 * kBlock], R[4 * kBlock],
@@ -1044,6 +1065,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   }
   if (tid == 0) nlog = 0;
   __syncthreads();
+  if (p.rb_stage) rb_publish(p.maps, rbs, tid, kBlock);
   uint64_t *e = &wdelta[0][0][0];
   constexpr uint32_t NE = kWaveCacheEntries;
   if (tid == 0) {

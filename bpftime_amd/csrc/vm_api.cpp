@@ -550,16 +550,28 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     }
   }
   // a scratch word per lane while prog arrays exist (device map_lookup_elem
-  // on one hands out a copy of the fd there, prog_array.cpp:113-143)
-  for (uint32_t fd = 0; fd < kMaxFds; fd++)
-    if (r.kind[fd] == HKind::MAP && r.maps[fd].type == MT_PROG_ARRAY) {
-      p.lane_scratch = (uint64_t *)scratch.get(s, (uint64_t)grid * kBlock * 8);
-      if (!p.lane_scratch) {
+  // on one hands out a copy of the fd there, prog_array.cpp:113-143), and
+  // after them the blocks' ring-buffer staging areas while ring buffers
+  // exist (dev_helpers.hpp RbStage; not in ORDERED batches: exact order)
+  {
+    bool prog_arrays = false, rings = false;
+    for (uint32_t fd = 0; fd < kMaxFds; fd++)
+      if (r.kind[fd] == HKind::MAP) {
+        prog_arrays |= r.maps[fd].type == MT_PROG_ARRAY;
+        rings |= r.maps[fd].type == MT_RINGBUF;
+      }
+    const bool stage = rings && !ordered && !getenv("BPFTIME_AMD_NO_RB_STAGE");
+    if (prog_arrays || stage) {
+      const uint64_t words = (uint64_t)grid * kBlock * 8;
+      uint8_t *base = (uint8_t *)scratch.get(s, words + (stage ? (uint64_t)grid * kRbStageBytes : 0));
+      if (!base) {
         error = "lane scratch allocation failed";
         return -1;
       }
-      break;
+      p.lane_scratch = (uint64_t *)base;
+      p.rb_stage = stage ? base + words : nullptr;
     }
+  }
   // a block-end flush log when the blocks hold per-lane counter tables:
   // merged by a second launch instead of every block adding its table
   if (p.comb_entries && grid > kMergeGroup && !getenv("BPFTIME_AMD_NO_MERGE")) {

@@ -68,8 +68,11 @@ def test_oracle_ringbuf_rules(fresh_oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("size,frac", [(1 << 20, None), (4096, 0)])
+@pytest.mark.parametrize("size,frac", [(1 << 20, None), (4096, 0), (1 << 26, None)])
 def test_device_ringbuf_sampler(fresh_oracle, fresh_runtime, size, frac):
+    """(1 << 26: a ring large enough for block staging, dev_helpers.hpp
+    RbStage: records reach the ring through per-block chunks whose unused
+    tails are DISCARD records the consumer skips)"""
     po, dev = fresh_oracle, fresh_runtime
     dm = dev.Map(RB, 0, 0, size)
     om = po.OracleMap(RB, 0, 0, size, fd=dm.fd)
