@@ -230,6 +230,7 @@ struct KParams {
   uint32_t lcache;           // 1 = the block's hash-lookup cache exists (common.hpp kLcacheEntries)
   uint64_t *gregs;           // r0..r10 copies for the C++ tier: [grid][11][kBlock] u64 (k_interp G), or nullptr (LDS)
   uint8_t *rb_stage;         // ring-buffer staging: [grid][kRbStageBytes] right after lane_scratch's words, or nullptr
+  uint8_t *gctx;             // XDP: the lanes' ctx in global memory ([grid lane] x 48 B, after the staging), or nullptr (LDS)
 };
 
 // Block-end counter deltas.  Every block holds its counter deltas (the wave
@@ -257,9 +258,9 @@ constexpr uint32_t kTenvBytes = 48;  // gen_fast.py TENV: tail-call constants, t
 constexpr uint32_t kLcacheEntries = 1024;
 constexpr uint32_t kLcacheBytes = 8 * kLcacheEntries;
 inline size_t dyn_lds_for(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
-                          bool lcache = false) {
-  return (size_t)kBlock * ((kind == CTX_XDP ? 48 : 0) + (big_stack ? 0 : stack_size)) + (lcache ? kLcacheBytes : 0) +
-         kTenvBytes + 20 * (size_t)comb_entries;
+                          bool lcache = false, bool ctx_lds = true) {
+  return (size_t)kBlock * ((kind == CTX_XDP && ctx_lds ? 48 : 0) + (big_stack ? 0 : stack_size)) +
+         (lcache ? kLcacheBytes : 0) + kTenvBytes + 20 * (size_t)comb_entries;
 }
 
 // Error codes recorded per unit (err_count counts units with any error)

@@ -329,8 +329,9 @@ class Gen:
                f"v_and_b32 v54, {-8 if pair else -16}, v54",
                f"v_or_b32 v54, {3 if sz == 4 else 2}, v54",                      # tag
                "v_lshrrev_b32 v41, 4, v54", "s_mov_b32 s69, 0x9e3779b1", "v_mul_lo_u32 v41, v41, s69",
-               "s_ff1_i32_b32 s69, %[combn]", "s_sub_u32 s69, 32, s69",          # 32 - log2(entries)
-               "v_lshrrev_b32 v41, s69, v41", f"v_and_b32 v41, -{WAYS}, v41",    # first way of the set
+               f"s_lshr_b32 s69, %[combn], {WAYS.bit_length() - 1}",             # sets (any count)
+               "v_mul_hi_u32 v41, v41, s69",                                     # the set: multiply-shift
+               f"v_lshlrev_b32 v41, {WAYS.bit_length() - 1}, v41",               # its first way
                "v_lshlrev_b32 v55, 4, v41", "v_lshlrev_b32 v41, 2, v41",
                "v_add_u32 v41, %[comb], v41",                                   # the set's tags
                "s_lshl_b32 s70, %[combn], 2", "s_add_u32 s70, s70, %[comb]",

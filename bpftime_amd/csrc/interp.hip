@@ -588,7 +588,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
   SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(flush_log); SRV(log_words); SRP(lane_scratch);
-  SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask); SRV(lcache); SRP(gregs); SRP(rb_stage);
+  SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask); SRV(lcache); SRP(gregs); SRP(rb_stage); SRP(gctx);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
 #undef SRP
 #undef SRV
@@ -600,17 +600,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   __shared__ uint64_t Rf[(IMAGE ? kDepth + 1 : kDummy + 1) * kBlock];
   uint64_t *const Rg = G ? p.gregs + (uint64_t)blockIdx.x * 11 * kBlock : Rf;  // r0..r10 columns
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
-  constexpr uint32_t CTXB = KIND == CTX_XDP ? 48 : 0;
+  // the lane's XDP ctx: in LDS, or (p.gctx: a program that only reads
+  // data / data_end, whose ctx only the C++ tier touches) in global memory
   const uint32_t tid = threadIdx.x;
-  uint8_t *my_ctx = dyn + tid * CTXB;
-  uint8_t *my_stack = dyn + kBlock * CTXB + tid * p.stack_size;
+  const uint32_t ctxb = KIND == CTX_XDP && !p.gctx ? 48 : 0;
+  uint8_t *my_ctx = KIND == CTX_XDP && p.gctx ? p.gctx + ((uint64_t)blockIdx.x * kBlock + tid) * 48 : dyn + tid * ctxb;
+  uint8_t *my_stack = dyn + kBlock * ctxb + tid * p.stack_size;
   // combining table for per-lane counter adds (gen_fast.py comb_add), after
   // the ctx and stack areas: comb_entries u32 tags {16-byte granule's arena
   // offset (8-byte aligned for 8-byte counters) | 2 | (4-byte ? 1 : 0)}
   // (4-way sets), then comb_entries 16-byte
   // delta granules (2 x u64 or 4 x u32), flushed when the block ends; sized 0
   // for programs that never need it
-  uint32_t *lcache = (uint32_t *)(dyn + kBlock * (CTXB + (BIGSTACK ? 0 : p.stack_size)));
+  uint32_t *lcache = (uint32_t *)(dyn + kBlock * (ctxb + (BIGSTACK ? 0 : p.stack_size)));
   uint64_t *tenv = (uint64_t *)((uint8_t *)lcache + (p.lcache ? kLcacheBytes : 0));
   uint32_t *comb = (uint32_t *)((uint8_t *)tenv + kTenvBytes);
   uint64_t *comb_d = (uint64_t *)(comb + p.comb_entries);
@@ -679,9 +681,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   {
     const uint64_t sl = (uint64_t)(uintptr_t)p.lane_scratch;
     // (the lane scratch words, then the blocks' ring-buffer staging areas:
-    // a program writes a record it reserved there)
+    // a program writes a record it reserved there; then the global ctxs)
     c.win = Win{p.data_lo, p.data_hi, p.arena_lo, p.arena_hi, sl,
-                sl ? sl + 8ull * gridDim.x * kBlock + (p.rb_stage ? (uint64_t)gridDim.x * kRbStageBytes : 0) : 0,
+                sl ? sl + 8ull * gridDim.x * kBlock + (p.rb_stage ? (uint64_t)gridDim.x * kRbStageBytes : 0) +
+                         (p.gctx ? 48ull * gridDim.x * kBlock : 0)
+                   : 0,
                 p.checked != 0};
   }
   c.dummy = (uint64_t)(uintptr_t)&Rf[kDummy * kBlock + tid];
@@ -1187,15 +1191,15 @@ static_assert(kMergeEntries == 4u << 10, "k_comb_merge hashes into 2^10 sets of 
 // Host-side launch wrappers
 // ---------------------------------------------------------------------------
 static size_t dyn_lds_bytes(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
-                            bool lcache) {
-  return dyn_lds_for(kind, big_stack, stack_size, comb_entries, lcache);
+                            bool lcache, bool ctx_lds) {
+  return dyn_lds_for(kind, big_stack, stack_size, comb_entries, lcache, ctx_lds);
 }
 
 extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind, bool big_stack, uint32_t grid,
                                                 uint32_t ordered, hipStream_t stream) {
   KParams q = *p;
   q.ordered = ordered;
-  const size_t dyn = dyn_lds_bytes(kind, big_stack, p->stack_size, p->comb_entries, p->lcache != 0);
+  const size_t dyn = dyn_lds_bytes(kind, big_stack, p->stack_size, p->comb_entries, p->lcache != 0, !p->gctx);
   dim3 g(grid), b(kBlock);
   const bool image = q.tail_entry && !big_stack;
   const bool g_regs = q.gregs && !big_stack;

@@ -454,6 +454,14 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   // hide the packet and probe loads)
   const bool greg = !(b->flags & EBPF_BATCH_ORDERED) && !prog.big_stack && (p.comb_entries || p.lcache) &&
                     !getenv("BPFTIME_AMD_LDS_REGS");
+  // ... and an XDP program that reads its ctx only through the specialised
+  // data / data_end loads (the loader's escape analysis) keeps the ctx there
+  // too: only the C++ tier reads it (48 B of LDS per lane)
+  const bool gctx = greg && b->ctx_kind == CTX_XDP && !p.needs_ctx && !im.d_tail_entry &&
+                    !getenv("BPFTIME_AMD_LDS_CTX");
+  auto dyn_of = [&](uint32_t e) {
+    return dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, e, p.lcache, !gctx);
+  };
   if (p.comb_entries) {
     // the table's reach: a counter that finds no entry is a device atomic
     // (memory-side, ~10 G/s chip-wide for scattered 8-byte adds), so the
@@ -471,12 +479,14 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       e = 1024;
     else
       while (e < kCombMax && 32ull * e < hint) e *= 2;
-    if (const char *ce = getenv("BPFTIME_AMD_COMB_ENTRIES")) e = (uint32_t)atoi(ce);
-    // (a block must still fit the CU's LDS beside the lanes' ctx and stacks)
-    while (e > kComb && bpftime_amd_occupancy(b->ctx_kind, prog.big_stack,
-                                              dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, e, p.lcache),
-                                              greg) < 1)
-      e /= 2;
+    // (a block must still fit the CU's LDS beside the lanes' ctx and stacks;
+    // the sets may be any count, gen_fast.py comb_add.  Measured: trading
+    // reach for a resident block does not pay -- flow-hash 2048 entries at 2
+    // blocks / CU 1.32 ms, 1792 at 3 1.57, 1536 at 3 1.42 -- nor does reach
+    // beyond hint / 32 at the same residency: flow-hash 3072 1.29,
+    // syscall-agg 768 / 984 0.672 / 0.677 against 512 0.664)
+    while (e > kComb && bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn_of(e), greg) < 1) e /= 2;
+    if (const char *ce = getenv("BPFTIME_AMD_COMB_ENTRIES")) e = (uint32_t)atoi(ce) & ~7u;
     p.comb_entries = e;
   }
   p.ncpu = r.ncpu;
@@ -509,7 +519,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       hipGetDeviceProperties(&prop, dev);
       cus = prop.multiProcessorCount;
     }
-    const size_t dyn = dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, p.comb_entries, p.lcache);
+    const size_t dyn = dyn_of(p.comb_entries);
     int occ = bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn, greg);
     if (occ < 1) occ = 1;
     uint64_t want = (b->count + kBlock - 1) / kBlock;
@@ -550,9 +560,10 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     }
   }
   // a scratch word per lane while prog arrays exist (device map_lookup_elem
-  // on one hands out a copy of the fd there, prog_array.cpp:113-143), and
-  // after them the blocks' ring-buffer staging areas while ring buffers
-  // exist (dev_helpers.hpp RbStage; not in ORDERED batches: exact order)
+  // on one hands out a copy of the fd there, prog_array.cpp:113-143), after
+  // them the blocks' ring-buffer staging areas while ring buffers exist
+  // (dev_helpers.hpp RbStage; not in ORDERED batches: exact order), then the
+  // lanes' global XDP ctx (gctx)
   {
     bool prog_arrays = false, rings = false;
     for (uint32_t fd = 0; fd < kMaxFds; fd++)
@@ -561,15 +572,16 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
         rings |= r.maps[fd].type == MT_RINGBUF;
       }
     const bool stage = rings && !ordered && !getenv("BPFTIME_AMD_NO_RB_STAGE");
-    if (prog_arrays || stage) {
-      const uint64_t words = (uint64_t)grid * kBlock * 8;
-      uint8_t *base = (uint8_t *)scratch.get(s, words + (stage ? (uint64_t)grid * kRbStageBytes : 0));
+    if (prog_arrays || stage || gctx) {
+      const uint64_t words = (uint64_t)grid * kBlock * 8, sbytes = stage ? (uint64_t)grid * kRbStageBytes : 0;
+      uint8_t *base = (uint8_t *)scratch.get(s, words + sbytes + (gctx ? 48ull * grid * kBlock : 0));
       if (!base) {
         error = "lane scratch allocation failed";
         return -1;
       }
       p.lane_scratch = (uint64_t *)base;
       p.rb_stage = stage ? base + words : nullptr;
+      p.gctx = gctx ? base + words + sbytes : nullptr;
     }
   }
   // a block-end flush log when the blocks hold per-lane counter tables:
@@ -587,9 +599,9 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     return -1;
   }
   if (getenv("BPFTIME_AMD_VERBOSE"))
-    fprintf(stderr, "bpftime_amd: launch units %llu grid %u comb %u lcache %u stage %u stack %u gregs %d\n",
+    fprintf(stderr, "bpftime_amd: launch units %llu grid %u comb %u lcache %u stage %u stack %u gregs %d gctx %d\n",
             (unsigned long long)b->count, grid, p.comb_entries, p.lcache, p.stage, (unsigned)prog.stack_size,
-            p.gregs ? 1 : 0);
+            p.gregs ? 1 : 0, p.gctx ? 1 : 0);
   hipError_t e = bpftime_amd_launch_interp(&p, b->ctx_kind, prog.big_stack, grid, ordered ? 1 : 0, s);
   if (e == hipSuccess && p.flush_log) e = bpftime_amd_launch_merge(p.flush_log, p.log_words, grid, s);
   if (e != hipSuccess) {
