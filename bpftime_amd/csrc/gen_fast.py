@@ -378,6 +378,7 @@ class Gen:
                f"{noclaim}:")
         self.e(f"{direct}:",
                "s_andn2_b64 exec, s[60:61], s[54:55]", f"s_cbranch_execz {done}",
+               "s_bitcmp1_b32 %[oflags], 2", f"s_cbranch_scc1 {done}",          # (BPFTIME_AMD_DBG 128: timing only)
                *glob_add)
         self.e(f"{done}:", "s_mov_b64 exec, s[60:61]")
 

@@ -702,7 +702,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   fe.comb = sreg((uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)comb));
   fe.combn = p.comb_entries;
   fe.head = p.head;
-  fe.oflags = sreg((uint32_t)__builtin_amdgcn_readfirstlane((p.verdicts ? 1u : 0u) | (p.rets ? 2u : 0u)));
+  // (bit 2, BPFTIME_AMD_DBG 128: counter adds that miss the combining table
+  // are dropped -- a timing experiment, never a result)
+  fe.oflags = sreg((uint32_t)__builtin_amdgcn_readfirstlane((p.verdicts ? 1u : 0u) | (p.rets ? 2u : 0u) |
+                                                            ((p.dbg & 128) ? 4u : 0u)));
   fe.dlo = sreg((uint64_t)(p.checked ? p.data_lo : 0));
   fe.dhi = sreg((uint64_t)(p.checked ? p.data_hi : ~(uint64_t)0));
   fe.alo = p.arena_lo;

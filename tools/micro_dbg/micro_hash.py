@@ -9,7 +9,7 @@ from bpftime_amd import vm as dev
 from bpftime_amd.isa import Asm
 from bpftime_amd.programs import BPF_FUNC_map_lookup_elem
 
-N = 1 << 22
+N = 1 << int(os.environ.get("LOG2N", "22"))
 
 
 def timeit(vm, kind, buf, stride, steps=10, **kw):
