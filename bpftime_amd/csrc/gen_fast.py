@@ -1353,6 +1353,7 @@ class Gen:
           "s_waitcnt vmcnt(0)",
           f"{nol}:",
           "s_bitcmp1_b32 %[entry], 6", f"s_cbranch_scc0 {nos}",
+          "s_bitcmp1_b32 %[entry], 1", f"s_cbranch_scc1 {nos}",                 # staged: filtered at fresh
           # syscall filter: nr = *(u64 *)(slot + 8) in {60, 231} -> r0 = 0
           "global_load_dwordx2 v[56:57], v[52:53], off offset:8",
           "s_movk_i32 s70, 0xe7", "s_mov_b32 s71, 0",
@@ -1750,12 +1751,38 @@ class Gen:
           "s_bitcmp1_b32 %[entry], 4", f"s_cbranch_scc0 {n2}",
           f"v_mov_b32 v{R0 + 4}, %[ulen]",
           f"{n2}:")
+        filt, fsv, fsr = self.label("filt"), self.label("fsv"), self.label("fsr")
         e("s_bitcmp1_b32 %[entry], 1", f"s_cbranch_scc0 {loaded}",
           "s_mov_b32 s80, %[stage]",
           f"global_load_dwordx4 v[{STG}:{STG + 3}], v[52:53], off")
         for c in range(1, 4):
-            e(f"s_cmp_lt_u32 %[stage], {16 * (c + 1)}", f"s_cbranch_scc1 {loaded}",
+            e(f"s_cmp_lt_u32 %[stage], {16 * (c + 1)}", f"s_cbranch_scc1 {filt}",
               f"global_load_dwordx4 v[{STG + 4 * c}:{STG + 4 * c + 3}], v[52:53], off offset:{16 * c}")
+        # syscall records (entry bit 6) of a staged unit: exit / exit_group
+        # lanes (nr = bytes 8..15, syscall_trace_attach_impl.cpp:25) finish
+        # with r0 = 0 here, from the staged bytes, instead of a separate load
+        # of nr before the staging loads (chain_routine: unstaged units)
+        e(f"{filt}:",
+          "s_bitcmp1_b32 %[entry], 6", f"s_cbranch_scc0 {loaded}",
+          "s_waitcnt vmcnt(0)",
+          f"v_cmp_eq_u64 s[54:55], 60, v[{STG + 2}:{STG + 3}]",
+          "s_movk_i32 s70, 0xe7", "s_mov_b32 s71, 0",
+          f"v_cmp_eq_u64 s[56:57], s[70:71], v[{STG + 2}:{STG + 3}]",
+          "s_or_b64 s[54:55], s[54:55], s[56:57]",
+          "s_and_b64 s[54:55], s[54:55], exec",
+          f"s_cbranch_scc0 {loaded}",
+          "s_andn2_b64 s[60:61], exec, s[54:55]",
+          "s_mov_b64 exec, s[54:55]",
+          "v_mov_b32 v56, 0", "v_mov_b32 v57, 0",
+          "s_bitcmp1_b32 %[oflags], 0", f"s_cbranch_scc0 {fsv}",
+          "global_store_dword %[vaddr], v56, off",
+          f"{fsv}:",
+          "s_bitcmp1_b32 %[oflags], 1", f"s_cbranch_scc0 {fsr}",
+          "global_store_dwordx2 %[raddr], v[56:57], off",
+          f"{fsr}:",
+          "s_mov_b64 exec, s[60:61]",
+          f"s_cbranch_execnz {loaded}",
+          "s_mov_b32 s84, 0", f"s_branch {L('chain')}")                  # every lane an exit record
         e(f"{loaded}:",
           "s_getpc_b64 s[50:51]",          # = address of the s_branch below
           f"s_branch {L('start')}")
