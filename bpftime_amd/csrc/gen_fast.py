@@ -1321,7 +1321,8 @@ class Gen:
     # (images), 16.. the per-unit step of the
     # virtual cpu (%[vcpu] = cpu | ncpu << 16, or ~0).
     def chain_routine(self):
-        nxt, nov, nol, nos, sv, sr, nod = (self.label(x) for x in ("cnext", "cnv", "cnl", "cns", "csv", "csr", "cnd"))
+        nxt, nov, nol, nos, sv, sr, nod, lw = (self.label(x) for x in ("cnext", "cnv", "cnl", "cns", "csv", "csr",
+                                                                       "cnd", "clw"))
         e = self.e
         e(f"{L('chain')}:",
           "s_cmp_eq_u32 %[chain], 0", f"s_cbranch_scc1 {L('cend')}",
@@ -1350,7 +1351,9 @@ class Gen:
           f"{nov}:",
           "s_bitcmp1_b32 %[entry], 5", f"s_cbranch_scc0 {nol}",
           "global_load_dword %[ulen], %[laddr], off",
-          "s_waitcnt vmcnt(0)",
+          "s_bitcmp1_b32 %[entry], 4", f"s_cbranch_scc1 {lw}",              # r2 = the length: wait now
+          "s_bitcmp1_b32 %[entry], 1", f"s_cbranch_scc1 {nol}",             # staged: waited for with its loads
+          f"{lw}:", "s_waitcnt vmcnt(0)",
           f"{nol}:",
           "s_bitcmp1_b32 %[entry], 6", f"s_cbranch_scc0 {nos}",
           "s_bitcmp1_b32 %[entry], 1", f"s_cbranch_scc1 {nos}",                 # staged: filtered at fresh
@@ -1762,7 +1765,13 @@ class Gen:
         # lanes (nr = bytes 8..15, syscall_trace_attach_impl.cpp:25) finish
         # with r0 = 0 here, from the staged bytes, instead of a separate load
         # of nr before the staging loads (chain_routine: unstaged units)
+        fchk = self.label("fchk")
         e(f"{filt}:",
+          # a chained unit's length load (chain_routine) completes with the
+          # staging loads: one memory round trip per unit instead of two
+          "s_bitcmp1_b32 %[entry], 5", f"s_cbranch_scc0 {fchk}",
+          "s_waitcnt vmcnt(0)",
+          f"{fchk}:",
           "s_bitcmp1_b32 %[entry], 6", f"s_cbranch_scc0 {loaded}",
           "s_waitcnt vmcnt(0)",
           f"v_cmp_eq_u64 s[54:55], 60, v[{STG + 2}:{STG + 3}]",
