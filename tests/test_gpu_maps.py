@@ -78,7 +78,9 @@ def _flow_setup(po, dev, nflows_max=65536):
     return make_maps([(isa.BPF_MAP_TYPE_HASH, 16, 16, nflows_max)], po, dev)
 
 
-@pytest.mark.parametrize("n,nflows", [(4096, 300), (50000, 4000)])
+# (1 << 21, 65536): config 3's own shape -- Zipf(1.1) keys over 65,536 flows
+# into the 65,537-bucket table, most flows present, at 2^21 frames
+@pytest.mark.parametrize("n,nflows", [(4096, 300), (50000, 4000), (1 << 21, 65536)])
 def test_flow_hash_parity(fresh_oracle, fresh_runtime, n, nflows):
     po, dev = fresh_oracle, fresh_runtime
     (om,), (dm,) = _flow_setup(po, dev)
@@ -99,6 +101,8 @@ def test_flow_hash_parity(fresh_oracle, fresh_runtime, n, nflows):
     d_items = dm.hash_items()
     assert d_items == o_items
     # size-independent property: totals = exact histogram of the input
+    if nflows == 65536:
+        assert len(d_items) > 50000
     tot_pkts = sum(struct.unpack("<QQ", v)[0] for v in d_items.values())
     tot_bytes = sum(struct.unpack("<QQ", v)[1] for v in d_items.values())
     ip = (slots[:, 12] == 0x08) & (slots[:, 13] == 0)
