@@ -19,7 +19,7 @@ constexpr uint32_t kMaxFds = 1024;      // device map table size
 constexpr uint32_t kBlock = 256;        // threads per workgroup (4 waves)
 constexpr uint32_t kLdsStackMax = 64;   // per-lane stack bytes kept in LDS
 constexpr uint32_t kComb = 256;         // per-block LDS combining entries (counter adds), minimum
-constexpr uint32_t kCombMax = 4096;     // ... and maximum (a power of two in between, vm_api.cpp)
+constexpr uint32_t kCombMax = 4096;     // ... and maximum (a multiple of 8 in between, vm_api.cpp)
 
 // Internal (pre-decoded) opcodes.  The device switch dispatches on these; the
 // set is dense so the compiler's binary search over cases stays shallow.
@@ -189,7 +189,7 @@ struct KParams {
   const DInsn *prog;
   const FInsn *fast;      // threaded-code form for the asm fast path
   uint32_t fast_div;      // lane groups (divergence) may be scheduled in asm
-  uint32_t comb_entries;  // LDS combining entries per block (0 or kComb)
+  uint32_t comb_entries;  // LDS combining entries per block (0: none; sized per launch, vm_api.cpp)
   const DMap *maps;
   uint8_t *data;          // base of unit slots (device)
   const uint32_t *lens;   // per-unit lengths or nullptr

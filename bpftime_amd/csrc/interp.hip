@@ -609,7 +609,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   // combining table for per-lane counter adds (gen_fast.py comb_add), after
   // the ctx and stack areas: comb_entries u32 tags {16-byte granule's arena
   // offset (8-byte aligned for 8-byte counters) | 2 | (4-byte ? 1 : 0)}
-  // (4-way sets), then comb_entries 16-byte
+  // (8-way sets), then comb_entries 16-byte
   // delta granules (2 x u64 or 4 x u32), flushed when the block ends; sized 0
   // for programs that never need it
   uint32_t *lcache = (uint32_t *)(dyn + kBlock * (ctxb + (BIGSTACK ? 0 : p.stack_size)));
