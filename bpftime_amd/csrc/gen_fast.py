@@ -288,8 +288,9 @@ class Gen:
         (4-byte ? 1 : 0); its deltas are two u64 (8-byte counters at +0 / +8)
         or four u32 (4-byte counters), so the {packets, bytes} pair of a flow
         value shares one entry.  (A counter may have deltas in two entries;
-        both reach it at the flush.)  The table is 4-way set associative: a lane reads
-        its set's four tags (one ds_read_b128), adds to the way holding its
+        both reach it at the flush.)  The table is 8-way set associative, any
+        number of sets (multiply-shift index): a lane reads its set's eight
+        tags (three ds_reads), adds to the way holding its
         granule (a tag never changes once set: no atomic claim), else claims
         an empty way with a compare-and-swap (a lane that loses the race to
         another granule re-reads its set once), else adds to memory directly;
