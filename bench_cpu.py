@@ -86,10 +86,61 @@ def _setup(workload, shard, sample_n):
             tot = sum(int(np.frombuffer(v[:8], dtype=np.uint64)[0]) for v in counts.items().values())
             return tot == runs[0] * live
         return run, check
+    if workload in ("lpm-route", "ringbuf-sample", "tail-call"):
+        import struct
+
+        import bench_workloads as bw
+        seed = {"lpm-route": gen.SEED_CFG2 ^ 0x6, "ringbuf-sample": gen.SEED_CFG2,
+                "tail-call": gen.SEED_CFG2 ^ 0x7}[workload]
+        pk = gen.xdp_packets(sample_n, 64, seed, first)   # = the device generator's frames (csrc/gen.hip)
+        ifindex, want = 0, None
+        if workload == "lpm-route":
+            routes = bw._lpm_routes(np.random.default_rng(0x5EED0006), 16384)
+            rt = po.OracleMap(isa.BPF_MAP_TYPE_LPM_TRIE, 8, 4, len(routes))
+            for plen, net, v in routes:
+                rt.update(struct.pack("<I", plen) + struct.pack(">I", net), struct.pack("<I", v))
+            code = programs.lpm_route(rt.fd)
+        elif workload == "ringbuf-sample":
+            rb = po.OracleMap(isa.BPF_MAP_TYPE_RINGBUF, 0, 0, 1 << 26)
+            code = programs.ringbuf_sampler(rb.fd, every_log2=6)
+            picked = int((pk[:, 0] % 64 == 0).sum())
+        else:
+            pa = po.OracleMap(isa.BPF_MAP_TYPE_PROG_ARRAY, 4, 4, 4)
+            cnt = po.OracleMap(isa.BPF_MAP_TYPE_PERCPU_ARRAY, 4, 8, 4)
+            targets = {0: programs.tail_target_write(0xA1), 1: programs.tail_target_count(cnt.fd),
+                       3: programs.tail_target_recurse(pa.fd, cnt.fd, 0)}
+            for k, c in targets.items():
+                po.prog_create(200 + k, c)
+                pa.update(struct.pack("<i", k), struct.pack("<i", 200 + k))
+            code = programs.tail_xdp_caller(pa.fd, cnt.fd)
+            ifindex = 5
+            idx = pk[:, 0] & 3
+            want = (np.array([64 + 0xA1, 2, 0xFFFFFFFF, 64 + 0xA1 + 1], dtype=np.uint64)[idx] + 1005) & 0xFFFFFFFF
+        ovm = po.OracleVM()
+        ovm.load(code)
+        res = {"ok": True}
+
+        def run():
+            s = pk.copy()
+            t0 = time.perf_counter()
+            v = ovm.run_xdp(s, fixed_len=64, ifindex=ifindex)
+            dt = time.perf_counter() - t0
+            if workload == "ringbuf-sample":
+                res["ok"] = res["ok"] and len(rb.ringbuf_fetch()) == picked   # (consumed outside the timing)
+            elif want is not None:
+                res["ok"] = res["ok"] and bool((v == want.astype(np.uint32)).all())
+            else:
+                res["ok"] = res["ok"] and bool(np.isin(v, [1, 2, 3]).all())
+            return dt, sample_n
+
+        def check():
+            return res["ok"]
+        return run, check
     raise SystemExit("unknown workload " + workload)
 
 
-SAMPLE = {"xdp-counter": 1 << 21, "flow-hash": 1 << 15, "syscall-agg": 1 << 17}
+SAMPLE = {"xdp-counter": 1 << 21, "flow-hash": 1 << 15, "syscall-agg": 1 << 17, "lpm-route": 1 << 16,
+          "ringbuf-sample": 1 << 18, "tail-call": 1 << 14}
 
 
 def _worker(a):

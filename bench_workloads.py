@@ -239,14 +239,13 @@ def lpm_route(args, dev, gen, isa, programs):
         om.update(struct.pack("<I", plen) + struct.pack(">I", net), struct.pack("<I", v))
     ovm = po.OracleVM()
     ovm.load(code)
-    t0 = time.perf_counter()
     want = ovm.run_xdp(sample.copy(), fixed_len=64)
-    cpu_s = time.perf_counter() - t0
     verd = dv.download(np.uint32)
     ok = bool((verd[:sn] == want).all()) and bool(np.isin(verd, [1, 2, 3]).all())
-    cpu = None if args.no_cpu_baseline else {
-        "value": round(sn / cpu_s / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
-        "sample": f"the oracle over the first 2^{int(np.log2(sn))} frames ({cpu_s:.2f} s)"}
+    cpu = None
+    if not args.no_cpu_baseline:   # one pinned core and 16 (bench_cpu.py), over shards of the same frames
+        from bench import cpu_baseline
+        cpu = cpu_baseline(args.cpu_seconds, "lpm-route")
     algo = 2 + 4 + 4 + 4.0   # ethertype + daddr + verdict + the route entry the lookup reads
     achieved = algo * n / kern_s / 1e9
     return {
@@ -307,12 +306,10 @@ def ringbuf_sample(args, dev, gen, isa, programs):
         om = po.OracleMap(isa.BPF_MAP_TYPE_RINGBUF, 0, 0, 1 << 24, fd=rb.fd)
         ovm = po.OracleVM()
         ovm.load(code)
-        t0 = time.perf_counter()
         ovm.run_xdp(sample.copy(), fixed_len=64)
-        cpu_s = time.perf_counter() - t0
         ok = ok and len(om.ringbuf_fetch()) == int((sample[:, 0] % 64 == 0).sum())
-        cpu = {"value": round(sn / cpu_s / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
-               "sample": f"the oracle over the first 2^{int(np.log2(sn))} frames ({cpu_s:.2f} s)"}
+        from bench import cpu_baseline   # one pinned core and 16 (bench_cpu.py)
+        cpu = cpu_baseline(args.cpu_seconds, "ringbuf-sample")
     return {
         "metric": "device-resident Mpps, ring-buffer sampling XDP prog (1/64 frames), 64B pkts",
         "value": round(n * args.steps / wall / 1e6, 3), "unit": "Mpps", "n_gpus": 1, "steps": args.steps,
@@ -380,12 +377,10 @@ def tail_call(args, dev, gen, isa, programs):
             opa.update(struct.pack("<i", k), struct.pack("<i", pfd[k]))
         ovm = po.OracleVM()
         ovm.load(code)
-        t0 = time.perf_counter()
         ov = ovm.run_xdp(frames[:sn].copy(), fixed_len=64, ifindex=5)
-        cpu_s = time.perf_counter() - t0
         ok = ok and bool((ov == verd[:sn]).all())
-        cpu = {"value": round(sn / cpu_s / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
-               "sample": f"the oracle over the first 2^{int(np.log2(sn))} frames ({cpu_s:.2f} s)"}
+        from bench import cpu_baseline   # one pinned core and 16 (bench_cpu.py)
+        cpu = cpu_baseline(args.cpu_seconds, "tail-call")
     algo = 1 + 4 + 0.5   # first byte + verdict + the writer's byte for half the frames (counters on-chip)
     achieved = algo * n / kern_s / 1e9
     return {
