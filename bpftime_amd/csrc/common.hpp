@@ -178,6 +178,10 @@ constexpr uint32_t CTX_RAW = 0;      // r1 = unit memory, r2 = length
 constexpr uint32_t CTX_XDP = 1;      // r1 = xdp_md_userspace (48 B, LDS)
 constexpr uint32_t CTX_SYSCALL = 2;  // r1 = 64-B trace_event_raw_sys_enter record
 
+// Launches of at least this many units build the flat table of an IPv4 LPM
+// trie changed since the last one (maps.cpp prepare_ix); smaller ones walk
+constexpr uint64_t kLpmFlatMinUnits = 1ull << 16;
+
 // Ring-buffer staging per block (dev_helpers.hpp RbStage)
 constexpr uint32_t kRbStageRec = 2048;                                // record bytes (a ring chunk) per block
 constexpr uint32_t kRbStageMaxRec = kRbStageRec / 8;                  // records per block (>= 8 B each)

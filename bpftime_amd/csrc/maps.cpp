@@ -701,8 +701,19 @@ static int lpm_upload(int fd) {
   if (hipDeviceSynchronize() != hipSuccess) return -1;  // no batch still reading the replica
   if (hipMemcpy((void *)m.d.data, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) return -1;
   r.lpm_stale.erase(fd);
-  // IPv4 tries also get the flat table (LpmTrie::flat) device lookups of
-  // full-length keys take in one or two loads instead of the trie walk
+  // device lookups walk the replica until a launch large enough builds the
+  // flat table (lpm_flat_build)
+  m.d.ix = 0;
+  if (m.lpm->dsz == 4) r.lpm_flat_pending.insert(fd);
+  return r.push_map(fd);
+}
+
+// IPv4 tries also get the flat table (LpmTrie::flat) device lookups of
+// full-length keys take in one or two loads instead of the trie walk
+static int lpm_flat_build(int fd) {
+  Runtime &r = rt();
+  MapRec &m = r.maps[fd];
+  r.lpm_flat_pending.erase(fd);
   uint64_t flat = 0;
   std::vector<uint32_t> t;
   if (m.lpm->dsz == 4 && !getenv("BPFTIME_AMD_NO_LPM_FLAT") && m.lpm->flat(t, 1u << 16)) {
@@ -783,13 +794,9 @@ static int ix_rebuild(int fd) {
   return r.push_map(fd);
 }
 
-int Runtime::prepare_ix(bool may_delete) {
+int Runtime::prepare_ix(bool may_delete, uint64_t units) {
   std::lock_guard<std::mutex> g(mu);
-  if (may_delete) {
-    for (int fd = 0; fd < (int)kMaxFds; fd++)
-      if (kind[fd] == HKind::MAP && maps[fd].ix_valid) ix_invalidate(fd);
-    return 0;
-  }
+  // every launch reads the current LPM tries (whatever else it does)
   while (!lpm_stale.empty()) {
     const int fd = *lpm_stale.begin();
     if (kind[fd] != HKind::MAP || !maps[fd].lpm) {
@@ -797,6 +804,22 @@ int Runtime::prepare_ix(bool may_delete) {
       continue;
     }
     if (lpm_upload(fd) < 0) return -1;
+  }
+  // the flat tables only for launches that pay for their build (a host fill
+  // of 2^24 entries and a 64-MiB upload after every change of the trie)
+  if (units >= kLpmFlatMinUnits)
+    while (!lpm_flat_pending.empty()) {
+      const int fd = *lpm_flat_pending.begin();
+      if (kind[fd] != HKind::MAP || !maps[fd].lpm) {
+        lpm_flat_pending.erase(fd);
+        continue;
+      }
+      if (lpm_flat_build(fd) < 0) return -1;
+    }
+  if (may_delete) {
+    for (int fd = 0; fd < (int)kMaxFds; fd++)
+      if (kind[fd] == HKind::MAP && maps[fd].ix_valid) ix_invalidate(fd);
+    return 0;
   }
   while (!ix_stale.empty()) {
     const int fd = *ix_stale.begin();

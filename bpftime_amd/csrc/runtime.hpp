@@ -80,9 +80,10 @@ struct Runtime {
   int push_map(int fd);         // upload DMap entry for fd
   std::set<int> ix_stale;       // hash maps whose lookup index needs a rebuild
   std::set<int> lpm_stale;      // LPM tries whose device replica needs an upload
+  std::set<int> lpm_flat_pending;  // IPv4 LPM tries whose flat table is not built (DMap.ix = 0: walk)
   // before a launch: a program that can delete invalidates every hash
   // lookup index; any other rebuilds the stale ones
-  int prepare_ix(bool may_delete);
+  int prepare_ix(bool may_delete, uint64_t units);
   std::set<int> lru_maps;                // LRU_HASH maps
   std::atomic<uint64_t> lru_seq{1};      // LRU stamp sequence: launches and host-side ops (common.hpp)
   uint32_t lru_launches = 0;             // launches since the last tombstone check

@@ -499,7 +499,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     error = "hipMemsetAsync failed";
     return -1;
   }
-  if (r.prepare_ix(prog.may_delete) < 0) {
+  if (r.prepare_ix(prog.may_delete, b->count) < 0) {
     error = "hash lookup index rebuild failed";
     return -1;
   }
