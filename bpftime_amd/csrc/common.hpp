@@ -259,7 +259,7 @@ constexpr uint32_t kTenvBytes = 48;  // gen_fast.py TENV: tail-call constants, t
 // FW_LCACHE: no deletions): kLcacheEntries {u32 tag, u32 (slot + 1) | fd << 22}
 // entries, 2-way sets, right below the tail-call constants.  A slot found for
 // a key stays that key's slot for the rest of a launch when nothing deletes.
-constexpr uint32_t kLcacheEntries = 1024;
+constexpr uint32_t kLcacheEntries = 2048;  // gen_fast.py LC_ENTRIES
 constexpr uint32_t kLcacheBytes = 8 * kLcacheEntries;
 inline size_t dyn_lds_for(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
                           bool lcache = false, bool ctx_lds = true) {

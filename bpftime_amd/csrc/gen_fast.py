@@ -112,6 +112,7 @@ PM = ["s[88:89]", "s[90:91]", "s[94:95]"]
 KP = 3
 WAYS = 8  # combining-table associativity
 TENV = 48  # launch constants below the combining table (common.hpp kTenvBytes)
+LC_ENTRIES = 2048  # hash-lookup cache entries, 2-way (common.hpp kLcacheEntries)
 
 # staged (link-resolved) packet / slot accesses
 STAGED_LD = ["LDXS1", "LDXS2", "LDXS4", "LDXS2X", "LDXS4X", "LDXS8A", "LDXS8U"]
@@ -983,7 +984,7 @@ class Gen:
                "v_cvt_u32_f64 v56, v[50:51]")
 
     # ---- the block's hash-lookup cache (common.hpp kLcacheEntries) ----
-    # 512 two-way sets of {u32 tag, u32 (slot + 1) | fd << 22} right below
+    # LC_ENTRIES / 2 two-way sets of {u32 tag, u32 (slot + 1) | fd << 22} right below
     # the launch constants (%[comb] - TENV - kLcacheBytes).  The tag is the
     # key itself for 4-byte keys (a hit needs no memory access) and the low
     # word of the h*31 hash otherwise (a hit re-reads the slot's key once,
@@ -1002,8 +1003,9 @@ class Gen:
         self.e("v_xor_b32 v41, v48, v49",
                "s_mul_i32 s69, s49, 0x9e3779b1", "v_xor_b32 v41, s69, v41",
                "s_mov_b32 s69, 0x85ebca6b", "v_mul_lo_u32 v41, v41, s69",
-               "v_lshrrev_b32 v41, 23, v41", "v_lshlrev_b32 v41, 4, v41",          # set * 16 (512 sets)
-               f"s_sub_u32 s69, %[comb], {TENV + 8 * 1024}", "v_add_u32 v82, s69, v41",
+               f"v_lshrrev_b32 v41, {32 - (LC_ENTRIES // 2).bit_length() + 1}, v41",
+               "v_lshlrev_b32 v41, 4, v41",                                     # set * 16 (LC_ENTRIES / 2 sets)
+               f"s_sub_u32 s69, %[comb], {TENV + 8 * LC_ENTRIES}", "v_add_u32 v82, s69, v41",
                f"v_mov_b32 v83, v{44 if kd == 1 else 48}",
                "ds_read_b128 v[54:57], v82", "s_waitcnt lgkmcnt(0)",
                "s_lshl_b32 s69, s49, 22")
