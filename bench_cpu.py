@@ -25,6 +25,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
+RING_LOG2 = 26   # ringbuf-sample's ring (the device line's); --ring-log2 shrinks it so tests wrap it
+
+
 def _setup(workload, shard, sample_n):
     """(oracle vm, run() -> (seconds, units), check() -> bool, units label)."""
     import numpy as np
@@ -101,7 +104,7 @@ def _setup(workload, shard, sample_n):
                 rt.update(struct.pack("<I", plen) + struct.pack(">I", net), struct.pack("<I", v))
             code = programs.lpm_route(rt.fd)
         elif workload == "ringbuf-sample":
-            rb = po.OracleMap(isa.BPF_MAP_TYPE_RINGBUF, 0, 0, 1 << 26)
+            rb = po.OracleMap(isa.BPF_MAP_TYPE_RINGBUF, 0, 0, 1 << RING_LOG2)
             code = programs.ringbuf_sampler(rb.fd, every_log2=6)
             picked = int((pk[:, 0] % 64 == 0).sum())
         else:
@@ -144,7 +147,10 @@ SAMPLE = {"xdp-counter": 1 << 21, "flow-hash": 1 << 15, "syscall-agg": 1 << 17, 
 
 
 def _worker(a):
-    workload, shard, core, budget = a
+    workload, shard, core, budget = a[:4]
+    if len(a) > 4:
+        global RING_LOG2
+        RING_LOG2 = a[4]
     if core is not None:
         try:
             os.sched_setaffinity(0, {core})
@@ -170,23 +176,26 @@ def cpu_model():
 
 
 def main():
+    global RING_LOG2
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="xdp-counter", choices=sorted(SAMPLE))
     ap.add_argument("--seconds", type=float, default=8.0, help="oracle time per leg")
     ap.add_argument("--cores", type=int, default=0, help="N-core leg width (0: the cores this process may use, "
                                                          "at most 16 -- the GPU box's CPU share per GPU)")
+    ap.add_argument("--ring-log2", type=int, default=26, help="ringbuf-sample: log2 of the ring's bytes")
     args = ap.parse_args()
+    RING_LOG2 = args.ring_log2
     cores = sorted(os.sched_getaffinity(0))
     ncore = args.cores or min(16, len(cores))
     ncore = max(1, min(ncore, len(cores)))
     unit = "Mrec/s" if args.workload == "syscall-agg" else "Mpps"
     # (i) one pinned core
-    done1, secs1, ok1 = _worker((args.workload, 0, cores[0], args.seconds))
+    done1, secs1, ok1 = _worker((args.workload, 0, cores[0], args.seconds, RING_LOG2))
     # (ii) ncore pinned processes, contiguous shards, private maps
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
     with ctx.Pool(ncore) as pool:
-        res = pool.map(_worker, [(args.workload, k, cores[k], args.seconds) for k in range(ncore)])
+        res = pool.map(_worker, [(args.workload, k, cores[k], args.seconds, RING_LOG2) for k in range(ncore)])
     wall = time.perf_counter() - t0
     done_n = sum(r[0] for r in res)
     # each worker's packet loop ran `secs` of its own steady clock; they ran

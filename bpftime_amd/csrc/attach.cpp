@@ -16,6 +16,7 @@
 #include <stdlib.h>
 
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 
@@ -36,8 +37,16 @@ struct SimpleImpl {
   int usable_id = -1;  // simple_attach_impl.hpp:114: one attach at a time
   int next_id = 1;     // base_attach_impl::allocate_id
   std::string argument;
-  bpftime_amd_attach *attach = nullptr;
+  // held by trigger() for the duration of its callback: a detach or impl
+  // destroy running beside it only drops its own reference, and the last
+  // holder destroys the attach (the reference's detach_by_id never destroys
+  // the callback at all)
+  std::shared_ptr<bpftime_amd_attach> attach;
 };
+
+std::shared_ptr<bpftime_amd_attach> hold(bpftime_amd_attach *a) {
+  return std::shared_ptr<bpftime_amd_attach>(a, bpftime_amd_attach_destroy);
+}
 
 std::mutex g_mu;
 std::map<int, SimpleImpl> g_impls;
@@ -117,23 +126,21 @@ int bpftime_amd_simple_attach(int impl, int prog_fd, int ctx_kind, const char *a
   }
   SimpleImpl &s = it->second;
   s.argument = argument ? argument : "";
-  s.attach = a;
+  s.attach = hold(a);
   s.usable_id = s.next_id++;
   return s.usable_id;
 }
 
 // simple_attach_impl::detach_by_id
 int bpftime_amd_simple_detach(int impl, int id) {
-  bpftime_amd_attach *a = nullptr;
+  std::shared_ptr<bpftime_amd_attach> a;  // released outside the lock
   {
     std::lock_guard<std::mutex> g(g_mu);
     auto it = g_impls.find(impl);
     if (it == g_impls.end() || it->second.usable_id == -1 || it->second.usable_id != id) return -1;
-    a = it->second.attach;
-    it->second.attach = nullptr;
+    a = std::move(it->second.attach);
     it->second.usable_id = -1;
   }
-  bpftime_amd_attach_destroy(a);
   return 0;
 }
 
@@ -141,7 +148,7 @@ int bpftime_amd_simple_detach(int impl, int id) {
 int bpftime_amd_simple_trigger(int impl, void *trigger_argument) {
   bpftime_amd_simple_callback cb;
   std::string arg;
-  bpftime_amd_attach *a;
+  std::shared_ptr<bpftime_amd_attach> a;
   {
     std::lock_guard<std::mutex> g(g_mu);
     auto it = g_impls.find(impl);
@@ -151,19 +158,18 @@ int bpftime_amd_simple_trigger(int impl, void *trigger_argument) {
     arg = it->second.argument;
     a = it->second.attach;
   }
-  return cb(arg.c_str(), trigger_argument, a);
+  return cb(arg.c_str(), trigger_argument, a.get());
 }
 
 int bpftime_amd_simple_attach_impl_destroy(int impl) {
-  bpftime_amd_attach *a = nullptr;
+  std::shared_ptr<bpftime_amd_attach> a;  // released outside the lock
   {
     std::lock_guard<std::mutex> g(g_mu);
     auto it = g_impls.find(impl);
     if (it == g_impls.end()) return -1;
-    a = it->second.attach;
+    a = std::move(it->second.attach);
     g_impls.erase(it);
   }
-  bpftime_amd_attach_destroy(a);
   return 0;
 }
 

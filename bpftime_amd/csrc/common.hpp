@@ -98,10 +98,12 @@ constexpr uint32_t MT_RINGBUF = 27;
 //                  at data + 256 (ringbuf_map.cpp layout and record format)
 //   PROG_ARRAY     int32 prog fd per index, -1 = empty (prog_array.cpp's
 //                  INVALID_ENTRY; host-authoritative, read-only on the device)
-//   LPM_TRIE       read-only device replica of the host trie: a 16-B header
-//                  {i32 root node, u32 nodes} then nodes of slot_size bytes
-//                  {u32 prefixlen, u32 intermediate, i32 child[2], prefix data
-//                  at key_off = 16, value at val_off}
+//   LPM_TRIE       device replica of the host trie: a 16-B header {i32 root
+//                  node, u32 nodes, u32 entries, u32 pool capacity} then nodes
+//                  of slot_size bytes {u32 prefixlen, u32 intermediate, i32
+//                  child[2], prefix data at key_off = 16, value at val_off};
+//                  read-only except in ORDERED batches of a program that
+//                  updates / deletes (dev_helpers.hpp lpm_update)
 struct DMap {
   uint32_t type;
   uint32_t key_size;
@@ -228,6 +230,7 @@ struct KParams {
   uint32_t log_words;     // u64 words per block: count, then {tag, delta} pairs
   uint64_t *lane_scratch; // a u64 per lane of the grid (PROG_ARRAY lookups hand out a copy there), or nullptr
   uint32_t dbg;           // BPFTIME_AMD_DBG experiment bits (0 in production)
+  int32_t unwind_idx;     // ebpf_set_unwind_function_index: helper whose 0 return ends the unit (-1 none)
   uint64_t lru_seq;       // this launch's LRU stamp sequence (common.hpp kLruSeqShift)
   uint32_t tail_ctx_mask;    // XDP images: ctx words / stack words a frame keeps (loader.cpp tail_save_masks)
   uint32_t tail_stack_mask;

@@ -417,8 +417,8 @@ __device__ uint64_t lru_delete(const DMap &m, uint64_t key) {
 // LPM trie lookup on the device replica: the walk of lpm_trie_map.cpp:
 // 192-264 (longest prefix match down the trie, the last non-intermediate
 // node on the path wins; an exact full-length match ends the walk).  The
-// replica is read-only during a batch (program-side updates / deletes of an
-// LPM trie are not supported on the device).
+// replica changes during a batch only in ORDERED batches of a program that
+// updates / deletes (lpm_update / lpm_remove below).
 __device__ __forceinline__ uint32_t lpm_bit(const uint8_t *d, uint32_t i) { return (d[i >> 3] >> (7 - (i & 7))) & 1; }
 
 __device__ uint64_t lpm_lookup(const DMap &m, uint64_t key) {
@@ -456,6 +456,147 @@ __device__ uint64_t lpm_lookup(const DMap &m, uint64_t key) {
   return found ? found + m.val_off : 0;
 }
 
+// Program-side LPM trie writes, ORDERED batches only (one lane runs the
+// units in order; vm_api.cpp refuses other batches of such programs):
+// lpm_trie_map.cpp:266-488 (elem_update) and :490-541 (elem_delete, a
+// logical deletion: the node becomes intermediate) restated over the
+// replica exactly as the host's LpmTrie::update / remove (maps.cpp) do over
+// its node pool -- new nodes appended at index `nodes`, the same numbering,
+// so the host takes the replica back as its trie after the batch
+// (maps.cpp lpm_pull).  Replica header {i32 root, u32 nodes, u32 entries,
+// u32 cap}; a node {u32 plen, u32 intermediate, i32 child[2], data at
+// key_off, value at val_off}.  Errors return -1 like the reference helper.
+struct LpmHdr {
+  int32_t root;
+  uint32_t nodes, entries, cap;
+};
+
+__device__ __forceinline__ uint32_t lpm_match(const DMap &m, uint64_t nb, const uint8_t *kd, uint32_t kp) {
+  const uint32_t np = *(const uint32_t *)(uintptr_t)nb;
+  const uint8_t *nd = (const uint8_t *)(uintptr_t)(nb + m.key_off);
+  const uint32_t lim = np < kp ? np : kp;
+  uint32_t ml = 0;
+  while (ml < lim && lpm_bit(nd, ml) == lpm_bit(kd, ml)) ml++;
+  return ml;
+}
+
+__device__ uint64_t lpm_update(const DMap &m, uint64_t key, uint64_t val, uint64_t flags) {
+  if (flags != 0 && flags != 1 && flags != 2) return (uint64_t)-1;  // EINVAL
+  const uint32_t dsz = m.key_size - 4, maxp = dsz * 8, vsz = m.value_size;
+  const uint32_t kp = *(const u32u *)key;
+  if (kp > maxp) return (uint64_t)-1;  // EINVAL
+  const uint8_t *kd = (const uint8_t *)(uintptr_t)(key + 4);
+  LpmHdr *h = (LpmHdr *)(uintptr_t)m.data;
+  auto at = [&](int32_t i) { return m.data + 16 + (uint64_t)i * m.slot_size; };
+  auto plen = [&](int32_t i) -> uint32_t & { return *(uint32_t *)(uintptr_t)at(i); };
+  auto inter = [&](int32_t i) -> uint32_t & { return *(uint32_t *)(uintptr_t)(at(i) + 4); };
+  auto child = [&](int32_t i, uint32_t b) -> int32_t & { return *(int32_t *)(uintptr_t)(at(i) + 8 + 4 * b); };
+  auto value = [&](int32_t i) { return at(i) + m.val_off; };
+  auto need_room = [&]() {
+    if (flags == 2) return false;                    // ENOENT
+    if (h->entries >= m.max_entries) return false;   // ENOSPC
+    return h->nodes + 2 <= h->cap;                   // the replica's node pool (maps.cpp)
+  };
+  auto make = [&](uint32_t p, bool in) -> int32_t {
+    const int32_t i = (int32_t)h->nodes++;
+    plen(i) = p;
+    inter(i) = in ? 1u : 0u;
+    child(i, 0) = child(i, 1) = -1;
+    copy_bytes(at(i) + m.key_off, (uint64_t)(uintptr_t)kd, dsz);
+    for (uint32_t j = 0; j < vsz; j++) ((uint8_t *)(uintptr_t)value(i))[j] = 0;
+    if (!in) copy_bytes(value(i), val, vsz);
+    return i;
+  };
+  if (h->root < 0) {
+    if (!need_room()) return (uint64_t)-1;
+    h->root = make(kp, false);
+    h->entries++;
+    return 0;
+  }
+  int32_t parent = -1, cur = h->root;
+  uint32_t pbit = 0, ml = 0;
+  while (cur >= 0) {
+    ml = lpm_match(m, at(cur), kd, kp);
+    const uint32_t np = plen(cur);
+    if (np != ml || np == kp || np == maxp) break;
+    parent = cur;
+    pbit = lpm_bit(kd, np);
+    cur = child(cur, pbit);
+  }
+  auto set_slot = [&](int32_t v) {
+    if (parent < 0)
+      h->root = v;
+    else
+      child(parent, pbit) = v;
+  };
+  auto split = [&](int32_t c) {  // an intermediate node at the split point
+    const int32_t nn = make(kp, false);
+    const int32_t im = make(ml, true);
+    const uint32_t b = lpm_bit(kd, ml);
+    child(im, b) = nn;
+    child(im, b ^ 1) = c;
+    set_slot(im);
+    h->entries++;
+    return (uint64_t)0;
+  };
+  if (cur >= 0 && plen(cur) == kp) {  // case 1
+    if (lpm_match(m, at(cur), kd, kp) == kp) {
+      if (flags == 1) return (uint64_t)-1;               // EEXIST
+      if (flags == 2 && inter(cur)) return (uint64_t)-1;  // ENOENT
+      if (inter(cur)) {
+        if (h->entries >= m.max_entries) return (uint64_t)-1;  // ENOSPC
+        inter(cur) = 0;
+        h->entries++;
+      }
+      copy_bytes(value(cur), val, vsz);
+      return 0;
+    }
+    if (!need_room()) return (uint64_t)-1;
+    return split(cur);
+  }
+  if (cur < 0) {  // case 2
+    if (!need_room()) return (uint64_t)-1;
+    set_slot(make(kp, false));
+    h->entries++;
+    return 0;
+  }
+  if (ml == kp) {  // case 3: the new prefix becomes cur's parent
+    if (!need_room()) return (uint64_t)-1;
+    const int32_t nn = make(kp, false);
+    child(nn, lpm_bit((const uint8_t *)(uintptr_t)(at(cur) + m.key_off), ml)) = cur;
+    set_slot(nn);
+    h->entries++;
+    return 0;
+  }
+  if (!need_room()) return (uint64_t)-1;  // case 4
+  return split(cur);
+}
+
+__device__ uint64_t lpm_remove(const DMap &m, uint64_t key) {
+  const uint32_t dsz = m.key_size - 4;
+  const uint32_t kp = *(const u32u *)key;
+  if (kp > dsz * 8) return (uint64_t)-1;  // EINVAL
+  const uint8_t *kd = (const uint8_t *)(uintptr_t)(key + 4);
+  LpmHdr *h = (LpmHdr *)(uintptr_t)m.data;
+  auto at = [&](int32_t i) { return m.data + 16 + (uint64_t)i * m.slot_size; };
+  int32_t cur = h->root, last = -1;
+  while (cur >= 0) {
+    last = cur;
+    const uint32_t np = *(const uint32_t *)(uintptr_t)at(cur);
+    if (np != lpm_match(m, at(cur), kd, kp) || np == kp) break;
+    cur = *(const int32_t *)(uintptr_t)(at(cur) + 8 + 4 * lpm_bit(kd, np));
+    last = cur;
+  }
+  if (last < 0) return (uint64_t)-1;  // ENOENT
+  const uint64_t nb = at(last);
+  uint32_t *in = (uint32_t *)(uintptr_t)(nb + 4);
+  if (*(const uint32_t *)(uintptr_t)nb != kp || lpm_match(m, nb, kd, kp) != kp || *in) return (uint64_t)-1;
+  *in = 1;
+  for (uint32_t j = 0; j < m.value_size; j++) ((uint8_t *)(uintptr_t)(nb + m.val_off))[j] = 0;
+  if (h->entries) h->entries--;
+  return 0;
+}
+
 // ---------------------------------------------------------------------------
 // Ring buffer (runtime/src/bpf_map/userspace/ringbuf_map.cpp, helpers
 // bpf_helper.cpp:451-504).  Records are [u32 len | BUSY | DISCARD][i32 fd]
@@ -487,8 +628,12 @@ constexpr uint64_t kRbSlack = kRbMaxWaves * kRbWaveMax;    // 32 MiB
 // the reference is the discarded tail, up to one chunk per block and launch
 // of ring space that a ring going from ample room to full inside one launch
 // can no longer give to records.  A wave whose records do not fit the chunk
-// reserves directly.  A host consumer reads the ring after the batch, so it
-// sees the same records in another parallel order.
+// reserves directly.  The ring's only consumer, bpftime_amd_ringbuf_fetch
+// (maps.cpp), synchronizes the device before it reads the positions, so it
+// never sees a chunk whose producer position has moved but whose records
+// the block has not published yet (the reference writes each BUSY header
+// before moving the position, under its spin lock); it sees the same
+// records in another parallel order.
 // (sizes: common.hpp kRbStage*)
 struct RbStage {
   uint8_t *buf = nullptr;  // this block's area: records, then u32 offsets (nullptr: no staging)
@@ -612,14 +757,20 @@ __device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size, con
   return d + ((pos + RB_HDR) & mask);
 }
 
-__device__ void rb_submit(const DMap *maps, uint64_t sample, bool discard, const RbStage &st) {
+// fd < 0: the ring named by the record header's fd, ptr[-1]
+// (bpf_helper.cpp:478-479, bpf_ringbuf_submit / _discard); for a record
+// whose data wrapped to the ring's first byte that word is the zeroed end of
+// the position area, fd 0, as the reference reads the zeroed end of its
+// producer page.  bpf_ringbuf_output passes the fd it reserved from
+// (bpf_helper.cpp:460-465).
+__device__ void rb_submit(const DMap *maps, uint64_t sample, bool discard, const RbStage &st, int32_t fd = -1) {
   if (st.buf && sample >= (uint64_t)(uintptr_t)st.buf + RB_HDR &&
       sample < (uint64_t)(uintptr_t)st.buf + kRbStageRec) {  // a staged record: published at block end
     uint32_t *h = (uint32_t *)(uintptr_t)(sample - RB_HDR);
     *h = (*h & ~RB_BUSY) | (discard ? RB_DISCARD : 0u);
     return;
   }
-  const int32_t fd = *(const int32_t *)(uintptr_t)(sample - 4);  // the header's fd (bpf_helper.cpp:484)
+  if (fd < 0) fd = *(const int32_t *)(uintptr_t)(sample - 4);
   if (fd < 0 || fd >= (int32_t)kMaxFds) return;
   const DMap m = maps[fd];
   if (m.type != MT_RINGBUF) return;
@@ -636,7 +787,7 @@ __device__ uint64_t rb_output(const DMap *maps, uint64_t fd, uint64_t data, uint
   const uint64_t buf = rb_reserve(maps, fd, size, st);
   if (!buf) return (uint64_t)-1;
   copy_bytes(buf, data, (uint32_t)size);
-  rb_submit(maps, buf, false, st);
+  rb_submit(maps, buf, false, st, (int32_t)fd);
   return 0;
 }
 
@@ -783,6 +934,8 @@ __device__ uint64_t helper_update(const DMap *maps, uint64_t fd, uint64_t key, u
       env.miss_fd = -1;
       return 0;
     }
+    case MT_LPM_TRIE:
+      return env.exact ? lpm_update(m, key, val, flags) : (uint64_t)-1;
     case MT_LRU_HASH: {
       // the lookup-miss race of MT_HASH above: an existing element is not
       // overwritten by the lane whose lookup of the key just missed
@@ -824,6 +977,8 @@ __device__ uint64_t helper_delete(const DMap *maps, uint64_t fd, uint64_t key, L
     }
     case MT_LRU_HASH:
       return lru_delete(m, key);
+    case MT_LPM_TRIE:
+      return env.exact ? lpm_remove(m, key) : (uint64_t)-1;
   }
   return (uint64_t)-1;
 }

@@ -989,8 +989,10 @@ class Gen:
     # key itself for 4-byte keys (a hit needs no memory access) and the low
     # word of the h*31 hash otherwise (a hit re-reads the slot's key once,
     # instead of the index entry and then the slot).  Only hash lookups the
-    # loader marked FW_LCACHE use it: nothing deletes during their launch, so
-    # a slot found for a key stays that key's slot.  v82 = the set's address,
+    # loader marked FW_LCACHE use it: nothing deletes during their launch (the
+    # program cannot, and vm_api.cpp / maps.cpp keep every other deleting
+    # launch and host delete from overlapping it), so a slot found for a key
+    # stays that key's slot.  v82 = the set's address,
     # v83 = the tag, s49 = the map fd, kept until the lookup ends.
     def lcache_on(self, skip):
         self.e("s_bitcmp1_b32 s41, 1", f"s_cbranch_scc0 {skip}",

@@ -3,26 +3,31 @@
 // Replaces, for batches of packets/records, the per-packet CPU call chain
 //   bpftime_prog::bpftime_prog_exec (runtime/src/bpftime_prog.cpp:231-260)
 //   -> ebpf_exec (vm/vm-core/src/ebpf-vm.cpp:56-60) -> ubpf_exec
-// with one wave64 lane per unit.  Design (DESIGN.md §3):
-//  * the program is pre-decoded to 16-B DInsn records fetched with scalar
-//    loads (the pc is wave-uniform) and dispatched by a scalar branch tree;
-//  * two interpreter loops: a UNIFORM loop (all live lanes at one pc: no
-//    per-lane pc, every case straight-line for the whole wave) and a
-//    DIVERGENT loop (per-lane pcs, min-pc scheduling, writes predicated by
-//    the selected lanes).  A split branch moves the wave from the first to
-//    the second; the second hands back as soon as the live lanes reconverge;
-//  * case bodies are branch-free: memory ops of lanes that must not act are
-//    redirected to a per-lane dummy LDS slot, so the compiler emits no
-//    exec-mask flow blocks per case;
-//  * helper calls leave both loops and run in the outer loop, keeping the
-//    helpers' divergent code (hash probing, copies) out of the hot loops;
-//  * r0-r10 live in LDS, lane-major (conflict-free ds_read_b64);
+// with one wave64 lane per unit.  Design (DESIGN.md §4):
+//  * tier 1, the threaded-code fast path (gen_fast.py -> fast_asm.inc): one
+//    inline-asm block whose handlers dispatch through s_setpc_b64 on 32-B
+//    FInsn records fetched with scalar loads; eBPF r0-r10 live in VGPRs
+//    (s_set_gpr_idx_on), the unit's first bytes are staged in VGPRs, split
+//    branches become lane groups scheduled by minimum pc, lookups / counter
+//    adds / tail calls / exits run in asm;
+//  * tier 2, this file's C++ interpreter (run_loop), for what the asm does
+//    not take (other helpers, div/mod, cmpxchg, accesses failing the fast
+//    checks, more lane groups than the asm holds): a UNIFORM loop (all live
+//    lanes at one pc) and a DIVERGENT loop (per-lane pcs, min-pc
+//    scheduling), with branch-free case bodies (lanes that must not act
+//    touch a per-lane dummy LDS slot).  It works on a [register][lane]
+//    copy of r0-r10 -- in LDS, or in global memory for launches whose LDS
+//    goes to a combining table / lookup cache (G) -- written when the asm
+//    exits and read when it re-enters;
+//  * helper calls leave both loops and run in the outer loop (R_CALL),
+//    keeping the helpers' divergent code out of the hot loops;
 //  * the XDP ctx (48 B) and a stack sized by the loader's analysis live in
-//    LDS; packet bytes and map values are read in place through flat
-//    addresses; global accesses are confined to the batch window and the
-//    map arena (a faulting program fails its lanes, never the GPU);
-//  * fused ldx/add/stx counters hit by a whole wave are summed across the
-//    wave into a per-wave delta cache flushed once per launch.
+//    LDS (else 512-B scratch); packet bytes and map values are read in
+//    place; global accesses are confined to the batch window and the map
+//    arena (a faulting program fails its lanes, never the GPU);
+//  * counter adds are deferred where the loader proves no later access of
+//    the unit observes them: per-wave delta caches and a per-block LDS
+//    combining table, flushed when the block ends (k_comb_merge).
 #include <hip/hip_runtime.h>
 
 #include "common.hpp"
@@ -1027,6 +1032,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         lru_ops = env.lru_ops;
         if (cerr != E_OK) {
           c.err = cerr;
+          c.alive = false;
+        }
+        // ebpf_set_unwind_function_index (ubpf unwind-on-success): the
+        // helper's 0 return ends the unit with r0 = 0, as its exit would --
+        // not inside a tail-call target, which the reference runs in a
+        // program of its own without the index
+        if (c.alive && (int32_t)c.call_id == p.unwind_idx && rv == 0 && tdep[0] == 0) {
+          if (c.verdicts) c.verdicts[c.unit] = 0;
+          if (c.rets) c.rets[c.unit] = 0;
           c.alive = false;
         }
       }

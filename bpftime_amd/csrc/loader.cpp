@@ -1070,6 +1070,38 @@ static bool rebinds(const std::vector<DInsn> &p, const PVal &b, bool may_delete)
   return false;
 }
 
+// map_update_elem / map_delete_elem calls that may change an LPM trie
+// (FastForm::lpm_writes): the call's map when the pointer kinds bind r1 to
+// an lddw map fd, else every LPM trie the program names in an lddw.
+static void lpm_write_sites(const std::vector<DInsn> &p, const std::vector<uint8_t> &lddw_src,
+                            const std::vector<std::vector<PVal>> *in, FastForm &out) {
+  std::vector<int32_t> named;
+  for (size_t i = 0; i < p.size(); i++) {
+    if (p[i].op != X_LDDW || i >= lddw_src.size() || lddw_src[i] != 1) continue;
+    const uint64_t v = (uint64_t)(uint32_t)p[i].imm | ((uint64_t)(uint32_t)p[i].hi << 32);
+    const MapRec *m = v < kMaxFds ? map_rec((int64_t)v) : nullptr;
+    if (m && m->type == MT_LPM_TRIE) named.push_back((int32_t)v);
+  }
+  auto add = [&](uint32_t h, int32_t fd) {
+    if (std::find(out.lpm_writes.begin(), out.lpm_writes.end(), std::make_pair(h, fd)) == out.lpm_writes.end())
+      out.lpm_writes.emplace_back(h, fd);
+  };
+  for (size_t i = 0; i < p.size(); i++) {
+    if (p[i].op != X_CALL || (p[i].hi != 2 && p[i].hi != 3)) continue;
+    const uint32_t h = (uint32_t)p[i].hi;
+    if (in) {
+      const PVal &r1 = (*in)[i][1];
+      if (r1.kind == P_UNDEF && (*in)[i][0].kind == P_UNDEF) continue;  // unreachable
+      if (r1.kind == P_MAPFD) {
+        const MapRec *m = map_rec(r1.id);
+        if (m && m->type == MT_LPM_TRIE) add(h, r1.id);
+        continue;
+      }
+    }
+    for (const int32_t fd : named) add(h, fd);
+  }
+}
+
 // The ctx and stack words a linked target may write (FastForm
 // tail_ctx_mask / tail_stack_mask): its stores through ctx / stack pointers
 // of known offset, and the helpers that write ctx fields or stack buffers.
@@ -1191,6 +1223,7 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
   } else {
     kinds_ok = pointer_kinds(prog, lo.lddw_src, xdp, pkt_ok, in);
   }
+  lpm_write_sites(prog, lo.lddw_src, kinds_ok ? &in : nullptr, out);
   if (!kinds_ok) {
     // ctx rewritten: generic handlers only, no pointer kinds to prove a
     // counter unobserved
@@ -1411,8 +1444,17 @@ static void link_staged(const FastForm &f, uint32_t head, uint32_t stage, bool o
                         const std::vector<DInsn> &prog, std::vector<FInsn> &out);
 
 void link_fast(const FastForm &f, uint32_t head, uint32_t stage, bool ordered, const std::vector<DInsn> &prog,
-               std::vector<FInsn> &out) {
+               std::vector<FInsn> &out, int32_t unwind_idx) {
   link_staged(f, head, stage, ordered, prog, out);
+  // an unwind helper (ebpf_set_unwind_function_index) is called from the
+  // C++ tier, which ends the unit when it returns 0: map_lookup_elem leaves
+  // its asm handlers then
+  if (unwind_idx == 1)
+    for (size_t i = 0; i < prog.size() && i < out.size(); i++)
+      if (prog[i].op == X_CALL && prog[i].hi == 1) {
+        out[i].hoff = 4 + 4 * F_SLOW;
+        out[i].w1 &= ~(uint32_t)FW_LCACHE;
+      }
   link_next(prog, out);
 }
 

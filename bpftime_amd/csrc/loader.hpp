@@ -54,6 +54,10 @@ struct FastForm {
   // LDS stack words (bit j = the j-th 8 bytes from the stack bottom) that a
   // tail-call target may write -- what a frame must save for its caller
   uint32_t tail_ctx_mask = 0x3f, tail_stack_mask = 0xffffffffu;
+  // map_update_elem (2) / map_delete_elem (3) call sites that may reach an
+  // LPM trie: {helper id, map fd}.  The device changes a trie only in ORDERED
+  // batches (dev_helpers.hpp lpm_update); vm_api.cpp refuses other batches
+  std::vector<std::pair<uint32_t, int32_t>> lpm_writes;
 };
 
 struct LoadOut {
@@ -88,8 +92,9 @@ uint32_t stage_need(const FastForm &f, uint32_t head);
 // `stage`-byte window get the staged handlers (dword index, shift, masks
 // precomputed), the rest keep their generic templates.
 // `ordered`: every counter add gets its direct (FW_NODEFER) handler.
+// `unwind_idx`: the VM's unwind helper (-1 none); its calls run in C++.
 void link_fast(const FastForm &f, uint32_t head, uint32_t stage, bool ordered, const std::vector<DInsn> &prog,
-               std::vector<FInsn> &out);
+               std::vector<FInsn> &out, int32_t unwind_idx = -1);
 
 // Runs the compat_ubpf.cpp:61-200 patching (call remap check, lddw pseudo
 // sources), ubpf-style validation, pre-decoding and the dataflow analyses

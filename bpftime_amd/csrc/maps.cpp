@@ -672,12 +672,15 @@ struct LpmTrie {
     errno = ENOENT;
     return -1;
   }
-  // device replica image (common.hpp DMap comment)
+  // device replica image (common.hpp DMap comment): header {i32 root,
+  // u32 nodes, u32 entries, u32 cap}, then the nodes in pool order
   void image(std::vector<uint8_t> &out, uint32_t slot, uint32_t key_off, uint32_t val_off) const {
     out.assign(16 + (size_t)nodes.size() * slot, 0);
-    const uint32_t nn = (uint32_t)nodes.size();
+    const uint32_t nn = (uint32_t)nodes.size(), ne = (uint32_t)entries;
     memcpy(out.data(), &root, 4);
     memcpy(out.data() + 4, &nn, 4);
+    memcpy(out.data() + 8, &ne, 4);
+    memcpy(out.data() + 12, &cap, 4);
     for (size_t i = 0; i < nodes.size(); i++) {
       uint8_t *b = out.data() + 16 + i * slot;
       const Node &n = nodes[i];
@@ -689,9 +692,97 @@ struct LpmTrie {
       memcpy(b + val_off, n.value.data(), vsz);
     }
   }
+  // the inverse of image(): the trie an ORDERED batch left in the replica
+  // (dev_helpers.hpp lpm_update / lpm_remove append nodes in pool order)
+  bool from_image(const uint8_t *img, size_t bytes, uint32_t slot, uint32_t key_off, uint32_t val_off) {
+    if (bytes < 16) return false;
+    int32_t rt_;
+    uint32_t nn, ne;
+    memcpy(&rt_, img, 4);
+    memcpy(&nn, img + 4, 4);
+    memcpy(&ne, img + 8, 4);
+    if (nn > cap || 16 + (size_t)nn * slot > bytes || rt_ >= (int32_t)nn) return false;
+    nodes.assign(nn, Node{});
+    for (uint32_t i = 0; i < nn; i++) {
+      const uint8_t *b = img + 16 + (size_t)i * slot;
+      Node &n = nodes[i];
+      uint32_t inter;
+      memcpy(&n.plen, b, 4);
+      memcpy(&inter, b + 4, 4);
+      n.inter = inter != 0;
+      memcpy(n.child, b + 8, 8);
+      n.data.assign(b + key_off, b + key_off + dsz);
+      n.value.assign(b + val_off, b + val_off + vsz);
+    }
+    root = rt_;
+    entries = ne;
+    return true;
+  }
 };
 
 static void lpm_touch(int fd) { rt().lpm_stale.insert(fd); }
+
+// A bigger node pool for the replica: logical deletions never free a node
+// (lpm_trie_map.cpp:490-541), so a trie that keeps learning new prefixes
+// outgrows any fixed pool; the reference's allocator just grows.  The
+// replica moves to a new arena block (values stay inside the arena, which
+// the device's access checks and counter tags rely on; the old block is
+// not reused) and is uploaded whole before the next launch.
+static int lpm_grow(int fd, uint64_t want_nodes) {
+  Runtime &r = rt();
+  MapRec &m = r.maps[fd];
+  if (lpm_pull(fd) < 0) return -1;
+  LpmTrie &t = *m.lpm;
+  if (want_nodes <= t.cap) return 0;
+  uint64_t cap = t.cap ? t.cap : 8;
+  while (cap < want_nodes) cap *= 2;
+  if (cap > (1ull << 26)) cap = 1ull << 26;
+  if (cap <= t.cap) {
+    errno = ENOMEM;
+    return -1;
+  }
+  const uint64_t bytes = 16 + cap * m.d.slot_size;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;  // no batch still reading the old replica
+  const uint64_t base = r.arena_alloc(bytes);
+  if (!base) {
+    errno = ENOMEM;
+    set_error("map arena exhausted growing an LPM trie (BPFTIME_AMD_ARENA_MB)");
+    return -1;
+  }
+  t.cap = (uint32_t)cap;
+  m.d.data = base;
+  m.bytes = bytes;
+  m.d.ix = 0;
+  if (r.push_map(fd) < 0) return -1;
+  lpm_touch(fd);
+  if (t.dsz == 4) r.lpm_flat_pending.insert(fd);
+  return 0;
+}
+
+int lpm_pull(int fd) {
+  Runtime &r = rt();
+  if (!r.lpm_dev_dirty.count(fd)) return 0;
+  MapRec &m = r.maps[fd];
+  r.lpm_dev_dirty.erase(fd);
+  if (r.kind[fd] != HKind::MAP || !m.lpm) return 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;  // the batch that wrote it
+  uint32_t hdr[4];
+  if (hipMemcpy(hdr, (void *)m.d.data, 16, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  const uint64_t bytes = 16 + (uint64_t)std::min(hdr[1], m.lpm->cap) * m.d.slot_size;
+  std::vector<uint8_t> img(bytes);
+  if (hipMemcpy(img.data(), (void *)m.d.data, bytes, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (!m.lpm->from_image(img.data(), bytes, m.d.slot_size, m.d.key_off, m.d.val_off)) {
+    set_error("LPM replica is corrupt");
+    return -1;
+  }
+  // the replica is current; the flat table of the old trie is not
+  if (m.d.ix) {
+    m.d.ix = 0;
+    if (r.push_map(fd) < 0) return -1;
+  }
+  if (m.lpm->dsz == 4) r.lpm_flat_pending.insert(fd);
+  return 0;
+}
 
 static int lpm_upload(int fd) {
   Runtime &r = rt();
@@ -713,6 +804,7 @@ static int lpm_upload(int fd) {
 static int lpm_flat_build(int fd) {
   Runtime &r = rt();
   MapRec &m = r.maps[fd];
+  if (lpm_pull(fd) < 0) return -1;
   r.lpm_flat_pending.erase(fd);
   uint64_t flat = 0;
   std::vector<uint32_t> t;
@@ -794,7 +886,8 @@ static int ix_rebuild(int fd) {
   return r.push_map(fd);
 }
 
-int Runtime::prepare_ix(bool may_delete, uint64_t units) {
+int Runtime::prepare_ix(bool may_delete, uint64_t units, const std::vector<int> &lpm_written,
+                        uint32_t lpm_update_sites) {
   std::lock_guard<std::mutex> g(mu);
   // every launch reads the current LPM tries (whatever else it does)
   while (!lpm_stale.empty()) {
@@ -807,15 +900,35 @@ int Runtime::prepare_ix(bool may_delete, uint64_t units) {
   }
   // the flat tables only for launches that pay for their build (a host fill
   // of 2^24 entries and a 64-MiB upload after every change of the trie)
-  if (units >= kLpmFlatMinUnits)
-    while (!lpm_flat_pending.empty()) {
-      const int fd = *lpm_flat_pending.begin();
+  // tries the program may write keep walking the replica: their flat
+  // table is dropped and rebuilt once the host has the trie back; their
+  // node pool gets room for two new nodes per update call site and unit
+  // (an insert makes at most two), up to 2^22 nodes more
+  for (const int fd : lpm_written) {
+    if (kind[fd] != HKind::MAP || !maps[fd].lpm) continue;
+    if (lpm_pull(fd) < 0) return -1;
+    const uint64_t room = std::min<uint64_t>(2 * units * std::max<uint32_t>(lpm_update_sites, 1), 1ull << 22);
+    if (maps[fd].lpm->nodes.size() + room > maps[fd].lpm->cap &&
+        lpm_grow(fd, maps[fd].lpm->nodes.size() + room) < 0)
+      return -1;
+    if (lpm_stale.count(fd) && lpm_upload(fd) < 0) return -1;
+    if (maps[fd].d.ix) {
+      maps[fd].d.ix = 0;
+      if (push_map(fd) < 0) return -1;
+    }
+    if (maps[fd].lpm->dsz == 4) lpm_flat_pending.insert(fd);
+  }
+  if (units >= kLpmFlatMinUnits) {
+    std::vector<int> pending(lpm_flat_pending.begin(), lpm_flat_pending.end());
+    for (const int fd : pending) {
       if (kind[fd] != HKind::MAP || !maps[fd].lpm) {
         lpm_flat_pending.erase(fd);
         continue;
       }
+      if (std::find(lpm_written.begin(), lpm_written.end(), fd) != lpm_written.end()) continue;
       if (lpm_flat_build(fd) < 0) return -1;
     }
+  }
   if (may_delete) {
     for (int fd = 0; fd < (int)kMaxFds; fd++)
       if (kind[fd] == HKind::MAP && maps[fd].ix_valid) ix_invalidate(fd);
@@ -971,9 +1084,9 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
     if (hipMemset((void *)base, 0xff, 2 * m.bytes) != hipSuccess) return -1;
     r.prog_gen++;
   }
-  if (m.lpm) {  // empty replica: root = -1
-    const int32_t none = -1;
-    if (hipMemcpy((void *)base, &none, 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
+  if (m.lpm) {  // empty replica: root = -1, no nodes or entries, the pool's capacity
+    const uint32_t hdr[4] = {~0u, 0, 0, m.lpm->cap};
+    if (hipMemcpy((void *)base, hdr, 16, hipMemcpyHostToDevice) != hipSuccess) return -1;
   }
   if (extra && m.type != MT_LRU_HASH && !getenv("BPFTIME_AMD_NO_HASH_INDEX")) {
     // lookup index (common.hpp ix_pos): a power of two >= 2 x buckets, so
@@ -1132,6 +1245,7 @@ const void *bpftime_map_lookup_elem(int fd, const void *key) {
         errno = EINVAL;
         return nullptr;
       }
+      if (lpm_pull(fd) < 0) return nullptr;
       const LpmTrie::Node *n = m->lpm->lookup((const uint8_t *)key);
       if (!n) return nullptr;
       buf = n->value;  // the reference also hands out a copy (lpm_trie_map.cpp:252-263)
@@ -1157,6 +1271,8 @@ long bpftime_map_update_elem(int fd, const void *key, const void *value, uint64_
       errno = EINVAL;
       return -1;
     }
+    if (lpm_pull(fd) < 0) return -1;
+    if (m->lpm->nodes.size() + 2 > m->lpm->cap && lpm_grow(fd, m->lpm->nodes.size() + 2) < 0) return -1;
     const long rc = m->lpm->update((const uint8_t *)key, value, flags);
     if (rc == 0) lpm_touch(fd);
     return rc;
@@ -1260,6 +1376,7 @@ long bpftime_map_delete_elem(int fd, const void *key) {
       errno = EINVAL;
       return -1;
     }
+    if (lpm_pull(fd) < 0) return -1;
     const long rc = m->lpm->remove((const uint8_t *)key);
     if (rc == 0) lpm_touch(fd);
     return rc;
@@ -1271,6 +1388,12 @@ long bpftime_map_delete_elem(int fd, const void *key) {
       return -1;
     case MT_HASH:
     case MT_PERCPU_HASH: {
+      // no launch that trusts its lookup cache may still run (runtime.hpp)
+      if (rt().lcache_inflight.load()) {
+        if (hipDeviceSynchronize() != hipSuccess) return -1;
+        rt().lcache_inflight = false;
+        rt().deleter_inflight = false;
+      }
       std::vector<uint8_t> slot;
       int64_t idx = host_hash_find(*m, key, slot, nullptr);
       if (idx < 0) {
@@ -1303,6 +1426,7 @@ int bpftime_map_get_next_key(int fd, const void *key, void *next_key) {
       errno = next_key ? ENOENT : EINVAL;
       return -1;
     }
+    if (lpm_pull(fd) < 0) return -1;
     return m->lpm->first_key((uint8_t *)next_key);
   }
   if (m->type == MT_PROG_ARRAY) return prog_array_next_key(*m, key, next_key);
@@ -1374,6 +1498,7 @@ void bpftime_close(int fd) {
     if (r.kind[fd] == HKind::MAP) {
       drop_host_view(r, fd);
       r.lru_maps.erase(fd);
+      r.lpm_dev_dirty.erase(fd);
       r.maps[fd] = MapRec();
       r.push_map(fd);
     } else if (r.kind[fd] == HKind::PROG) {
@@ -1399,6 +1524,7 @@ void bpftime_amd_reset(void) {
     r.kind[i] = HKind::NONE;
     r.maps[i] = MapRec();
     r.lru_maps.erase((int)i);
+    r.lpm_dev_dirty.erase((int)i);
     r.progs[i] = ProgRec();
     r.links[i] = LinkRec();
     r.perfs[i] = PerfRec();
@@ -1526,7 +1652,7 @@ int64_t bpftime_amd_ringbuf_fetch(int fd, void *out, uint64_t cap, uint64_t *use
 
 uint64_t bpftime_amd_map_count(int fd) {
   MapRec *m = map_of(fd);
-  if (m && m->lpm) return m->lpm->entries;
+  if (m && m->lpm) return lpm_pull(fd) < 0 ? 0 : m->lpm->entries;
   if (!m || !m->d.count_addr) return 0;
   return read_count(*m);
 }
@@ -1650,17 +1776,28 @@ void *bpftime_get_array_map_raw_data(int fd) {
   return p;
 }
 
-// host writes -> device: the bytes that differ from the last exchange
+// host writes -> device: exactly the bytes that differ from the last
+// exchange, run by run.  A byte the host did not write is never uploaded,
+// so a counter a batch advanced since the last exchange survives a host
+// write next to it; batches still running on any stream finish first (they
+// may be writing the same map).
 static int view_push(MapRec &m) {
-  uint64_t lo = m.bytes, hi = 0;
-  for (uint64_t i = 0; i < m.bytes; i++)
-    if (m.host_view[i] != m.host_shadow[i]) {
-      lo = std::min(lo, i);
-      hi = i + 1;
+  bool synced = false;
+  for (uint64_t i = 0; i < m.bytes;) {
+    if (m.host_view[i] == m.host_shadow[i]) {
+      i++;
+      continue;
     }
-  if (lo >= hi) return 0;
-  if (hipMemcpy((void *)(m.d.data + lo), m.host_view + lo, hi - lo, hipMemcpyHostToDevice) != hipSuccess) return -1;
-  memcpy(m.host_shadow.data() + lo, m.host_view + lo, hi - lo);
+    uint64_t j = i + 1;
+    while (j < m.bytes && m.host_view[j] != m.host_shadow[j]) j++;
+    if (!synced) {
+      if (hipDeviceSynchronize() != hipSuccess) return -1;
+      synced = true;
+    }
+    if (hipMemcpy((void *)(m.d.data + i), m.host_view + i, j - i, hipMemcpyHostToDevice) != hipSuccess) return -1;
+    memcpy(m.host_shadow.data() + i, m.host_view + i, j - i);
+    i = j;
+  }
   return 0;
 }
 

@@ -81,9 +81,22 @@ struct Runtime {
   std::set<int> ix_stale;       // hash maps whose lookup index needs a rebuild
   std::set<int> lpm_stale;      // LPM tries whose device replica needs an upload
   std::set<int> lpm_flat_pending;  // IPv4 LPM tries whose flat table is not built (DMap.ix = 0: walk)
+  // LPM tries an ORDERED batch of a program that writes them may have
+  // changed on the device: the replica is authoritative until the host pulls
+  // it back (maps.cpp lpm_pull) before its next operation on the trie
+  std::set<int> lpm_dev_dirty;
   // before a launch: a program that can delete invalidates every hash
-  // lookup index; any other rebuilds the stale ones
-  int prepare_ix(bool may_delete, uint64_t units);
+  // lookup index; any other rebuilds the stale ones.  `lpm_written`: the LPM
+  // tries the launch's program may update / delete (ORDERED batches only):
+  // their lookups walk the replica (no flat table) while they change
+  int prepare_ix(bool may_delete, uint64_t units, const std::vector<int> &lpm_written = {},
+                 uint32_t lpm_update_sites = 0);
+  // launches that may still run: one whose hash lookups use the block LDS
+  // lookup cache (a found slot is trusted for the rest of the launch), one of
+  // a program that can delete.  A cached launch never overlaps a deletion
+  // (a program's, on any stream, or the host's): whichever comes second
+  // waits for the device first (vm_api.cpp exec_batch, maps.cpp host delete)
+  std::atomic<bool> lcache_inflight{false}, deleter_inflight{false};
   std::set<int> lru_maps;                // LRU_HASH maps
   std::atomic<uint64_t> lru_seq{1};      // LRU stamp sequence: launches and host-side ops (common.hpp)
   uint32_t lru_launches = 0;             // launches since the last tombstone check
@@ -95,6 +108,9 @@ struct Runtime {
 
 // hash lookup index upkeep for host-side writes (maps.cpp)
 void ix_invalidate(int fd);
+// the device replica of an LPM trie an ORDERED batch wrote, back into the
+// host trie (no-op unless the trie is in lpm_dev_dirty)
+int lpm_pull(int fd);
 
 Runtime &rt();
 void set_error(const std::string &e);

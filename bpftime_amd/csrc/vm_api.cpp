@@ -60,14 +60,15 @@ struct Image {
     if (d_tail_entry) hipFree(d_tail_entry);
     for (auto &kv : links) hipFree(kv.second);
   }
-  const FInsn *linked(bool xdp, uint32_t head, uint32_t stage, bool ordered) {
+  const FInsn *linked(bool xdp, uint32_t head, uint32_t stage, bool ordered, int32_t unwind_idx) {
     std::lock_guard<std::mutex> g(link_mu);
-    const uint64_t key =
-        ((uint64_t)xdp << 63) | ((uint64_t)ordered << 62) | ((uint64_t)stage << 40) | (stage ? head : 0);
+    const bool uw = unwind_idx == 1;  // the only helper with asm handlers an unwind index changes
+    const uint64_t key = ((uint64_t)xdp << 63) | ((uint64_t)ordered << 62) | ((uint64_t)uw << 61) |
+                         ((uint64_t)stage << 40) | (stage ? head : 0);
     auto it = links.find(key);
     if (it != links.end()) return it->second;
     std::vector<FInsn> out;
-    link_fast(xdp ? fx : fr, head, stage, ordered, prog.prog, out);
+    link_fast(xdp ? fx : fr, head, stage, ordered, prog.prog, out, uw ? 1 : -1);
     FInsn *d = nullptr;
     const size_t bytes = out.size() * sizeof(FInsn);
     if (hipMalloc((void **)&d, bytes) != hipSuccess) return nullptr;
@@ -401,6 +402,15 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     return -1;
   }
   Image &im = *imp;
+  // the unwind helper as the device knows helpers (bpftime ids): the
+  // registration that was given ubpf id unwind_idx
+  int32_t unwind_helper = -1;
+  for (const auto &kv : helper_id_map)
+    if ((int)kv.second == unwind_idx) unwind_helper = (int32_t)kv.first;
+  if (unwind_helper == (int)kTailHelper && im.d_tail_entry) {
+    error = "an unwind index on bpf_tail_call is not supported on the device";
+    return -1;
+  }
   const LoadOut &prog = im.prog;
   KParams p{};
   p.prog = im.d_prog;
@@ -415,7 +425,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     const bool aligned = ((uint64_t)(uintptr_t)b->data % 16) == 0 &&
                          (b->descs ? true : (b->stride % 16) == 0 && b->stride >= need);
     p.stage = (need && aligned && !getenv("BPFTIME_AMD_NO_STAGING")) ? need : 0;
-    p.fast = im.linked(xdp, head, p.stage, (b->flags & EBPF_BATCH_ORDERED) != 0);
+    p.fast = im.linked(xdp, head, p.stage, (b->flags & EBPF_BATCH_ORDERED) != 0, unwind_helper);
     if (!p.fast) {
       error = "device upload failed";
       return -1;
@@ -490,6 +500,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     p.comb_entries = e;
   }
   p.ncpu = r.ncpu;
+  p.unwind_idx = unwind_helper;
   p.ifindex = b->ingress_ifindex;
   p.rxq = b->rx_queue_index;
   p.head = b->head;
@@ -499,7 +510,32 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     error = "hipMemsetAsync failed";
     return -1;
   }
-  if (r.prepare_ix(prog.may_delete, b->count) < 0) {
+  // program-side LPM trie updates / deletes: the device changes a trie only
+  // in ORDERED batches (one lane, the reference's order: dev_helpers.hpp
+  // lpm_update), the host takes the replica back afterwards (lpm_pull)
+  std::vector<int> lpm_w;
+  uint32_t lpm_updates = 0;
+  for (const auto &w : (b->ctx_kind == CTX_XDP ? im.fx : im.fr).lpm_writes) {
+    lpm_updates += w.first == 2;
+    if (!(b->flags & EBPF_BATCH_ORDERED)) {
+      error = std::string(w.first == 2 ? "bpf_map_update_elem" : "bpf_map_delete_elem") +
+              " on LPM_TRIE map fd " + std::to_string(w.second) +
+              ": program-side LPM trie writes run only in EBPF_BATCH_ORDERED batches";
+      return -1;
+    }
+    if (std::find(lpm_w.begin(), lpm_w.end(), w.second) == lpm_w.end()) lpm_w.push_back(w.second);
+  }
+  // the lookup cache trusts a found slot for the whole launch: no deletion
+  // may run beside it (Runtime::lcache_inflight)
+  if ((p.lcache && r.deleter_inflight.load()) || (prog.may_delete && r.lcache_inflight.load())) {
+    if (hipDeviceSynchronize() != hipSuccess) {
+      error = "device synchronize failed";
+      return -1;
+    }
+    r.lcache_inflight = false;
+    r.deleter_inflight = false;
+  }
+  if (r.prepare_ix(prog.may_delete, b->count, lpm_w, lpm_updates) < 0) {
     error = "hash lookup index rebuild failed";
     return -1;
   }
@@ -607,6 +643,12 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   if (e != hipSuccess) {
     error = std::string("kernel launch failed: ") + hipGetErrorString(e);
     return -1;
+  }
+  if (p.lcache) r.lcache_inflight = true;
+  if (prog.may_delete) r.deleter_inflight = true;
+  if (!lpm_w.empty()) {
+    std::lock_guard<std::mutex> g(r.mu);
+    for (const int fd : lpm_w) r.lpm_dev_dirty.insert(fd);
   }
   if (b->flags & EBPF_BATCH_SYNC) {
     uint32_t failed = 0;
@@ -762,9 +804,13 @@ ebpf_jit_fn ebpf_compile(struct ebpf_vm *vm, char **errmsg) {
   return nullptr;
 }
 
+// compat_ubpf.cpp:239-241 -> ubpf_set_unwind_function_index: a call of
+// helper idx that returns 0 ends the program with r0 = 0 (interp.hip R_CALL)
+// (idx is a ubpf helper id, the id register_external_function gave it)
 int ebpf_set_unwind_function_index(struct ebpf_vm *vm, unsigned int idx) {
+  if (idx >= 64) return -1;  // ubpf's MAX_EXT_FUNCS
   vm->impl->unwind_idx = (int)idx;
-  return -1;  // tail-call unwinding is not implemented on the device
+  return 0;
 }
 
 int ebpf_set_pointer_secret(struct ebpf_vm *vm, uint64_t secret) {

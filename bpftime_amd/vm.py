@@ -209,6 +209,11 @@ class VM:
     def register(self, index: int, name: str) -> int:
         return lib().ebpf_register(C.c_void_p(self.h), index, name.encode(), None)
 
+    def set_unwind(self, idx: int) -> int:
+        """ebpf_set_unwind_function_index (idx = the ubpf id a helper was
+        registered under: the order of registration, from 1)."""
+        return lib().ebpf_set_unwind_function_index(C.c_void_p(self.h), idx)
+
     def load(self, code: bytes) -> None:
         err = C.c_void_p()
         buf = C.create_string_buffer(code, len(code))

@@ -138,7 +138,11 @@ int orc_vm_register_xdp_load_bytes(struct orc_vm *vm)
 	return orc_vm_register(vm, 189, "bpf_xdp_load_bytes", h_xdp_load_bytes);
 }
 
-/* bpf_helper.cpp:451-504 (map "pointer" = fd; flags other than 0 only warn) */
+/* bpf_helper.cpp:451-504 (map "pointer" = fd; flags other than 0 only warn).
+ * bpf_ringbuf_output submits to the fd it reserved from (:460-465);
+ * bpf_ringbuf_submit / _discard read the fd from the record header, ptr[-1]
+ * (:478-479), which for a record whose data wrapped to the ring's first byte
+ * is the zeroed word in front of the data (fd 0). */
 static uint64_t h_rb_output(uint64_t rb, uint64_t data, uint64_t size, uint64_t flags, uint64_t c)
 {
 	(void)flags, (void)c;
@@ -146,7 +150,7 @@ static uint64_t h_rb_output(uint64_t rb, uint64_t data, uint64_t size, uint64_t 
 	if (!buf)
 		return (uint64_t)-1;
 	memcpy(buf, (const void *)(uintptr_t)data, size);
-	orc_ringbuf_submit(buf, 0);
+	orc_ringbuf_submit_fd((int)rb, buf, 0);
 	return 0;
 }
 
@@ -159,14 +163,14 @@ static uint64_t h_rb_reserve(uint64_t rb, uint64_t size, uint64_t flags, uint64_
 static uint64_t h_rb_submit(uint64_t data, uint64_t flags, uint64_t a, uint64_t b, uint64_t c)
 {
 	(void)flags, (void)a, (void)b, (void)c;
-	orc_ringbuf_submit((const void *)(uintptr_t)data, 0);
+	orc_ringbuf_submit_fd(((const int32_t *)(uintptr_t)data)[-1], (const void *)(uintptr_t)data, 0);
 	return 0;
 }
 
 static uint64_t h_rb_discard(uint64_t data, uint64_t flags, uint64_t a, uint64_t b, uint64_t c)
 {
 	(void)flags, (void)a, (void)b, (void)c;
-	orc_ringbuf_submit((const void *)(uintptr_t)data, 1);
+	orc_ringbuf_submit_fd(((const int32_t *)(uintptr_t)data)[-1], (const void *)(uintptr_t)data, 1);
 	return 0;
 }
 

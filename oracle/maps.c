@@ -33,6 +33,12 @@ struct orc_map {
 	/* PERCPU_HASH: keys[i], vals[i] (ncpu*vsize), insertion ordered */
 	uint8_t *pkeys, *pvals;
 	uint64_t pcount, pcap;
+	/* key -> position + 1, open addressing; a lookup aid only (positions
+	 * keep the insertion order the maps' iteration follows), rebuilt after
+	 * an erase shifts the positions */
+	uint32_t *pix;
+	uint64_t pix_cap;
+	int pix_valid;
 	/* LPM_TRIE: node pool (lpm_trie_map.cpp keeps heap nodes; same tree) */
 	struct lpm_node *nodes;
 	int64_t nnodes, ncap, root;
@@ -46,6 +52,7 @@ struct orc_map {
 	/* RINGBUF (ringbuf_map.cpp): consumer / producer positions, 2 x max_ent data */
 	uint64_t rb_cons, rb_prod;
 };
+#define RB_PREFIX 8 /* zero bytes allocated in front of a ring's data */
 
 struct lpm_node {
 	uint32_t prefixlen;
@@ -91,8 +98,9 @@ static void free_map(struct orc_map *m)
 {
 	if (m->type == T_LPM_TRIE)
 		free_lpm(m);
-	free(m->data);
+	free(m->type == T_RINGBUF && m->data ? m->data - RB_PREFIX : m->data);
 	free(m->pkeys);
+	free(m->pix);
 	free(m->pvals);
 	free(m->lkeys);
 	free(m->lvals);
@@ -201,7 +209,12 @@ int orc_map_create(int fd, uint32_t type, uint32_t ksize, uint32_t vsize, uint32
 			g_errno = EINVAL;
 			return -1;
 		}
-		m->data = calloc((size_t)max_entries * 2, 1);
+		/* behind data: the zeroed tail of the reference's producer page
+		 * (raw_buffer[2 * page - RB_PREFIX ..]), which bpf_ringbuf_submit's
+		 * ptr[-1] reads as the fd of a record whose data wrapped to data[0] */
+		m->data = calloc((size_t)max_entries * 2 + RB_PREFIX, 1);
+		if (m->data)
+			m->data += RB_PREFIX;
 		break;
 	case T_LPM_TRIE: /* lpm_trie_map.cpp:43-81: key = u32 prefixlen + 1..256 data bytes */
 		if (ksize < 5 || ksize > 260 || vsize == 0 || max_entries == 0) {
@@ -289,11 +302,43 @@ static int hash_delete(struct orc_map *m, const void *key)
 }
 
 /* ---- per-cpu hash (per_cpu_hash_map.cpp) ---- */
+static uint64_t pix_hash(const void *key, uint32_t n) /* FNV-1a */
+{
+	uint64_t h = 1469598103934665603ull;
+	for (uint32_t i = 0; i < n; i++)
+		h = (h ^ ((const uint8_t *)key)[i]) * 1099511628211ull;
+	return h ^ (h >> 29);
+}
+
+static void pix_put(struct orc_map *m, uint64_t i)
+{
+	uint64_t p = pix_hash(m->pkeys + i * m->ksize, m->ksize) & (m->pix_cap - 1);
+	while (m->pix[p])
+		p = (p + 1) & (m->pix_cap - 1);
+	m->pix[p] = (uint32_t)i + 1;
+}
+
+static void pix_rebuild(struct orc_map *m)
+{
+	uint64_t cap = 64;
+	while (cap < 4 * (m->pcount + 1))
+		cap *= 2;
+	free(m->pix);
+	m->pix = calloc(cap, 4);
+	m->pix_cap = cap;
+	for (uint64_t i = 0; i < m->pcount; i++)
+		pix_put(m, i);
+	m->pix_valid = 1;
+}
+
 static int64_t phash_find(struct orc_map *m, const void *key)
 {
-	for (uint64_t i = 0; i < m->pcount; i++)
-		if (memcmp(m->pkeys + i * m->ksize, key, m->ksize) == 0)
-			return (int64_t)i;
+	if (!m->pix_valid || m->pix_cap < 2 * (m->pcount + 1))
+		pix_rebuild(m);
+	uint64_t p = pix_hash(key, m->ksize) & (m->pix_cap - 1);
+	for (; m->pix[p]; p = (p + 1) & (m->pix_cap - 1))
+		if (memcmp(m->pkeys + (uint64_t)(m->pix[p] - 1) * m->ksize, key, m->ksize) == 0)
+			return (int64_t)m->pix[p] - 1;
 	return -1;
 }
 
@@ -307,6 +352,10 @@ static uint64_t phash_insert(struct orc_map *m, const void *key)
 	uint64_t i = m->pcount++;
 	memcpy(m->pkeys + i * m->ksize, key, m->ksize);
 	memset(m->pvals + i * (size_t)m->ncpu * m->vsize, 0, (size_t)m->ncpu * m->vsize);
+	if (m->pix_valid && m->pix_cap >= 2 * (m->pcount + 1))
+		pix_put(m, i);
+	else
+		m->pix_valid = 0;
 	return i;
 }
 
@@ -316,6 +365,7 @@ static void phash_erase(struct orc_map *m, uint64_t i)
 	memmove(m->pkeys + i * m->ksize, m->pkeys + (i + 1) * m->ksize, (m->pcount - i - 1) * m->ksize);
 	memmove(m->pvals + i * vs, m->pvals + (i + 1) * vs, (m->pcount - i - 1) * vs);
 	m->pcount--;
+	m->pix_valid = 0;
 }
 
 /* ---- LRU hash (runtime/src/bpf_map/userspace/lru_var_hash_map.cpp) ----
@@ -447,9 +497,10 @@ void *orc_ringbuf_reserve(int fd, uint64_t size) /* ringbuf::reserve */
 	return ptr;
 }
 
-void orc_ringbuf_submit(const void *sample, int discard) /* ringbuf::submit (fd from the header) */
+/* bpftime_ringbuf_submit(fd, sample, discard) (bpftime_shm.cpp:401-411) ->
+ * ringbuf::submit (ringbuf_map.cpp:297-309) */
+void orc_ringbuf_submit_fd(int fd, const void *sample, int discard)
 {
-	int fd = ((const int32_t *)sample)[-1];
 	struct orc_map *m = get(fd);
 	if (!m || m->type != T_RINGBUF)
 		return;

@@ -61,7 +61,7 @@ void orc_maps_reset(void);
 /* ring buffer (ringbuf_map.cpp): reserve / submit as the helpers use them,
  * fetch = the consumer (ringbuf::fetch_data) */
 void *orc_ringbuf_reserve(int fd, uint64_t size);
-void orc_ringbuf_submit(const void *sample, int discard);
+void orc_ringbuf_submit_fd(int fd, const void *sample, int discard);
 int64_t orc_ringbuf_fetch(int fd, uint8_t *out, uint64_t cap, uint64_t *used);
 int orc_map_create(int fd, uint32_t type, uint32_t key_size, uint32_t value_size,
                    uint32_t max_entries, uint32_t flags);

@@ -103,6 +103,10 @@ class OracleVM:
         rc = lib().orc_vm_exec(self.h, buf, len(mem), C.byref(r))
         return rc, r.value
 
+    def set_unwind(self, idx: int) -> None:
+        """ubpf_set_unwind_function_index (idx = ubpf helper id)."""
+        lib().orc_vm_set_unwind_index(self.h, idx)
+
     def register_xdp_load_bytes(self) -> None:
         """bpf_xdp_load_bytes (id 189), defined but not in a default group."""
         lib().orc_vm_register_xdp_load_bytes(self.h)

@@ -89,3 +89,132 @@ def test_lpm_routing_program(fresh_oracle, fresh_runtime):
     assert vm.exec_batch(dev.CTX_XDP, d, n, 64, fixed_len=64, verdicts=dv) == 0
     np.testing.assert_array_equal(dv.download(np.uint32), want2)
     assert not np.array_equal(want, want2)
+
+
+def learn_prog(fd):
+    """Route learning over 16-B raw units {u32 op, u32 prefixlen, 4 address
+    bytes (network order), u32 value}: op & 0xff = 0 lookup (r0 = the value,
+    0xffff on a miss), 1 map_update_elem with flags op >> 8 (r0 = 1000 +
+    result), 2 map_delete_elem (r0 = 2000 + result)."""
+    a = Asm().mov64(6, "r1").ldx(4, 7, 6, 0)
+    a.ldx(4, 2, 6, 4).stx(4, 10, -8, "r2").ldx(4, 2, 6, 8).stx(4, 10, -4, "r2")
+    a.ldx(4, 2, 6, 12).stx(4, 10, -16, "r2")
+    a.mov64(8, "r7").alu64("and", 8, 0xff)
+    a.jmp("jeq", 8, 1, "upd").jmp("jeq", 8, 2, "del")
+    a.ld_map_fd(1, fd).mov64(2, "r10").add64(2, -8).call(1)
+    a.jmp("jeq", 0, 0, "miss").ldx(4, 0, 0, 0).exit()
+    a.label("miss").mov64(0, 0xffff).exit()
+    a.label("upd").ld_map_fd(1, fd).mov64(2, "r10").add64(2, -8).mov64(3, "r10").add64(3, -16)
+    a.mov64(4, "r7").alu64("rsh", 4, 8).call(2).add64(0, 1000).exit()
+    a.label("del").ld_map_fd(1, fd).mov64(2, "r10").add64(2, -8).call(3).add64(0, 2000).exit()
+    return a.assemble()
+
+
+def learn_units(rng, n, nets=400):
+    """A stream of lookups, updates (flags ANY / NOEXIST / EXIST, some
+    invalid) and deletes over a small pool of prefixes, so keys repeat, get
+    deleted and come back, and the trie splits, grows parents and fills."""
+    pool = []
+    for _ in range(nets):
+        plen = int(rng.choice([0, 1, 7, 8, 12, 16, 20, 23, 24, 28, 31, 32]))
+        net = int(rng.integers(0, 1 << 32)) & ((0xFFFFFFFF << (32 - plen)) & 0xFFFFFFFF)
+        pool.append((plen, net))
+    u = np.zeros((n, 16), np.uint8)
+    w = u.view(np.uint32)
+    pick = rng.integers(0, nets, n)
+    op = rng.choice([0, 0, 0, 1, 1, 2], n)
+    flags = rng.choice([0, 1, 2, 0, 4], n)                        # 4: EINVAL
+    w[:, 0] = op | np.where(op == 1, flags, 0) << 8
+    w[:, 1] = [pool[i][0] for i in pick]
+    addr = np.array([pool[i][1] for i in pick], np.uint64)
+    noise = rng.integers(0, 1 << 32, n, dtype=np.uint64)
+    look = op == 0
+    addr = np.where(look & (rng.random(n) < 0.7), addr | (noise & np.uint64(0xFF)), addr)
+    w[:, 1] = np.where(look, 32, w[:, 1])
+    w[:, 1] = np.where(rng.random(n) < 0.01, 33, w[:, 1])          # prefixlen > 32: EINVAL
+    u[:, 8:12] = addr.astype(np.uint32).astype(">u4").view(np.uint8).reshape(n, 4)
+    w[:, 3] = rng.integers(1, 1 << 31, n)
+    return u
+
+
+@pytest.mark.parametrize("mx", [64, 4096])
+def test_lpm_program_writes_ordered(fresh_oracle, fresh_runtime, mx):
+    """Program-side map_update_elem / map_delete_elem on an LPM trie
+    (lpm_trie_map.cpp:266-541) in ORDERED batches, bit-exact against the
+    oracle: every unit's r0 (lookups see the writes of the units before
+    them; EEXIST / ENOENT / ENOSPC (mx 64 fills) / EINVAL), then the host's
+    view of the trie (lookups of every prefix, count, first key), a host
+    write after the batch and a parallel routing launch over the result."""
+    po, dev = fresh_oracle, fresh_runtime
+    rng = np.random.default_rng(11)
+    (om,), (dm,) = make_maps([(LPM, 8, 4, mx)], po, dev)
+    for plen, net in ((8, 0x0A000000), (16, 0x0A010000)):
+        key = struct.pack("<I", plen) + struct.pack(">I", net)
+        for m in (om, dm):
+            m.update(key, struct.pack("<I", 7))
+    code = learn_prog(dm.fd)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    vm = dev.VM()
+    vm.load(code)
+    seen = set()
+    for rnd in range(3):
+        n = 3000
+        units = learn_units(rng, n)
+        want = ovm.run_raw(units.copy(), 16)
+        d = dev.DeviceBuffer.from_array(units)
+        dr = dev.DeviceBuffer(8 * n)
+        assert vm.exec_batch(dev.CTX_RAW, d, n, 16, fixed_len=16, rets=dr,
+                             flags=dev.BATCH_SYNC | dev.BATCH_ORDERED) == 0
+        got = dr.download(np.uint64)
+        np.testing.assert_array_equal(got, want)
+        seen |= set(got.tolist())
+        assert dm.count() == om.count()
+        for row in units[::7]:
+            for plen in (32, int(row[4])):
+                key = struct.pack("<I", min(plen, 32)) + bytes(row[8:12])
+                assert dm.lookup(key) == om.lookup(key), (rnd, key)
+        assert dm.next_key(None) == om.next_key(None)
+    assert {999, 1000, 1999, 0xffff} <= seen and len(seen) > 50
+    # a host write on the trie the batch left, then a parallel launch of a
+    # reading program (flat table rebuilt from the pulled trie at 2^16 units)
+    for m in (om, dm):
+        m.update(k4(0, "0.0.0.0"), struct.pack("<I", 1))
+    n = 1 << 16
+    pk = gen.xdp_packets(n, seed=12)
+    pk[:, 12:14] = [0x08, 0x00]
+    pk[: n // 2, 30:34] = units[rng.integers(0, len(units), n // 2), 8:12]
+    rcode = route_prog(dm.fd)
+    ovm2 = po.OracleVM()
+    ovm2.load(rcode)
+    want = ovm2.run_xdp(pk.copy(), fixed_len=64)
+    vm2 = dev.VM()
+    vm2.load(rcode)
+    d = dev.DeviceBuffer.from_array(pk)
+    dv = dev.DeviceBuffer(4 * n)
+    assert vm2.exec_batch(dev.CTX_XDP, d, n, 64, fixed_len=64, verdicts=dv) == 0
+    np.testing.assert_array_equal(dv.download(np.uint32), want)
+
+
+def test_lpm_program_writes_refused_in_parallel(fresh_runtime):
+    """A parallel batch of a program that may write an LPM trie is refused
+    with an error naming the helper and the map; ORDERED batches run it,
+    and programs that only read the trie run in parallel."""
+    dev = fresh_runtime
+    dm = dev.Map(LPM, 8, 4, 64)
+    vm = dev.VM()
+    vm.load(learn_prog(dm.fd))
+    units = np.zeros((64, 16), np.uint8)
+    d = dev.DeviceBuffer.from_array(units)
+    with pytest.raises(dev.EbpfError, match=r"bpf_map_(update|delete)_elem on LPM_TRIE map fd %d" % dm.fd):
+        vm.exec_batch(dev.CTX_RAW, d, 64, 16, fixed_len=16)
+    assert vm.exec_batch(dev.CTX_RAW, d, 64, 16, fixed_len=16, flags=dev.BATCH_SYNC | dev.BATCH_ORDERED) == 0
+    # a program that updates another map and only looks the trie up
+    (hm,) = [dev.Map(isa.BPF_MAP_TYPE_HASH, 4, 4, 16)]
+    a = Asm().st(4, 10, -8, 32).st(4, 10, -4, 0)
+    a.ld_map_fd(1, dm.fd).mov64(2, "r10").add64(2, -8).call(1)
+    a.st(4, 10, -12, 1).ld_map_fd(1, hm.fd).mov64(2, "r10").add64(2, -4).mov64(3, "r10").add64(3, -12)
+    a.mov64(4, 0).call(2).exit()
+    vm2 = dev.VM()
+    vm2.load(a.assemble())
+    assert vm2.exec_batch(dev.CTX_RAW, d, 64, 16, fixed_len=16) == 0

@@ -314,3 +314,47 @@ def test_flow_hash_full_table(fresh_oracle, fresh_runtime, monkeypatch, index):
     assert _duplicate_keys(dm) == 0
     assert dm.hash_items() == om.items()
     assert dm.count() == len(om.items())
+
+
+def test_lookup_cache_against_concurrent_deleter(fresh_runtime):
+    """A launch whose hash lookups use the block's LDS lookup cache trusts a
+    found slot for the rest of the launch.  A deleting program launched on
+    another stream, or a host delete, therefore waits for it (and a cached
+    launch waits for a deleter): the results are those of the serial order
+    of the calls.  Reader: r0 = the value or 0xdead; deleter:
+    deletes the unit's key; 4-byte keys (the cache holds them as tags)."""
+    dev = fresh_runtime
+    L = dev.lib()
+    m = dev.Map(isa.BPF_MAP_TYPE_HASH, 4, 8, 4096)
+    for k in range(2000):
+        m.update(struct.pack("<I", k), struct.pack("<Q", 1000 + k))
+    rd = Asm().ldx(4, 2, 1, 0).stx(4, 10, -4, "r2")
+    rd.ld_map_fd(1, m.fd).mov64(2, "r10").add64(2, -4).call(1)
+    rd.jmp("jeq", 0, 0, "miss").ldx(8, 0, 0, 0).exit().label("miss").mov64(0, 0xdead).exit()
+    de = Asm().ldx(4, 2, 1, 0).stx(4, 10, -4, "r2")
+    de.ld_map_fd(1, m.fd).mov64(2, "r10").add64(2, -4).call(3).mov64(0, 0).exit()
+    reader, deleter = dev.VM(), dev.VM()
+    reader.load(rd.assemble())
+    deleter.load(de.assemble())
+    n = 1 << 18
+    keys = (np.arange(n, dtype=np.uint64) % 2000).astype(np.uint32)
+    units = np.zeros((n, 8), np.uint8)
+    units.view(np.uint32)[:, 0] = keys
+    evens = units[keys % 2 == 0]
+    d = dev.DeviceBuffer.from_array(units)
+    de_d = dev.DeviceBuffer.from_array(evens)
+    r1, r2 = dev.DeviceBuffer(8 * n), dev.DeviceBuffer(8 * n)
+    s1, s2 = L.bpftime_amd_stream_create(), L.bpftime_amd_stream_create()
+    try:
+        reader.exec_batch(dev.CTX_RAW, d, n, 8, fixed_len=8, rets=r1, flags=0, stream=s1)
+        deleter.exec_batch(dev.CTX_RAW, de_d, len(evens), 8, fixed_len=8, flags=0, stream=s2)
+        reader.exec_batch(dev.CTX_RAW, d, n, 8, fixed_len=8, rets=r2, flags=0, stream=s1)
+        m.delete(struct.pack("<I", 1))                 # a host delete behind the cached launch
+        L.bpftime_amd_sync()
+    finally:
+        L.bpftime_amd_stream_destroy(s1)
+        L.bpftime_amd_stream_destroy(s2)
+    vals = 1000 + keys.astype(np.uint64)
+    np.testing.assert_array_equal(r1.download(np.uint64), vals)
+    np.testing.assert_array_equal(r2.download(np.uint64), np.where(keys % 2 == 0, 0xdead, vals))
+    assert m.lookup(struct.pack("<I", 1)) is None and m.lookup(struct.pack("<I", 3)) is not None

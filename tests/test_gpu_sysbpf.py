@@ -116,6 +116,20 @@ def test_bss_mmap_view_write_read(fresh_oracle, fresh_runtime):
     out, op = _buf(bytes(4096))
     assert dev.sys_bpf(dev.BPF_MAP_LOOKUP_ELEM, dev.attr_map_elem(bss, kp, op))[0] == 0
     assert struct.unpack_from("<QQQ", out) == (2 * n, 7, 42)
+    # host writes on both sides of a counter an asynchronous batch is
+    # advancing: only the written bytes reach the device, so the counter's
+    # increments the view has not seen survive (the push used to upload the
+    # whole span between the first and last changed byte, stale counter
+    # included)
+    inc = dev.VM()
+    inc.load(isa.Asm().ld_map_value(1, bss, 8).mov64(2, 1).atomic(8, isa.ATOMIC_ADD, 1, 0, "r2")
+             .mov64(0, 2).exit().assemble())
+    c0 = view[1]
+    assert inc.exec_batch(dev.CTX_XDP, pk, n, 64, fixed_len=64, verdicts=dv, flags=0) == 0
+    view[0], view[2] = 111, 222
+    assert inc.exec_batch(dev.CTX_XDP, pk, n, 64, fixed_len=64, verdicts=dv, flags=0) == 0
+    assert L.bpftime_amd_map_msync(bss) == 0
+    assert (view[0], view[1], view[2]) == (111, c0 + 2 * n, 222)
     dev.close_fd(bss)
     assert L.bpftime_amd_map_msync(bss) == -1
 

@@ -14,8 +14,8 @@ from bpftime_amd.isa import Asm
 RB = isa.BPF_MAP_TYPE_RINGBUF
 
 
-def sampler(rb_fd):
-    """byte0 % 16 == 0: ringbuf_output(first 12 bytes); == 1: reserve 16 B,
+def sampler(rb_fd, out_size=12):
+    """byte0 % 16 == 0: ringbuf_output(first out_size bytes); == 1: reserve 16 B,
     fill {u64 bytes 0-7, u32 len, u32 byte1}, submit if byte1 is odd else
     discard.  Verdict PASS, DROP when the ring had no room."""
     a = Asm().ldx(8, 2, 1, 0).ldx(8, 3, 1, 8).mov64(0, 2)
@@ -24,7 +24,7 @@ def sampler(rb_fd):
     a.ldx(1, 8, 6, 0).alu64("and", 8, 15)
     a.jmp("jeq", 8, 0, "out0").jmp("jeq", 8, 1, "res").ja("out")
     a.label("out0")
-    a.ld_map_fd(1, rb_fd).mov64(2, "r6").mov64(3, 12).mov64(4, 0).call(130)
+    a.ld_map_fd(1, rb_fd).mov64(2, "r6").mov64(3, out_size).mov64(4, 0).call(130)
     a.mov64(1, "r0").mov64(0, 2).jmp("jeq", 1, 0, "out").mov64(0, 1).ja("out")
     a.label("res")
     a.ld_map_fd(1, rb_fd).mov64(2, 16).mov64(3, 0).call(131)
@@ -100,3 +100,112 @@ def test_device_ringbuf_sampler(fresh_oracle, fresh_runtime, size, frac):
         assert len(drecs) == len(orecs) == size // 24
         assert set(drecs) <= {bytes(p[:12]) for p in pk}
     assert dm.ringbuf_fetch() == []                          # consumed
+
+
+def _wrap_stream(rounds, n, seed):
+    """Per-round frames of a wrap test: every 16th frame outputs 12 B (a 24-B
+    record), frames with byte0 % 16 == 1 reserve 16 B and submit or discard."""
+    for r in range(rounds):
+        pk = gen.xdp_packets(n, seed=seed + r)
+        sel = np.arange(n) % 16
+        pk[:, 0] = np.where(sel == 0, 0, np.where(sel == 5, 1, 2))
+        yield pk
+
+
+def test_oracle_ringbuf_wraps(fresh_oracle):
+    """A 4096-B ring wrapped 40 times by bpf_ringbuf_output records (24 B;
+    4096 is not a multiple, so records straddle the end and one in 512 has
+    its data at the ring's first byte), consumed after every round.
+    bpf_ringbuf_output submits by the fd it reserved from
+    (bpf_helper.cpp:460-465) -- the oracle once read the fd in front of the
+    data there and left that record BUSY, stalling the consumer.
+    The reference ring is not double-mapped (ringbuf_map.cpp:157-176: a plain
+    2 x max_ent buffer): a record whose data wrapped is written at data[0]
+    but fetch_data hands out data + (cons & mask) + 8 = data[max_ent..], the
+    bytes the last straddling record left past the end (4 of them; the rest
+    zero).  Restated exactly."""
+    po = fresh_oracle
+    size = 4096
+    m = po.OracleMap(RB, 0, 0, size)
+    v = po.OracleVM()
+    v.load(sampler(m.fd))
+    pos, tail, wrapped = 0, bytes(12), 0
+    for pk in _wrap_stream(40, 1024, 100):
+        pk[:, 0] = np.where(pk[:, 0] == 1, 2, pk[:, 0])      # output records only
+        out = v.run_xdp(pk.copy(), fixed_len=64)
+        assert (out == 2).all()
+        want = []
+        for p in pk[pk[:, 0] == 0]:
+            rec = bytes(p[:12])
+            o = (pos + 8) % size
+            if o == 0:                                       # data wrapped to data[0]
+                want.append(tail)
+                wrapped += 1
+            else:
+                want.append(rec)
+                if o + 12 > size:                            # straddles: bytes past the end
+                    tail = rec[size - o:] + bytes(12 - (o + 12 - size))
+            pos += 24
+        assert m.ringbuf_fetch() == want
+    assert wrapped >= 2
+
+
+def test_oracle_ringbuf_submit_at_wrap(fresh_oracle):
+    """bpf_ringbuf_submit reads the fd from ptr[-1] (bpf_helper.cpp:478-479).
+    A reserved record whose data wrapped to the ring's first byte has the
+    zeroed word in front of the ring's data there (the reference's producer
+    page), fd 0: unless fd 0 is a ring the submit fails and the record stays
+    BUSY, and the consumer stops at it."""
+    po = fresh_oracle
+    m = po.OracleMap(RB, 0, 0, 4096, fd=7)
+    v = po.OracleVM()
+    v.load(sampler(m.fd))
+    pk = gen.xdp_packets(512, seed=3)
+    pk[:, 0] = 1
+    pk[:, 1] = 1                                             # reserve 16 B + submit: 24-B records
+    got = 0
+    for r in range(15):
+        out = v.run_xdp(pk[:50].copy(), fixed_len=64)
+        got += len(m.ringbuf_fetch())
+    # the record at position 2 * 4096 - 8 (data at offset 0) stays BUSY
+    assert got == (2 * 4096 - 8) // 24
+    assert (out == 1).any()                                  # the ring then fills: DROP
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ordered", [False, True])
+def test_device_ringbuf_wraps(fresh_oracle, fresh_runtime, ordered):
+    """40 rounds over a 4096-B ring (no staging: rings under 64 MiB reserve
+    directly), consumed between rounds.  ORDERED batches run the mixed
+    sampler (12-B outputs, reserve + submit / discard): records straddle the
+    end, some have their data at the ring's first byte (fetched from past
+    the end, and a reserved one stays BUSY: its submit reads fd 0, not a map
+    here), the consumer stalls and the ring fills -- records and verdicts
+    identical to the oracle's in order.  Parallel batches run 8-B outputs
+    (16-B records that never straddle), record multisets equal per round."""
+    po, dev = fresh_oracle, fresh_runtime
+    dm = dev.Map(RB, 0, 0, 4096, fd=7)
+    om = po.OracleMap(RB, 0, 0, 4096, fd=7)
+    code = sampler(dm.fd, 12 if ordered else 8)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    vm = dev.VM()
+    vm.load(code)
+    n = 1024
+    drops = 0
+    for pk in _wrap_stream(40, n, 200):
+        if not ordered:
+            pk[:, 0] = np.where(pk[:, 0] == 1, 2, pk[:, 0])
+        want = ovm.run_xdp(pk.copy(), fixed_len=64)
+        d = dev.DeviceBuffer.from_array(pk)
+        dv = dev.DeviceBuffer(4 * n)
+        flags = dev.BATCH_SYNC | (dev.BATCH_ORDERED if ordered else 0)
+        assert vm.exec_batch(dev.CTX_XDP, d, n, 64, fixed_len=64, verdicts=dv, flags=flags) == 0
+        np.testing.assert_array_equal(dv.download(np.uint32), want)
+        drops += int((want == 1).sum())
+        drecs, orecs = dm.ringbuf_fetch(), om.ringbuf_fetch()
+        if ordered:
+            assert drecs == orecs
+        else:
+            assert sorted(drecs) == sorted(orecs) and len(drecs) == (pk[:, 0] == 0).sum()
+    assert (drops > 0) == ordered
