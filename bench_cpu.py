@@ -5,14 +5,17 @@ on the host cores over a bounded sample of the same workload.
     python bench_cpu.py --workload xdp-counter --seconds 8 [--cores N]
 
 Runs in its own process (bench.py starts it after the GPU part; this process
-never touches the GPU).  Two legs, SURVEY.md §8d:
-  (i)  one thread pinned to one core;
-  (ii) N worker processes pinned to N cores, each over its own contiguous
-       shard of the stream with private map copies, their map deltas merged
-       like the GPUs' (the harness shape of tools/bpftimetool/main.cpp:42-58,
-       steady clock around the packet loop only).
-Prints one JSON object: the N-core leg as value/cores, the 1-core leg as
-single_core.
+never touches the GPU).  Three legs, SURVEY.md §8d:
+  (i)   one thread pinned to one core;
+  (ii)  16 worker processes pinned to 16 cores (the GPU box's CPU share per
+        GPU);
+  (iii) one worker process per core this process may use (nproc);
+each worker over its own contiguous shard of the stream with private map
+copies, their map totals checked (the harness shape of
+tools/bpftimetool/main.cpp:42-58, steady clock around the packet loop only).
+Prints one JSON object: the nproc leg as value/cores (with the cgroup's CPU
+quota and the cores the workers kept busy on average, which a quota below
+nproc caps), the 16-core leg as cores_16, the 1-core leg as single_core.
 """
 import argparse
 import json
@@ -175,39 +178,77 @@ def cpu_model():
     return ""
 
 
+def cpu_quota():
+    """The cgroup's CPU limit in cores (cgroup v2 cpu.max), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def leg(workload, cores, seconds):
+    """len(cores) pinned oracle processes, contiguous shards, private maps:
+    (Munits/s, longest loop s, wall s, checks ok, effective cores = the
+    processes' CPU seconds / wall)."""
+    ctx = mp.get_context("fork")
+    c0 = os.times()
+    t0 = time.perf_counter()
+    pool = ctx.Pool(len(cores))
+    try:
+        res = pool.map(_worker, [(workload, k, c, seconds, RING_LOG2) for k, c in enumerate(cores)])
+        pool.close()
+        pool.join()
+    finally:
+        pool.terminate()
+    wall = time.perf_counter() - t0
+    c1 = os.times()
+    cpu = (c1.children_user - c0.children_user) + (c1.children_system - c0.children_system)
+    # each worker's packet loop ran `secs` of its own steady clock; they ran
+    # side by side, so the aggregate rate is units / the longest loop time
+    loop = max(r[1] for r in res)
+    return (sum(r[0] for r in res) / loop / 1e6, loop, wall, all(r[2] for r in res),
+            round(cpu / wall, 1) if wall > 0 else None)
+
+
 def main():
     global RING_LOG2
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="xdp-counter", choices=sorted(SAMPLE))
     ap.add_argument("--seconds", type=float, default=8.0, help="oracle time per leg")
-    ap.add_argument("--cores", type=int, default=0, help="N-core leg width (0: the cores this process may use, "
-                                                         "at most 16 -- the GPU box's CPU share per GPU)")
+    ap.add_argument("--cores", type=int, default=0, help="width of the all-core leg (0: every core this process "
+                                                         "may use, i.e. nproc)")
     ap.add_argument("--ring-log2", type=int, default=26, help="ringbuf-sample: log2 of the ring's bytes")
     args = ap.parse_args()
     RING_LOG2 = args.ring_log2
     cores = sorted(os.sched_getaffinity(0))
-    ncore = args.cores or min(16, len(cores))
-    ncore = max(1, min(ncore, len(cores)))
+    nall = max(1, min(args.cores or len(cores), len(cores)))
     unit = "Mrec/s" if args.workload == "syscall-agg" else "Mpps"
+    bits = SAMPLE[args.workload].bit_length() - 1
     # (i) one pinned core
     done1, secs1, ok1 = _worker((args.workload, 0, cores[0], args.seconds, RING_LOG2))
-    # (ii) ncore pinned processes, contiguous shards, private maps
-    ctx = mp.get_context("fork")
-    t0 = time.perf_counter()
-    with ctx.Pool(ncore) as pool:
-        res = pool.map(_worker, [(args.workload, k, cores[k], args.seconds, RING_LOG2) for k in range(ncore)])
-    wall = time.perf_counter() - t0
-    done_n = sum(r[0] for r in res)
-    # each worker's packet loop ran `secs` of its own steady clock; they ran
-    # side by side, so the aggregate rate is units / the longest loop time
-    loop_n = max(r[1] for r in res)
-    ok = ok1 and all(r[2] for r in res)
+    # (ii) 16 pinned processes (the GPU box's CPU share per GPU), (iii) one per
+    # core this process may use (nproc; tools/bpftimetool/main.cpp:42-58 runs
+    # the CPU path on every core)
+    n16 = min(16, nall)
+    v16, loop16, wall16, ok16, eff16 = leg(args.workload, cores[:n16], args.seconds)
+    if nall > n16:
+        vn, loopn, walln, okn, effn = leg(args.workload, cores[:nall], args.seconds)
+    else:
+        vn, loopn, walln, okn, effn = v16, loop16, wall16, ok16, eff16
+    ok = ok1 and ok16 and okn
+    quota = cpu_quota()
     out = {
-        "value": round(done_n / loop_n / 1e6, 3), "unit": unit, "cores": ncore, "kind": "port",
-        "sample": "%s: %d oracle processes pinned to %d cores, each over its own contiguous 2^%d-unit shard of "
-                  "the same stream with private maps (%.1f s loops, %.1f s wall, map totals %s), cpu %s"
-                  % (args.workload, ncore, ncore, SAMPLE[args.workload].bit_length() - 1, loop_n, wall,
-                     "ok" if ok else "MISMATCH", cpu_model()),
+        "value": round(vn, 3), "unit": unit, "cores": nall, "kind": "port",
+        "sample": "%s: %d oracle processes pinned one per core (every core in this process's affinity; "
+                  "os.cpu_count() %d, cgroup CPU quota %s), each over its own contiguous 2^%d-unit shard of the "
+                  "same stream with private maps (%.1f s loops, %.1f s wall, %s cores busy on average, map totals "
+                  "%s), cpu %s" % (args.workload, nall, os.cpu_count() or 0, quota, bits, loopn, walln, effn,
+                                   "ok" if ok else "MISMATCH", cpu_model()),
+        "nproc": os.cpu_count(), "affinity_cores": len(cores), "cpu_quota_cores": quota, "effective_cores": effn,
+        "cores_16": {"value": round(v16, 3), "unit": unit, "cores": n16, "effective_cores": eff16,
+                     "sample": "%d pinned oracle processes (the GPU box's CPU share per GPU), %.1f s loops"
+                               % (n16, loop16)},
         "single_core": {"value": round(done1 / secs1 / 1e6, 3), "unit": unit, "cores": 1,
                         "sample": "1 oracle thread pinned to core %d, %.1f s" % (cores[0], secs1)},
         "ok": ok,

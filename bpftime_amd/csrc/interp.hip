@@ -1038,6 +1038,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         // helper's 0 return ends the unit with r0 = 0, as its exit would --
         // not inside a tail-call target, which the reference runs in a
         // program of its own without the index
+        if ((p.dbg & 256) && blockIdx.x == 0 && tid < 4)
+          printf("R_CALL lane %u unit %llu cid %u unwind %d rv %llu tdep %u alive %d\n", tid,
+                 (unsigned long long)c.unit, c.call_id, p.unwind_idx, (unsigned long long)rv, tdep[0], (int)c.alive);
         if (c.alive && (int32_t)c.call_id == p.unwind_idx && rv == 0 && tdep[0] == 0) {
           if (c.verdicts) c.verdicts[c.unit] = 0;
           if (c.rets) c.rets[c.unit] = 0;

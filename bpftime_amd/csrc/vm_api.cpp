@@ -635,9 +635,10 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     return -1;
   }
   if (getenv("BPFTIME_AMD_VERBOSE"))
-    fprintf(stderr, "bpftime_amd: launch units %llu grid %u comb %u lcache %u stage %u stack %u gregs %d gctx %d\n",
+    fprintf(stderr,
+            "bpftime_amd: launch units %llu grid %u comb %u lcache %u stage %u stack %u gregs %d gctx %d unwind %d\n",
             (unsigned long long)b->count, grid, p.comb_entries, p.lcache, p.stage, (unsigned)prog.stack_size,
-            p.gregs ? 1 : 0, p.gctx ? 1 : 0);
+            p.gregs ? 1 : 0, p.gctx ? 1 : 0, p.unwind_idx);
   hipError_t e = bpftime_amd_launch_interp(&p, b->ctx_kind, prog.big_stack, grid, ordered ? 1 : 0, s);
   if (e == hipSuccess && p.flush_log) e = bpftime_amd_launch_merge(p.flush_log, p.log_words, grid, s);
   if (e != hipSuccess) {
