@@ -191,6 +191,8 @@ constexpr uint32_t kRbStageBytes = kRbStageRec + 4 * kRbStageMaxRec;  // + u32 r
 
 // Kernel launch parameters (passed by value).
 struct FInsn;
+// (k_interp copies every field through an SGPR barrier, interp.hip: a new
+// field must be copied there too)
 struct KParams {
   const DInsn *prog;
   const FInsn *fast;      // threaded-code form for the asm fast path

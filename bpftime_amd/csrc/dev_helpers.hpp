@@ -140,8 +140,13 @@ constexpr uint32_t ST_EMPTY = 0, ST_FILLED = 1, ST_BUSY = 2;
 // (bpftime_hash_map.hpp:127-180).  Lanes never wait on a lane of their own
 // wave: a BUSY slot is re-read on the next loop trip, by which time the
 // claiming lane (same wave, same trip) has published it.
+// (part / part_off / part_bytes: bytes written over the zero-initialised
+// value of a new element before it is published -- a per-CPU element's
+// value for the inserting lane's CPU, which a lane adding to that CPU's
+// slot right after the publish must not see overwritten)
 __device__ uint64_t hash_find(const DMap &m, uint64_t key, bool insert, uint64_t init,
-                              uint32_t init_bytes, bool *inserted) {
+                              uint32_t init_bytes, bool *inserted, uint64_t part = 0, uint32_t part_off = 0,
+                              uint32_t part_bytes = 0) {
   *inserted = false;
   const uint64_t nb = m.nbuckets;
   const uint64_t h = key_hash(key, m.key_size);
@@ -197,6 +202,7 @@ __device__ uint64_t hash_find(const DMap &m, uint64_t key, bool insert, uint64_t
           for (uint32_t i = 0; i < init_bytes; i += 4)
             __hip_atomic_store(G32(s + m.val_off + i), 0u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+        if (part) copy_bytes_publish(s + m.val_off + part_off, part, part_bytes);
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // key/value stores drained first
         __hip_atomic_store(G32(s), ST_FILLED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -643,11 +649,19 @@ struct RbStage {
 };
 
 __device__ __forceinline__ uint64_t rb_cas_reserve(const DMap &m, uint64_t total) {
-  // returns the old producer position, or ~0 if total does not fit
+  // returns the old producer position, or ~0 if total does not fit.  The
+  // loop always ends by a successful CAS or a failed room check, as the
+  // reference's spin-locked reserve does: the consumer position does not
+  // move while a launch runs (its only consumer, bpftime_amd_ringbuf_fetch,
+  // synchronizes the device first), and every lost CAS means another
+  // reservation moved the producer position by >= 8 bytes, so after at most
+  // max_entries / 8 lost CASes the room check fails.  The bound below is
+  // that count plus one and is never the reason the loop ends.
   const uint64_t cons = __hip_atomic_load(G64(m.data), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   unsigned long long p = __hip_atomic_load(G64(m.data + 128), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   uint32_t backoff = 1;
-  for (uint32_t spin = 0; spin < (1u << 20); spin++) {
+  const uint64_t bound = (uint64_t)m.max_entries / 8 + 2;
+  for (uint64_t spin = 0; spin < bound; spin++) {
     if ((uint64_t)m.max_entries - (p - cons) < total) return ~0ull;
     if (__hip_atomic_compare_exchange_strong(G64(m.data + 128), &p, p + total, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT))
@@ -925,12 +939,14 @@ __device__ uint64_t helper_update(const DMap *maps, uint64_t fd, uint64_t key, u
     }
     case MT_PERCPU_HASH: {
       if (!flags_ok) return (uint64_t)-1;
-      // per_cpu_hash_map.cpp:66-94: insert zeroed ncpu*vsize, then write slot
+      // per_cpu_hash_map.cpp:66-94: insert zeroed ncpu*vsize, then write
+      // the slot (a new element's slot before it is published)
       bool ins;
-      uint64_t s = hash_find(m, key, true, 0, m.value_size * m.ncpu, &ins);
+      const uint32_t off = (uint32_t)(env.vcpu % m.ncpu) * m.value_size;
+      uint64_t s = hash_find(m, key, true, 0, m.value_size * m.ncpu, &ins, val, off, m.value_size);
       if (!s) return 0;
       bool race = !ins && env.miss_fd == (int32_t)fd && env.miss_hash == key_hash(key, m.key_size);
-      if (!race) copy_bytes(s + m.val_off + (env.vcpu % m.ncpu) * m.value_size, val, m.value_size);
+      if (!ins && !race) copy_bytes(s + m.val_off + off, val, m.value_size);
       env.miss_fd = -1;
       return 0;
     }

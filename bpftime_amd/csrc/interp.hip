@@ -595,6 +595,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(flush_log); SRV(log_words); SRP(lane_scratch);
   SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask); SRV(lcache); SRP(gregs); SRP(rb_stage); SRP(gctx);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
+  p.unwind_idx = (int32_t)sreg((uint64_t)(uint32_t)pin.unwind_idx);
 #undef SRP
 #undef SRV
   // r0..r10, a dummy slot, and (images) the lane's tail-call depth | its
@@ -1038,9 +1039,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         // helper's 0 return ends the unit with r0 = 0, as its exit would --
         // not inside a tail-call target, which the reference runs in a
         // program of its own without the index
-        if ((p.dbg & 256) && blockIdx.x == 0 && tid < 4)
-          printf("R_CALL lane %u unit %llu cid %u unwind %d rv %llu tdep %u alive %d\n", tid,
-                 (unsigned long long)c.unit, c.call_id, p.unwind_idx, (unsigned long long)rv, tdep[0], (int)c.alive);
         if (c.alive && (int32_t)c.call_id == p.unwind_idx && rv == 0 && tdep[0] == 0) {
           if (c.verdicts) c.verdicts[c.unit] = 0;
           if (c.rets) c.rets[c.unit] = 0;

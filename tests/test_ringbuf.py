@@ -209,3 +209,70 @@ def test_device_ringbuf_wraps(fresh_oracle, fresh_runtime, ordered):
         else:
             assert sorted(drecs) == sorted(orecs) and len(drecs) == (pk[:, 0] == 0).sum()
     assert (drops > 0) == ordered
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ordered", [True, False])
+def test_device_ringbuf_fills_within_launch(fresh_oracle, fresh_runtime, ordered):
+    """A 1 MiB ring that starts the launch empty and fills part way through
+    it (2^17 frames, each writing a 24-B record, 43690 fit): ORDERED batches
+    reproduce the oracle's records, order and verdicts exactly; parallel
+    batches accept exactly as many records as fit (lane-exact CAS
+    reservations once the ring is too full for a wave's fetch-and-add), with
+    DROP verdicts for the rest."""
+    po, dev = fresh_oracle, fresh_runtime
+    size = 1 << 20
+    dm = dev.Map(RB, 0, 0, size, fd=7)
+    om = po.OracleMap(RB, 0, 0, size, fd=7)
+    code = sampler(dm.fd)
+    n = 1 << 17
+    pk = gen.xdp_packets(n, seed=31)
+    pk[:, 0] = 0                                             # every frame outputs 12 B
+    ovm = po.OracleVM()
+    ovm.load(code)
+    want = ovm.run_xdp(pk.copy(), fixed_len=64)
+    vm = dev.VM()
+    vm.load(code)
+    d = dev.DeviceBuffer.from_array(pk)
+    dv = dev.DeviceBuffer(4 * n)
+    flags = dev.BATCH_SYNC | (dev.BATCH_ORDERED if ordered else 0)
+    assert vm.exec_batch(dev.CTX_XDP, d, n, 64, fixed_len=64, verdicts=dv, flags=flags) == 0
+    got = dv.download(np.uint32)
+    drecs, orecs = dm.ringbuf_fetch(), om.ringbuf_fetch()
+    assert (want == 2).sum() == size // 24 and len(orecs) == size // 24
+    if ordered:
+        np.testing.assert_array_equal(got, want)
+        assert drecs == orecs
+    else:
+        assert (got == 2).sum() == size // 24 and (got == 1).sum() == n - size // 24
+        assert len(drecs) == size // 24
+        assert set(drecs) <= {bytes(p[:12]) for p in pk}
+
+
+@pytest.mark.gpu
+def test_device_ringbuf_staged_ring_fills_within_launch(fresh_oracle, fresh_runtime):
+    """A 64 MiB ring (large enough for block staging, dev_helpers.hpp RbStage)
+    filled part way through one parallel launch.  Staging stops once the
+    ring is within kRbSlack (32 MiB) of full, and the chunks reserved before
+    that may end with DISCARD tails the reference would have filled, so the
+    accepted count can fall short of the reference's by at most one chunk
+    (2 KiB) per block of the launch -- the documented difference of staged
+    rings; every accepted record is delivered and the verdicts
+    agree with the records."""
+    po, dev = fresh_oracle, fresh_runtime
+    size = 1 << 26
+    dm = dev.Map(RB, 0, 0, size, fd=7)
+    n = 3 << 20                                              # 72 MiB of 24-B records
+    pk = gen.xdp_packets(n, seed=32)
+    pk[:, 0] = 0
+    vm = dev.VM()
+    vm.load(sampler(dm.fd))
+    d = dev.DeviceBuffer.from_array(pk)
+    dv = dev.DeviceBuffer(4 * n)
+    assert vm.exec_batch(dev.CTX_XDP, d, n, 64, fixed_len=64, verdicts=dv) == 0
+    got = dv.download(np.uint32)
+    drecs = dm.ringbuf_fetch(cap=1 << 27)
+    fit = size // 24
+    ok = int((got == 2).sum())
+    assert ok == len(drecs) and ok + int((got == 1).sum()) == n
+    assert fit - (4096 * 2048) // 24 <= ok <= fit

@@ -54,7 +54,7 @@ def test_oracle_unwind(fresh_oracle):
     (isa.BPF_MAP_TYPE_ARRAY, UBPF_LOOKUP, False),    # lookup (asm-tier helper) misses unwind
     (isa.BPF_MAP_TYPE_ARRAY, UBPF_UPDATE, False),    # failing updates (E2BIG) do not
     (isa.BPF_MAP_TYPE_HASH, UBPF_UPDATE, True),      # the inserting unit of each key unwinds
-    (isa.BPF_MAP_TYPE_HASH, UBPF_CPU, False),        # a helper the program never calls
+    (isa.BPF_MAP_TYPE_ARRAY, UBPF_CPU, False),       # a helper the program never calls
     (isa.BPF_MAP_TYPE_HASH, -1, True),
 ])
 def test_device_unwind(fresh_oracle, fresh_runtime, mtype, unwind, ordered):
