@@ -32,6 +32,7 @@ run sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_
 run sq2 SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_WAVES || exit $?
 run fetch FETCH_SIZE || exit $?
 run write WRITE_SIZE || exit $?
+run l2 TCC_HIT_sum TCC_MISS_sum || exit $?
 run tcp TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum || true
 U=${UNITS:-16777216}
 python3 tools/pmc_table.py $D $U $D.pmc.json > $D.summary.txt 2>&1 || true
