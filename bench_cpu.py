@@ -161,7 +161,12 @@ def _worker(a):
             pass
     run, check = _setup(workload, shard, SAMPLE[workload])
     secs, done = 0.0, 0
-    while secs < budget:
+    # a wall-clock cap as well: with more processes than the cgroup's CPUs
+    # (the nproc leg on the GPU box: 256 processes, 16 CPUs) the untimed part
+    # of a run (copies, the ring consumer) stretches the wall time, and the
+    # rate is units / the timed loop anyway
+    t_end = time.perf_counter() + 3 * budget + 5
+    while secs < budget and (done == 0 or time.perf_counter() < t_end):
         dt, k = run()
         secs += dt
         done += k

@@ -112,6 +112,34 @@ __global__ KB void c_atom8_4M(uint8_t *d, uint32_t *sink, uint64_t n) {
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// the same adds with workgroup scope into a per-XCD copy of the 4 MiB
+// region (HW_REG_XCC_ID picks the copy): performed in the XCD's L2, which
+// no other XCD shares, instead of at the memory side
+__device__ __forceinline__ uint32_t xcc_id() {
+  uint32_t x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 0xf;
+}
+
+__global__ KB void c_atom8_4M_xcd(uint8_t *d, uint32_t *sink, uint64_t n) {
+  uint8_t *mine = d + (uint64_t)(xcc_id() & 7) * (4ull << 20);
+  for (uint64_t u = blockIdx.x * 256ull + threadIdx.x; u < n; u += gridDim.x * 256ull)
+    __hip_atomic_fetch_add((uint64_t *)(mine + (mix(u) % ((4ull << 20) / 8)) * 8), 1ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__global__ KB void c_atom8_1M_xcd(uint8_t *d, uint32_t *sink, uint64_t n) {
+  uint8_t *mine = d + (uint64_t)(xcc_id() & 7) * (1ull << 20);
+  for (uint64_t u = blockIdx.x * 256ull + threadIdx.x; u < n; u += gridDim.x * 256ull)
+    __hip_atomic_fetch_add((uint64_t *)(mine + (mix(u) % ((1ull << 20) / 8)) * 8), 1ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// which XCD runs which block: blockIdx.x % 8 under round-robin placement
+__global__ KB void c_xcc_map(uint8_t *d, uint32_t *sink, uint64_t n) {
+  if (threadIdx.x == 0 && blockIdx.x < 64) sink[blockIdx.x] = xcc_id();
+}
+
 int main(int argc, char **argv) {
   const int lg = argc > 1 ? atoi(argv[1]) : 24;
   const uint64_t n = 1ull << lg;
@@ -159,5 +187,25 @@ int main(int argc, char **argv) {
   run("c_gather8_1G", c_gather8<1ull << 30>, t, n, 8, 0);
   run("c_wr32of64", c_wr32of64, d, n, 0, 32);
   run("c_atom8_4M", c_atom8_4M, t, n, 8, 8);
+  run("c_atom8_4M_xcd", c_atom8_4M_xcd, t, n, 8, 8);
+  run("c_atom8_1M_xcd", c_atom8_1M_xcd, t, n, 8, 8);
+  // the per-XCD copies hold every add: their sum over the copies is REPS + 1 adds per unit
+  {
+    uint64_t *h = (uint64_t *)malloc(32ull << 20);
+    hipMemset(t, 0, 32ull << 20);
+    hipLaunchKernelGGL(c_atom8_4M_xcd, dim3(grid), dim3(256), 0, 0, t, v, n);
+    hipMemcpy(h, t, 32ull << 20, hipMemcpyDeviceToHost);
+    uint64_t sum = 0;
+    for (uint64_t i = 0; i < (32ull << 20) / 8; i++) sum += h[i];
+    printf("{\"check\": \"c_atom8_4M_xcd adds\", \"sum\": %llu, \"want\": %llu}\n", (unsigned long long)sum,
+           (unsigned long long)n);
+    free(h);
+    hipLaunchKernelGGL(c_xcc_map, dim3(64), dim3(256), 0, 0, t, v, 64);
+    uint32_t m[64];
+    hipMemcpy(m, v, sizeof(m), hipMemcpyDeviceToHost);
+    printf("{\"xcc_of_block\": [");
+    for (int i = 0; i < 64; i++) printf("%u%s", m[i], i < 63 ? ", " : "");
+    printf("]}\n");
+  }
   return 0;
 }
