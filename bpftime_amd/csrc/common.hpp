@@ -249,11 +249,21 @@ struct KParams {
 // kMergeGroup blocks' logs in an LDS table before adding: the same addresses
 // are hot in every block, and same-address device atomics serialize at the
 // memory side (a map of a few hundred values sits in a handful of channels).
-constexpr uint32_t kWaveCacheEntries = (kBlock / 64) * 2;
+BA_HD constexpr uint32_t wave_cache_entries(uint32_t block) { return (block / 64) * 2; }
 constexpr uint32_t kMergeGroup = 16;
 constexpr uint32_t kMergeEntries = 4096;  // merge table entries (64 KiB of LDS)
 // (a combining-table entry flushes up to four counters: gen_fast.py comb_add)
-inline uint32_t log_words_for(uint32_t comb_entries) { return 1 + 2 * (kWaveCacheEntries + 4 * comb_entries); }
+inline uint32_t log_words_for(uint32_t comb_entries, uint32_t block = kBlock) {
+  return 1 + 2 * (wave_cache_entries(block) + 4 * comb_entries);
+}
+
+// Launches whose C++-tier register copy lives in global memory (k_interp G:
+// a combining table or lookup cache, no tail-call image, no ring staging)
+// run kBigBlock-lane blocks: one combining table and lookup cache serve 16
+// waves instead of 4, so the LDS a table takes no longer caps the CU at 2
+// blocks of 4 waves (flow-hash: 8 -> 16 resident waves per CU at the same
+// or a larger table reach)
+constexpr uint32_t kBigBlock = 1024;
 
 // Dynamic LDS of an interpreter block: the lanes' XDP ctx (48 B each), their
 // stacks (LDS-stack programs), 48 B of launch constants (interp.hip
@@ -267,8 +277,8 @@ constexpr uint32_t kTenvBytes = 48;  // gen_fast.py TENV: tail-call constants, t
 constexpr uint32_t kLcacheEntries = 2048;  // gen_fast.py LC_ENTRIES
 constexpr uint32_t kLcacheBytes = 8 * kLcacheEntries;
 inline size_t dyn_lds_for(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
-                          bool lcache = false, bool ctx_lds = true) {
-  return (size_t)kBlock * ((kind == CTX_XDP && ctx_lds ? 48 : 0) + (big_stack ? 0 : stack_size)) +
+                          bool lcache = false, bool ctx_lds = true, uint32_t block = kBlock) {
+  return (size_t)block * ((kind == CTX_XDP && ctx_lds ? 48 : 0) + (big_stack ? 0 : stack_size)) +
          (lcache ? kLcacheBytes : 0) + kTenvBytes + 20 * (size_t)comb_entries;
 }
 

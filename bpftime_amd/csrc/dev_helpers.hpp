@@ -634,12 +634,12 @@ constexpr uint64_t kRbSlack = kRbMaxWaves * kRbWaveMax;    // 32 MiB
 // the reference is the discarded tail, up to one chunk per block and launch
 // of ring space that a ring going from ample room to full inside one launch
 // can no longer give to records.  A wave whose records do not fit the chunk
-// reserves directly.  The ring's only consumer, bpftime_amd_ringbuf_fetch
-// (maps.cpp), synchronizes the device before it reads the positions, so it
-// never sees a chunk whose producer position has moved but whose records
-// the block has not published yet (the reference writes each BUSY header
-// before moving the position, under its spin lock); it sees the same
-// records in another parallel order.
+// reserves directly.  Right after the chunk's reservation its first header
+// reads BUSY (one record spanning the chunk), and rb_publish writes that
+// header last, after every other byte of the chunk: a consumer polling while
+// the block runs stops at the chunk as it stops at any reserved record (the
+// reference writes each BUSY header before moving the position, under its
+// spin lock).  Consumers see the same records in another parallel order.
 // (sizes: common.hpp kRbStage*)
 struct RbStage {
   uint8_t *buf = nullptr;  // this block's area: records, then u32 offsets (nullptr: no staging)
@@ -706,8 +706,14 @@ __device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size, con
             int32_t got = -2;
             // the fast path's condition (below), for a chunk
             if (m.max_entries >= 2 * kRbSlack && (uint64_t)m.max_entries - (prod - cons) >= kRbStageRec + kRbSlack) {
-              *st.base = __hip_atomic_fetch_add(G64(m.data + 128), (uint64_t)kRbStageRec, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
+              const uint64_t cb = __hip_atomic_fetch_add(G64(m.data + 128), (uint64_t)kRbStageRec,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              *st.base = cb;
+              // the chunk reads as one reserved record until the block publishes
+              const uint64_t h = m.data + 256 + (cb & (m.max_entries - 1));
+              __hip_atomic_store(G32(h + 4), (uint32_t)fd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(G32(h), (kRbStageRec - RB_HDR) | RB_BUSY, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
               got = (int32_t)fd;
             }
             __hip_atomic_store(st.fd, got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -806,8 +812,10 @@ __device__ uint64_t rb_output(const DMap *maps, uint64_t fd, uint64_t data, uint
 }
 
 // The block's staged records into its chunk of the ring (every wave of the
-// block is done), one thread per record, and the chunk's unused tail as one
-// DISCARD record.
+// block is done; called by every thread of the block), one thread per
+// record, and the chunk's unused tail as one DISCARD record.  The chunk's
+// first header word (BUSY since the reservation) is written last, with
+// release order after every other byte of the chunk.
 __device__ void rb_publish(const DMap *maps, const RbStage &st, uint32_t tid, uint32_t nthreads) {
   const int32_t fd = *st.fd;
   if (!st.buf || fd < 0) return;
@@ -821,13 +829,24 @@ __device__ void rb_publish(const DMap *maps, const RbStage &st, uint32_t tid, ui
     const uint32_t total = ((h & ~(RB_BUSY | RB_DISCARD)) + RB_HDR + 7) / 8 * 8;
     const uint64_t *src = (const uint64_t *)(st.buf + off);
     uint64_t *dst = (uint64_t *)(uintptr_t)(d + ((base + off) & mask));
-    for (uint32_t w = 0; w < total / 8; w++) dst[w] = src[w];
+    for (uint32_t w = off ? 0 : 1; w < total / 8; w++) dst[w] = src[w];
+    if (!off) ((int32_t *)dst)[1] = ((const int32_t *)src)[1];
   }
-  if (tid == 0 && end < kRbStageRec) {
-    const uint64_t h = d + ((base + end) & mask);
-    *(uint32_t *)(uintptr_t)h = (kRbStageRec - end - RB_HDR) | RB_DISCARD;
-    *(int32_t *)(uintptr_t)(h + 4) = fd;
+  uint32_t first = 0;  // the chunk's first header word
+  if (end < kRbStageRec) {
+    const uint32_t tail = (kRbStageRec - end - RB_HDR) | RB_DISCARD;
+    if (end == 0) {
+      first = tail;
+    } else if (tid == 0) {
+      const uint64_t h = d + ((base + end) & mask);
+      *(uint32_t *)(uintptr_t)h = tail;
+      *(int32_t *)(uintptr_t)(h + 4) = fd;
+    }
   }
+  if (end) first = *(const uint32_t *)st.buf;  // the record staged at offset 0
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(G32(d + (base & mask)), first, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 struct LaneEnv {

@@ -580,8 +580,9 @@ __device__ __forceinline__ void write_xdp_ctx(XdpCtx *x, uint64_t slot, uint32_t
 // block's [register][lane] columns) instead of LDS: 22 KiB of LDS per block
 // go to residency (launches with a combining table or lookup cache, whose
 // units stay in the asm tier)
-template <uint32_t KIND, bool BIGSTACK, bool IMAGE, bool G>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_interp(KParams pin) {
+template <uint32_t KIND, bool BIGSTACK, bool IMAGE, bool G, uint32_t BS>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_interp(KParams pin) {
+  static_assert(BS == kBlock || (BS == kBigBlock && G && !IMAGE && !BIGSTACK), "big blocks: G launches only");
   // Copy every kernel argument through an SGPR barrier: without it the
   // compiler keeps the argument block as one 16-dword tuple that it spills
   // and reloads whole inside the dispatch loop.
@@ -603,28 +604,30 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   // between 3 and 4 resident blocks of the headline program: images only.)
   // (G: the dummy and depth slots only)
   constexpr uint32_t kDummy = G ? 0 : 11, kDepth = G ? 1 : 12;
-  __shared__ uint64_t Rf[(IMAGE ? kDepth + 1 : kDummy + 1) * kBlock];
-  uint64_t *const Rg = G ? p.gregs + (uint64_t)blockIdx.x * 11 * kBlock : Rf;  // r0..r10 columns
+  __shared__ uint64_t Rf[(IMAGE ? kDepth + 1 : kDummy + 1) * BS];
+  // r0..r10 columns: [register][lane] per 256 lanes (kBlock), so a block of
+  // BS > kBlock lanes (G launches only) holds BS / kBlock such column sets
+  uint64_t *const Rg = G ? p.gregs + (uint64_t)blockIdx.x * 11 * BS : Rf;
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
   // the lane's XDP ctx: in LDS, or (p.gctx: a program that only reads
   // data / data_end, whose ctx only the C++ tier touches) in global memory
   const uint32_t tid = threadIdx.x;
   const uint32_t ctxb = KIND == CTX_XDP && !p.gctx ? 48 : 0;
-  uint8_t *my_ctx = KIND == CTX_XDP && p.gctx ? p.gctx + ((uint64_t)blockIdx.x * kBlock + tid) * 48 : dyn + tid * ctxb;
-  uint8_t *my_stack = dyn + kBlock * ctxb + tid * p.stack_size;
+  uint8_t *my_ctx = KIND == CTX_XDP && p.gctx ? p.gctx + ((uint64_t)blockIdx.x * BS + tid) * 48 : dyn + tid * ctxb;
+  uint8_t *my_stack = dyn + BS * ctxb + tid * p.stack_size;
   // combining table for per-lane counter adds (gen_fast.py comb_add), after
   // the ctx and stack areas: comb_entries u32 tags {16-byte granule's arena
   // offset (8-byte aligned for 8-byte counters) | 2 | (4-byte ? 1 : 0)}
   // (8-way sets), then comb_entries 16-byte
   // delta granules (2 x u64 or 4 x u32), flushed when the block ends; sized 0
   // for programs that never need it
-  uint32_t *lcache = (uint32_t *)(dyn + kBlock * (ctxb + (BIGSTACK ? 0 : p.stack_size)));
+  uint32_t *lcache = (uint32_t *)(dyn + BS * (ctxb + (BIGSTACK ? 0 : p.stack_size)));
   uint64_t *tenv = (uint64_t *)((uint8_t *)lcache + (p.lcache ? kLcacheBytes : 0));
   uint32_t *comb = (uint32_t *)((uint8_t *)tenv + kTenvBytes);
   uint64_t *comb_d = (uint64_t *)(comb + p.comb_entries);
-  for (uint32_t i = tid; i < 5 * p.comb_entries; i += kBlock) comb[i] = 0;
+  for (uint32_t i = tid; i < 5 * p.comb_entries; i += BS) comb[i] = 0;
   if (p.lcache)
-    for (uint32_t i = tid; i < 2 * kLcacheEntries; i += kBlock) lcache[i] = 0;
+    for (uint32_t i = tid; i < 2 * kLcacheEntries; i += BS) lcache[i] = 0;
   // ring-buffer staging (dev_helpers.hpp RbStage): LDS counters of the block
   __shared__ uint32_t rb_used, rb_end, rb_nrec;
   __shared__ int32_t rb_fd;
@@ -681,7 +684,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                                       : (uint64_t)(uintptr_t)(my_stack + p.stack_size);
 
   Ctx c;
-  c.R = &Rg[tid];
+  c.R = G ? &Rg[(tid & ~(kBlock - 1)) * 11 + (tid & (kBlock - 1))] : &Rg[tid];
   c.prog = (prog_ptr)p.prog;
   c.fast = p.fast;
   {
@@ -689,12 +692,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     // (the lane scratch words, then the blocks' ring-buffer staging areas:
     // a program writes a record it reserved there; then the global ctxs)
     c.win = Win{p.data_lo, p.data_hi, p.arena_lo, p.arena_hi, sl,
-                sl ? sl + 8ull * gridDim.x * kBlock + (p.rb_stage ? (uint64_t)gridDim.x * kRbStageBytes : 0) +
-                         (p.gctx ? 48ull * gridDim.x * kBlock : 0)
+                sl ? sl + 8ull * gridDim.x * BS + (p.rb_stage ? (uint64_t)gridDim.x * kRbStageBytes : 0) +
+                         (p.gctx ? 48ull * gridDim.x * BS : 0)
                    : 0,
                 p.checked != 0};
   }
-  c.dummy = (uint64_t)(uintptr_t)&Rf[kDummy * kBlock + tid];
+  c.dummy = (uint64_t)(uintptr_t)&Rf[kDummy * BS + tid];
   c.verdicts = p.verdicts;
   c.rets = p.rets;
   c.step_limit = p.step_limit > 0xffffffffull ? 0xffffffffu : (uint32_t)p.step_limit;
@@ -720,7 +723,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   fe.phi = BIGSTACK ? sreg((uint32_t)__builtin_amdgcn_readfirstlane(
                           (uint32_t)((uint64_t)(uintptr_t)&big_stack[0] >> 32)))
                     : fe.shi;
-  fe.rb = (uint32_t)(uintptr_t)&Rf[tid];
+  // (G: v40 + r * 2048 + tenv[4] addresses the lane's copy of r, gen_fast.py
+  // rgb; v40 is no LDS address there)
+  fe.rb = (uint32_t)(uintptr_t)&Rf[0] + 8 * (uint32_t)(G ? (c.R - Rg) : tid);
 
   // the host sized the staged window (gen_fast.py, unit staging) from the
   // program's static packet / slot accesses, 16-B aligned slots only
@@ -728,7 +733,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   fe.ncpu = p.ncpu ? p.ncpu : 1;
 
   const bool ordered = p.ordered != 0;
-  const uint64_t ustep = ordered ? 1 : (uint64_t)gridDim.x * kBlock;
+  const uint64_t ustep = ordered ? 1 : (uint64_t)gridDim.x * BS;
   // Chained units (gen_fast.py chain_routine): while every lane of the wave
   // has a unit, the asm tier starts the wave's next unit itself.  Plain
   // strided batches only: no descriptors, no per-unit ctx in LDS or ctx
@@ -739,7 +744,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                         ustep * p.stride < (1ull << 32) && !(p.dbg & 64);
   uint64_t full = 0;  // iterations in which every lane of this wave has a unit
   if (chain_ok) {
-    const uint64_t wb = (uint64_t)blockIdx.x * kBlock + (tid & ~63u);
+    const uint64_t wb = (uint64_t)blockIdx.x * BS + (tid & ~63u);
     full = p.n >= wb + 64 ? (p.n - 64 - wb) / ustep + 1 : 0;
   }
   fe.sstep = (uint32_t)(ustep * p.stride);
@@ -750,7 +755,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                               (KIND == CTX_SYSCALL ? 64u : 0u) | (IMAGE ? 128u : 0u) |
                               ((uint32_t)((ustep / 64) % ncpu) << 16);
   uint64_t it = 0;
-  for (uint64_t u0 = ordered ? 0 : (uint64_t)blockIdx.x * kBlock; u0 < p.n; u0 += ustep, it++) {
+  for (uint64_t u0 = ordered ? 0 : (uint64_t)blockIdx.x * BS; u0 < p.n; u0 += ustep, it++) {
     uint64_t unit, slot, chunk, vcpu;
     bool active, desc_ok;
     uint32_t len;
@@ -934,7 +939,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         uint32_t next = c.lpc;
         if (csel) {
           ctx_for_cpp();
-          uint64_t *R = &Rg[tid];
+          uint64_t *R = c.R;
           // frames word-interleaved across the grid's lanes ([depth][word][lane]):
           // a wave's save of one word is one coalesced 512-B store
           uint64_t *const fbase = (uint64_t *)p.frames + (blockIdx.x * kBlock + tid);
@@ -1015,7 +1020,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       if (csel) {
         LaneEnv env;
         env.vcpu = vcpu;
-        env.scratch = p.lane_scratch ? (uint64_t)(uintptr_t)(p.lane_scratch + (uint64_t)blockIdx.x * kBlock + tid) : 0;
+        env.scratch = p.lane_scratch ? (uint64_t)(uintptr_t)(p.lane_scratch + (uint64_t)blockIdx.x * BS + tid) : 0;
         env.miss_fd = miss_fd;
         env.miss_hash = miss_hash;
         env.lru_stamp = (p.lru_seq << kLruSeqShift) | ((unit & 0xffffffffull) << kLruUnitShift);
@@ -1023,7 +1028,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         env.exact = ordered;
         env.rb = rbs;
         uint32_t cerr = E_OK;
-        uint64_t *R = &Rg[tid];
+        uint64_t *R = c.R;
         const uint64_t rv = call_helper(c.call_id, R[1 * kBlock], R[2 * kBlock], R[3 * kBlock], R[4 * kBlock],
                                         R[5 * kBlock], p.maps, p.ncpu,
                                         (p.first_unit + unit) ^ ((uint64_t)c.steps << 40), env, &cerr);
@@ -1076,7 +1081,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   // same-address device atomics serialize at the memory side (~12 ns each,
   // MI355X_MICROARCH.md 'fanin'), so one add per block instead of per wave
   // shortens the kernel's tail four-fold
-  __shared__ uint64_t wdelta[kBlock / 64][2][2];  // {tag = address | (4-byte ? 1 : 0), delta}
+  __shared__ uint64_t wdelta[BS / 64][2][2];  // {tag = address | (4-byte ? 1 : 0), delta}
   __shared__ uint32_t nlog;
   if ((tid & 63) == 0) {
     const uint32_t w = tid >> 6;
@@ -1087,9 +1092,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   }
   if (tid == 0) nlog = 0;
   __syncthreads();
-  if (p.rb_stage) rb_publish(p.maps, rbs, tid, kBlock);
+  if (p.rb_stage) rb_publish(p.maps, rbs, tid, BS);
   uint64_t *e = &wdelta[0][0][0];
-  constexpr uint32_t NE = kWaveCacheEntries;
+  constexpr uint32_t NE = wave_cache_entries(BS);
   if (tid == 0) {
     for (uint32_t i = 0; i < NE; i++) {
       if (!e[2 * i]) continue;
@@ -1103,7 +1108,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   }
   if (!p.flush_log) {
     if (!(p.dbg & 1))
-      for (uint32_t i = tid; i < 4 * p.comb_entries; i += kBlock) {
+      for (uint32_t i = tid; i < 4 * p.comb_entries; i += BS) {
         uint64_t tag, delta;
         comb_counter(i, tag, delta);
         flush_delta_tag(tag, delta);
@@ -1126,7 +1131,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       comb_counter(i - NE, tag, delta);
     }
   };
-  for (uint32_t r0 = 0; r0 < total; r0 += kBlock) {
+  for (uint32_t r0 = 0; r0 < total; r0 += BS) {
     uint64_t tag, delta;
     entry(r0 + tid, tag, delta);
     const uint64_t m = __ballot(tag && delta);
@@ -1136,7 +1141,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   const uint32_t used = nlog;
   __syncthreads();
   if (used > kMergeEntries / 8) {
-    for (uint32_t i = tid; i < total; i += kBlock) {
+    for (uint32_t i = tid; i < total; i += BS) {
       uint64_t tag, delta;
       entry(i, tag, delta);
       flush_delta_tag(tag, delta);
@@ -1146,7 +1151,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   }
   if (tid == 0) nlog = 0;
   __syncthreads();
-  for (uint32_t r0 = 0; r0 < total; r0 += kBlock) {
+  for (uint32_t r0 = 0; r0 < total; r0 += BS) {
     uint64_t tag, delta;
     entry(r0 + tid, tag, delta);
     const bool nz = tag && delta;
@@ -1208,23 +1213,21 @@ static_assert(kMergeEntries == 4u << 10, "k_comb_merge hashes into 2^10 sets of 
 // ---------------------------------------------------------------------------
 // Host-side launch wrappers
 // ---------------------------------------------------------------------------
-static size_t dyn_lds_bytes(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
-                            bool lcache, bool ctx_lds) {
-  return dyn_lds_for(kind, big_stack, stack_size, comb_entries, lcache, ctx_lds);
-}
-
+// block: kBlock, or kBigBlock for G launches without a tail-call image
 extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind, bool big_stack, uint32_t grid,
-                                                uint32_t ordered, hipStream_t stream) {
+                                                uint32_t ordered, uint32_t block, hipStream_t stream) {
   KParams q = *p;
   q.ordered = ordered;
-  const size_t dyn = dyn_lds_bytes(kind, big_stack, p->stack_size, p->comb_entries, p->lcache != 0, !p->gctx);
-  dim3 g(grid), b(kBlock);
   const bool image = q.tail_entry && !big_stack;
   const bool g_regs = q.gregs && !big_stack;
-#define L(K, B, I, G) hipLaunchKernelGGL((k_interp<K, B, I, G>), g, b, dyn, stream, q)
+  if (block != kBlock && (block != kBigBlock || !g_regs || image || ordered)) return hipErrorInvalidValue;
+  const size_t dyn = dyn_lds_for(kind, big_stack, p->stack_size, p->comb_entries, p->lcache != 0, !p->gctx, block);
+  dim3 g(grid), b(block);
+#define L(K, B, I, G) hipLaunchKernelGGL((k_interp<K, B, I, G, kBlock>), g, b, dyn, stream, q)
 #define LK(K)                                                          \
   if (big_stack) L(K, true, false, false);                             \
   else if (image) { if (g_regs) L(K, false, true, true); else L(K, false, true, false); } \
+  else if (g_regs && block == kBigBlock) hipLaunchKernelGGL((k_interp<K, false, false, true, kBigBlock>), g, b, dyn, stream, q); \
   else { if (g_regs) L(K, false, false, true); else L(K, false, false, false); }
   if (kind == CTX_XDP) {
     LK(CTX_XDP)
@@ -1246,12 +1249,14 @@ extern "C" hipError_t bpftime_amd_launch_merge(const uint64_t *log, uint32_t log
   return hipGetLastError();
 }
 
-extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds, bool gregs) {
+extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds, bool gregs, uint32_t block) {
   int n = 0;
   hipError_t e;
-#define O(K, B, G) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_interp<K, B, false, G>, kBlock, dyn_lds)
+#define O(K, B, G) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_interp<K, B, false, G, kBlock>, kBlock, dyn_lds)
 #define OK(K)                         \
   if (big_stack) O(K, true, false);   \
+  else if (gregs && block == kBigBlock) \
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_interp<K, false, false, true, kBigBlock>, kBigBlock, dyn_lds); \
   else if (gregs) O(K, false, true);  \
   else O(K, false, false);
   if (kind == CTX_XDP) {

@@ -26,8 +26,8 @@
 
 namespace bpftime_amd {
 extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind, bool big_stack, uint32_t grid,
-                                                uint32_t ordered, hipStream_t stream);
-extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds, bool gregs);
+                                                uint32_t ordered, uint32_t block, hipStream_t stream);
+extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds, bool gregs, uint32_t block);
 extern "C" hipError_t bpftime_amd_launch_merge(const uint64_t *log, uint32_t log_words, uint32_t nblocks,
                                                 hipStream_t stream);
 
@@ -469,8 +469,22 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   // too: only the C++ tier reads it (48 B of LDS per lane)
   const bool gctx = greg && b->ctx_kind == CTX_XDP && !p.needs_ctx && !im.d_tail_entry &&
                     !getenv("BPFTIME_AMD_LDS_CTX");
+  bool prog_arrays = false, rings = false;
+  for (uint32_t fd = 0; fd < kMaxFds; fd++)
+    if (r.kind[fd] == HKind::MAP) {
+      prog_arrays |= r.maps[fd].type == MT_PROG_ARRAY;
+      rings |= r.maps[fd].type == MT_RINGBUF;
+    }
+  const bool ordered = (b->flags & EBPF_BATCH_ORDERED) != 0;
+  const bool stage = rings && !ordered && !getenv("BPFTIME_AMD_NO_RB_STAGE");
+  // G launches without a tail-call image or ring staging run kBigBlock-lane
+  // blocks (common.hpp): one table and lookup cache per 16 waves
+  // (BPFTIME_AMD_BLOCK=256 keeps 4-wave blocks)
+  uint32_t block = greg && !im.d_tail_entry && !stage ? kBigBlock : kBlock;
+  if (const char *bs = getenv("BPFTIME_AMD_BLOCK"))
+    if (atoi(bs) == (int)kBlock) block = kBlock;
   auto dyn_of = [&](uint32_t e) {
-    return dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, e, p.lcache, !gctx);
+    return dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, e, p.lcache, !gctx, block);
   };
   if (p.comb_entries) {
     // the table's reach: a counter that finds no entry is a device atomic
@@ -495,7 +509,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     // blocks / CU 1.32 ms, 1792 at 3 1.57, 1536 at 3 1.42 -- nor does reach
     // beyond hint / 32 at the same residency: flow-hash 3072 1.29,
     // syscall-agg 768 / 984 0.672 / 0.677 against 512 0.664)
-    while (e > kComb && bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn_of(e), greg) < 1) e /= 2;
+    while (e > kComb && bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn_of(e), greg, block) < 1) e /= 2;
     if (const char *ce = getenv("BPFTIME_AMD_COMB_ENTRIES")) e = (uint32_t)atoi(ce) & ~7u;
     p.comb_entries = e;
   }
@@ -544,7 +558,6 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     error = "LRU table upkeep failed";
     return -1;
   }
-  const bool ordered = (b->flags & EBPF_BATCH_ORDERED) != 0;
   uint32_t grid = 1;
   if (!ordered) {
     static int cus = 0;
@@ -556,9 +569,9 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       cus = prop.multiProcessorCount;
     }
     const size_t dyn = dyn_of(p.comb_entries);
-    int occ = bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn, greg);
+    int occ = bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn, greg, block);
     if (occ < 1) occ = 1;
-    uint64_t want = (b->count + kBlock - 1) / kBlock;
+    uint64_t want = (b->count + block - 1) / block;
     // resident blocks x 4 when the program has no combining table: more,
     // shorter-lived blocks keep more packet loads in flight at the kernel's
     // tail (xdp-counter 0.453 -> 0.423 ms per 2^24 packets, r01d sweep);
@@ -575,7 +588,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     if (im.d_tail_entry && grid > kTailGrid) grid = kTailGrid;  // one frame stack per lane of the grid
   }
   if (greg) {
-    p.gregs = (uint64_t *)regs.get(s, (uint64_t)grid * 11 * kBlock * 8);
+    p.gregs = (uint64_t *)regs.get(s, (uint64_t)grid * 11 * block * 8);
     if (!p.gregs) {
       error = "register copy allocation failed";
       return -1;
@@ -601,16 +614,9 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   // (dev_helpers.hpp RbStage; not in ORDERED batches: exact order), then the
   // lanes' global XDP ctx (gctx)
   {
-    bool prog_arrays = false, rings = false;
-    for (uint32_t fd = 0; fd < kMaxFds; fd++)
-      if (r.kind[fd] == HKind::MAP) {
-        prog_arrays |= r.maps[fd].type == MT_PROG_ARRAY;
-        rings |= r.maps[fd].type == MT_RINGBUF;
-      }
-    const bool stage = rings && !ordered && !getenv("BPFTIME_AMD_NO_RB_STAGE");
     if (prog_arrays || stage || gctx) {
-      const uint64_t words = (uint64_t)grid * kBlock * 8, sbytes = stage ? (uint64_t)grid * kRbStageBytes : 0;
-      uint8_t *base = (uint8_t *)scratch.get(s, words + sbytes + (gctx ? 48ull * grid * kBlock : 0));
+      const uint64_t words = (uint64_t)grid * block * 8, sbytes = stage ? (uint64_t)grid * kRbStageBytes : 0;
+      uint8_t *base = (uint8_t *)scratch.get(s, words + sbytes + (gctx ? 48ull * grid * block : 0));
       if (!base) {
         error = "lane scratch allocation failed";
         return -1;
@@ -623,7 +629,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   // a block-end flush log when the blocks hold per-lane counter tables:
   // merged by a second launch instead of every block adding its table
   if (p.comb_entries && grid > kMergeGroup && !getenv("BPFTIME_AMD_NO_MERGE")) {
-    p.log_words = log_words_for(p.comb_entries);
+    p.log_words = log_words_for(p.comb_entries, block);
     p.flush_log = (uint64_t *)logs.get(s, (uint64_t)grid * p.log_words * 8);
     if (!p.flush_log) {
       error = "flush log allocation failed";
@@ -636,10 +642,10 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   }
   if (getenv("BPFTIME_AMD_VERBOSE"))
     fprintf(stderr,
-            "bpftime_amd: launch units %llu grid %u comb %u lcache %u stage %u stack %u gregs %d gctx %d unwind %d\n",
-            (unsigned long long)b->count, grid, p.comb_entries, p.lcache, p.stage, (unsigned)prog.stack_size,
+            "bpftime_amd: launch units %llu grid %u block %u comb %u lcache %u stage %u stack %u gregs %d gctx %d unwind %d\n",
+            (unsigned long long)b->count, grid, block, p.comb_entries, p.lcache, p.stage, (unsigned)prog.stack_size,
             p.gregs ? 1 : 0, p.gctx ? 1 : 0, p.unwind_idx);
-  hipError_t e = bpftime_amd_launch_interp(&p, b->ctx_kind, prog.big_stack, grid, ordered ? 1 : 0, s);
+  hipError_t e = bpftime_amd_launch_interp(&p, b->ctx_kind, prog.big_stack, grid, ordered ? 1 : 0, block, s);
   if (e == hipSuccess && p.flush_log) e = bpftime_amd_launch_merge(p.flush_log, p.log_words, grid, s);
   if (e != hipSuccess) {
     error = std::string("kernel launch failed: ") + hipGetErrorString(e);
