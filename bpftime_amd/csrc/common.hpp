@@ -236,7 +236,7 @@ struct KParams {
   uint64_t lru_seq;       // this launch's LRU stamp sequence (common.hpp kLruSeqShift)
   uint32_t tail_ctx_mask;    // XDP images: ctx words / stack words a frame keeps (loader.cpp tail_save_masks)
   uint32_t tail_stack_mask;
-  uint32_t lcache;           // 1 = the block's hash-lookup cache exists (common.hpp kLcacheEntries)
+  uint32_t lcache;           // 1 = the block's hash-lookup cache exists (common.hpp kLcacheSets)
   uint64_t *gregs;           // r0..r10 copies for the C++ tier: [grid][11][kBlock] u64 (k_interp G), or nullptr (LDS)
   uint8_t *rb_stage;         // ring-buffer staging: [grid][kRbStageBytes] right after lane_scratch's words, or nullptr
   uint8_t *gctx;             // XDP: the lanes' ctx in global memory ([grid lane] x 48 B, after the staging), or nullptr (LDS)
@@ -271,11 +271,12 @@ constexpr uint32_t kBigBlock = 1024;
 // table (a u32 tag + a 16-byte delta granule per entry).
 constexpr uint32_t kTenvBytes = 48;  // gen_fast.py TENV: tail-call constants, the register copy base
 // Hash-lookup cache of a block (programs whose hash lookups the loader marks
-// FW_LCACHE: no deletions): kLcacheEntries {u32 tag, u32 (slot + 1) | fd << 22}
-// entries, 2-way sets, right below the tail-call constants.  A slot found for
-// a key stays that key's slot for the rest of a launch when nothing deletes.
-constexpr uint32_t kLcacheEntries = 2048;  // gen_fast.py LC_ENTRIES
-constexpr uint32_t kLcacheBytes = 8 * kLcacheEntries;
+// FW_LCACHE: no deletions): kLcacheSets 2-way sets, the ways' 16-B keys
+// ([set][way]) then their u32 entries {(slot + 1) | fd << 22}, right below
+// the tail-call constants (gen_fast.py lcache_probe).  A slot found for a key
+// stays that key's slot for the rest of a launch when nothing deletes.
+constexpr uint32_t kLcacheSets = 1024;  // gen_fast.py LC_SETS
+constexpr uint32_t kLcacheBytes = (32 + 8) * kLcacheSets;
 inline size_t dyn_lds_for(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
                           bool lcache = false, bool ctx_lds = true, uint32_t block = kBlock) {
   return (size_t)block * ((kind == CTX_XDP && ctx_lds ? 48 : 0) + (big_stack ? 0 : stack_size)) +

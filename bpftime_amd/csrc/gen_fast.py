@@ -112,7 +112,9 @@ PM = ["s[88:89]", "s[90:91]", "s[94:95]"]
 KP = 3
 WAYS = 8  # combining-table associativity
 TENV = 48  # launch constants below the combining table (common.hpp kTenvBytes)
-LC_ENTRIES = 2048  # hash-lookup cache entries, 2-way (common.hpp kLcacheEntries)
+LC_SETS = 1024  # hash-lookup cache sets of 2 ways (common.hpp kLcacheSets)
+LC_KEYS = 32 * LC_SETS  # the ways' 16-B keys, then their u32 entries
+LC_BYTES = LC_KEYS + 8 * LC_SETS
 
 # staged (link-resolved) packet / slot accesses
 STAGED_LD = ["LDXS1", "LDXS2", "LDXS4", "LDXS2X", "LDXS4X", "LDXS8A", "LDXS8U"]
@@ -983,67 +985,90 @@ class Gen:
                "v_cndmask_b32 v50, v50, v42, vcc", "v_cndmask_b32 v51, v51, v43, vcc",
                "v_cvt_u32_f64 v56, v[50:51]")
 
-    # ---- the block's hash-lookup cache (common.hpp kLcacheEntries) ----
-    # LC_ENTRIES / 2 two-way sets of {u32 tag, u32 (slot + 1) | fd << 22} right below
-    # the launch constants (%[comb] - TENV - kLcacheBytes).  The tag is the
-    # key itself for 4-byte keys (a hit needs no memory access) and the low
-    # word of the h*31 hash otherwise (a hit re-reads the slot's key once,
-    # instead of the index entry and then the slot).  Only hash lookups the
-    # loader marked FW_LCACHE use it: nothing deletes during their launch (the
-    # program cannot, and vm_api.cpp / maps.cpp keep every other deleting
-    # launch and host delete from overlapping it), so a slot found for a key
-    # stays that key's slot.  v82 = the set's address,
-    # v83 = the tag, s49 = the map fd, kept until the lookup ends.
+    # ---- the block's hash-lookup cache (common.hpp kLcacheSets) ----
+    # LC_SETS two-way sets right below the launch constants (%[comb] - TENV -
+    # LC_BYTES): the ways' keys (16 B each, [set][way], the key's first kd
+    # words), then the ways' entries {u32 (slot + 1) | fd << 22} ([set][way],
+    # at + LC_KEYS).  The set is a mix of the key words and the fd, so a hit
+    # needs neither the h*31 hash nor a memory access: the whole key is
+    # compared in LDS.  Entries are written once: a lane that found its key
+    # claims an empty way (0 -> -1 by compare-and-swap), writes the key, then
+    # the entry; a reader reads the entries before the keys, and one CU's LDS
+    # keeps every wave's accesses in order, so an entry it sees is complete.
+    # Only hash lookups the loader marked FW_LCACHE use it: nothing deletes
+    # during their launch (the program cannot, and vm_api.cpp / maps.cpp keep
+    # every other deleting launch and host delete from overlapping it), so a
+    # slot found for a key stays that key's slot.  A probe leaves v82 / v83 =
+    # the key / entry address of the set's first empty way (v83 = -1: none)
+    # for the fill; s49 = the map fd.
     def lcache_on(self, skip):
         self.e("s_bitcmp1_b32 s41, 1", f"s_cbranch_scc0 {skip}",
                "s_cmp_gt_u32 s66, 0x3ffffe", f"s_cbranch_scc1 {skip}")      # slot + 1 in 22 bits
 
     def lcache_probe(self, kd, done):
-        """Lanes whose key the cache holds get r0 and leave s[60:61]."""
+        """Lanes whose key (v44..v(43 + kd)) the cache holds get r0 and leave
+        s[60:61]; the others go on to the hash with exec = s[60:61]."""
         skip = self.label("lcs")
+        self.e("v_mov_b32 v83, -1")
         self.lcache_on(skip)
-        self.e("v_xor_b32 v41, v48, v49",
-               "s_mul_i32 s69, s49, 0x9e3779b1", "v_xor_b32 v41, s69, v41",
-               "s_mov_b32 s69, 0x85ebca6b", "v_mul_lo_u32 v41, v41, s69",
-               f"v_lshrrev_b32 v41, {32 - (LC_ENTRIES // 2).bit_length() + 1}, v41",
-               "v_lshlrev_b32 v41, 4, v41",                                     # set * 16 (LC_ENTRIES / 2 sets)
-               f"s_sub_u32 s69, %[comb], {TENV + 8 * LC_ENTRIES}", "v_add_u32 v82, s69, v41",
-               f"v_mov_b32 v83, v{44 if kd == 1 else 48}",
-               "ds_read_b128 v[54:57], v82", "s_waitcnt lgkmcnt(0)",
+        mult = ["0x9e3779b1", "0x85ebca6b", "0xc2b2ae35", "0x27d4eb2f"]
+        self.e("s_mul_i32 s69, s49, 0x165667b1", "v_mov_b32 v41, s69")
+        for j in range(kd):
+            self.e(f"s_mov_b32 s69, {mult[j]}", f"v_mul_lo_u32 v42, v{44 + j}, s69", "v_xor_b32 v41, v41, v42")
+        self.e("v_lshrrev_b32 v42, 15, v41", "v_xor_b32 v41, v41, v42",
+               "s_mov_b32 s69, 0x2c1b3c6d", "v_mul_lo_u32 v41, v41, s69",
+               f"v_lshrrev_b32 v41, {32 - LC_SETS.bit_length() + 1}, v41",        # the set
+               f"s_sub_u32 s69, %[comb], {TENV + LC_BYTES}",
+               "v_lshl_add_u32 v82, v41, 5, s69",                                 # its keys
+               f"s_add_u32 s69, s69, {LC_KEYS}",
+               "v_lshl_add_u32 v83, v41, 3, s69",                                 # its entries
+               "ds_read_b64 v[54:55], v83",                                       # entries first
+               "ds_read_b128 v[56:59], v82",
+               "ds_read_b128 v[48:51], v82 offset:16",
+               "s_waitcnt lgkmcnt(0)",
                "s_lshl_b32 s69, s49, 22")
-        for way, (t, v, m) in enumerate(((54, 55, "s[56:57]"), (56, 57, "s[54:55]"))):
-            self.e(f"v_cmp_eq_u32 vcc, v{t}, v83",
-                   f"v_and_b32 v58, 0xffc00000, v{v}", f"v_cmp_eq_u32 {m}, s69, v58", f"s_and_b64 {m}, {m}, vcc",
-                   f"v_cmp_ne_u32 vcc, 0, v{v}", f"s_and_b64 {m}, {m}, vcc")
-        self.e("v_cndmask_b32 v58, v57, v55, s[56:57]",
+        for way, (ent, k0, m) in enumerate(((54, 56, "s[56:57]"), (55, 48, "s[54:55]"))):
+            self.e(f"v_and_b32 v42, 0xffc00000, v{ent}", f"v_cmp_eq_u32 {m}, s69, v42",
+                   f"v_cmp_ne_u32 vcc, 0, v{ent}", f"s_and_b64 {m}, {m}, vcc",
+                   f"v_cmp_ne_u32 vcc, -1, v{ent}", f"s_and_b64 {m}, {m}, vcc")
+            for j in range(kd):
+                self.e(f"v_cmp_eq_u32 vcc, v{k0 + j}, v{44 + j}", f"s_and_b64 {m}, {m}, vcc")
+        # the fill's way: the first empty one (v83 = -1: both taken)
+        self.e("v_cmp_eq_u32 vcc, 0, v54",
+               "v_add_u32 v42, 4, v83", "v_add_u32 v41, 16, v82",
+               "v_cmp_eq_u32 s[52:53], 0, v55",
+               "v_cndmask_b32 v42, -1, v42, s[52:53]",
+               "v_cndmask_b32 v83, v42, v83, vcc",
+               "v_cndmask_b32 v82, v41, v82, vcc",
+               "v_cndmask_b32 v58, v55, v54, s[56:57]",
                "v_and_b32 v58, 0x3fffff, v58", "v_add_u32 v58, -1, v58",          # the slot
                "s_or_b64 s[56:57], s[56:57], s[54:55]", "s_and_b64 s[56:57], s[56:57], exec",
                f"s_cbranch_scc0 {skip}",
                "v_mov_b32 v59, s68",
-               "v_mad_u64_u32 v[42:43], s[54:55], v58, v59, s[64:65]")
-        if kd > 1:  # a hash tag: compare the slot's key
-            self.e("s_mov_b64 exec, s[56:57]",
-                   "global_load_dwordx4 v[54:57], v[42:43], off offset:8 sc1",
-                   "s_waitcnt vmcnt(0)",
-                   "v_cmp_eq_u32 s[54:55], v54, v44")
-            for j in range(1, kd):
-                self.e(f"v_cmp_eq_u32 vcc, v{54 + j}, v{44 + j}", "s_and_b64 s[54:55], s[54:55], vcc")
-            self.e("s_and_b64 s[56:57], s[56:57], s[54:55]",
-                   "s_mov_b64 exec, s[60:61]")
-        self.e("s_mov_b64 s[54:55], exec", "s_mov_b64 exec, s[56:57]",            # exec = hits
+               "v_mad_u64_u32 v[42:43], s[54:55], v58, v59, s[64:65]",
+               "s_mov_b64 s[54:55], exec", "s_mov_b64 exec, s[56:57]",            # exec = hits
                f"v_add_co_u32 v{R0}, vcc, s70, v42", f"v_addc_co_u32 v{R0 + 1}, vcc, 0, v43, vcc",
                "s_andn2_b64 s[60:61], s[54:55], s[56:57]", "s_mov_b64 exec, s[60:61]",
                f"s_cbranch_execz {done}",
                f"{skip}:")
 
     def lcache_fill(self, vslot):
-        """exec = lanes that found their key in slot v<vslot>: remember it
-        (the way picked by a tag bit; a racing lane of the same set may win)."""
-        skip = self.label("lcf")
+        """exec = lanes that found their key in slot v<vslot>: claim the
+        probe's empty way (v83) and write the key, then the entry (a lane
+        that loses the claim to another key leaves the cache as it is)."""
+        skip, out = self.label("lcf"), self.label("lco")
         self.lcache_on(skip)
-        self.e(f"v_add_u32 v59, 1, v{vslot}", "s_lshl_b32 s69, s49, 22", "v_or_b32 v59, s69, v59",
-               "v_bfe_u32 v58, v83, 3, 1", "v_lshlrev_b32 v58, 3, v58", "v_add_u32 v58, v82, v58",
-               "ds_write2_b32 v58, v83, v59 offset1:1",
+        self.e("s_mov_b64 s[52:53], exec",
+               "v_cmp_ne_u32 vcc, -1, v83", "s_and_b64 exec, exec, vcc", f"s_cbranch_execz {out}",
+               "v_mov_b32 v58, 0", "v_mov_b32 v59, -1",
+               "ds_cmpst_rtn_b32 v42, v83, v58, v59",                            # claim: 0 -> -1
+               "s_waitcnt lgkmcnt(0)",
+               "v_cmp_eq_u32 vcc, 0, v42", "s_and_b64 exec, exec, vcc", f"s_cbranch_execz {out}",
+               f"v_add_u32 v59, 1, v{vslot}", "s_lshl_b32 s69, s49, 22", "v_or_b32 v59, s69, v59",
+               "ds_write_b128 v82, v[44:47]",                                     # the key, then
+               "ds_write_b32 v83, v59",                                           # the entry
+               f"{out}:",
+               "s_mov_b64 exec, s[52:53]",
                f"{skip}:")
 
     def index_probe(self, kd, done):
@@ -1101,6 +1126,7 @@ class Gen:
         for kd in (1, 2, 3, 4):
             nxt = self.label("kdn")
             self.e(f"s_cmp_lg_u32 s73, {4 * kd}", f"s_cbranch_scc1 {nxt}")
+            self.lcache_probe(kd, done)
             # h = sum over key bytes of h * 31 + byte (size_t arithmetic)
             self.e("v_mov_b32 v48, 0", "v_mov_b32 v49, 0")
             for i in range(4 * kd):
@@ -1108,7 +1134,6 @@ class Gen:
                        "v_sub_co_u32 v48, vcc, v50, v48", "v_subb_co_u32 v49, vcc, v51, v49, vcc",
                        f"v_bfe_u32 v50, v{44 + i // 4}, {8 * (i % 4)}, 8",
                        "v_add_co_u32 v48, vcc, v48, v50", "v_addc_co_u32 v49, vcc, 0, v49, vcc")
-            self.lcache_probe(kd, done)
             self.index_probe(kd, done)
             # idx = h % nbuckets: h = ((hi * 2^16 + lo >> 16) * 2^16 + lo & 0xffff)
             self.e("v_cvt_f64_u32 v[58:59], s66", "v_rcp_f64 v[54:55], v[58:59]",

@@ -627,7 +627,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   uint64_t *comb_d = (uint64_t *)(comb + p.comb_entries);
   for (uint32_t i = tid; i < 5 * p.comb_entries; i += BS) comb[i] = 0;
   if (p.lcache)
-    for (uint32_t i = tid; i < 2 * kLcacheEntries; i += BS) lcache[i] = 0;
+    for (uint32_t i = tid; i < kLcacheBytes / 4; i += BS) lcache[i] = 0;
   // ring-buffer staging (dev_helpers.hpp RbStage): LDS counters of the block
   __shared__ uint32_t rb_used, rb_end, rb_nrec;
   __shared__ int32_t rb_fd;
