@@ -1141,7 +1141,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const uint32_t used = nlog;
   __syncthreads();
   if (used > kMergeEntries / 8) {
-    for (uint32_t i = tid; i < total; i += BS) {
+    for (uint32_t i = tid; i < total && !(p.dbg & 1); i += BS) {
       uint64_t tag, delta;
       entry(i, tag, delta);
       flush_delta_tag(tag, delta);

@@ -510,6 +510,24 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     // beyond hint / 32 at the same residency: flow-hash 3072 1.29,
     // syscall-agg 768 / 984 0.672 / 0.677 against 512 0.664)
     while (e > kComb && bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn_of(e), greg, block) < 1) e /= 2;
+    // one 1024-lane block per CU: a table that wants 2048 entries or more
+    // takes the rest of the CU's LDS (multiples of 8 ways), since every
+    // counter it misses is a memory-side atomic.  Measured (flow-hash, one
+    // MI355X, same box): 2048 entries 1.027 ms, 2560 0.980, 3072 0.945,
+    // 3584 0.914, 3840 0.898, 4032 0.891
+    if (block == kBigBlock && e >= 2048) {
+      static std::mutex fill_mu;
+      static std::map<size_t, uint32_t> fill;  // (dyn_of(0), ctx kind) -> the largest table that fits
+      std::lock_guard<std::mutex> g(fill_mu);
+      const size_t key = dyn_of(0) * 4 + b->ctx_kind;
+      auto it = fill.find(key);
+      if (it == fill.end()) {
+        uint32_t f = kCombMax;
+        while (f > e && bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn_of(f), greg, block) < 1) f -= 32;
+        it = fill.emplace(key, f).first;
+      }
+      e = it->second > e ? it->second : e;
+    }
     if (const char *ce = getenv("BPFTIME_AMD_COMB_ENTRIES")) e = (uint32_t)atoi(ce) & ~7u;
     p.comb_entries = e;
   }
