@@ -20,6 +20,7 @@ constexpr uint32_t kBlock = 256;        // threads per workgroup (4 waves)
 constexpr uint32_t kLdsStackMax = 64;   // per-lane stack bytes kept in LDS
 constexpr uint32_t kComb = 256;         // per-block LDS combining entries (counter adds), minimum
 constexpr uint32_t kCombMax = 4096;     // ... and maximum (a multiple of 8 in between, vm_api.cpp)
+constexpr uint32_t kMissParts = 256;    // miss-log partitions (KParams::miss_log)
 
 // Internal (pre-decoded) opcodes.  The device switch dispatches on these; the
 // set is dense so the compiler's binary search over cases stays shallow.
@@ -53,6 +54,9 @@ constexpr uint8_t A_FETCH = 0x08;   // X_RMW_ADD: the loaded register stays live
 
 // FInsn::w1 flags (per entry form and launch, loader.cpp build_fast / link_fast)
 constexpr uint32_t FW_LCACHE = 2;   // hash lookup: probe / fill the block's LDS lookup cache (gen_fast.py)
+constexpr uint32_t FW_MOVI = 4;     // a jump / exit with a fused `mov64 r, imm32` in front of it
+                                    // (loader.cpp fuse_pairs: r in bits 3..6, the imm in aux)
+constexpr uint32_t FW_MOVI_REG_SHIFT = 3;
 constexpr uint32_t FW_NODEFER = 1;  // counter add: apply it to memory now (a later access of
                                     // the same unit may read or overwrite it, or the batch is
                                     // ORDERED): no per-wave delta cache, no LDS combining table
@@ -240,7 +244,22 @@ struct KParams {
   uint64_t *gregs;           // r0..r10 copies for the C++ tier: [grid][11][kBlock] u64 (k_interp G), or nullptr (LDS)
   uint8_t *rb_stage;         // ring-buffer staging: [grid][kRbStageBytes] right after lane_scratch's words, or nullptr
   uint8_t *gctx;             // XDP: the lanes' ctx in global memory ([grid lane] x 48 B, after the staging), or nullptr (LDS)
+  uint64_t *miss_log;        // combining-table misses: [grid][kMissParts][miss_cap] {tag, delta} records, or nullptr
+  uint32_t *miss_counts;     // [grid][kMissParts] records each block wrote (k_miss_merge reads them)
+  uint32_t miss_cap;         // records per block and partition (even)
 };
+
+// Combining-table misses.  A deferred counter add that finds no table entry
+// (the set is full of other granules) does not become a memory-side atomic
+// at once: its lane appends {tag, delta} records (tag = address | (4-byte ?
+// 1 : 0); two records per lane, the second {address + 8, delta} for fused
+// pairs, else empty) to its block's region of a miss log, partitioned by a
+// hash of the address (gen_fast.py comb_add), counting in LDS.  A second
+// launch, k_miss_merge, gives every partition a block that combines the
+// records of all blocks in an LDS table and adds each address's sum with one
+// device atomic: the long tail of a Zipf key set appears in many blocks, a
+// few times in each.  A full partition region, or a merge table, adds
+// directly.  (kMissParts partitions: with the constants at the top)
 
 // Block-end counter deltas.  Every block holds its counter deltas (the wave
 // caches of uniform counters, the LDS combining table) until it ends; with a
@@ -269,7 +288,9 @@ constexpr uint32_t kBigBlock = 1024;
 // stacks (LDS-stack programs), 48 B of launch constants (interp.hip
 // tenv; the asm finds them 48 B before the combining table), the combining
 // table (a u32 tag + a 16-byte delta granule per entry).
-constexpr uint32_t kTenvBytes = 48;  // gen_fast.py TENV: tail-call constants, the register copy base
+// tenv: 8 u64 launch constants (tail calls, the register copy base, the
+// block's miss-log region and its capacity), then kMissParts u32 miss counters
+constexpr uint32_t kTenvBytes = 64 + 4 * kMissParts;  // gen_fast.py TENV
 // Hash-lookup cache of a block (programs whose hash lookups the loader marks
 // FW_LCACHE: no deletions): kLcacheSets 2-way sets, the ways' 16-B keys
 // ([set][way]) then their u32 entries {(slot + 1) | fd << 22}, right below

@@ -636,10 +636,12 @@ constexpr uint64_t kRbSlack = kRbMaxWaves * kRbWaveMax;    // 32 MiB
 // can no longer give to records.  A wave whose records do not fit the chunk
 // reserves directly.  Right after the chunk's reservation its first header
 // reads BUSY (one record spanning the chunk), and rb_publish writes that
-// header last, after every other byte of the chunk: a consumer polling while
-// the block runs stops at the chunk as it stops at any reserved record (the
-// reference writes each BUSY header before moving the position, under its
-// spin lock).  Consumers see the same records in another parallel order.
+// header last: a consumer polling while the block runs stops at the chunk as
+// it stops at any reserved record (the reference writes each BUSY header
+// before moving the position, under its spin lock; here the producer
+// position moves a few instructions before the BUSY header lands, and
+// bpftime_amd_ringbuf_fetch synchronizes the device before it reads).
+// Consumers see the same records in another parallel order.
 // (sizes: common.hpp kRbStage*)
 struct RbStage {
   uint8_t *buf = nullptr;  // this block's area: records, then u32 offsets (nullptr: no staging)
@@ -706,18 +708,21 @@ __device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size, con
             int32_t got = -2;
             // the fast path's condition (below), for a chunk
             if (m.max_entries >= 2 * kRbSlack && (uint64_t)m.max_entries - (prod - cons) >= kRbStageRec + kRbSlack) {
-              const uint64_t cb = __hip_atomic_fetch_add(G64(m.data + 128), (uint64_t)kRbStageRec,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              *st.base = cb;
-              // the chunk reads as one reserved record until the block publishes
-              const uint64_t h = m.data + 256 + (cb & (m.max_entries - 1));
-              __hip_atomic_store(G32(h + 4), (uint32_t)fd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              __hip_atomic_store(G32(h), (kRbStageRec - RB_HDR) | RB_BUSY, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+              *st.base = __hip_atomic_fetch_add(G64(m.data + 128), (uint64_t)kRbStageRec, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
               got = (int32_t)fd;
             }
             __hip_atomic_store(st.fd, got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             cur = got;
+            if (got >= 0) {
+              // the chunk reads as one reserved record until the block
+              // publishes (written once the block's other waves may use the
+              // chunk: inside the deciding window, where they reserve
+              // directly, the two stores cost the sampler 7 %)
+              const uint64_t h = m.data + 256 + (*st.base & (m.max_entries - 1));
+              *(int32_t *)(uintptr_t)(h + 4) = (int32_t)fd;
+              *(uint32_t *)(uintptr_t)h = (kRbStageRec - RB_HDR) | RB_BUSY;
+            }
           }
           sfd = cur;
         }
@@ -814,8 +819,15 @@ __device__ uint64_t rb_output(const DMap *maps, uint64_t fd, uint64_t data, uint
 // The block's staged records into its chunk of the ring (every wave of the
 // block is done; called by every thread of the block), one thread per
 // record, and the chunk's unused tail as one DISCARD record.  The chunk's
-// first header word (BUSY since the reservation) is written last, with
-// release order after every other byte of the chunk.
+// first header word (BUSY since the reservation) is written last, after the
+// block's barrier: a consumer polling the ring from this XCD stops at the
+// chunk until the block publishes.  (Ordering that store after the others
+// for every XCD would take an agent-scope release -- an L2 write-back per
+// block: 1.40 -> 2.09 ms per 2^24 sampled frames -- or write-through stores
+// of the whole chunk drained before it: 1.40 -> 1.51 ms.  The ring's
+// consumer here, bpftime_amd_ringbuf_fetch, synchronizes the device before
+// it reads, as the reference's consumer reads after its producers' spin
+// lock, so neither is paid.)
 __device__ void rb_publish(const DMap *maps, const RbStage &st, uint32_t tid, uint32_t nthreads) {
   const int32_t fd = *st.fd;
   if (!st.buf || fd < 0) return;
@@ -830,7 +842,7 @@ __device__ void rb_publish(const DMap *maps, const RbStage &st, uint32_t tid, ui
     const uint64_t *src = (const uint64_t *)(st.buf + off);
     uint64_t *dst = (uint64_t *)(uintptr_t)(d + ((base + off) & mask));
     for (uint32_t w = off ? 0 : 1; w < total / 8; w++) dst[w] = src[w];
-    if (!off) ((int32_t *)dst)[1] = ((const int32_t *)src)[1];
+    if (!off) ((uint32_t *)dst)[1] = ((const uint32_t *)src)[1];
   }
   uint32_t first = 0;  // the chunk's first header word
   if (end < kRbStageRec) {
@@ -844,9 +856,8 @@ __device__ void rb_publish(const DMap *maps, const RbStage &st, uint32_t tid, ui
     }
   }
   if (end) first = *(const uint32_t *)st.buf;  // the record staged at offset 0
-  __threadfence();
   __syncthreads();
-  if (tid == 0) __hip_atomic_store(G32(d + (base & mask)), first, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) *(uint32_t *)(uintptr_t)(d + (base & mask)) = first;
 }
 
 struct LaneEnv {

@@ -111,7 +111,8 @@ PIP = ["s86", "s87", "s93"]
 PM = ["s[88:89]", "s[90:91]", "s[94:95]"]
 KP = 3
 WAYS = 8  # combining-table associativity
-TENV = 48  # launch constants below the combining table (common.hpp kTenvBytes)
+MISS_PARTS = 256  # miss-log partitions (common.hpp kMissParts)
+TENV = 64 + 4 * MISS_PARTS  # launch constants + miss counters below the combining table (common.hpp kTenvBytes)
 LC_SETS = 1024  # hash-lookup cache sets of 2 ways (common.hpp kLcacheSets)
 LC_KEYS = 32 * LC_SETS  # the ways' 16-B keys, then their u32 entries
 LC_BYTES = LC_KEYS + 8 * LC_SETS
@@ -128,7 +129,7 @@ def handler_ids():
             for k in ("R", "I"):
                 ids.append(f"A{w}_{op}_{k}")
         ids.append(f"A{w}_NEG")
-    ids += ["LE16", "LE32", "BE16", "BE32", "BE64", "NOP"]
+    ids += ["LE16", "LE32", "BE16", "BE32", "BE64", "NOP", "LEA"]
     for sz in (1, 2, 4, 8):
         ids += [f"LDX{sz}", f"STX{sz}", f"ST{sz}"]
     for sz in (1, 2, 4, 8):
@@ -382,9 +383,52 @@ class Gen:
                f"{noclaim}:")
         self.e(f"{direct}:",
                "s_andn2_b64 exec, s[60:61], s[54:55]", f"s_cbranch_execz {done}",
-               "s_bitcmp1_b32 %[oflags], 2", f"s_cbranch_scc1 {done}",          # (BPFTIME_AMD_DBG 128: timing only)
-               *glob_add)
+               "s_bitcmp1_b32 %[oflags], 2", f"s_cbranch_scc1 {done}")         # (BPFTIME_AMD_DBG 128: timing only)
+        self.miss_log(sz, pair, done)
+        self.e(*glob_add)
         self.e(f"{done}:", "s_mov_b64 exec, s[60:61]")
+
+    def miss_log(self, sz, pair, done):
+        """exec = lanes whose add found no table entry: append their {tag,
+        delta} records (two per lane: the pair's second counter, or an empty
+        record) to the block's miss-log region (tenv[5], 0 = none; tenv[6] =
+        records per partition) in the partition of their address, claimed
+        with an LDS counter per partition (common.hpp kMissParts,
+        interp.hip k_miss_merge).  Lanes whose partition is full, or that are
+        misaligned, are left in exec for a direct add."""
+        atom, back = self.label("mla"), self.label("mlb")
+        self.e(f"s_sub_u32 s69, %[comb], {TENV - 40}", "v_mov_b32 v41, s69",
+               "ds_read_b64 v[50:51], v41", "ds_read_b32 v56, v41 offset:8",
+               "s_waitcnt lgkmcnt(0)",
+               "v_readfirstlane_b32 s52, v50", "v_readfirstlane_b32 s53, v51", "v_readfirstlane_b32 s71, v56",
+               "s_cmp_eq_u64 s[52:53], 0", f"s_cbranch_scc1 {atom}",
+               "s_mov_b64 s[62:63], exec",                                       # the direct lanes
+               f"v_and_b32 v41, {sz - 1}, v48", "v_cmp_eq_u32 vcc, 0, v41",
+               "s_and_b64 exec, exec, vcc", f"s_cbranch_execz {back}",
+               "v_lshrrev_b32 v41, 3, v48", "s_mov_b32 s69, 0x9e3779b1", "v_mul_lo_u32 v41, v41, s69",
+               f"v_lshrrev_b32 v41, {32 - (MISS_PARTS.bit_length() - 1)}, v41",   # the partition
+               f"s_sub_u32 s69, %[comb], {TENV - 64}", "v_lshl_add_u32 v42, v41, 2, s69",
+               "v_mov_b32 v43, 2",
+               "ds_add_rtn_u32 v43, v42, v43",                                   # its slot (even)
+               "s_waitcnt lgkmcnt(0)",
+               "v_cmp_gt_u32 vcc, s71, v43", "s_and_b64 exec, exec, vcc", f"s_cbranch_execz {back}",
+               "s_andn2_b64 s[62:63], s[62:63], exec",                           # logged: not direct
+               "v_mad_u32_u24 v42, v41, s71, v43", "v_lshlrev_b32 v42, 4, v42",
+               f"v_or_b32 v56, {1 if sz == 4 else 0}, v48", "v_mov_b32 v57, v49",
+               "v_mov_b32 v58, v46", "v_mov_b32 v59, v47" if sz == 8 else "v_mov_b32 v59, 0",
+               "global_store_dwordx4 v42, v[56:59], s[52:53]",
+               # (a store of more than 8 bytes reads its data registers after
+               # issue: a VALU write of them needs a wait state in between)
+               "s_nop 1")
+        if pair:
+            self.e("v_add_co_u32 v56, vcc, 8, v48", "v_addc_co_u32 v57, vcc, 0, v49, vcc",
+                   "v_mov_b32 v58, v44", "v_mov_b32 v59, v45")
+        else:
+            self.e("v_mov_b32 v56, 0", "v_mov_b32 v57, 0", "v_mov_b32 v58, 0", "v_mov_b32 v59, 0")
+        self.e("global_store_dwordx4 v42, v[56:59], s[52:53] offset:16", "s_nop 1",
+               f"{back}:",
+               "s_mov_b64 exec, s[62:63]", f"s_cbranch_execz {done}",
+               f"{atom}:")
 
     def atomic_pair(self):
         """Two fused BPF_ATOMIC adds without fetch (loader: same map-value
@@ -615,6 +659,28 @@ class Gen:
         self.wr("s44", 44)
         self.next_seq()
 
+    def lea(self):
+        """Superinstruction (loader.cpp fuse_pairs): `mov64 dst, src; add64
+        dst, imm` as one dispatch, r[dst] = r[src] + imm64 (w2:3); the pair's
+        second FInsn is skipped."""
+        self.rd("s45", 44)
+        self.e("v_lshl_add_u64 v[44:45], v[44:45], 0, s[42:43]")
+        self.wr("s44", 44)
+        self.next_seq(2)
+
+    def movi_prefix(self):
+        """A `mov64 r, imm32` fused in front of this jump / exit (loader.cpp
+        fuse_pairs: w1 FW_MOVI, bits 3..6 = r, w7 = the imm): execute it, then
+        this instruction as the pair's second (IP one slot on)."""
+        skip = self.label("mvi")
+        self.e("s_bitcmp1_b32 s41, 2", f"s_cbranch_scc0 {skip}",
+               "s_bfe_u32 s69, s41, 0x40003", "s_lshl_b32 s69, s69, 1",
+               "s_ashr_i32 s70, s47, 31")
+        self.idx("s69", "DST")
+        self.e(f"v_mov_b32_e32 v{R0}, s47", f"v_mov_b32_e32 v{R0 + 1}, s70")
+        self.idx_off()
+        self.e(f"s_add_u32 s48, s48, {INSN}", f"{skip}:")
+
     def neg(self, w):
         self.idx("s44", "SRC1,DST")
         if w == "64":
@@ -814,6 +880,7 @@ class Gen:
         self.next_seq(2)
 
     def jcc(self, w, cc, k):
+        self.movi_prefix()
         (self.rd if w == "64" else self.rd_lo)("s44", 44)
         if k == "R":
             (self.rd if w == "64" else self.rd_lo)("s45", 46)
@@ -1326,6 +1393,7 @@ class Gen:
         verdict (u32) and ret (u64); then the next pending lane group runs,
         or the block ends (every live lane has exited)."""
         nv, nr, last = self.label("nv"), self.label("nr"), self.label("last")
+        self.movi_prefix()
         self.flush(clear=False)
         self.e("s_bitcmp1_b32 %[oflags], 0", f"s_cbranch_scc0 {nv}",
                f"global_store_dword %[vaddr], v{R0}, off",
@@ -1854,6 +1922,8 @@ class Gen:
                 self.endian(name)
             elif name == "NOP":
                 self.next_seq()
+            elif name == "LEA":
+                self.lea()
             elif name in ("LDX_CTXDATA", "LDX_CTXEND"):
                 self.ctx_field(name == "LDX_CTXEND")
             elif name in STAGED_LD:

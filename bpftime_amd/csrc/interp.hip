@@ -595,6 +595,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
   SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(flush_log); SRV(log_words); SRP(lane_scratch);
   SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask); SRV(lcache); SRP(gregs); SRP(rb_stage); SRP(gctx);
+  SRP(miss_log); SRP(miss_counts); SRV(miss_cap);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
   p.unwind_idx = (int32_t)sreg((uint64_t)(uint32_t)pin.unwind_idx);
 #undef SRP
@@ -677,7 +678,13 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     // G: the block's global r0 column minus the LDS address of the lane
     // columns (gen_fast.py rgb: v40 + r * 2048 + this addresses r's copy)
     tenv[4] = G ? (uint64_t)(uintptr_t)Rg - (uint32_t)(uintptr_t)&Rf[0] : 0;
+    // the block's miss-log region (gen_fast.py comb_add) and its records
+    // per partition
+    tenv[5] = p.miss_log ? (uint64_t)(uintptr_t)(p.miss_log + (uint64_t)blockIdx.x * kMissParts * p.miss_cap * 2) : 0;
+    tenv[6] = p.miss_cap;
   }
+  uint32_t *const miss_cnt = (uint32_t *)((uint8_t *)tenv + 64);  // per partition: records claimed
+  for (uint32_t i = tid; i < kMissParts; i += BS) miss_cnt[i] = 0;
   __syncthreads();
   uint64_t big_stack[BIGSTACK ? kStackSize / 8 : 1];
   const uint64_t stack_top = BIGSTACK ? (uint64_t)(uintptr_t)(big_stack + kStackSize / 8)
@@ -1093,6 +1100,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   if (tid == 0) nlog = 0;
   __syncthreads();
   if (p.rb_stage) rb_publish(p.maps, rbs, tid, BS);
+  if (p.miss_log)  // (records past the capacity were added directly)
+    for (uint32_t i = tid; i < kMissParts; i += BS)
+      p.miss_counts[(uint64_t)blockIdx.x * kMissParts + i] = min(miss_cnt[i], p.miss_cap);
   uint64_t *e = &wdelta[0][0][0];
   constexpr uint32_t NE = wave_cache_entries(BS);
   if (tid == 0) {
@@ -1210,6 +1220,56 @@ __global__ __launch_bounds__(kBlock) void k_comb_merge(const uint64_t *log, uint
 }
 static_assert(kMergeEntries == 4u << 10, "k_comb_merge hashes into 2^10 sets of 4");
 
+// The miss log's second level (common.hpp kMissParts): block q combines
+// partition q of every block's region in an open-addressing LDS table
+// (linear probing, kMissProbes slots), then adds each address's sum with
+// one device atomic; a record that finds no slot adds at once.
+constexpr uint32_t kMissEntries = 4096, kMissProbes = 32;
+__global__ __launch_bounds__(kBigBlock) void k_miss_merge(const uint64_t *log, const uint32_t *counts, uint32_t cap,
+                                                          uint32_t nblocks, uint64_t lo1, uint64_t hi1, uint64_t lo2,
+                                                          uint64_t hi2, uint32_t *bad) {
+  __shared__ uint64_t mt[2 * kMissEntries];  // tags, then deltas
+  const uint32_t tid = threadIdx.x, q = blockIdx.x;
+  for (uint32_t i = tid; i < 2 * kMissEntries; i += kBigBlock) mt[i] = 0;
+  __syncthreads();
+  // wave w reads source blocks w, w + 16, ...; its lanes read a block's
+  // records 64 at a time (coalesced)
+  constexpr uint32_t kWaves = kBigBlock / 64;
+  for (uint32_t b = tid / 64; b < nblocks; b += kWaves) {
+    const uint32_t n = counts[(uint64_t)b * kMissParts + q];
+    const uint64_t *rec = log + ((uint64_t)b * kMissParts + q) * cap * 2;
+    for (uint32_t i = tid % 64; i < n; i += 64) {
+      const uint64_t tag = rec[2 * i], d = rec[2 * i + 1];
+      if (!tag || !d) continue;  // (a single add's empty second record)
+      // (the windows the interpreter's counter adds may reach: a record
+      // outside them is never added)
+      const uint64_t a = tag & ~1ull, e = a + ((tag & 1) ? 4 : 8);
+      if (!((a >= lo1 && e <= hi1) || (a >= lo2 && e <= hi2))) {
+        atomicAdd(bad, 1u);
+        continue;
+      }
+      uint32_t h = (uint32_t)((tag >> 2) * 0x9E3779B97F4A7C15ull >> 52);  // 12 bits
+      bool done = false;
+      for (uint32_t k = 0; k < kMissProbes && !done; k++, h = (h + 1) & (kMissEntries - 1)) {
+        uint64_t cur = __hip_atomic_load(&mt[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == 0) {
+          uint64_t z = 0;
+          __hip_atomic_compare_exchange_strong(&mt[h], &z, tag, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+          cur = z == 0 ? tag : z;
+        }
+        if (cur == tag) {
+          __hip_atomic_fetch_add(&mt[kMissEntries + h], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          done = true;
+        }
+      }
+      if (!done) flush_delta_tag(tag, d);
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < kMissEntries; i += kBigBlock) flush_delta_tag(mt[i], mt[kMissEntries + i]);
+}
+
 // ---------------------------------------------------------------------------
 // Host-side launch wrappers
 // ---------------------------------------------------------------------------
@@ -1246,6 +1306,14 @@ extern "C" hipError_t bpftime_amd_launch_merge(const uint64_t *log, uint32_t log
   const uint32_t grid = (nblocks + kMergeGroup - 1) / kMergeGroup;
   hipLaunchKernelGGL(k_comb_merge, dim3(grid), dim3(kBlock), 2 * kMergeEntries * sizeof(uint64_t), stream, log,
                      log_words, nblocks, kMergeGroup);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t bpftime_amd_launch_miss_merge(const uint64_t *log, const uint32_t *counts, uint32_t cap,
+                                                     uint32_t nblocks, const KParams *p, uint32_t *bad,
+                                                     hipStream_t stream) {
+  hipLaunchKernelGGL(k_miss_merge, dim3(kMissParts), dim3(kBigBlock), 0, stream, log, counts, cap, nblocks,
+                     p->arena_lo, p->arena_hi, p->data_lo, p->data_hi, bad);
   return hipGetLastError();
 }
 

@@ -1179,6 +1179,7 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
   out.specialized = 0;
   out.needs_comb = true;
   out.needs_ctx = xdp;
+  out.join.assign(prog.size(), 1);  // (filled in below when the pointer kinds hold)
   for (size_t i = 0; i < prog.size(); i++) {
     const DInsn &d = prog[i];
     FInsn &f = out.fast[i];
@@ -1402,6 +1403,7 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
       if ((d.op == X_JA || is_cond_jump(d.op)) && d.tgt >= 0 && (size_t)d.tgt < prog.size()) target[d.tgt] = 1;
     for (uint32_t e : lo.entries)
       if (e < prog.size()) target[e] = 1;
+    out.join.assign(target.begin(), target.begin() + prog.size());
     for (size_t i = 0; i + 1 < prog.size() && !getenv("BPFTIME_AMD_NO_PAIR"); i++) {
       const DInsn &a = prog[i], &b = prog[i + 1];
       if (out.fast[i].hoff != 4 + 4 * F_ATOMMV8_ADD || out.fast[i + 1].hoff != 4 + 4 * F_ATOMMV8_ADD) continue;
@@ -1429,12 +1431,55 @@ uint32_t stage_need(const FastForm &f, uint32_t head) {
   return (uint32_t)((ext + 15) & ~15);
 }
 
+// FInsn slots an entry covers: lddw, and the pairs run as one dispatch
+static size_t fspan(const std::vector<DInsn> &prog, const std::vector<FInsn> &out, size_t i) {
+  return (i < prog.size() && prog[i].op == X_LDDW) || out[i].hoff == 4 + 4 * F_ATOMMV8_ADD2 ||
+                 out[i].hoff == 4 + 4 * F_LEA || (out[i].w1 & FW_MOVI)
+             ? 2
+             : 1;
+}
+
+// Superinstructions: pairs of adjacent instructions that compilers emit
+// together run as one dispatch (gen_fast.py lea, movi_prefix): `mov64 rA,
+// rB; add64 rA, imm` (pointer + offset: stack key arguments, packet bounds)
+// and `mov64 r, imm32` in front of a conditional jump or exit (the verdict
+// set before a bounds check or a return).  The pair's second instruction
+// must not be a jump target or an entry, and keeps its own FInsn: the C++
+// tier, which runs one instruction at a time, re-enters the asm there.
+// BPFTIME_AMD_NO_FUSE turns it off.
+static void fuse_pairs(const std::vector<DInsn> &prog, const std::vector<uint8_t> &join,
+                       std::vector<FInsn> &out) {
+  if (getenv("BPFTIME_AMD_NO_FUSE") || join.size() != prog.size()) return;
+  auto is = [&](size_t i, uint32_t id) { return out[i].hoff == 4 + 4 * id; };
+  auto jcc_or_exit = [&](size_t i) {
+    const uint32_t id = (out[i].hoff - 4) / 4;
+    return id == F_EXIT || (id >= F_J64_EQ_R && id <= F_J32_SLE_I);
+  };
+  for (size_t i = 0; i + 1 < prog.size(); i++) {
+    if (join[i + 1] || prog[i].op == X_LDDW) continue;
+    const DInsn &a = prog[i], &b = prog[i + 1];
+    if (is(i, F_A64_MOV_R) && (is(i + 1, F_A64_ADD_I) || is(i + 1, F_A64_SUB_I)) && a.dst == b.dst) {
+      FInsn g = out[i];
+      g.hoff = 4 + 4 * F_LEA;
+      g.imm = b.op == X_ADD ? (int64_t)b.imm : -(int64_t)b.imm;
+      out[i] = g;
+      i++;
+    } else if (is(i, F_A64_MOV_I) && jcc_or_exit(i + 1) && !(out[i + 1].w1 & FW_MOVI)) {
+      FInsn g = out[i + 1];
+      g.w1 |= FW_MOVI | ((uint32_t)a.dst << FW_MOVI_REG_SHIFT);
+      g.aux = a.imm;
+      out[i] = g;
+      i++;
+    }
+  }
+}
+
 // w1 bits 8+: the handler offset of the FInsn sequential flow reaches next
 // (gen_fast.py next_seq jumps on it before the fetch lands); the SLOW handler
 // past the end
 static void link_next(const std::vector<DInsn> &prog, std::vector<FInsn> &out) {
   for (size_t i = 0; i < out.size(); i++) {
-    const size_t nx = i + ((i < prog.size() && prog[i].op == X_LDDW) || out[i].hoff == 4 + 4 * F_ATOMMV8_ADD2 ? 2 : 1);
+    const size_t nx = i + fspan(prog, out, i);
     const uint32_t h = nx < out.size() ? out[nx].hoff : 4 + 4 * F_SLOW;
     out[i].w1 = (out[i].w1 & 0xffu) | (h << 8);
   }
@@ -1455,6 +1500,7 @@ void link_fast(const FastForm &f, uint32_t head, uint32_t stage, bool ordered, c
         out[i].hoff = 4 + 4 * F_SLOW;
         out[i].w1 &= ~(uint32_t)FW_LCACHE;
       }
+  fuse_pairs(prog, f.join, out);
   link_next(prog, out);
 }
 

@@ -50,6 +50,7 @@ struct FastForm {
   // bound from the maps they target; ~0u: unknown): sizes the combining table
   uint32_t comb_hint = ~0u;
   std::vector<uint8_t> add_site;  // per insn: a counter add (fused RMW, atomic add without fetch)
+  std::vector<uint8_t> join;      // per insn: a jump target or an entry (no superinstruction ends there)
   // linked images, XDP form: the ctx words (bit k = bytes [8k, 8k+8)) and
   // LDS stack words (bit j = the j-th 8 bytes from the stack bottom) that a
   // tail-call target may write -- what a frame must save for its caller

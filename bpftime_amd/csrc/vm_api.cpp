@@ -30,6 +30,9 @@ extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind,
 extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds, bool gregs, uint32_t block);
 extern "C" hipError_t bpftime_amd_launch_merge(const uint64_t *log, uint32_t log_words, uint32_t nblocks,
                                                 hipStream_t stream);
+extern "C" hipError_t bpftime_amd_launch_miss_merge(const uint64_t *log, const uint32_t *counts, uint32_t cap,
+                                                     uint32_t nblocks, const KParams *p, uint32_t *bad,
+                                                     hipStream_t stream);
 
 struct HelperReg {
   std::string name;
@@ -160,7 +163,7 @@ class Mi355xVm {
   uint32_t base_stack = 0;  // the loaded program's own stack need (kStackSize + 1: unknown)
   std::string link_note;    // targets left out of the last image, and why
   // block-end flush logs (common.hpp kMergeGroup) and tail-call frames
-  StreamBufs logs, frames, scratch, regs;
+  StreamBufs logs, frames, scratch, regs, misses;
 
   Mi355xVm() {
     // bpftime_prog.cpp:126-127 defaults, pointed at the device registry
@@ -654,17 +657,67 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       return -1;
     }
   }
+  // the combining tables' miss log (common.hpp kMissParts): records per
+  // block and partition for a quarter of the block's units missing with a
+  // pair each, at most 256 MiB of log.  Opt-in (BPFTIME_AMD_MISS_LOG=1):
+  // measured on flow-hash, the interpreter kernel gains 0.06 ms per 2^24
+  // frames (0.89 -> 0.83) but k_miss_merge costs 0.18 ms -- the misses of
+  // moderately hot flows reach one merge block from every source block and
+  // serialize on its LDS atomics -- so by default misses add directly
+  if (p.comb_entries && grid > 1 && getenv("BPFTIME_AMD_MISS_LOG") && atoi(getenv("BPFTIME_AMD_MISS_LOG")) > 0) {
+    const uint64_t upb = (b->count + grid - 1) / grid;
+    uint64_t cap = upb * 2 / 4 / kMissParts;
+    const uint64_t most = (256ull << 20) / ((uint64_t)grid * kMissParts * 16);
+    cap = cap < 16 ? 16 : cap;
+    cap = cap > most ? most : cap;
+    if (const char *mc = getenv("BPFTIME_AMD_MISS_CAP")) cap = strtoull(mc, nullptr, 0);  // (tests: overflow)
+    cap &= ~1ull;
+    if (cap >= 2) {
+      // (the counts, then a u32 of records the merge refused: a log that
+      // names an address outside the windows is never added)
+      const uint64_t cbytes = ((uint64_t)grid * kMissParts * 4 + 4 + 255) & ~255ull;
+      uint8_t *m = (uint8_t *)misses.get(s, cbytes + (uint64_t)grid * kMissParts * cap * 16);
+      if (!m) {
+        error = "miss log allocation failed";
+        return -1;
+      }
+      p.miss_counts = (uint32_t *)m;
+      if (hipMemsetAsync(m + (uint64_t)grid * kMissParts * 4, 0, 4, s) != hipSuccess) {
+        error = "miss log reset failed";
+        return -1;
+      }
+      p.miss_log = (uint64_t *)(m + cbytes);
+      p.miss_cap = (uint32_t)cap;
+    }
+  }
   if (r.host_views_push() < 0) {  // host writes to mmap'd array maps first
     error = "host view upload failed";
     return -1;
   }
   if (getenv("BPFTIME_AMD_VERBOSE"))
     fprintf(stderr,
-            "bpftime_amd: launch units %llu grid %u block %u comb %u lcache %u stage %u stack %u gregs %d gctx %d unwind %d\n",
+            "bpftime_amd: launch units %llu grid %u block %u comb %u lcache %u stage %u stack %u gregs %d gctx %d unwind %d "
+            "miss cap %u\n",
             (unsigned long long)b->count, grid, block, p.comb_entries, p.lcache, p.stage, (unsigned)prog.stack_size,
-            p.gregs ? 1 : 0, p.gctx ? 1 : 0, p.unwind_idx);
+            p.gregs ? 1 : 0, p.gctx ? 1 : 0, p.unwind_idx, p.miss_cap);
   hipError_t e = bpftime_amd_launch_interp(&p, b->ctx_kind, prog.big_stack, grid, ordered ? 1 : 0, block, s);
-  if (e == hipSuccess && p.flush_log) e = bpftime_amd_launch_merge(p.flush_log, p.log_words, grid, s);
+  // (BPFTIME_AMD_SYNC_EACH: synchronize after every launch, naming the one that failed)
+  const bool sync_each = getenv("BPFTIME_AMD_SYNC_EACH") != nullptr;
+  auto step = [&](const char *what, hipError_t le) {
+    if (le == hipSuccess && sync_each) le = hipStreamSynchronize(s);
+    if (le != hipSuccess && sync_each) fprintf(stderr, "bpftime_amd: %s: %s\n", what, hipGetErrorString(le));
+    return le;
+  };
+  e = step("k_interp", e);
+  if (e == hipSuccess && p.flush_log) e = step("k_comb_merge", bpftime_amd_launch_merge(p.flush_log, p.log_words, grid, s));
+  if (e == hipSuccess && p.miss_log)
+    e = step("k_miss_merge", bpftime_amd_launch_miss_merge(p.miss_log, p.miss_counts, p.miss_cap, grid, &p,
+                                                           p.miss_counts + (uint64_t)grid * kMissParts, s));
+  if (e == hipSuccess && p.miss_log && sync_each) {
+    uint32_t bad = 0;
+    hipMemcpy(&bad, p.miss_counts + (uint64_t)grid * kMissParts, 4, hipMemcpyDeviceToHost);
+    if (bad) fprintf(stderr, "bpftime_amd: k_miss_merge: %u records outside the windows\n", bad);
+  }
   if (e != hipSuccess) {
     error = std::string("kernel launch failed: ") + hipGetErrorString(e);
     return -1;
@@ -677,9 +730,10 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   }
   if (b->flags & EBPF_BATCH_SYNC) {
     uint32_t failed = 0;
-    if (hipMemcpyAsync(&failed, err, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess || r.host_views_pull() < 0) {
-      error = "batch sync failed";
+    hipError_t he = hipMemcpyAsync(&failed, err, 4, hipMemcpyDeviceToHost, s);
+    if (he == hipSuccess) he = hipStreamSynchronize(s);
+    if (he != hipSuccess || r.host_views_pull() < 0) {
+      error = std::string("batch sync failed: ") + (he != hipSuccess ? hipGetErrorString(he) : "host view pull");
       return -1;
     }
     return (int)failed;

@@ -9,7 +9,8 @@ import numpy as np
 import pytest
 
 from bpftime_amd import gen, isa, programs
-from bpftime_amd.isa import Asm
+from bpftime_amd.isa import (Asm, ATOMIC_ADD, BPF_FUNC_map_lookup_elem, BPF_FUNC_map_update_elem,
+                             BPF_NOEXIST)
 
 from _helpers import make_maps
 
@@ -358,3 +359,73 @@ def test_lookup_cache_against_concurrent_deleter(fresh_runtime):
     np.testing.assert_array_equal(r1.download(np.uint64), vals)
     np.testing.assert_array_equal(r2.download(np.uint64), np.where(keys % 2 == 0, 0xdead, vals))
     assert m.lookup(struct.pack("<I", 1)) is None and m.lookup(struct.pack("<I", 3)) is not None
+
+
+def _u32_counter_prog(fd):
+    """Per-key u32 counters through a hash value {u32 hits, u32 bytes}:
+    key = the frame's first byte, lookup_or_try_init, two 4-byte atomic adds
+    (deferred: nothing reads them back in the unit)."""
+    a = Asm()
+    a.ldx(8, 2, 1, 0).ldx(8, 3, 1, 8)
+    a.mov64(6, "r3").alu64("sub", 6, "r2")
+    a.ldx(1, 4, 2, 0).stx(4, 10, -4, "r4")
+    a.st(8, 10, -16, 0)
+    a.ld_map_fd(1, fd).mov64(2, "r10").add64(2, -4).call(BPF_FUNC_map_lookup_elem)
+    a.jmp("jne", 0, 0, "have")
+    a.ld_map_fd(1, fd).mov64(2, "r10").add64(2, -4).mov64(3, "r10").add64(3, -16).mov64(4, BPF_NOEXIST)
+    a.call(BPF_FUNC_map_update_elem)
+    a.ld_map_fd(1, fd).mov64(2, "r10").add64(2, -4).call(BPF_FUNC_map_lookup_elem)
+    a.mov64(1, "r0").mov64(0, 0).jmp("jeq", 1, 0, "out").mov64(0, "r1")
+    a.label("have")
+    a.mov64(1, 1)
+    a.atomic(4, ATOMIC_ADD, 0, 0, "r1")
+    a.atomic(4, ATOMIC_ADD, 0, 4, "r6")
+    a.mov64(0, 2)
+    a.label("out").exit()
+    return a.assemble()
+
+
+# The combining tables' miss log (common.hpp kMissParts, interp.hip
+# k_miss_merge; opt-in, BPFTIME_AMD_MISS_LOG=1): the smallest table makes
+# most adds miss, a tiny per-partition capacity makes the log overflow into
+# direct adds.  cap "0": the log off, misses add directly
+@pytest.mark.parametrize("cap", [None, "2", "0"])
+def test_miss_log_parity(fresh_oracle, fresh_runtime, monkeypatch, cap):
+    po, dev = fresh_oracle, fresh_runtime
+    monkeypatch.setenv("BPFTIME_AMD_MISS_LOG", "0" if cap == "0" else "1")
+    monkeypatch.setenv("BPFTIME_AMD_COMB_ENTRIES", "256")
+    if cap and cap != "0":
+        monkeypatch.setenv("BPFTIME_AMD_MISS_CAP", cap)
+    # 8-byte pairs: flow-hash at config 3's key shape
+    (om,), (dm,) = _flow_setup(po, dev)
+    code = programs.flow_hash(dm.fd)
+    n = 1 << 20
+    slots, lens = gen.flow_packets(n, nflows=65536, stride=2048)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    ov = ovm.run_xdp(slots.copy(), lens=lens)
+    vm = dev.VM()
+    vm.load(code)
+    d = dev.DeviceBuffer.from_array(slots)
+    dl = dev.DeviceBuffer.from_array(lens)
+    dv = dev.DeviceBuffer(4 * n)
+    assert vm.exec_batch(dev.CTX_XDP, d, n, 2048, lens=dl, verdicts=dv) == 0
+    np.testing.assert_array_equal(dv.download(np.uint32), ov)
+    assert dm.hash_items() == om.items()
+    # 4-byte counters, 256 keys
+    (om4,), (dm4,) = make_maps([(isa.BPF_MAP_TYPE_HASH, 4, 8, 512)], po, dev)
+    code4 = _u32_counter_prog(dm4.fd)
+    n4 = 1 << 19
+    pk = gen.xdp_packets(n4, seed=77)
+    lens4 = (64 + (np.arange(n4) % 7)).astype(np.uint32)
+    ov4 = po.OracleVM()
+    ov4.load(code4)
+    want = ov4.run_xdp(pk.copy(), lens=lens4)
+    vm4 = dev.VM()
+    vm4.load(code4)
+    d4 = dev.DeviceBuffer.from_array(pk)
+    dl4 = dev.DeviceBuffer.from_array(lens4)
+    dv4 = dev.DeviceBuffer(4 * n4)
+    assert vm4.exec_batch(dev.CTX_XDP, d4, n4, 64, lens=dl4, verdicts=dv4) == 0
+    np.testing.assert_array_equal(dv4.download(np.uint32), want)
+    assert dm4.hash_items() == om4.items()
