@@ -247,6 +247,7 @@ struct KParams {
   uint64_t *miss_log;        // combining-table misses: [grid][kMissParts][miss_cap] {tag, delta} records, or nullptr
   uint32_t *miss_counts;     // [grid][kMissParts] records each block wrote (k_miss_merge reads them)
   uint32_t miss_cap;         // records per block and partition (even)
+  const int32_t *tail_slots; // images: per PROG_ARRAY fd the offset of its slots' entry pcs, then those (vm_api.cpp)
 };
 
 // Combining-table misses.  A deferred counter add that finds no table entry

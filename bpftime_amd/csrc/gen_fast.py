@@ -169,6 +169,7 @@ class Gen:
         self.uid = 0
         self.greg = greg
         self.depth_off = 2048 if greg else 12 * 2048  # the lane's tail-call depth slot
+        self.hdr_off = self.depth_off + 2048          # ... and its depth-0 frame header (interp.hip kHdr0)
 
     def e(self, *lines):
         self.out.extend(lines)
@@ -1600,19 +1601,24 @@ class Gen:
                "s_cmpk_ge_u32 s62, 0x400", f"s_cbranch_scc1 {L('slow')}",
                "s_lshl_b32 s69, s62, 6",
                "s_load_dwordx4 s[64:67], %[maps], s69",                       # type, ksz, vsz, max
-               "s_add_u32 s69, s69, 16",
-               "s_load_dwordx2 s[70:71], %[maps], s69",                       # slots
+               # the image's slot -> entry pc table (tenv[7], vm_api.cpp
+               # d_tail_slots): one load per lane instead of the slot's prog
+               # fd and then that fd's entry
+               f"s_sub_u32 s69, %[comb], {TENV - 56}", "v_mov_b32 v41, s69",
+               "ds_read_b64 v[48:49], v41",
                "s_waitcnt lgkmcnt(0)",
+               "v_readfirstlane_b32 s70, v48", "v_readfirstlane_b32 s71, v49", "s_nop 4",
                "s_cmp_lg_u32 s64, 3", f"s_cbranch_scc1 {L('slow')}",         # BPF_MAP_TYPE_PROG_ARRAY
+               "s_cmp_eq_u64 s[70:71], 0", f"s_cbranch_scc1 {L('slow')}",
+               "s_lshl_b32 s69, s62, 2",
+               "s_load_dword s69, s[70:71], s69",                            # the array's offset
+               "s_waitcnt lgkmcnt(0)",
+               "s_cmp_lt_i32 s69, 0", f"s_cbranch_scc1 {L('slow')}",         # not in the image
                f"v_mov_b32 v46, v{R0 + 6}",                                  # `int idx = index`
                "v_cmp_gt_u32 s[54:55], s67, v46",                            # 0 <= idx < max_entries
                "v_cndmask_b32 v46, 0, v46, s[54:55]",
-               "v_mad_u64_u32 v[48:49], s[56:57], v46, 4, s[70:71]",
-               "global_load_dword v47, v[48:49], off",
-               "s_waitcnt vmcnt(0)",
-               "v_cmp_gt_u32 vcc, 0x400, v47", "s_and_b64 s[54:55], s[54:55], vcc",
-               "v_cndmask_b32 v47, 0, v47, s[54:55]",
-               "v_mad_u64_u32 v[48:49], s[56:57], v47, 4, s[74:75]",
+               "v_add_u32 v47, s69, v46",
+               "v_mad_u64_u32 v[48:49], s[56:57], v47, 4, s[70:71]",
                "global_load_dword v50, v[48:49], off",
                "s_waitcnt vmcnt(0)",
                "v_cmp_le_i32 s[56:57], 0, v50", "s_and_b64 s[54:55], s[54:55], s[56:57]",
@@ -1637,7 +1643,12 @@ class Gen:
         self.word_addr(11)
         self.e("s_lshl_b32 s69, s42, 8", "s_or_b32 s69, s69, 0x100",              # masked | live << 8
                "v_mov_b32 v44, s49", "v_mov_b32 v45, s69",
-               "global_store_dwordx2 v[58:59], v[44:45], off")
+               "global_store_dwordx2 v[58:59], v[44:45], off",
+               # depth 0: the header in LDS as well (the pop reads it there)
+               "s_mov_b64 s[64:65], exec",
+               "v_cmp_eq_u32 vcc, 0, v54", "s_and_b64 exec, exec, vcc",
+               f"ds_write_b64 v40, v[44:45] offset:{self.hdr_off}",
+               "s_mov_b64 exec, s[64:65]")
         for k in range(6):
             skip = self.label("tpc")
             self.e(f"s_bitcmp1_b32 s68, {k}", f"s_cbranch_scc0 {skip}",
@@ -1672,8 +1683,18 @@ class Gen:
                "s_waitcnt vmcnt(0)")
         self.frame_ptr()
         self.word_addr(11)
-        self.e("global_load_dwordx2 v[46:47], v[58:59], off",                 # return pc | flags
+        # frames of depth 0: the header from LDS when every lane has it
+        # there (a C++ push zeroes the copy), else from the frame
+        glb, got = self.label("trg"), self.label("trh")
+        self.e("v_cmp_ne_u32 vcc, 0, v54", "s_and_b64 vcc, vcc, exec", f"s_cbranch_vccnz {glb}",
+               f"ds_read_b64 v[46:47], v40 offset:{self.hdr_off}",
+               "s_waitcnt lgkmcnt(0)",
+               "v_and_b32 v41, 0x100, v47", "v_cmp_eq_u32 vcc, 0, v41", "s_and_b64 vcc, vcc, exec",
+               f"s_cbranch_vccz {got}",
+               f"{glb}:",
+               "global_load_dwordx2 v[46:47], v[58:59], off",                 # return pc | flags
                "s_waitcnt vmcnt(0)",
+               f"{got}:",
                "v_and_b32 v41, 0x100, v47", "v_cmp_ne_u32 vcc, 0, v41",
                "s_andn2_b64 s[54:55], exec, vcc", f"s_cbranch_scc1 {L('slow')}",
                f"ds_write_b32 v40, v54 offset:{self.depth_off}",

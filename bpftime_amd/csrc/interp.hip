@@ -595,7 +595,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
   SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(flush_log); SRV(log_words); SRP(lane_scratch);
   SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask); SRV(lcache); SRP(gregs); SRP(rb_stage); SRP(gctx);
-  SRP(miss_log); SRP(miss_counts); SRV(miss_cap);
+  SRP(miss_log); SRP(miss_counts); SRV(miss_cap); SRP(tail_slots);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
   p.unwind_idx = (int32_t)sreg((uint64_t)(uint32_t)pin.unwind_idx);
 #undef SRP
@@ -604,8 +604,10 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   // grid lane index << 32 (gen_fast.py tail_env).  (2 KiB of LDS decide
   // between 3 and 4 resident blocks of the headline program: images only.)
   // (G: the dummy and depth slots only)
-  constexpr uint32_t kDummy = G ? 0 : 11, kDepth = G ? 1 : 12;
-  __shared__ uint64_t Rf[(IMAGE ? kDepth + 1 : kDummy + 1) * BS];
+  // (images: then the header word of the lane's depth-0 frame as the asm
+  // tier pushed it, 0 = none: gen_fast.py tail_call / tail_ret)
+  constexpr uint32_t kDummy = G ? 0 : 11, kDepth = G ? 1 : 12, kHdr0 = kDepth + 1;
+  __shared__ uint64_t Rf[(IMAGE ? kHdr0 + 1 : kDummy + 1) * BS];
   // r0..r10 columns: [register][lane] per 256 lanes (kBlock), so a block of
   // BS > kBlock lanes (G launches only) holds BS / kBlock such column sets
   uint64_t *const Rg = G ? p.gregs + (uint64_t)blockIdx.x * 11 * BS : Rf;
@@ -682,6 +684,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     // per partition
     tenv[5] = p.miss_log ? (uint64_t)(uintptr_t)(p.miss_log + (uint64_t)blockIdx.x * kMissParts * p.miss_cap * 2) : 0;
     tenv[6] = p.miss_cap;
+    // images: the slot -> entry pc table of the asm tier's bpf_tail_call
+    tenv[7] = (uint64_t)(uintptr_t)p.tail_slots;
   }
   uint32_t *const miss_cnt = (uint32_t *)((uint8_t *)tenv + 64);  // per partition: records claimed
   for (uint32_t i = tid; i < kMissParts; i += BS) miss_cnt[i] = 0;
@@ -975,6 +979,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
             const bool in_stack = a1 + 64 > stack_top - sbytes && a1 < stack_top;
             if (entry >= 0 && tdep[0] < kTailDepth && a1 != 0 && !in_stack) {
               const uint32_t d = tdep[0];
+              if (d == 0) Rf[kHdr0 * kBlock + tid] = 0;  // (the asm's LDS copy of a depth-0 header)
               for (int r = 1; r <= 10; r++) FW(d, r - 1) = R[r * kBlock];
               FW(d, 10) = a1;
               FW(d, 11) = (uint64_t)next | ((uint64_t)cb << 32);

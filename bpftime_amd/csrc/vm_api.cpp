@@ -51,6 +51,10 @@ struct Image {
   // unit's slot) differ in the loader's pointer kinds
   FastForm fx, fr;
   int32_t *d_tail_entry = nullptr;  // prog fd -> entry pc (tail-call images)
+  // the asm tier's one-load form of the same: [kMaxFds] offsets of each
+  // reachable PROG_ARRAY's slots (-1: not in the image), then per slot the
+  // entry pc of the program it held at link time (-1: none / not linked)
+  int32_t *d_tail_slots = nullptr;
   uint32_t frame_words = 0;         // tail-call frame: header + ctx + the image's stack bytes, / 8
   uint64_t gen = 0;                 // rt().prog_gen it was linked at
   // linked FInsn arrays per launch configuration (entry form, ORDERED,
@@ -61,6 +65,7 @@ struct Image {
   ~Image() {
     if (d_prog) hipFree(d_prog);
     if (d_tail_entry) hipFree(d_tail_entry);
+    if (d_tail_slots) hipFree(d_tail_slots);
     for (auto &kv : links) hipFree(kv.second);
   }
   const FInsn *linked(bool xdp, uint32_t head, uint32_t stage, bool ordered, int32_t unwind_idx) {
@@ -266,6 +271,7 @@ class Mi355xVm {
     // the prog arrays each program loads, and the targets each array names
     std::map<int32_t, std::set<int32_t>> arrays_of_prog;  // target prog fd -> arrays
     std::map<int32_t, std::vector<int32_t>> slots_of;     // array fd -> target prog fds
+    std::map<int32_t, std::vector<int32_t>> slot_fds;     // array fd -> its slots (prog fds) at link time
     std::set<int32_t> root_arrays, pending;
     arrays_of(raw.data(), raw.size(), root_arrays);
     pending = root_arrays;
@@ -280,6 +286,7 @@ class Mi355xVm {
         error = "prog array read failed";
         return -1;
       }
+      slot_fds[fd] = slots;
       std::vector<int32_t> &ts = slots_of[fd];
       for (int32_t v : slots)
         if (v >= 0 && v < (int32_t)kMaxFds && r.kind[v] == HKind::PROG) {
@@ -365,8 +372,18 @@ class Mi355xVm {
     im->frame_words = (kFrameHdr + kFrameCtx + (out.big_stack ? kStackSize : out.stack_size)) / 8;
     im->gen = r.prog_gen;
     if (im->upload(std::move(out), error) < 0) return -1;
+    // slot -> entry pc per reachable prog array (the image is relinked when
+    // a prog, an array or a slot changes: Runtime::prog_gen)
+    std::vector<int32_t> tslots(kMaxFds, -1);
+    for (const auto &kv : slot_fds) {
+      tslots[kv.first] = (int32_t)tslots.size();
+      for (const int32_t v : kv.second)
+        tslots.push_back(v >= 0 && v < (int32_t)kMaxFds && r.kind[v] == HKind::PROG ? entry[v] : -1);
+    }
     if (hipMalloc((void **)&im->d_tail_entry, 4 * kMaxFds) != hipSuccess ||
-        hipMemcpy(im->d_tail_entry, entry.data(), 4 * kMaxFds, hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(im->d_tail_entry, entry.data(), 4 * kMaxFds, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMalloc((void **)&im->d_tail_slots, 4 * tslots.size()) != hipSuccess ||
+        hipMemcpy(im->d_tail_slots, tslots.data(), 4 * tslots.size(), hipMemcpyHostToDevice) != hipSuccess) {
       error = "device upload failed";
       return -1;
     }
@@ -619,6 +636,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     // tail-call frames for the lanes of this launch ([depth][word][lane]),
     // one buffer per stream: concurrent batches never share frames
     p.tail_entry = im.d_tail_entry;
+    p.tail_slots = im.d_tail_slots;
     p.frame_words = im.frame_words;
     p.tail_ctx_mask = im.fx.tail_ctx_mask;
     p.tail_stack_mask = im.fx.tail_stack_mask;
