@@ -240,7 +240,7 @@ struct KParams {
   uint64_t lru_seq;       // this launch's LRU stamp sequence (common.hpp kLruSeqShift)
   uint32_t tail_ctx_mask;    // XDP images: ctx words / stack words a frame keeps (loader.cpp tail_save_masks)
   uint32_t tail_stack_mask;
-  uint32_t lcache;           // 1 = the block's hash-lookup cache exists (common.hpp kLcacheSets)
+  uint32_t lcache;           // the block's hash-lookup cache: its sets (0 = none; lcache_sets())
   uint64_t *gregs;           // r0..r10 copies for the C++ tier: [grid][11][kBlock] u64 (k_interp G), or nullptr (LDS)
   uint8_t *rb_stage;         // ring-buffer staging: [grid][kRbStageBytes] right after lane_scratch's words, or nullptr
   uint8_t *gctx;             // XDP: the lanes' ctx in global memory ([grid lane] x 48 B, after the staging), or nullptr (LDS)
@@ -293,16 +293,17 @@ constexpr uint32_t kBigBlock = 1024;
 // block's miss-log region and its capacity), then kMissParts u32 miss counters
 constexpr uint32_t kTenvBytes = 64 + 4 * kMissParts;  // gen_fast.py TENV
 // Hash-lookup cache of a block (programs whose hash lookups the loader marks
-// FW_LCACHE: no deletions): kLcacheSets 2-way sets, the ways' 16-B keys
+// FW_LCACHE: no deletions): `sets` 2-way sets, the ways' 16-B keys
 // ([set][way]) then their u32 entries {(slot + 1) | fd << 22}, right below
-// the tail-call constants (gen_fast.py lcache_probe).  A slot found for a key
-// stays that key's slot for the rest of a launch when nothing deletes.
-constexpr uint32_t kLcacheSets = 1024;  // gen_fast.py LC_SETS
-constexpr uint32_t kLcacheBytes = (32 + 8) * kLcacheSets;
+// the tail-call constants (gen_fast.py lcache_probe; the lookup's FInsn w4
+// carries the set count).  A slot found for a key stays that key's slot for
+// the rest of a launch when nothing deletes.
+constexpr uint32_t kLcacheSets = 1024;  // default set count (BPFTIME_AMD_LCACHE_SETS: vm_api.cpp lcache_sets)
+BA_HD inline size_t lcache_bytes(uint32_t sets) { return (size_t)(32 + 8) * sets; }
 inline size_t dyn_lds_for(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
-                          bool lcache = false, bool ctx_lds = true, uint32_t block = kBlock) {
+                          uint32_t lcache_sets = 0, bool ctx_lds = true, uint32_t block = kBlock) {
   return (size_t)block * ((kind == CTX_XDP && ctx_lds ? 48 : 0) + (big_stack ? 0 : stack_size)) +
-         (lcache ? kLcacheBytes : 0) + kTenvBytes + 20 * (size_t)comb_entries;
+         lcache_bytes(lcache_sets) + kTenvBytes + 20 * (size_t)comb_entries;
 }
 
 // Error codes recorded per unit (err_count counts units with any error)

@@ -113,9 +113,8 @@ KP = 3
 WAYS = 8  # combining-table associativity
 MISS_PARTS = 256  # miss-log partitions (common.hpp kMissParts)
 TENV = 64 + 4 * MISS_PARTS  # launch constants + miss counters below the combining table (common.hpp kTenvBytes)
-LC_SETS = 1024  # hash-lookup cache sets of 2 ways (common.hpp kLcacheSets)
-LC_KEYS = 32 * LC_SETS  # the ways' 16-B keys, then their u32 entries
-LC_BYTES = LC_KEYS + 8 * LC_SETS
+# hash-lookup cache: w4 of a FW_LCACHE lookup = its 2-way set count (common.hpp
+# lcache_bytes: the ways' 16-B keys, then their u32 entries)
 
 # staged (link-resolved) packet / slot accesses
 STAGED_LD = ["LDXS1", "LDXS2", "LDXS4", "LDXS2X", "LDXS4X", "LDXS8A", "LDXS8U"]
@@ -1054,10 +1053,10 @@ class Gen:
                "v_cvt_u32_f64 v56, v[50:51]")
 
     # ---- the block's hash-lookup cache (common.hpp kLcacheSets) ----
-    # LC_SETS two-way sets right below the launch constants (%[comb] - TENV -
-    # LC_BYTES): the ways' keys (16 B each, [set][way], the key's first kd
+    # w4 (s44) two-way sets right below the launch constants (%[comb] - TENV -
+    # 40 * sets): the ways' keys (16 B each, [set][way], the key's first kd
     # words), then the ways' entries {u32 (slot + 1) | fd << 22} ([set][way],
-    # at + LC_KEYS).  The set is a mix of the key words and the fd, so a hit
+    # at + 32 * sets).  The set is a mix of the key words and the fd, so a hit
     # needs neither the h*31 hash nor a memory access: the whole key is
     # compared in LDS.  Entries are written once: a lane that found its key
     # claims an empty way (0 -> -1 by compare-and-swap), writes the key, then
@@ -1085,11 +1084,13 @@ class Gen:
             self.e(f"s_mov_b32 s69, {mult[j]}", f"v_mul_lo_u32 v42, v{44 + j}, s69", "v_xor_b32 v41, v41, v42")
         self.e("v_lshrrev_b32 v42, 15, v41", "v_xor_b32 v41, v41, v42",
                "s_mov_b32 s69, 0x2c1b3c6d", "v_mul_lo_u32 v41, v41, s69",
-               f"v_lshrrev_b32 v41, {32 - LC_SETS.bit_length() + 1}, v41",        # the set
-               f"s_sub_u32 s69, %[comb], {TENV + LC_BYTES}",
+               "v_mul_hi_u32 v41, v41, s44",                                       # the set (w4 sets)
+               "s_mul_i32 s69, s44, 40", "s_add_u32 s69, s69, " + str(TENV),
+               "s_sub_u32 s69, %[comb], s69",                                     # the cache
                "v_lshl_add_u32 v82, v41, 5, s69",                                 # its keys
-               f"s_add_u32 s69, s69, {LC_KEYS}",
-               "v_lshl_add_u32 v83, v41, 3, s69",                                 # its entries
+               # (s64..s71 hold the map's words here: val_off in s70)
+               "v_mul_u32_u24_e64 v83, s44, 32", "v_add_u32 v83, s69, v83",
+               "v_lshl_add_u32 v83, v41, 3, v83",                                 # its entries
                "ds_read_b64 v[54:55], v83",                                       # entries first
                "ds_read_b128 v[56:59], v82",
                "ds_read_b128 v[48:51], v82 offset:16",

@@ -625,12 +625,11 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   // delta granules (2 x u64 or 4 x u32), flushed when the block ends; sized 0
   // for programs that never need it
   uint32_t *lcache = (uint32_t *)(dyn + BS * (ctxb + (BIGSTACK ? 0 : p.stack_size)));
-  uint64_t *tenv = (uint64_t *)((uint8_t *)lcache + (p.lcache ? kLcacheBytes : 0));
+  uint64_t *tenv = (uint64_t *)((uint8_t *)lcache + lcache_bytes(p.lcache));
   uint32_t *comb = (uint32_t *)((uint8_t *)tenv + kTenvBytes);
   uint64_t *comb_d = (uint64_t *)(comb + p.comb_entries);
   for (uint32_t i = tid; i < 5 * p.comb_entries; i += BS) comb[i] = 0;
-  if (p.lcache)
-    for (uint32_t i = tid; i < kLcacheBytes / 4; i += BS) lcache[i] = 0;
+  for (uint32_t i = tid; i < lcache_bytes(p.lcache) / 4; i += BS) lcache[i] = 0;
   // ring-buffer staging (dev_helpers.hpp RbStage): LDS counters of the block
   __shared__ uint32_t rb_used, rb_end, rb_nrec;
   __shared__ int32_t rb_fd;
@@ -1286,7 +1285,7 @@ extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind,
   const bool image = q.tail_entry && !big_stack;
   const bool g_regs = q.gregs && !big_stack;
   if (block != kBlock && (block != kBigBlock || !g_regs || image || ordered)) return hipErrorInvalidValue;
-  const size_t dyn = dyn_lds_for(kind, big_stack, p->stack_size, p->comb_entries, p->lcache != 0, !p->gctx, block);
+  const size_t dyn = dyn_lds_for(kind, big_stack, p->stack_size, p->comb_entries, p->lcache, !p->gctx, block);
   dim3 g(grid), b(block);
 #define L(K, B, I, G) hipLaunchKernelGGL((k_interp<K, B, I, G, kBlock>), g, b, dyn, stream, q)
 #define LK(K)                                                          \

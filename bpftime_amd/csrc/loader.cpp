@@ -1170,6 +1170,18 @@ static bool is_counter_add(const DInsn &d) {
   return d.op == X_RMW_ADD || (d.op == X_ATOMIC && d.hi == 0x00);
 }
 
+uint32_t lcache_sets() {
+  static const uint32_t sets = [] {
+    uint32_t s = kLcacheSets;
+    if (const char *e = getenv("BPFTIME_AMD_LCACHE_SETS")) {
+      const uint32_t v = (uint32_t)atoi(e);
+      if (v >= 256 && v <= 4096 && (v & (v - 1)) == 0) s = v;
+    }
+    return s;
+  }();
+  return sets;
+}
+
 void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
   const std::vector<DInsn> &prog = lo.prog;
   out.fast.assign(prog.size(), FInsn{});
@@ -1324,6 +1336,7 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
           if (m && m->type == MT_HASH && !lo.may_delete && m->key_size % 4 == 0 && m->key_size <= 16 &&
               !getenv("BPFTIME_AMD_NO_LCACHE")) {
             f.w1 |= FW_LCACHE;
+            f.dst_x2 = lcache_sets();  // (gen_fast.py lcache_probe: the cache's set count)
             out.needs_lcache = true;
           }
         }
@@ -1489,8 +1502,11 @@ static void link_staged(const FastForm &f, uint32_t head, uint32_t stage, bool o
                         const std::vector<DInsn> &prog, std::vector<FInsn> &out);
 
 void link_fast(const FastForm &f, uint32_t head, uint32_t stage, bool ordered, const std::vector<DInsn> &prog,
-               std::vector<FInsn> &out, int32_t unwind_idx) {
+               std::vector<FInsn> &out, int32_t unwind_idx, uint32_t lc_sets) {
   link_staged(f, head, stage, ordered, prog, out);
+  // the launch's lookup-cache set count (vm_api.cpp) into the lookups that use it
+  for (FInsn &x : out)
+    if ((x.w1 & FW_LCACHE) && lc_sets) x.dst_x2 = lc_sets;
   // an unwind helper (ebpf_set_unwind_function_index) is called from the
   // C++ tier, which ends the unit when it returns 0: map_lookup_elem leaves
   // its asm handlers then

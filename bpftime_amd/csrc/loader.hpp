@@ -39,6 +39,10 @@ struct FStatic {
 };
 
 // Threaded-code form of a program for one entry convention.
+// The blocks' hash-lookup cache sets (common.hpp kLcacheSets; a power of two
+// in [256, 4096] from BPFTIME_AMD_LCACHE_SETS, read once)
+uint32_t lcache_sets();
+
 struct FastForm {
   std::vector<FInsn> fast;     // templates (generic handlers for static accesses)
   std::vector<FStatic> stat;   // per insn
@@ -95,7 +99,7 @@ uint32_t stage_need(const FastForm &f, uint32_t head);
 // `ordered`: every counter add gets its direct (FW_NODEFER) handler.
 // `unwind_idx`: the VM's unwind helper (-1 none); its calls run in C++.
 void link_fast(const FastForm &f, uint32_t head, uint32_t stage, bool ordered, const std::vector<DInsn> &prog,
-               std::vector<FInsn> &out, int32_t unwind_idx = -1);
+               std::vector<FInsn> &out, int32_t unwind_idx = -1, uint32_t lc_sets = 0);
 
 // Runs the compat_ubpf.cpp:61-200 patching (call remap check, lddw pseudo
 // sources), ubpf-style validation, pre-decoding and the dataflow analyses

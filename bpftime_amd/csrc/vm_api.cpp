@@ -68,15 +68,15 @@ struct Image {
     if (d_tail_slots) hipFree(d_tail_slots);
     for (auto &kv : links) hipFree(kv.second);
   }
-  const FInsn *linked(bool xdp, uint32_t head, uint32_t stage, bool ordered, int32_t unwind_idx) {
+  const FInsn *linked(bool xdp, uint32_t head, uint32_t stage, bool ordered, int32_t unwind_idx, uint32_t lc_sets) {
     std::lock_guard<std::mutex> g(link_mu);
     const bool uw = unwind_idx == 1;  // the only helper with asm handlers an unwind index changes
     const uint64_t key = ((uint64_t)xdp << 63) | ((uint64_t)ordered << 62) | ((uint64_t)uw << 61) |
-                         ((uint64_t)stage << 40) | (stage ? head : 0);
+                         ((uint64_t)(lc_sets & 0x1fff) << 47) | ((uint64_t)stage << 40) | (stage ? head : 0);
     auto it = links.find(key);
     if (it != links.end()) return it->second;
     std::vector<FInsn> out;
-    link_fast(xdp ? fx : fr, head, stage, ordered, prog.prog, out, uw ? 1 : -1);
+    link_fast(xdp ? fx : fr, head, stage, ordered, prog.prog, out, uw ? 1 : -1, lc_sets);
     FInsn *d = nullptr;
     const size_t bytes = out.size() * sizeof(FInsn);
     if (hipMalloc((void **)&d, bytes) != hipSuccess) return nullptr;
@@ -445,13 +445,8 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     const bool aligned = ((uint64_t)(uintptr_t)b->data % 16) == 0 &&
                          (b->descs ? true : (b->stride % 16) == 0 && b->stride >= need);
     p.stage = (need && aligned && !getenv("BPFTIME_AMD_NO_STAGING")) ? need : 0;
-    p.fast = im.linked(xdp, head, p.stage, (b->flags & EBPF_BATCH_ORDERED) != 0, unwind_helper);
-    if (!p.fast) {
-      error = "device upload failed";
-      return -1;
-    }
     p.needs_ctx = xdp && im.fx.needs_ctx ? 1 : 0;
-    p.lcache = (xdp ? im.fx : im.fr).needs_lcache ? 1 : 0;
+    p.lcache = (xdp ? im.fx : im.fr).needs_lcache ? lcache_sets() : 0;  // (sized below)
     p.fast_div = getenv("BPFTIME_AMD_NO_ASM_DIVERGENCE") ? 0 : 1;
   }
   p.maps = r.d_maptab;
@@ -503,6 +498,28 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   uint32_t block = greg && !im.d_tail_entry && !stage ? kBigBlock : kBlock;
   if (const char *bs = getenv("BPFTIME_AMD_BLOCK"))
     if (atoi(bs) == (int)kBlock) block = kBlock;
+  // the lookup cache: 1024 sets, or 2048 in a 1024-lane block whose
+  // combining table would stay below 2048 entries (the LDS is there:
+  // syscall-agg 0.645 -> 0.61 ms; flow-hash, whose table fills the CU, is
+  // best at 1024: 2048 sets 1.08 ms, 512 0.93, 1024 0.89)
+  {
+    const FastForm &ff = b->ctx_kind == CTX_XDP ? im.fx : im.fr;
+    uint32_t want = 0;
+    if (prog.comb_entries) {
+      want = 2 * kComb;
+      if (ff.comb_hint == ~0u)
+        want = 1024;
+      else
+        while (want < kCombMax && 32ull * want < ff.comb_hint) want *= 2;
+    }
+    if (p.lcache && block == kBigBlock && want < 2048 && !getenv("BPFTIME_AMD_LCACHE_SETS")) p.lcache = 2 * kLcacheSets;
+    p.fast = im.linked(b->ctx_kind == CTX_XDP, b->ctx_kind == CTX_XDP ? b->head : 0, p.stage, ordered, unwind_helper,
+                       p.lcache);
+    if (!p.fast) {
+      error = "device upload failed";
+      return -1;
+    }
+  }
   auto dyn_of = [&](uint32_t e) {
     return dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, e, p.lcache, !gctx, block);
   };

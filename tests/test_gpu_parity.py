@@ -631,3 +631,12 @@ def test_random_xdp_programs(fresh_oracle, fresh_runtime, monkeypatch, asm_group
         for k in range(4):
             key = struct.pack("<I", k)
             assert dm.lookup(key) == om.lookup(key), (t, k)
+
+
+def test_random_programs_unfused(fresh_oracle, fresh_runtime, monkeypatch):
+    """The same random programs with the loader's superinstructions off
+    (loader.cpp fuse_pairs: `mov; add` and `mov imm; jump / exit` pairs run
+    as two dispatches): the fused and unfused forms both match the oracle."""
+    monkeypatch.setenv("BPFTIME_AMD_NO_FUSE", "1")
+    test_random_xdp_programs(fresh_oracle, fresh_runtime, monkeypatch, True)
+    test_random_programs(fresh_oracle, fresh_runtime, monkeypatch, True)
