@@ -39,6 +39,13 @@ class EbpfBatch(C.Structure):  # include/ebpf-vm.h struct ebpf_batch
                 ("umem_bytes", C.c_uint64), ("sys_nr", C.c_int64)]
 
 
+class PerfEvent(C.Structure):
+    """struct bpftime_amd_perf_event (include/bpftime_amd.h)"""
+    _fields_ = [("type", C.c_int), ("pid", C.c_int), ("enabled", C.c_int), ("tracepoint_id", C.c_int32),
+                ("sys_nr", C.c_int64), ("offset", C.c_uint64), ("ref_ctr_off", C.c_uint64),
+                ("module_name", C.c_char_p), ("cpu", C.c_int), ("sample_type", C.c_int32), ("config", C.c_int64)]
+
+
 # (name, restype, argtypes) for every exported symbol of include/*.h
 SIGNATURES = [
     # include/ebpf-vm.h
@@ -122,6 +129,18 @@ SIGNATURES = [
     ("bpftime_amd_perf_event_syscall", C.c_int, [C.c_int, C.c_int64]),
     ("bpftime_is_perf_event_fd", C.c_int, [C.c_int]),
     ("bpftime_attach_perf_to_bpf", C.c_int, [C.c_int, C.c_int]),
+    ("bpftime_tracepoint_create", C.c_int, [C.c_int, C.c_int, C.c_int32]),
+    ("bpftime_uprobe_create", C.c_int, [C.c_int, C.c_int, C.c_char_p, C.c_uint64, C.c_bool, C.c_size_t]),
+    ("bpftime_perf_event_enable", C.c_int, [C.c_int]),
+    ("bpftime_perf_event_disable", C.c_int, [C.c_int]),
+    ("bpftime_amd_perf_event_record", C.c_int, [C.c_int, C.POINTER(PerfEvent)]),
+    ("bpftime_amd_perf_event_get", C.c_int, [C.c_int, C.POINTER(PerfEvent)]),
+    ("bpftime_amd_link_perf", C.c_int, [C.c_int, C.c_int, C.c_int]),
+    ("bpftime_amd_link_attached", C.c_int, [C.c_int]),
+    ("bpftime_amd_set_tracefs_events", C.c_int, [C.c_char_p]),
+    ("bpftime_amd_tracepoint_resolve", C.c_int, [C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int)]),
+    ("bpftime_amd_tracepoint_id", C.c_int32, [C.c_int64, C.c_int]),
+    ("bpftime_amd_syscall_nr", C.c_int64, [C.c_char_p]),
     ("bpftime_amd_attach_create", C.c_void_p, [C.c_int, C.c_int]),
     ("bpftime_amd_attach_run", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint64)]),
     ("bpftime_amd_attach_run_batch", C.c_int, [C.c_void_p, C.POINTER(EbpfBatch)]),

@@ -284,6 +284,7 @@ inline uint32_t log_words_for(uint32_t comb_entries, uint32_t block = kBlock) {
 // blocks of 4 waves (flow-hash: 8 -> 16 resident waves per CU at the same
 // or a larger table reach)
 constexpr uint32_t kBigBlock = 1024;
+constexpr size_t kCuLds = 160 * 1024;  // LDS per CU (gfx950)
 
 // Dynamic LDS of an interpreter block: the lanes' XDP ctx (48 B each), their
 // stacks (LDS-stack programs), 48 B of launch constants (interp.hip

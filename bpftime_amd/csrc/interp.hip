@@ -1322,6 +1322,9 @@ extern "C" hipError_t bpftime_amd_launch_miss_merge(const uint64_t *log, const u
 }
 
 extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds, bool gregs, uint32_t block) {
+  // (a block asking for more LDS than a CU has never fits, whatever the
+  // occupancy query answers for it)
+  if (dyn_lds > kCuLds) return 0;
   int n = 0;
   hipError_t e;
 #define O(K, B, G) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_interp<K, B, false, G, kBlock>, kBlock, dyn_lds)

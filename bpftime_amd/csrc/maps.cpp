@@ -979,6 +979,7 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
   m.btf_id = attr.btf_id;
   m.btf_key_type_id = attr.btf_key_type_id;
   m.btf_value_type_id = attr.btf_value_type_id;
+  m.kernel_bpf_map_id = attr.kernel_bpf_map_id;
   m.map_extra = attr.map_extra;
   DMap &d = m.d;
   d.type = m.type;
@@ -1673,10 +1674,26 @@ int bpftime_progs_create(int fd, const void *insns, size_t insn_cnt, const char 
   return fd;
 }
 
+static int link_perf(int fd, int prog_fd, int perf_fd, bool strict);
+
 // bpftime_shm_internal.cpp:566-607: only prog_fd is validated; the target of
 // an XDP link is an ifindex.
 int bpftime_link_create(int fd, struct bpf_link_create_args *args) {
   Runtime &r = rt();
+  if (args && args->attach_type == BPFTIME_AMD_BPF_PERF_EVENT) {
+    // :578-600: a perf-event link's target must be a perf event (libbpf
+    // probes with target_fd -1 and expects EBADF); it attaches like
+    // BPF_PROG_ATTACH
+    if (!bpftime_is_perf_event_fd((int)args->target_fd)) {
+      errno = EBADF;
+      return -1;
+    }
+    if (!bpftime_is_prog_fd((int)args->prog_fd)) {
+      errno = EBADF;
+      return -1;
+    }
+    return link_perf(fd, (int)args->prog_fd, (int)args->target_fd, true);
+  }
   std::lock_guard<std::mutex> g(r.mu);
   if (!args) {
     errno = EINVAL;
@@ -1833,54 +1850,181 @@ int bpftime_amd_map_msync(int fd) {
   return view_push(*m) < 0 || view_pull(*m) < 0 ? -1 : 0;
 }
 
-// ---- tracepoint perf events + BPF_PROG_ATTACH (bpftime_shm.cpp:249-253,
-// bpftime_shm_internal.cpp:282-314) -----------------------------------------
-int bpftime_amd_perf_event_syscall(int fd, int64_t sys_nr) {
+// ---- perf events + BPF_PROG_ATTACH (bpftime_shm.cpp:227-253,
+// bpftime_shm_internal.cpp:212-315) ------------------------------------------
+static int perf_create(int fd, const PerfRec &p) {
   Runtime &r = rt();
   std::lock_guard<std::mutex> g(r.mu);
-  if (sys_nr < -1) {
-    errno = EINVAL;
-    return -1;
-  }
   fd = alloc_fd(fd);
   if (fd < 0) return -1;
-  r.perfs[fd].sys_nr = sys_nr;
+  r.perfs[fd] = p;
   r.kind[fd] = HKind::PERF;
   return fd;
 }
 
+int bpftime_amd_perf_event_syscall(int fd, int64_t sys_nr) {
+  if (sys_nr < -1) {
+    errno = EINVAL;
+    return -1;
+  }
+  PerfRec p;
+  p.sys_nr = sys_nr;
+  return perf_create(fd, p);
+}
+
+// add_tracepoint (:254-264): the id is resolved when a program attaches
+int bpftime_tracepoint_create(int fd, int pid, int32_t tp_id) {
+  PerfRec p;
+  p.pid = pid;
+  p.tracepoint_id = tp_id;
+  return perf_create(fd, p);
+}
+
+// add_uprobe / add_uprobe_override (:212-252): records only, nothing on this
+// path probes a process
+int bpftime_uprobe_create(int fd, int pid, const char *name, uint64_t offset, bool retprobe, size_t ref_ctr_off) {
+  PerfRec p;
+  p.type = retprobe ? 7 : 6;
+  p.pid = pid;
+  p.module = name ? name : "";
+  p.offset = offset;
+  p.ref_ctr_off = ref_ctr_off;
+  return perf_create(fd, p);
+}
+
+int bpftime_amd_perf_event_record(int fd, const struct bpftime_amd_perf_event *e) {
+  if (!e) {
+    errno = EINVAL;
+    return -1;
+  }
+  PerfRec p;
+  p.type = e->type;
+  p.pid = e->pid;
+  p.enabled = e->enabled != 0;
+  p.tracepoint_id = e->tracepoint_id;
+  p.sys_nr = e->sys_nr;
+  p.offset = e->offset;
+  p.ref_ctr_off = e->ref_ctr_off;
+  p.module = e->module_name ? e->module_name : "";
+  p.cpu = e->cpu;
+  p.sample_type = e->sample_type;
+  p.config = e->config;
+  return perf_create(fd, p);
+}
+
+int bpftime_amd_perf_event_get(int fd, struct bpftime_amd_perf_event *e) {
+  Runtime &r = rt();
+  std::lock_guard<std::mutex> g(r.mu);
+  if (fd < 0 || fd >= (int)kMaxFds || r.kind[fd] != HKind::PERF || !e) {
+    errno = ENOENT;
+    return -1;
+  }
+  const PerfRec &p = r.perfs[fd];
+  e->type = p.type;
+  e->pid = p.pid;
+  e->enabled = p.enabled;
+  e->tracepoint_id = p.tracepoint_id;
+  e->sys_nr = p.sys_nr;
+  e->offset = p.offset;
+  e->ref_ctr_off = p.ref_ctr_off;
+  e->module_name = p.module.c_str();  // valid until the record changes
+  e->cpu = p.cpu;
+  e->sample_type = p.sample_type;
+  e->config = p.config;
+  return 0;
+}
+
+static int perf_enable(int fd, bool on) {  // :317-337
+  Runtime &r = rt();
+  std::lock_guard<std::mutex> g(r.mu);
+  if (fd < 0 || fd >= (int)kMaxFds || r.kind[fd] != HKind::PERF) {
+    errno = ENOENT;
+    return -1;
+  }
+  r.perfs[fd].enabled = on;
+  return 0;
+}
+int bpftime_perf_event_enable(int fd) { return perf_enable(fd, true); }
+int bpftime_perf_event_disable(int fd) { return perf_enable(fd, false); }
+
 int bpftime_is_perf_event_fd(int fd) { return fd >= 0 && fd < (int)kMaxFds && rt().kind[fd] == HKind::PERF; }
 
-int bpftime_attach_perf_to_bpf(int perf_fd, int bpf_fd) {
+// What a link to perf event p drives: 1 + the sys_enter dispatch slot for a
+// syscall enter tracepoint (the global one: sys_nr -1), 0 for a record that
+// runs nothing on this path (sys_exit tracepoints: the replay holds enter
+// records only; uprobes, software events), -1 for a tracepoint id that does
+// not resolve (the reference's attach fails there too,
+// syscall_trace_attach_private_data.cpp:51-62)
+static int perf_drives(const PerfRec &p, int64_t *nr) {
+  if (p.type != 2) return 0;
+  int enter = 1;
+  *nr = p.sys_nr;
+  if (p.tracepoint_id >= 0 && bpftime_amd_tracepoint_resolve(p.tracepoint_id, nr, &enter) < 0) return -1;
+  return enter ? 1 : 0;
+}
+
+// A link from prog_fd to perf_fd at `fd` (-1: a fresh one).  A link to a
+// sys_enter tracepoint attaches the program to the syscall dispatch (it is
+// instantiated: a program the device cannot load fails the link); any other
+// perf target gives a link record that runs nothing.  `strict`: a
+// tracepoint id that does not resolve fails the link (BPF_PROG_ATTACH,
+// BPF_LINK_CREATE) instead of leaving it inert (a JSON import, which the
+// reference accepts and resolves only when its agent attaches).
+static int link_perf(int fd, int prog_fd, int perf_fd, bool strict) {
   Runtime &r = rt();
-  int64_t nr;
+  int64_t nr = -1;
+  int drives;
   {
     std::lock_guard<std::mutex> g(r.mu);
-    if (!bpftime_is_perf_event_fd(perf_fd)) {  // "Fd is not a perf fd"
+    if (perf_fd < 0 || perf_fd >= (int)kMaxFds || r.kind[perf_fd] != HKind::PERF) {  // "Fd is not a perf fd"
       errno = ENOENT;
       return -1;
     }
-    if (bpf_fd < 0 || bpf_fd >= (int)kMaxFds || r.kind[bpf_fd] != HKind::PROG) {
+    if (prog_fd < 0 || prog_fd >= (int)kMaxFds || r.kind[prog_fd] != HKind::PROG) {
       errno = ENOENT;
       return -1;
     }
-    nr = r.perfs[perf_fd].sys_nr;
+    if (fd >= 0 && (fd >= (int)kMaxFds || r.kind[fd] != HKind::NONE)) {
+      errno = EBADF;
+      return -1;
+    }
+    drives = perf_drives(r.perfs[perf_fd], &nr);
   }
-  const int id = bpftime_amd_syscall_attach(bpf_fd, nr);  // instantiates the program (outside the lock)
-  if (id < 0) return -1;
+  if (drives < 0 && strict) {
+    errno = EEXIST;
+    return -1;
+  }
+  int id = 0;
+  if (drives > 0) {
+    id = bpftime_amd_syscall_attach(prog_fd, nr);  // instantiates the program (outside the lock)
+    if (id < 0) return -1;
+  }
   std::lock_guard<std::mutex> g(r.mu);
-  const int fd = alloc_fd(-1);
+  fd = alloc_fd(fd);
   if (fd < 0) {
-    bpftime_amd_syscall_detach(id);
+    if (id) bpftime_amd_syscall_detach(id);
     return -1;
   }
   LinkRec l;
-  l.prog_fd = (uint32_t)bpf_fd;
+  l.prog_fd = (uint32_t)prog_fd;
   l.target = (uint32_t)perf_fd;
+  l.attach_type = BPFTIME_AMD_BPF_PERF_EVENT;
+  l.perf = true;
   l.attach_id = id;
   r.links[fd] = l;
   r.kind[fd] = HKind::LINK;
   return fd;
+}
+
+int bpftime_attach_perf_to_bpf(int perf_fd, int bpf_fd) { return link_perf(-1, bpf_fd, perf_fd, true); }
+
+int bpftime_amd_link_perf(int fd, int prog_fd, int perf_fd) { return link_perf(fd, prog_fd, perf_fd, false); }
+
+int bpftime_amd_link_attached(int fd) {
+  Runtime &r = rt();
+  std::lock_guard<std::mutex> g(r.mu);
+  if (fd < 0 || fd >= (int)kMaxFds || r.kind[fd] != HKind::LINK) return -1;
+  return r.links[fd].attach_id ? 1 : 0;
 }
 
 // ---- host merge ------------------------------------------------------------

@@ -28,6 +28,7 @@ struct MapRec {
   // BPF_MAP_CREATE attributes as given (BPF_OBJ_GET_INFO_BY_FD reports them)
   uint32_t ifindex = 0, btf_vmlinux_value_type_id = 0, btf_id = 0, btf_key_type_id = 0, btf_value_type_id = 0;
   uint64_t map_extra = 0;
+  uint32_t kernel_bpf_map_id = 0;
   // host view of an ARRAY map (bpftime_get_array_map_raw_data, the mmap a
   // libbpf loader makes of .bss / .data): page-aligned host bytes kept
   // coherent with the device copy at batch boundaries (maps.cpp host_view_*)
@@ -36,10 +37,22 @@ struct MapRec {
   std::vector<uint8_t> host_shadow;  // the bytes last exchanged with the device
 };
 
-// A tracepoint perf event (perf_event_open of a syscall sys_enter
-// tracepoint, the target BPF_PROG_ATTACH links a program to)
+// A perf event record (bpf_perf_event_handler, runtime/src/handler/
+// perf_event_handler.hpp:161-215): what a link's target_fd names.  Only a
+// syscall sys_enter tracepoint drives anything here (the syscall replay
+// dispatch); the other kinds are kept as records, so state that holds them
+// imports, exports and links unchanged.
 struct PerfRec {
-  int64_t sys_nr = -1;  // -1: every syscall (raw_syscalls:sys_enter)
+  int type = 2;                // bpf_event_type (bpftime_shm.hpp:48-64); 2 = PERF_TYPE_TRACEPOINT
+  int pid = -1;
+  bool enabled = false;        // perf_event_enable / _disable (a flag only, as in the reference)
+  int32_t tracepoint_id = -1;  // tracepoint: the kernel id (tracepoints.cpp), or -1 when made from
+  int64_t sys_nr = -1;         // ... a syscall number (bpftime_amd_perf_event_syscall; -1: every syscall)
+  uint64_t offset = 0, ref_ctr_off = 0;  // uprobe / uretprobe / uprobe override
+  std::string module;
+  int cpu = 0;                 // software perf event
+  int32_t sample_type = 0;
+  int64_t config = 0;
 };
 
 struct ProgRec {
@@ -50,7 +63,8 @@ struct ProgRec {
 
 struct LinkRec {
   uint32_t prog_fd = 0, target = 0, attach_type = 0, flags = 0;
-  int attach_id = 0;  // a perf link: its syscall attachment (syscall_dispatch.cpp)
+  bool perf = false;  // target is a perf event record (maps.cpp link_perf)
+  int attach_id = 0;  // a perf link to a sys_enter tracepoint: its syscall attachment (syscall_dispatch.cpp)
 };
 
 enum class HKind : uint8_t { NONE, MAP, PROG, LINK, PERF };

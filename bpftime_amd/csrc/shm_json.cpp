@@ -10,14 +10,28 @@
 //              insns: hex bytes, cnt, attach_fds?}},
 //     "<fd>": {"type": "bpf_link_handler", "attr": {prog_fd, target_fd}} }
 //
+//     "<fd>": {"type": "bpf_perf_event_handler", "enabled": bool, "attr":
+//              {type, pid, tracepoint_id | offset, ref_ctr_off, _module_name
+//              | cpu, sample_type, config}},
+//     "<fd>": {"type": "bpf_link_handler", "attr": {prog_fd, target_fd}} }
+//
 // Importing such a file recreates the records at the same fds in this
 // runtime's registry (maps in HBM), so state loaded by the reference's
 // libbpf path (real clang objects, LD_PRELOAD syscall server) runs on the
-// GPU unchanged.  The format does not keep a link's attach type; a link to an
-// XDP program (prog type 6) is taken as a BPF_XDP link, since that is the
-// only kind this runtime executes.  Handler kinds outside this path (perf
-// events, epoll, memfd) are rejected, as the reference rejects the kinds it
-// cannot import.  Host-only code.
+// GPU unchanged.  The format does not keep a link's attach type: a link
+// whose target is a perf event record (and whose program is not XDP) is a
+// perf link, and one to a syscall sys_enter tracepoint attaches its program
+// to the replay dispatch (tracepoint id -> syscall number as the reference
+// resolves it, tracepoints.cpp); a link to an XDP program is a BPF_XDP link.
+// A prog's `attach_fds` (:123-125) become links at fresh fds, after every
+// record of the file exists.  Perf events that run nothing on this path
+// (uprobes, software events, sys_exit tracepoints) are kept as records.
+// Handler kinds outside this path (epoll, memfd) are rejected, as the
+// reference rejects the kinds it cannot import.  Export writes what the
+// reference's export writes (:235-327: attachments as link records, no
+// attach_fds -- its comment at :271 has no code behind it, and writing both
+// would attach twice on re-import), plus "sys_nr" beside a tracepoint made
+// from a syscall number when the tracefs has no id for it.  Host-only code.
 #include <ctype.h>
 #include <errno.h>
 #include <stdio.h>
@@ -258,7 +272,9 @@ bool from_hex(const std::string &s, std::vector<uint8_t> &out, size_t n) {
   return true;
 }
 
-int import_handler(int fd, const J &v, std::string &err) {
+// attach: where a prog's attach_fds go ({prog fd, perf fd}), linked by the
+// caller once the records they name exist
+int import_handler(int fd, const J &v, std::string &err, std::vector<std::pair<int, int>> *attach) {
   using namespace bpftime_amd;
   const J *type = v.get("type");
   const J *attr = v.get("attr");
@@ -307,6 +323,69 @@ int import_handler(int fd, const J &v, std::string &err) {
       err = "prog " + std::to_string(fd) + ": cannot create";
       return -1;
     }
+    if (const J *af = attr->get("attach_fds")) {
+      if (af->k != J::ARR && af->k != J::NUL) {
+        err = "prog " + std::to_string(fd) + ": attach_fds is not an array";
+        return -1;
+      }
+      for (const J &x : af->a) {
+        bool k = true;
+        const long long t = num(&x, &k);
+        if (!k) {
+          err = "prog " + std::to_string(fd) + ": bad attach fd";
+          return -1;
+        }
+        if (attach) attach->emplace_back(fd, (int)t);
+      }
+    }
+    return 0;
+  }
+  if (type->s == "bpf_perf_event_handler") {
+    bpftime_amd_perf_event e{};
+    e.type = (int)num(attr->get("type"), &ok);
+    e.pid = (int)num(attr->get("pid"), &ok);
+    e.tracepoint_id = -1;
+    e.sys_nr = -1;
+    std::string module;
+    switch (e.type) {
+      case 2: {  // PERF_TYPE_TRACEPOINT
+        e.tracepoint_id = (int32_t)num(attr->get("tracepoint_id"), &ok);
+        bool has = true;
+        const long long nr = num(attr->get("sys_nr"), &has);  // (this runtime's export, see above)
+        if (has && e.tracepoint_id < 0) e.sys_nr = nr;
+        break;
+      }
+      case 6:  // BPF_TYPE_UPROBE
+      case 7:  // BPF_TYPE_URETPROBE
+        e.ref_ctr_off = (uint64_t)num(attr->get("ref_ctr_off"), &ok);
+        /* fall through */
+      case 1008: {  // BPF_TYPE_UPROBE_OVERRIDE
+        e.offset = (uint64_t)num(attr->get("offset"), &ok);
+        const J *mn = attr->get("_module_name");
+        if (!mn || mn->k != J::STR) ok = false;
+        else module = mn->s;
+        e.module_name = module.c_str();
+        break;
+      }
+      case 1:  // PERF_TYPE_SOFTWARE
+        e.cpu = (int)num(attr->get("cpu"), &ok);
+        e.sample_type = (int32_t)num(attr->get("sample_type"), &ok);
+        e.config = (int64_t)num(attr->get("config"), &ok);
+        break;
+      default:
+        err = "perf event " + std::to_string(fd) + ": Unsupported perf event type " + std::to_string(e.type);
+        return -1;
+    }
+    if (!ok) {
+      err = "perf event " + std::to_string(fd) + ": missing attribute";
+      return -1;
+    }
+    const J *en = v.get("enabled");
+    e.enabled = en && en->k == J::BOOL && en->b;
+    if (bpftime_amd_perf_event_record(fd, &e) != fd) {
+      err = "perf event " + std::to_string(fd) + ": cannot create";
+      return -1;
+    }
     return 0;
   }
   if (type->s == "bpf_link_handler") {
@@ -317,11 +396,21 @@ int import_handler(int fd, const J &v, std::string &err) {
       err = "link " + std::to_string(fd) + ": missing prog_fd / target_fd";
       return -1;
     }
+    bool xdp = false, perf = false;
     {
       Runtime &r = rt();
       std::lock_guard<std::mutex> g(r.mu);
-      if (a.prog_fd < kMaxFds && r.kind[a.prog_fd] == HKind::PROG && r.progs[a.prog_fd].type == BPFTIME_AMD_PROG_TYPE_XDP)
-        a.attach_type = BPFTIME_AMD_BPF_XDP;
+      xdp = a.prog_fd < kMaxFds && r.kind[a.prog_fd] == HKind::PROG && r.progs[a.prog_fd].type == BPFTIME_AMD_PROG_TYPE_XDP;
+      perf = a.target_fd < kMaxFds && r.kind[a.target_fd] == HKind::PERF;
+    }
+    if (xdp) a.attach_type = BPFTIME_AMD_BPF_XDP;
+    if (perf && !xdp) {
+      if (bpftime_amd_link_perf(fd, (int)a.prog_fd, (int)a.target_fd) != fd) {
+        err = "link " + std::to_string(fd) + ": prog fd " + std::to_string(a.prog_fd) + " -> perf event " +
+              std::to_string(a.target_fd) + ": " + bpftime_amd_last_error();
+        return -1;
+      }
+      return 0;
     }
     if (bpftime_link_create(fd, &a) != fd) {
       err = "link " + std::to_string(fd) + ": prog fd " + std::to_string(a.prog_fd) + " is not a program";
@@ -331,6 +420,29 @@ int import_handler(int fd, const J &v, std::string &err) {
   }
   err = "unsupported handler type " + type->s;
   return -1;
+}
+
+// add_bpf_prog_attach_target (bpftime_shm_internal.cpp:293-315): a link
+// at a fresh fd; the target is not checked there, so a target that is no
+// perf event gives a plain link record
+int link_attach_fds(const std::vector<std::pair<int, int>> &attach, std::string &err) {
+  for (const auto &pa : attach) {
+    int rc;
+    if (bpftime_is_perf_event_fd(pa.second)) {
+      rc = bpftime_amd_link_perf(-1, pa.first, pa.second);
+    } else {
+      bpf_link_create_args a{};
+      a.prog_fd = (uint32_t)pa.first;
+      a.target_fd = (uint32_t)pa.second;
+      rc = bpftime_link_create(-1, &a);
+    }
+    if (rc < 0) {
+      err = "prog " + std::to_string(pa.first) + ": attach fd " + std::to_string(pa.second) + ": " +
+            bpftime_amd_last_error();
+      return -1;
+    }
+  }
+  return 0;
 }
 
 bool read_file(const char *path, std::string &out) {
@@ -355,7 +467,8 @@ int bpftime_import_shm_handler_from_json(int fd, const char *json_string) {
     errno = EINVAL;
     return -1;
   }
-  if (import_handler(fd, v, err) < 0) {
+  std::vector<std::pair<int, int>> attach;
+  if (import_handler(fd, v, err, &attach) < 0 || link_attach_fds(attach, err) < 0) {
     bpftime_amd::set_error(err);
     errno = EINVAL;
     return -1;
@@ -376,7 +489,9 @@ int bpftime_import_global_shm_from_json(const char *filename) {
     errno = EINVAL;
     return -1;
   }
-  // maps and programs before links (a link names its program's fd)
+  // maps, programs and perf events before links (a link names its program
+  // and its target), a prog's attach_fds last
+  std::vector<std::pair<int, int>> attach;
   for (int pass = 0; pass < 2; pass++)
     for (auto &kv : root.o) {
       const J *t = kv.second.get("type");
@@ -389,12 +504,17 @@ int bpftime_import_global_shm_from_json(const char *filename) {
         errno = EINVAL;
         return -1;
       }
-      if (import_handler((int)fd, kv.second, err) < 0) {
+      if (import_handler((int)fd, kv.second, err, &attach) < 0) {
         bpftime_amd::set_error(err);
         errno = EINVAL;
         return -1;
       }
     }
+  if (link_attach_fds(attach, err) < 0) {
+    bpftime_amd::set_error(err);
+    errno = EINVAL;
+    return -1;
+  }
   return 0;
 }
 
@@ -411,16 +531,42 @@ int bpftime_export_global_shm_to_json(const char *filename) {
         const MapRec &m = r.maps[fd];
         char buf[512];
         snprintf(buf, sizeof buf,
-                 "{\"attr\": {\"btf_id\": 0, \"btf_key_type_id\": 0, \"btf_value_type_id\": 0, "
-                 "\"btf_vmlinux_value_type_id\": 0, \"flags\": %llu, \"ifindex\": 0, \"kernel_bpf_map_id\": 0, "
-                 "\"key_size\": %u, \"map_extra\": 0, \"map_type\": %u, \"max_entries\": %u, \"value_size\": %u}, ",
-                 (unsigned long long)m.flags, m.key_size, m.type, m.max_entries, m.value_size);
+                 "{\"attr\": {\"btf_id\": %u, \"btf_key_type_id\": %u, \"btf_value_type_id\": %u, "
+                 "\"btf_vmlinux_value_type_id\": %u, \"flags\": %llu, \"ifindex\": %u, \"kernel_bpf_map_id\": %u, "
+                 "\"key_size\": %u, \"map_extra\": %llu, \"map_type\": %u, \"max_entries\": %u, \"value_size\": %u}, ",
+                 m.btf_id, m.btf_key_type_id, m.btf_value_type_id, m.btf_vmlinux_value_type_id,
+                 (unsigned long long)m.flags, m.ifindex, m.kernel_bpf_map_id, m.key_size,
+                 (unsigned long long)m.map_extra, m.type, m.max_entries, m.value_size);
         item = std::string(buf) + "\"name\": " + quote(m.name) + ", \"type\": \"bpf_map_handler\"}";
       } else if (r.kind[fd] == HKind::PROG) {
         const ProgRec &p = r.progs[fd];
         item = "{\"attr\": {\"cnt\": " + std::to_string(p.insns.size() / 8) + ", \"insns\": \"" +
                to_hex(p.insns.data(), p.insns.size()) + "\", \"type\": " + std::to_string(p.type) +
                "}, \"name\": " + quote(p.name) + ", \"type\": \"bpf_prog_handler\"}";
+      } else if (r.kind[fd] == HKind::PERF) {
+        // bpf_perf_event_handler_attr_to_json (:66-95), keys in its order
+        const PerfRec &p = r.perfs[fd];
+        std::string a;
+        if (p.type == 6 || p.type == 7 || p.type == 1008) {
+          a = "\"_module_name\": " + quote(p.module) + ", \"data_type\": \"uprobe_perf_event_data\", \"offset\": " +
+              std::to_string(p.offset) + ", \"pid\": " + std::to_string(p.pid) + ", \"ref_ctr_off\": " +
+              std::to_string(p.ref_ctr_off) + ", ";
+        } else if (p.type == 2) {
+          int32_t id = p.tracepoint_id;
+          std::string nr;
+          if (id < 0) {
+            id = bpftime_amd_tracepoint_id(p.sys_nr, 1);
+            if (id < 0) nr = "\"sys_nr\": " + std::to_string(p.sys_nr) + ", ";
+          }
+          a = "\"data_type\": \"tracepoint_perf_event_data\", \"pid\": " + std::to_string(p.pid) + ", " + nr +
+              "\"tracepoint_id\": " + std::to_string(id) + ", ";
+        } else if (p.type == 1) {
+          a = "\"config\": " + std::to_string(p.config) + ", \"cpu\": " + std::to_string(p.cpu) +
+              ", \"data_type\": \"software_perf_event_shared_ptr\", \"pid\": " + std::to_string(p.pid) +
+              ", \"sample_type\": " + std::to_string(p.sample_type) + ", ";
+        }
+        item = "{\"attr\": {" + a + "\"type\": " + std::to_string(p.type) + "}, \"enabled\": " +
+               (p.enabled ? "true" : "false") + ", \"type\": \"bpf_perf_event_handler\"}";
       } else if (r.kind[fd] == HKind::LINK) {
         const LinkRec &l = r.links[fd];
         item = "{\"attr\": {\"prog_fd\": " + std::to_string(l.prog_fd) + ", \"target_fd\": " +

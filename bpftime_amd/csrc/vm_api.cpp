@@ -513,6 +513,23 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
         while (want < kCombMax && 32ull * want < ff.comb_hint) want *= 2;
     }
     if (p.lcache && block == kBigBlock && want < 2048 && !getenv("BPFTIME_AMD_LCACHE_SETS")) p.lcache = 2 * kLcacheSets;
+    // a 1024-lane block must fit the CU with the smallest table it may get
+    // (lanes' ctx and stacks, lookup cache, launch constants): drop the
+    // doubled lookup cache first, then fall back to 256-lane blocks
+    if (block == kBigBlock) {
+      const uint32_t e_min = prog.comb_entries ? kComb : 0;
+      auto fits = [&](uint32_t lc) {
+        return bpftime_amd_occupancy(b->ctx_kind, prog.big_stack,
+                                     dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, e_min, lc, !gctx,
+                                                 kBigBlock),
+                                     greg, kBigBlock) >= 1;
+      };
+      if (!fits(p.lcache) && p.lcache > kLcacheSets && !getenv("BPFTIME_AMD_LCACHE_SETS")) p.lcache = kLcacheSets;
+      if (!fits(p.lcache)) {
+        block = kBlock;
+        if (!getenv("BPFTIME_AMD_LCACHE_SETS")) p.lcache = p.lcache ? lcache_sets() : 0;
+      }
+    }
     p.fast = im.linked(b->ctx_kind == CTX_XDP, b->ctx_kind == CTX_XDP ? b->head : 0, p.stage, ordered, unwind_helper,
                        p.lcache);
     if (!p.fast) {

@@ -94,7 +94,10 @@ class Map:
             raise EbpfError(f"fd {fd} is not a map")
         m = cls.__new__(cls)
         m.fd = fd
-        m.type = m.key_size = m.value_size = m.max_entries = None
+        a = BpfMapAttr()
+        if lib().bpftime_map_get_info(fd, C.byref(a), None, None) < 0:
+            raise EbpfError(f"fd {fd}: no map info")
+        m.type, m.key_size, m.value_size, m.max_entries = a.type, a.key_size, a.value_size, a.max_ents
         return m
 
     def ringbuf_fetch(self, cap: int = 1 << 24) -> list:

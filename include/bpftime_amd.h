@@ -11,6 +11,7 @@
 #ifndef BPFTIME_AMD_H
 #define BPFTIME_AMD_H
 
+#include <stdbool.h>
 #include <stddef.h>
 #include <stdint.h>
 #include "ebpf-vm.h"
@@ -46,6 +47,7 @@ struct bpf_link_create_args {
 };
 
 #define BPFTIME_AMD_BPF_XDP 37
+#define BPFTIME_AMD_BPF_PERF_EVENT 41      /* BPFTIME_BPF_PERF_EVENT_ATTACH_TYPE, bpftime_shm.hpp:247 */
 #define BPFTIME_AMD_PROG_TYPE_XDP 6        /* bpftime_shm.hpp:144-151 */
 #define BPFTIME_AMD_PROG_TYPE_TRACEPOINT 5
 
@@ -83,16 +85,71 @@ int bpftime_amd_map_msync(int fd); /* push host writes, wait for the device, pul
 /* ---- progs / links (bpftime_shm.hpp:303-309) ---- */
 int bpftime_progs_create(int fd, const void *insns, size_t insn_cnt, const char *prog_name, int prog_type);
 int bpftime_link_create(int fd, struct bpf_link_create_args *args);
-/* A syscall sys_enter tracepoint perf event (what perf_event_open of
- * syscalls:sys_enter_<nr>, or raw_syscalls:sys_enter for sys_nr = -1,
- * creates in the reference's syscall server): a new fd, or `fd` when >= 0. */
+/* ---- perf events (bpftime_shm.hpp:351-380; bpf_perf_event_handler,
+ * runtime/src/handler/perf_event_handler.hpp:161-215) ----
+ * The targets a link or BPF_PROG_ATTACH names.  A syscall sys_enter
+ * tracepoint drives the replay dispatch (bpftime_amd_syscall_dispatch); the
+ * other kinds (sys_exit tracepoints, uprobes, software events) are kept as
+ * records so the reference's state imports, exports and links unchanged.
+ *
+ * A syscall sys_enter tracepoint perf event by syscall number (what
+ * perf_event_open of syscalls:sys_enter_<nr>, or raw_syscalls:sys_enter for
+ * sys_nr = -1, creates): a new fd, or `fd` when >= 0. */
 int bpftime_amd_perf_event_syscall(int fd, int64_t sys_nr);
+/* bpftime_shm.hpp:368 (add_tracepoint): by tracepoint id; the id resolves to
+ * (syscall number, enter / exit) when a program attaches
+ * (bpftime_amd_tracepoint_resolve). */
+int bpftime_tracepoint_create(int fd, int pid, int32_t tp_id);
+/* bpftime_shm.hpp:356-357: a uprobe / uretprobe record. */
+int bpftime_uprobe_create(int fd, int pid, const char *name, uint64_t offset, bool retprobe, size_t ref_ctr_off);
+/* bpftime_shm.hpp:371-374: the handler's enabled flag. */
+int bpftime_perf_event_enable(int fd);
+int bpftime_perf_event_disable(int fd);
 int bpftime_is_perf_event_fd(int fd);
+/* Any perf event record, with every field the reference's JSON carries
+ * (bpftime_shm_json.cpp:66-95, :130-180); get: the record at fd (module_name
+ * points into the record). */
+struct bpftime_amd_perf_event {
+  int type;               /* bpf_event_type: 1 software, 2 tracepoint, 6 uprobe, 7 uretprobe, 1008 override */
+  int pid;
+  int enabled;
+  int32_t tracepoint_id;  /* tracepoint: kernel id, or -1 with sys_nr */
+  int64_t sys_nr;         /* tracepoint without an id: the syscall (-1: every syscall) */
+  uint64_t offset;        /* uprobe kinds */
+  uint64_t ref_ctr_off;
+  const char *module_name;
+  int cpu;                /* software */
+  int32_t sample_type;
+  int64_t config;
+};
+int bpftime_amd_perf_event_record(int fd, const struct bpftime_amd_perf_event *e);
+int bpftime_amd_perf_event_get(int fd, struct bpftime_amd_perf_event *e);
 /* bpftime_shm.cpp:249-253 (BPF_PROG_ATTACH): link prog bpf_fd to the perf
- * event: a link fd whose close detaches it; the program then runs in
- * bpftime_amd_syscall_dispatch.  -1 + ENOENT when perf_fd is not a perf
- * event or bpf_fd not a program. */
+ * event: a link fd whose close detaches it; a program linked to a sys_enter
+ * tracepoint then runs in bpftime_amd_syscall_dispatch.  -1 + ENOENT when
+ * perf_fd is not a perf event or bpf_fd not a program, -1 + EEXIST when a
+ * tracepoint id does not resolve, -1 when the device cannot load the
+ * program. */
 int bpftime_attach_perf_to_bpf(int perf_fd, int bpf_fd);
+/* The same link at `fd` (-1: a fresh one), leaving a link to an unresolvable
+ * tracepoint id as a record (the JSON import's add_bpf_link: the reference
+ * resolves the id only when its agent attaches). */
+int bpftime_amd_link_perf(int fd, int prog_fd, int perf_fd);
+/* 1: the link drives a syscall attachment, 0: a record only, -1: not a link. */
+int bpftime_amd_link_attached(int fd);
+
+/* Syscall tracepoint ids (attach/syscall_trace_attach_impl/src/
+ * syscall_table.cpp:17-98, syscall_trace_attach_private_data.cpp:8-63):
+ * the tracefs events directory the ids are read from (default
+ * /sys/kernel/tracing/events, or $BPFTIME_AMD_TRACEFS_EVENTS); an id ->
+ * (syscall number, enter) with the reference's rules (raw_syscalls sys_enter
+ * / sys_exit -> -1; sys_enter_<name> / sys_exit_<name> -> <name>'s number),
+ * 0 or -EEXIST; the reverse (-1 when the directory has no such tracepoint);
+ * a syscall's number by name (-1 unknown). */
+int bpftime_amd_set_tracefs_events(const char *dir);
+int bpftime_amd_tracepoint_resolve(int32_t tp_id, int64_t *sys_nr, int *is_enter);
+int32_t bpftime_amd_tracepoint_id(int64_t sys_nr, int is_enter);
+int64_t bpftime_amd_syscall_nr(const char *name);
 
 /* ---- bpf(2) commands from an interposed loader ----
  * syscall_context::handle_sysbpf's userspace branch

@@ -10,14 +10,20 @@
  *   28 csum_diff                      :713-744
  *   44 xdp_adjust_head                :748-764
  *   65 xdp_adjust_tail                :766-776
+ *   6 trace_printk                    :64-76   (orc_vm_register_trace_helpers;
+ *   14 get_current_pid_tgid           :330-348  the host-process helpers of
+ *                                               tools/aot/example/malloc.json)
  * Registration order follows the kernel + shm-maps helper groups
  * (bpf_helper.cpp:1177-1401).
  */
 #include "oracle.h"
 #include <errno.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/syscall.h>
 #include <time.h>
+#include <unistd.h>
 
 struct xdp_md_userspace { /* runtime/extension/userspace_xdp.h:6-17 */
 	uint64_t data, data_end;
@@ -131,6 +137,114 @@ static uint64_t h_xdp_load_bytes(uint64_t ctx, uint64_t off_, uint64_t buf, uint
 		return (uint64_t)(int64_t)-EINVAL;
 	memcpy((void *)(uintptr_t)buf, (const void *)(uintptr_t)data, len);
 	return 0;
+}
+
+/* bpftime_trace_printk (:64-76): vprintf(fmt, r3..r5), returns 0.  Here the
+ * formatted text is appended to a log the tests read (orc_trace_log) instead
+ * of stdout; conversions d i u x X c s %% with l / ll length, as printf. */
+static char g_trace[1 << 16];
+static size_t g_trace_len;
+
+size_t orc_trace_log(char *out, size_t cap)
+{
+	size_t n = g_trace_len < cap ? g_trace_len : cap;
+	if (out)
+		memcpy(out, g_trace, n);
+	return g_trace_len;
+}
+
+void orc_trace_log_reset(void)
+{
+	g_trace_len = 0;
+}
+
+static void trace_put(const char *s, size_t n)
+{
+	if (n > sizeof(g_trace) - g_trace_len)
+		n = sizeof(g_trace) - g_trace_len;
+	memcpy(g_trace + g_trace_len, s, n);
+	g_trace_len += n;
+}
+
+static uint64_t h_trace_printk(uint64_t fmt_, uint64_t fmt_size, uint64_t a3, uint64_t a4, uint64_t a5)
+{
+	const char *f = (const char *)(uintptr_t)fmt_;
+	const uint64_t args[3] = { a3, a4, a5 };
+	int ai = 0;
+	char buf[64];
+	(void)fmt_size; /* vprintf reads up to the NUL, whatever the size says */
+	for (; *f; f++) {
+		if (*f != '%') {
+			trace_put(f, 1);
+			continue;
+		}
+		f++;
+		int l = 0;
+		while (*f == 'l') {
+			l++;
+			f++;
+		}
+		if (!*f)
+			break;
+		const uint64_t v = ai < 3 ? args[ai] : 0;
+		int n = 0;
+		switch (*f) {
+		case '%':
+			trace_put("%", 1);
+			continue;
+		case 'd':
+		case 'i':
+			n = l ? snprintf(buf, sizeof(buf), "%lld", (long long)v) : snprintf(buf, sizeof(buf), "%d", (int)v);
+			break;
+		case 'u':
+			n = l ? snprintf(buf, sizeof(buf), "%llu", (unsigned long long)v) :
+				snprintf(buf, sizeof(buf), "%u", (unsigned)v);
+			break;
+		case 'x':
+		case 'X':
+			n = l ? snprintf(buf, sizeof(buf), *f == 'x' ? "%llx" : "%llX", (unsigned long long)v) :
+				snprintf(buf, sizeof(buf), *f == 'x' ? "%x" : "%X", (unsigned)v);
+			break;
+		case 'c':
+			buf[0] = (char)v;
+			n = 1;
+			break;
+		case 's':
+			if (v)
+				trace_put((const char *)(uintptr_t)v, strlen((const char *)(uintptr_t)v));
+			ai++;
+			continue;
+		default:
+			continue;
+		}
+		ai++;
+		trace_put(buf, (size_t)n);
+	}
+	return 0;
+}
+
+/* bpftime_get_current_pid_tgid (:330-348): getpid() << 32 | gettid(), or
+ * the value a test fixes with orc_set_pid_tgid */
+static int g_pid_set;
+static uint64_t g_pid_tgid;
+
+void orc_set_pid_tgid(uint64_t v)
+{
+	g_pid_tgid = v;
+	g_pid_set = 1;
+}
+
+static uint64_t h_pid_tgid(uint64_t a, uint64_t b, uint64_t c, uint64_t d, uint64_t e)
+{
+	if (g_pid_set)
+		return g_pid_tgid;
+	return ((uint64_t)getpid() << 32) | (uint32_t)syscall(SYS_gettid);
+}
+
+int orc_vm_register_trace_helpers(struct orc_vm *vm)
+{
+	return orc_vm_register(vm, 6, "bpf_trace_printk", h_trace_printk) |
+	       orc_vm_register(vm, 14, "bpf_get_current_pid_tgid", h_pid_tgid);
 }
 
 int orc_vm_register_xdp_load_bytes(struct orc_vm *vm)

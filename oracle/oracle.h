@@ -45,6 +45,11 @@ int orc_vm_register_default_helpers(struct orc_vm *vm);
 /* bpf_xdp_load_bytes (id 189): defined in bpf_helper.cpp:778-788 but not in
  * any default helper group; an embedder registers it explicitly. */
 int orc_vm_register_xdp_load_bytes(struct orc_vm *vm);
+/* helpers 6 (trace_printk, text to a log) and 14 (get_current_pid_tgid) */
+int orc_vm_register_trace_helpers(struct orc_vm *vm);
+size_t orc_trace_log(char *out, size_t cap);  /* bytes logged; copies up to cap */
+void orc_trace_log_reset(void);
+void orc_set_pid_tgid(uint64_t v);
 void orc_vm_set_unwind_index(struct orc_vm *vm, int idx);
 /* ebpf_load: 0 / <0, errbuf receives the message (compat_ubpf.cpp:61-200) */
 int orc_vm_load(struct orc_vm *vm, const void *code, uint32_t code_len, char *errbuf, size_t errlen);

@@ -65,6 +65,10 @@ def lib():
             "orc_hash_bytes": (u64, [vp, u64]),
             "orc_run_xdp": (C.c_int, [vp, vp, u64, u64, vp, u32, vp, vp, vp, u32, u32, u32]),
             "orc_vm_register_xdp_load_bytes": (C.c_int, [vp]),
+            "orc_vm_register_trace_helpers": (C.c_int, [vp]),
+            "orc_trace_log": (C.c_size_t, [vp, C.c_size_t]),
+            "orc_trace_log_reset": (None, []),
+            "orc_set_pid_tgid": (None, [u64]),
             "orc_run_raw": (C.c_int, [vp, vp, u64, u64, u32, vp]),
             "orc_run_syscall": (C.c_int, [vp, vp, u64, vp, vp]),
             "orc_time_xdp": (C.c_double, [vp, vp, u64, u64, u32, vp, C.c_int]),
@@ -110,6 +114,10 @@ class OracleVM:
     def register_xdp_load_bytes(self) -> None:
         """bpf_xdp_load_bytes (id 189), defined but not in a default group."""
         lib().orc_vm_register_xdp_load_bytes(self.h)
+
+    def register_trace_helpers(self) -> None:
+        """bpf_trace_printk (6) and bpf_get_current_pid_tgid (14)."""
+        lib().orc_vm_register_trace_helpers(self.h)
 
     def run_xdp(self, slots: np.ndarray, lens: Optional[np.ndarray] = None, fixed_len: int = 0,
                 want_meta: bool = False, ifindex: int = 0, rxq: int = 0, ncpu: int = 0, head: int = 0):
@@ -244,6 +252,22 @@ def prog_create(fd: int, code: bytes) -> int:
 
 def prog_close(fd: int) -> None:
     lib().orc_prog_close(fd)
+
+
+def trace_log() -> bytes:
+    """What bpf_trace_printk printed since the last trace_log_reset()."""
+    n = lib().orc_trace_log(None, 0)
+    buf = C.create_string_buffer(max(n, 1))
+    lib().orc_trace_log(buf, n)
+    return buf.raw[:n]
+
+
+def trace_log_reset() -> None:
+    lib().orc_trace_log_reset()
+
+
+def set_pid_tgid(v: int) -> None:
+    lib().orc_set_pid_tgid(v)
 
 
 def set_ncpu(n: int) -> None:

@@ -9,6 +9,7 @@
 // maps.cpp's only references outside itself (the perf-event attach path)
 extern "C" int bpftime_amd_syscall_attach(int, int64_t) { return -1; }
 extern "C" int bpftime_amd_syscall_detach(int) { return -1; }
+extern "C" int bpftime_amd_tracepoint_resolve(int32_t, int64_t *, int *) { return -1; }
 
 using bpftime_amd::LpmTrie;
 

@@ -429,3 +429,50 @@ def test_miss_log_parity(fresh_oracle, fresh_runtime, monkeypatch, cap):
     assert vm4.exec_batch(dev.CTX_XDP, d4, n4, 64, lens=dl4, verdicts=dv4) == 0
     np.testing.assert_array_equal(dv4.download(np.uint32), want)
     assert dm4.hash_items() == om4.items()
+
+
+def _ctx_flow_program(flows_fd):
+    """flow_hash with a generic ctx read (ctx->ingress_ifindex: the lanes'
+    48-B ctx must sit in LDS), a 64-B stack and the same hash lookup, whose
+    pkts counter adds the ifindex: a 1024-lane block of it would not fit
+    the CU with a doubled lookup cache."""
+    from bpftime_amd.isa import Asm
+    body = programs.flow_hash(flows_fd)
+    a = Asm()
+    a.ldx(4, 9, 1, 20)                    # r9 = ctx->ingress_ifindex
+    a.stx(8, 10, -64, "r9")               # the stack reaches fp-64
+    pre = a.assemble()
+    insns = [body[i:i + 8] for i in range(0, len(body), 8)]
+    # the body's `pkts += 1` (mov64 r1, 1 before the first atomic add) adds
+    # the ifindex spilled at fp-64 instead
+    out = []
+    for i, ins in enumerate(insns):
+        if ins[0] == 0xb7 and ins[1] & 0xf == 1 and struct.unpack("<i", ins[4:])[0] == 1 and \
+                i + 1 < len(insns) and insns[i + 1][0] == 0xdb:
+            out.append(bytes([0x79, 0x01 | (10 << 4)]) + struct.pack("<hi", -64, 0))  # r1 = *(u64 *)(fp-64)
+        else:
+            out.append(ins)
+    return pre + b"".join(out)
+
+
+@pytest.mark.parametrize("nflows", [300, 4000])
+def test_ctx_stack_lookup_fits_cu(fresh_oracle, fresh_runtime, nflows):
+    po, dev = fresh_oracle, fresh_runtime
+    (om,), (dm,) = _flow_setup(po, dev)
+    code = _ctx_flow_program(dm.fd)
+    n = 1 << 17
+    slots, lens = gen.flow_packets(n, nflows=nflows, stride=2048)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    ov = ovm.run_xdp(slots.copy(), lens=lens, ifindex=7)
+    vm = dev.VM()
+    vm.load(code)
+    d = dev.DeviceBuffer.from_array(slots)
+    dl = dev.DeviceBuffer.from_array(lens)
+    dv = dev.DeviceBuffer(4 * n)
+    assert vm.exec_batch(dev.CTX_XDP, d, n, 2048, lens=dl, verdicts=dv, ifindex=7) == 0
+    np.testing.assert_array_equal(dv.download(np.uint32), ov)
+    assert dm.hash_items() == om.items()
+    tot = sum(struct.unpack("<QQ", v)[0] for v in om.items().values())
+    ip = (slots[:, 12] == 0x08) & (slots[:, 13] == 0)
+    assert tot == 7 * int(ip.sum())
