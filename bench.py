@@ -54,13 +54,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
+    rz = None
     if world > 1:
-        # control plane only (barrier, timing max, map-shard gather) over gloo;
-        # the data path has no collective.  torch is imported
-        # before libbpftime_amd so one HIP runtime is loaded.
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
+        # control plane only (barrier, timing max, map-shard gather) through
+        # files, with no torch import: torch would load its own HIP runtime,
+        # and every rank count must run the kernel on the library's
+        # (bpftime_amd/rendezvous.py); the data path has no collective
+        # 
+        from bpftime_amd.rendezvous import Rendezvous
+        rz = Rendezvous(rank, world)
 
     import numpy as np
 
@@ -96,8 +98,8 @@ def main():
     for _ in range(args.warmup):
         step()
     dev.lib().bpftime_amd_sync()
-    if dist:
-        dist.barrier()
+    if rz:
+        rz.barrier()
     dev.lib().bpftime_amd_sync()
     # two events on the launch stream bracket the K back-to-back launches (an
     # event between launches would add its own end-of-kernel cache
@@ -110,8 +112,8 @@ def main():
     ev1.record()
     dev.lib().bpftime_amd_sync()
     t1 = time.perf_counter()
-    if dist:
-        dist.barrier()
+    if rz:
+        rz.barrier()
     wall = t1 - t0
     kern_avg_s = ev0.elapsed_ms(ev1) / args.steps / 1e3
 
@@ -132,16 +134,17 @@ def main():
     shard = bss.snapshot()
     e2e = None
     if not args.no_e2e:
-        e2e = e2e_leg(dev, vm, bss, n, first, args.e2e_chunk_log2, dist, nstreams=args.e2e_streams)
-    gathered = gather_ranks(dist, world, (wall, shard.tobytes(), ok_verdicts and ok_counter and ok_bytes, e2e))
+        e2e = e2e_leg(dev, vm, bss, n, first, args.e2e_chunk_log2, rz, nstreams=args.e2e_streams)
+    hip = dev.hip_runtime()
+    gathered = gather_ranks(rz, world, (wall, shard.tobytes(), ok_verdicts and ok_counter and ok_bytes, e2e,
+                                        hip["version"]))
     times = [g[0] for g in gathered]
     shards = [np.frombuffer(g[1], dtype=np.uint8) for g in gathered]
     oks = [g[2] for g in gathered]
     e2es = [g[3] for g in gathered]
+    hip_versions = sorted({g[4] for g in gathered})
     if rank != 0:
-        if dist:
-            dist.barrier()
-            dist.destroy_process_group()
+        rz.close()
         return
 
     merged = merge_counter_shards(init_bss, shards)
@@ -204,21 +207,21 @@ def main():
         },
         "cpu_baseline": cpu,
         "e2e": merge_e2e(e2es, world, n),
+        "hip_runtime": {"version": hip_versions[0] if len(hip_versions) == 1 else hip_versions, "lib": hip["lib"],
+                        "control_plane": "files (bpftime_amd/rendezvous.py)" if rz else None},
     }
     print(json.dumps(out))
-    if dist:
-        dist.barrier()
-        dist.destroy_process_group()
+    if rz:
+        rz.close()
 
 
-def gather_ranks(dist, world, payload):
-    """Every rank's (wall seconds, map shard bytes, parity, e2e) on every
-    rank: the control plane over gloo, no data-path collective."""
-    if not dist or world == 1:
+def gather_ranks(rz, world, payload):
+    """Every rank's (wall seconds, map shard bytes, parity, e2e, HIP runtime
+    version) on every rank: the control plane of bpftime_amd/rendezvous.py,
+    no data-path collective."""
+    if not rz or world == 1:
         return [payload]
-    gathered = [None] * world
-    dist.all_gather_object(gathered, payload)
-    return gathered
+    return rz.all_gather(payload)
 
 
 def merge_counter_shards(init, shards, width=8):
@@ -228,7 +231,7 @@ def merge_counter_shards(init, shards, width=8):
     return sh.merge_array_delta(init, shards, width)
 
 
-def e2e_leg(dev, vm, bss, n, first, chunk_log2, dist, passes=3, nstreams=2):
+def e2e_leg(dev, vm, bss, n, first, chunk_log2, rz, passes=3, nstreams=2):
     """Path that starts and ends in host memory: pinned host frames -> chunked
     hipMemcpyAsync H2D -> interpreter -> verdicts (and, in the second mode,
     the rewritten frames) D2H, double-buffered on two streams.  Reported
@@ -285,8 +288,8 @@ def e2e_leg(dev, vm, bss, n, first, chunk_log2, dist, passes=3, nstreams=2):
                  ("zero_copy", True, True))
         for mode, back, zc in modes:
             one_pass(back, zc)  # warm-up
-            if dist:
-                dist.barrier()
+            if rz:
+                rz.barrier()
             t0 = time.perf_counter()
             for _ in range(passes):
                 one_pass(back, zc)

@@ -1055,6 +1055,10 @@ int bpftime_amd_device_count(void) {
   return n;
 }
 int bpftime_amd_set_device(int dev) { return hipSetDevice(dev) == hipSuccess ? 0 : -1; }
+int bpftime_amd_hip_runtime_version(void) {
+  int v = 0;
+  return hipRuntimeGetVersion(&v) == hipSuccess ? v : -1;
+}
 void *bpftime_amd_dev_alloc(uint64_t bytes) {
   void *p = nullptr;
   if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;

@@ -327,6 +327,23 @@ def xdp_links() -> list:
     return [(lf[i], pf[i], ifx[i]) for i in range(n)]
 
 
+def hip_runtime() -> dict:
+    """The HIP runtime this process's library runs on: hipRuntimeGetVersion
+    and the libamdhip64 file mapped into the process (torch bundles its own
+    with the same SONAME)."""
+    ver = lib().bpftime_amd_hip_runtime_version()
+    libs = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1]
+                if "libamdhip64" in p:
+                    libs.add(p)
+    except OSError:
+        pass
+    return {"version": ver, "lib": sorted(libs)}
+
+
 def prog_instantiate(prog_fd: int) -> VM:
     err = C.c_void_p()
     h = lib().bpftime_amd_prog_instantiate(prog_fd, C.byref(err))

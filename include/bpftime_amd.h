@@ -302,6 +302,7 @@ int bpftime_amd_merge_delta(void *acc, const void *init, const void *shard, uint
 
 /* ---- device utilities (HIP runtime plumbing for callers without one) ---- */
 int bpftime_amd_device_count(void);
+int bpftime_amd_hip_runtime_version(void);  /* hipRuntimeGetVersion of the runtime this library runs on, -1 on error */
 int bpftime_amd_set_device(int dev);
 void *bpftime_amd_dev_alloc(uint64_t bytes);
 void bpftime_amd_dev_free(void *p);

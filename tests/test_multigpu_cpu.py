@@ -101,44 +101,90 @@ def test_shard_range_covers_exactly():
                 assert f0 + c0 == f1
 
 
-def _bench_worker(rank, world, port, q):
-    """bench.py's own N>1 control plane: gather_ranks over gloo, then the
-    rank-0 merge (merge_counter_shards) of per-rank .bss shards."""
+def _bench_worker(rank, world, path, q):
+    """bench.py's own N>1 control plane: gather_ranks over the file
+    rendezvous (no torch: bpftime_amd/rendezvous.py), then the rank-0 merge
+    (merge_counter_shards) of per-rank .bss shards."""
     sys.path.insert(0, ROOT)
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    import torch.distributed as dist
-
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world))
     import bench
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        init = np.zeros(4096, np.uint8)
-        init.view(np.uint64)[:3] = (7, 1 << 40, 5)
-        shard = init.copy()
-        shard.view(np.uint64)[0] += 1000 * (rank + 1)      # this rank's packets
-        shard.view(np.uint64)[1] += rank                    # a second counter
-        got = bench.gather_ranks(dist, world, (0.5 + rank, shard.tobytes(), True, None))
-        if rank == 0:
-            merged = bench.merge_counter_shards(init, [np.frombuffer(g[1], np.uint8) for g in got])
-            q.put((merged.view(np.uint64)[:3].tolist(), [g[0] for g in got]))
-        dist.barrier()
-    finally:
-        dist.destroy_process_group()
+    from bpftime_amd.rendezvous import Rendezvous
+    rz = Rendezvous(rank, world, path=path, timeout=120)
+    init = np.zeros(4096, np.uint8)
+    init.view(np.uint64)[:3] = (7, 1 << 40, 5)
+    shard = init.copy()
+    shard.view(np.uint64)[0] += 1000 * (rank + 1)      # this rank's packets
+    shard.view(np.uint64)[1] += rank                    # a second counter
+    rz.barrier()
+    got = bench.gather_ranks(rz, world, (0.5 + rank, shard.tobytes(), True, None, 70200000 + rank % 1))
+    if rank == 0:
+        merged = bench.merge_counter_shards(init, [np.frombuffer(g[1], np.uint8) for g in got])
+        q.put((merged.view(np.uint64)[:3].tolist(), [g[0] for g in got], sorted({g[4] for g in got}),
+               "torch" in sys.modules))
+    rz.close()
 
 
-def test_bench_control_plane_two_ranks():
+def test_bench_control_plane_two_ranks(tmp_path):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, q)) for r in range(2)]
+    path = str(tmp_path / "rdzv")
+    procs = [ctx.Process(target=_bench_worker, args=(r, 2, path, q)) for r in range(2)]
     for p in procs:
         p.start()
-    counters, times = q.get(timeout=180)
+    counters, times, versions, torch_loaded = q.get(timeout=180)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert counters == [7 + 1000 + 2000, (1 << 40) + 1, 5]
     assert times == [0.5, 1.5]   # bench.py reports world * n * steps / max(times)
+    assert versions == [70200000]
+    assert not torch_loaded      # the control plane never imports torch
+    assert not os.path.exists(path)  # rank 0 removed the rendezvous directory
+
+
+def _rdzv_worker(rank, world, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_PORT="29533")
+    import time
+    from bpftime_amd.rendezvous import Rendezvous, launch_dir
+    rz = Rendezvous(rank, world, timeout=120)
+    order = []
+    rz.barrier()                        # (processes start with a skew of their own)
+    for step in range(5):
+        if rank == step % world:
+            time.sleep(0.05)            # a late rank: nobody may pass the barrier before it arrives
+        t = time.monotonic()
+        rz.barrier()
+        order.append(time.monotonic() - t)
+    got = rz.all_gather({"rank": rank, "blob": bytes([rank]) * (rank + 1), "t": (rank, [1, 2])})
+    q.put((rank, launch_dir(), order, got))
+    rz.close()
+
+
+def test_rendezvous_barrier_and_gather():
+    """Four ranks started by one parent (as torchrun's agent starts a
+    launch's workers) meet in the same directory; each barrier holds every
+    rank until the late one arrives; the gather returns every rank's
+    payload (bytes included) in rank order on every rank."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world = 4
+    procs = [ctx.Process(target=_rdzv_worker, args=(r, world, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    dirs = {r[1] for r in res}
+    assert len(dirs) == 1 and f"_{os.getpid()}_" in dirs.pop()
+    for rank, _, waits, got in res:
+        for step, w in enumerate(waits):
+            if rank != step % world:
+                assert w >= 0.03, (rank, step, w)
+        assert got == [{"rank": r, "blob": bytes([r]) * (r + 1), "t": [r, [1, 2]]} for r in range(world)]
 
 
 def test_merge_at_counter_width():
