@@ -2044,17 +2044,55 @@ def relocate(line):
     return re.sub(r"\bv(\d+)\b", lambda m: f"v{vmap(int(m.group(1)))}", line)
 
 
+def inc_blocks(path):
+    """The asm lines of each BPFTIME_AMD_FAST_ASM* macro of a written
+    fast_asm.inc (what the kernel compiles)."""
+    blocks, cur = {}, None
+    for line in open(path):
+        m = re.match(r"#define (BPFTIME_AMD_FAST_ASM\w*) \\$", line)
+        if m:
+            cur = blocks.setdefault(m.group(1), [])
+            continue
+        m = re.match(r'\s*"(.*)\\n" \\$', line)
+        if m and cur is not None:
+            cur.append(m.group(1))
+        elif not line.startswith("  "):
+            cur = None
+    return blocks
+
+
+def check_hazards(blocks):
+    """hazards.py over each block; exits non-zero on a violation."""
+    import hazards
+    bad = []
+    for name, lines in blocks.items():
+        bad += [f"{name}: {v}" for v in hazards.check(lines)]
+    if bad:
+        raise SystemExit("wait-state hazards in the fast path:\n  " + "\n  ".join(bad))
+
+
 def main():
+    import sys
+    if "--check" in sys.argv:  # (make: the committed fast_asm.inc, every build)
+        blocks = inc_blocks(os.path.join(HERE, "fast_asm.inc"))
+        assert len(blocks) == 2, sorted(blocks)
+        check_hazards(blocks)
+        print("fast_asm.inc: no wait-state hazards (%d lines)" % sum(len(b) for b in blocks.values()))
+        return
     # v126/v127 (v100/v101 before relocation) are read, never written, by
     # staged loads near the window end
     clob = [f"s{i}" for i in range(40, 96)] + [f"v{vmap(i)}" for i in range(40, 102)]
+    gens = {}
+    for suffix, greg in (("", False), ("_G", True)):
+        g = Gen(greg)
+        ids = g.build()
+        g.out = [relocate(x) for x in g.out]
+        gens[suffix] = g
+    check_hazards({"BPFTIME_AMD_FAST_ASM" + k: g.out for k, g in gens.items()})
     with open(os.path.join(HERE, "fast_asm.inc"), "w") as f:
         f.write("// Generated by gen_fast.py; do not edit.\n")
         # register spill copy in LDS, and (_G) in global memory
-        for suffix, greg in (("", False), ("_G", True)):
-            g = Gen(greg)
-            ids = g.build()
-            g.out = [relocate(x) for x in g.out]
+        for suffix, g in gens.items():
             f.write("#define BPFTIME_AMD_FAST_ASM%s \\\n" % suffix)
             for line in g.out:
                 f.write('  "%s\\n" \\\n' % line)
