@@ -644,12 +644,17 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     int occ = bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn, greg, block);
     if (occ < 1) occ = 1;
     uint64_t want = (b->count + block - 1) / block;
-    // resident blocks x 4 when the program has no combining table: more,
-    // shorter-lived blocks keep more packet loads in flight at the kernel's
-    // tail (xdp-counter 0.453 -> 0.423 ms per 2^24 packets, r01d sweep);
-    // x 1 with one, since every block flushes its table when it ends
-    // (flow-hash 0.60 -> 1.09 ms at x 4).  BPFTIME_AMD_GRID_MULT overrides.
-    uint32_t mult = p.comb_entries ? 1 : 4;
+    // one wave per resident wave slot (x 1): every wave launch writes the
+    // kernel's register spills (ScratchSize ~200 B / lane) once, and at x 4
+    // those writes were 12 B of memory-side traffic per packet
+    // (tools/grid_write_probe.sh, xdp-counter WRITE_SIZE 39.1 / 42.3 / 48.5 /
+    // 61.0 B per packet at x 1 / 2 / 4 / 8; 0.467 / 0.479 / 0.496 / 0.484 ms;
+    // lpm-route 0.467 / 0.479 / 0.506 ms at x 1 / 2 / 4); a combining table
+    // is flushed once per block (flow-hash 0.60 -> 1.09 ms at x 4).  Ring
+    // staging keeps x 4: a block's 2-KiB ring chunk must hold the records of
+    // its units (ringbuf-sample 7.46 / 4.03 / 1.43 ms at x 1 / 2 / 4).
+    // BPFTIME_AMD_GRID_MULT overrides.
+    uint32_t mult = stage && !p.comb_entries ? 4 : 1;
     if (const char *g = getenv("BPFTIME_AMD_GRID_MULT"))
       if (atoi(g) > 0) mult = (uint32_t)atoi(g);
     uint64_t cap = (uint64_t)cus * (uint64_t)occ * mult;
