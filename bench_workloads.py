@@ -33,6 +33,19 @@ def pmc_traffic(workload, units):
         return None
 
 
+def _dbg_lcache(dev):
+    """BPFTIME_AMD_DBG=512: the hash lookup cache's hit / miss lanes over
+    the whole run (timing-perturbing counters, never a bench number)."""
+    if not int(os.environ.get("BPFTIME_AMD_DBG", "0"), 0) & 512:
+        return {}
+    import ctypes as C
+    out = (C.c_uint64 * 4)()
+    if dev.lib().bpftime_amd_dbg_counters(out, 4, 1) < 2:
+        return {"dbg_lcache": None}
+    return {"dbg_lcache": {"hit_lanes": out[0], "miss_lanes": out[1],
+                           "hit_rate": round(out[0] / max(1, out[0] + out[1]), 4)}}
+
+
 def _timed(dev, step, steps, warmup):
     """(wall seconds, average kernel seconds) over `steps` back-to-back
     launches bracketed by two events on the launch stream."""
@@ -70,8 +83,19 @@ def flow_hash(args, dev, gen, isa, programs):
     def step():
         vm.exec_batch(dev.CTX_XDP, pk, n, stride, lens=dl, verdicts=dv, flags=0)
 
+    # the cold launch: the first batch over the empty map inserts every flow
+    # it meets (BASELINE configs[2] traffic keeps adding flows; the timed
+    # steps after it are the steady state with the table full)
+    dev.lib().bpftime_amd_sync()
+    c0, c1 = dev.Event(), dev.Event()
+    c0.record()
+    step()
+    c1.record()
+    dev.lib().bpftime_amd_sync()
+    cold_s = c0.elapsed_ms(c1) / 1e3
+    cold_flows = flows.count()
     wall, kern_s = _timed(dev, step, args.steps, args.warmup)
-    runs = args.steps + args.warmup
+    runs = args.steps + args.warmup + 1
     # ---- expected totals from the generator's streams ----
     idx = np.arange(n, dtype=np.uint64)
     r = gen.sm64(gen.SEED_CFG3 ^ 0x1111, idx)
@@ -120,6 +144,9 @@ def flow_hash(args, dev, gen, isa, programs):
                    "packets": n, "interp": {"fast_specialized": vm.fast_specialized(dev.CTX_XDP)}},
         "parity": {"per_flow_totals_exact": ok_map, "verdict_classes": ok_verd, "flows": len(got),
                    "ok": ok_map and ok_verd},
+        "cold": {"note": "the first launch, over the empty map: every flow it meets is inserted",
+                 "ms": round(cold_s * 1e3, 4), "Mpps": round(n / cold_s / 1e6, 3), "flows_inserted": cold_flows},
+        **_dbg_lcache(dev),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic("flow-hash", n),
                      "kernel_avg_ms": round(kern_s * 1e3, 4), "algo_bytes_per_pkt": round(algo, 2)},
@@ -190,6 +217,7 @@ def syscall_agg(args, dev, gen, isa, programs):
                                             "fast_specialized": vm.fast_specialized(dev.CTX_SYSCALL)}},
         "parity": {"per_id_totals_exact": ok_map, "r0_all_zero": ok_ret, "keys": len(got),
                    "ok": ok_map and ok_ret},
+        **_dbg_lcache(dev),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic("syscall-agg", n),
                      "kernel_avg_ms": round(kern_s * 1e3, 4), "algo_bytes_per_rec": round(algo, 2)},

@@ -154,6 +154,7 @@ SIGNATURES = [
     ("bpftime_amd_merge_delta", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32]),
     ("bpftime_amd_device_count", C.c_int, []),
     ("bpftime_amd_hip_runtime_version", C.c_int, []),
+    ("bpftime_amd_dbg_counters", C.c_int, [C.POINTER(C.c_uint64), C.c_int, C.c_int]),
     ("bpftime_amd_set_device", C.c_int, [C.c_int]),
     ("bpftime_amd_dev_alloc", C.c_void_p, [C.c_uint64]),
     ("bpftime_amd_dev_free", None, [C.c_void_p]),

@@ -139,7 +139,14 @@ inline BA_HD uint32_t ix_pos(uint64_t h, uint32_t mask) {
   uint32_t g = ((uint32_t)h ^ ((uint32_t)(h >> 32) * 0x85EBCA6Bu)) * 0x9E3779B1u;
   return (g ^ (g >> 16)) & mask;
 }
-constexpr uint32_t kIxProbes = 8;  // index probes before the reference probe
+constexpr uint32_t kIxProbes = 8;  // asm tier: index probes before the C++ tier's lookup
+// An index entry an insert holds while it claims a bucket for its key
+// (dev_helpers.hpp hash_find_ix), and the table's bucket bitmap after the
+// index: bit b = bucket b is not EMPTY (bits past nbuckets set), kept by
+// device inserts while the index is valid and rebuilt with it (maps.cpp)
+constexpr uint32_t kIxRes = 0xffffffffu;
+inline BA_HD uint64_t ix_bitmap(uint64_t ix, uint32_t mask) { return ix + 4ull * ((uint64_t)mask + 1); }
+inline BA_HD uint64_t ix_bitmap_words(uint64_t nbuckets) { return (nbuckets + 63) / 64; }
 
 // LRU_HASH recency (lru_var_hash_map.cpp keeps a doubly linked list, head =
 // most recently used).  Here every element carries the stamp of its last
@@ -236,6 +243,7 @@ struct KParams {
   uint32_t log_words;     // u64 words per block: count, then {tag, delta} pairs
   uint64_t *lane_scratch; // a u64 per lane of the grid (PROG_ARRAY lookups hand out a copy there), or nullptr
   uint32_t dbg;           // BPFTIME_AMD_DBG experiment bits (0 in production)
+  uint64_t *dbg_counts;   // dbg 512: lookup-cache hits, misses (u64 each), or nullptr
   int32_t unwind_idx;     // ebpf_set_unwind_function_index: helper whose 0 return ends the unit (-1 none)
   uint64_t lru_seq;       // this launch's LRU stamp sequence (common.hpp kLruSeqShift)
   uint32_t tail_ctx_mask;    // XDP images: ctx words / stack words a frame keeps (loader.cpp tail_save_masks)
@@ -270,6 +278,13 @@ struct KParams {
 // are hot in every block, and same-address device atomics serialize at the
 // memory side (a map of a few hundred values sits in a handful of channels).
 BA_HD constexpr uint32_t wave_cache_entries(uint32_t block) { return (block / 64) * 2; }
+// A combining-table entry e = set * 8 + way: its u32 tag sits in the tags of
+// ways 0-3 of every set ([set][4]) or, for ways 4-7, in the same array after
+// them (gen_fast.py comb_add: a set's first four tags are one 16-byte LDS
+// slot, and consecutive sets take consecutive slots of a bank row)
+BA_HD constexpr uint32_t comb_tag_pos(uint32_t e, uint32_t entries) {
+  return (e & 7) < 4 ? (e >> 3) * 4 + (e & 3) : entries / 2 + (e >> 3) * 4 + (e & 3);
+}
 constexpr uint32_t kMergeGroup = 16;
 constexpr uint32_t kMergeEntries = 4096;  // merge table entries (64 KiB of LDS)
 // (a combining-table entry flushes up to four counters: gen_fast.py comb_add)

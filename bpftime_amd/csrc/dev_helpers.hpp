@@ -133,8 +133,133 @@ __device__ __forceinline__ void copy_bytes(uint64_t dst, uint64_t src, uint32_t 
 
 constexpr uint32_t ST_EMPTY = 0, ST_FILLED = 1, ST_BUSY = 2;
 
+__device__ __forceinline__ uint64_t ald64(uint64_t a) {
+  return __hip_atomic_load(G64(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// An insert into a table whose lookup index is valid (common.hpp kIxRes),
+// holding the index entry `ea` reserved for its key, which is absent: claim
+// the first EMPTY bucket of the reference probe from h % nb
+// (bpftime_hash_map.hpp:127-180) -- found through the table's bucket bitmap
+// (64 buckets per word, a stale bit is only a failed claim), claimed by
+// compare-and-swap on its state -- publish key and value, then the index
+// entry.  Never waits on another lane: a lane of the same wave that waits on
+// the reservation re-reads it on its next loop trip (hash_find_ix).
+__device__ uint64_t ix_insert(const DMap &m, uint64_t key, uint64_t h, uint64_t ea, uint64_t init,
+                              uint32_t init_bytes, bool *inserted, uint64_t part, uint32_t part_off,
+                              uint32_t part_bytes) {
+  const uint64_t nb = m.nbuckets, bm = ix_bitmap(m.ix, m.ix_mask);
+  uint64_t b = h % nb, left = nb;
+  while (left) {
+    const uint64_t w = b >> 6, o = b & 63;
+    uint64_t span = 64 - o;
+    if (span > left) span = left;
+    if (span > nb - b) span = nb - b;
+    uint64_t freeb = ~ald64(bm + 8 * w) >> o;
+    if (span < 64) freeb &= (1ull << span) - 1;
+    if (!freeb) {
+      b += span;
+      left -= span;
+      if (b == nb) b = 0;
+      continue;
+    }
+    const uint64_t i = (uint64_t)__builtin_ctzll(freeb);
+    b += i;
+    left -= i;
+    const uint64_t s = m.data + b * (uint64_t)m.slot_size;
+    const uint64_t bit = 1ull << (b & 63);
+    uint32_t prev = ST_EMPTY;
+    __hip_atomic_compare_exchange_strong(G32(s), &prev, ST_BUSY, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_or(G64(bm + 8 * (b >> 6)), bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == ST_EMPTY) {
+      // the element count check (bpftime_hash_map.hpp:153-156) by the lane
+      // that owns the bucket, as in hash_find
+      unsigned long long c = __hip_atomic_fetch_add(G64(m.count_addr), 1ull, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+      if (c >= m.max_entries) {
+        __hip_atomic_fetch_add(G64(m.count_addr), ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(G32(s), ST_EMPTY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_and(G64(bm + 8 * (b >> 6)), ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      copy_bytes_publish(s + m.key_off, key, m.key_size);
+      if (init)
+        copy_bytes_publish(s + m.val_off, init, init_bytes);
+      else
+        for (uint32_t k = 0; k < init_bytes; k += 4)
+          __hip_atomic_store(G32(s + m.val_off + k), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (part) copy_bytes_publish(s + m.val_off + part_off, part, part_bytes);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // key/value stores drained first
+      __hip_atomic_store(G32(s), ST_FILLED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(G32(ea), (uint32_t)b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      *inserted = true;
+      return s;
+    }
+    // claimed by another insert: go on after it
+    b = b + 1 == nb ? 0 : b + 1;
+    left--;
+  }
+  // full: the reservation goes back (a lane waiting on it tries its own)
+  __hip_atomic_store(G32(ea), 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  return 0;
+}
+
+// hash_find over a valid lookup index: the index holds exactly the keys the
+// reference probe reaches (maps.cpp ix_rebuild; device inserts index what
+// they publish), so walking it from ix_pos(h) to an empty entry decides
+// presence without the reference probe's walk of a nearly full table (config
+// 3: 65,536 flows in 65,537 buckets).  An empty entry is confirmed at the
+// coherence point (a line of this XCD's L2 may predate another XCD's
+// insert).  An insert reserves the empty entry that proved its key absent
+// (0 -> kIxRes): any other insert of the same key walks the same entries and
+// waits at the reservation until it holds the new bucket, so two inserts of
+// one key meet in one element; lookups pass reserved entries (an insert in
+// flight).  Waiting is re-reading on the next loop trip, never a spin inside
+// a trip, so a lane never waits on a lane of its own wave.
+__device__ uint64_t hash_find_ix(const DMap &m, uint64_t key, uint64_t h, bool insert, uint64_t init,
+                                 uint32_t init_bytes, bool *inserted, uint64_t part, uint32_t part_off,
+                                 uint32_t part_bytes) {
+  uint32_t p = ix_pos(h, m.ix_mask), spins = 0;
+  for (uint32_t t = 0; t <= m.ix_mask;) {
+    const uint64_t ea = m.ix + 4ull * p;
+    uint32_t e = ald32(ea);
+    if (e == 0 || e == kIxRes) e = acoh32(ea);
+    if (e == 0) {
+      if (!insert) return 0;
+      uint32_t z = 0;
+      if (__hip_atomic_compare_exchange_strong(G32(ea), &z, kIxRes, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT))
+        return ix_insert(m, key, h, ea, init, init_bytes, inserted, part, part_off, part_bytes);
+      e = z;
+    }
+    if (e == kIxRes) {
+      if (insert) {  // maybe this key's: read the entry again on the next trip
+        if (++spins > (1u << 22)) return 0;  // bounded: never hang the GPU
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+    } else {
+      const uint64_t s = m.data + (uint64_t)(e - 1) * m.slot_size;
+      uint32_t st = ald32(s);
+      bool coh = false;
+      if (st != ST_FILLED) {
+        st = acoh32(s);
+        coh = true;
+      }
+      if (st == ST_FILLED && key_eq(s + m.key_off, key, m.key_size, coh)) return s;
+    }
+    p = (p + 1) & m.ix_mask;
+    t++;
+  }
+  return 0;
+}
+
 // Find `key`; if absent and `insert`, claim a slot and publish key + init
-// value (init == 0 -> zero).  Returns slot address or 0.  *inserted tells
+// value (init == 0 -> zero).  Returns slot address or 0.  A table with a
+// valid lookup index goes through it (hash_find_ix); the rest of this
+// function is the reference probe, for tables without one.  *inserted tells
 // whether this lane created the element.  The probe order is the
 // reference's: start at hash % nbuckets, linear, wrap once
 // (bpftime_hash_map.hpp:127-180).  Lanes never wait on a lane of their own
@@ -150,20 +275,7 @@ __device__ uint64_t hash_find(const DMap &m, uint64_t key, bool insert, uint64_t
   *inserted = false;
   const uint64_t nb = m.nbuckets;
   const uint64_t h = key_hash(key, m.key_size);
-  if (m.ix) {
-    // lookup index (common.hpp ix_pos): a hit is the slot the reference
-    // probe below would reach; an empty entry or too many probes fall
-    // through to that probe (an insert in flight is only indexed after it
-    // is published)
-    uint32_t p = ix_pos(h, m.ix_mask);
-    for (uint32_t t = 0; t < kIxProbes; t++) {
-      const uint32_t e = ald32(m.ix + 4ull * p);
-      if (!e) break;
-      const uint64_t s = m.data + (uint64_t)(e - 1) * m.slot_size;
-      if (ald32(s) == ST_FILLED && key_eq(s + m.key_off, key, m.key_size, false)) return s;
-      p = (p + 1) & m.ix_mask;
-    }
-  }
+  if (m.ix) return hash_find_ix(m, key, h, insert, init, init_bytes, inserted, part, part_off, part_bytes);
   uint64_t idx = h % nb;
   uint64_t start = idx;
   uint32_t spins = 0;
@@ -206,16 +318,6 @@ __device__ uint64_t hash_find(const DMap &m, uint64_t key, bool insert, uint64_t
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // key/value stores drained first
         __hip_atomic_store(G32(s), ST_FILLED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        if (m.ix) {  // index the new element (at most nbuckets entries: never full)
-          uint32_t p = ix_pos(h, m.ix_mask);
-          for (uint32_t t = 0; t <= m.ix_mask; t++) {
-            uint32_t z = 0;
-            if (__hip_atomic_compare_exchange_strong(G32(m.ix + 4ull * p), &z, (uint32_t)idx + 1, __ATOMIC_RELAXED,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-              break;
-            p = (p + 1) & m.ix_mask;
-          }
-        }
         *inserted = true;
         return s;
       }

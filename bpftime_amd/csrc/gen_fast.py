@@ -284,7 +284,9 @@ class Gen:
         """Per-lane add of Y (v46, v[46:47] for 8 B) at the global address Z
         through the workgroup's LDS combining table (interp.hip: %[combn] u32
         tags, then %[combn] 16-byte delta granules, flushed when the block
-        ends): Zipf-hot counters cost an LDS add instead of a same-address
+        ends; the tags of ways 0-3 of every set, [set][4], then those of ways
+        4-7, so a set's first four tags are one 16-byte slot and sets spread
+        over all sixteen slots of a bank row, common.hpp comb_tag_pos): Zipf-hot counters cost an LDS add instead of a same-address
         device atomic per lane (those serialize at the memory side, ~12 ns
         each).  An entry stands for the 16-byte granule of the map arena
         holding the counter (for fused pairs: the 16 bytes at the pair's
@@ -336,17 +338,20 @@ class Gen:
                "v_lshrrev_b32 v41, 4, v54", "s_mov_b32 s69, 0x9e3779b1", "v_mul_lo_u32 v41, v41, s69",
                f"s_lshr_b32 s69, %[combn], {WAYS.bit_length() - 1}",             # sets (any count)
                "v_mul_hi_u32 v41, v41, s69",                                     # the set: multiply-shift
-               f"v_lshlrev_b32 v41, {WAYS.bit_length() - 1}, v41",               # its first way
-               "v_lshlrev_b32 v55, 4, v41", "v_lshlrev_b32 v41, 2, v41",
-               "v_add_u32 v41, %[comb], v41",                                   # the set's tags
+               f"v_lshlrev_b32 v55, {WAYS.bit_length() - 1 + 4}, v41",           # its first way's delta
+               "v_lshlrev_b32 v41, 4, v41",
+               "v_add_u32 v41, %[comb], v41",                                   # ways 0-3's tags
                "s_lshl_b32 s70, %[combn], 2", "s_add_u32 s70, s70, %[comb]",
                "v_add3_u32 v55, s70, v55, v43",                                 # way 0's delta + byte
+               "s_lshl_b32 s71, %[combn], 1",                                   # ways 4-7's tags: + sets * 16
+               "s_sub_u32 s69, s71, 16",
                "s_mov_b32 s85, 0",
                f"{retry}:",
                "s_mov_b64 s[62:63], exec",                                       # lanes of this pass
+               "v_add_u32 v42, s71, v41",
                "ds_read_b128 v[56:59], v41",
-               "ds_read_b64 v[82:83], v41 offset:16",
-               "ds_read_b64 v[50:51], v41 offset:24",
+               "ds_read_b64 v[82:83], v42",
+               "ds_read_b64 v[50:51], v42 offset:8",
                "s_waitcnt lgkmcnt(0)",
                "v_mov_b32 v42, -1")
         tags = ["v56", "v57", "v58", "v59", "v82", "v83", "v50", "v51"]
@@ -364,7 +369,9 @@ class Gen:
             self.e(f"v_cmp_eq_u32 vcc, 0, {tags[k]}", f"v_cndmask_b32_e64 v42, v42, {k}, vcc")
         self.e("v_cmp_ne_u32 s[56:57], -1, v42", "s_and_b64 exec, exec, s[56:57]",
                f"s_cbranch_execz {noclaim}",                                    # a full set: direct
-               "v_lshl_add_u32 v43, v42, 2, v41",
+               "v_lshl_add_u32 v43, v42, 2, v41",                                # way k's tag: k < 4
+               "v_cmp_le_u32 vcc, 4, v42", "v_mov_b32 v50, s69",
+               "v_cndmask_b32 v50, 0, v50, vcc", "v_add_u32 v43, v43, v50",     # ... else + sets * 16 - 16
                "v_mov_b32 v50, 0",
                "ds_cmpst_rtn_b32 v51, v43, v50, v54",
                "s_waitcnt lgkmcnt(0)",
@@ -1054,9 +1061,10 @@ class Gen:
 
     # ---- the block's hash-lookup cache (common.hpp kLcacheSets) ----
     # w4 (s44) two-way sets right below the launch constants (%[comb] - TENV -
-    # 40 * sets): the ways' keys (16 B each, [set][way], the key's first kd
-    # words), then the ways' entries {u32 (slot + 1) | fd << 22} ([set][way],
-    # at + 32 * sets).  The set is a mix of the key words and the fd, so a hit
+    # 40 * sets): the ways' keys (16 B each, [way][set], the key's first kd
+    # words: a way's keys of consecutive sets are consecutive 16-byte slots
+    # of a bank row), then the ways' entries {u32 (slot + 1) | fd << 22}
+    # ([set][way], at + 32 * sets).  The set is a mix of the key words and the fd, so a hit
     # needs neither the h*31 hash nor a memory access: the whole key is
     # compared in LDS.  Entries are written once: a lane that found its key
     # claims an empty way (0 -> -1 by compare-and-swap), writes the key, then
@@ -1087,13 +1095,15 @@ class Gen:
                "v_mul_hi_u32 v41, v41, s44",                                       # the set (w4 sets)
                "s_mul_i32 s69, s44, 40", "s_add_u32 s69, s69, " + str(TENV),
                "s_sub_u32 s69, %[comb], s69",                                     # the cache
-               "v_lshl_add_u32 v82, v41, 5, s69",                                 # its keys
+               "v_lshl_add_u32 v82, v41, 4, s69",                                 # its way-0 key
+               "s_lshl_b32 s85, s44, 4",                                          # way 1: + sets * 16
                # (s64..s71 hold the map's words here: val_off in s70)
                "v_mul_u32_u24_e64 v83, s44, 32", "v_add_u32 v83, s69, v83",
                "v_lshl_add_u32 v83, v41, 3, v83",                                 # its entries
                "ds_read_b64 v[54:55], v83",                                       # entries first
+               "v_add_u32 v41, s85, v82",
                "ds_read_b128 v[56:59], v82",
-               "ds_read_b128 v[48:51], v82 offset:16",
+               "ds_read_b128 v[48:51], v41",
                "s_waitcnt lgkmcnt(0)",
                "s_lshl_b32 s69, s49, 22")
         for way, (ent, k0, m) in enumerate(((54, 56, "s[56:57]"), (55, 48, "s[54:55]"))):
@@ -1104,15 +1114,16 @@ class Gen:
                 self.e(f"v_cmp_eq_u32 vcc, v{k0 + j}, v{44 + j}", f"s_and_b64 {m}, {m}, vcc")
         # the fill's way: the first empty one (v83 = -1: both taken)
         self.e("v_cmp_eq_u32 vcc, 0, v54",
-               "v_add_u32 v42, 4, v83", "v_add_u32 v41, 16, v82",
+               "v_add_u32 v42, 4, v83", "v_add_u32 v41, s85, v82",
                "v_cmp_eq_u32 s[52:53], 0, v55",
                "v_cndmask_b32 v42, -1, v42, s[52:53]",
                "v_cndmask_b32 v83, v42, v83, vcc",
                "v_cndmask_b32 v82, v41, v82, vcc",
                "v_cndmask_b32 v58, v55, v54, s[56:57]",
                "v_and_b32 v58, 0x3fffff, v58", "v_add_u32 v58, -1, v58",          # the slot
-               "s_or_b64 s[56:57], s[56:57], s[54:55]", "s_and_b64 s[56:57], s[56:57], exec",
-               f"s_cbranch_scc0 {skip}",
+               "s_or_b64 s[56:57], s[56:57], s[54:55]", "s_and_b64 s[56:57], s[56:57], exec")
+        self.lcache_count()
+        self.e(f"s_cbranch_scc0 {skip}",
                "v_mov_b32 v59, s68",
                "v_mad_u64_u32 v[42:43], s[54:55], v58, v59, s[64:65]",
                "s_mov_b64 s[54:55], exec", "s_mov_b64 exec, s[56:57]",            # exec = hits
@@ -1120,6 +1131,26 @@ class Gen:
                "s_andn2_b64 s[60:61], s[54:55], s[56:57]", "s_mov_b64 exec, s[60:61]",
                f"s_cbranch_execz {done}",
                f"{skip}:")
+
+    def lcache_count(self):
+        """BPFTIME_AMD_DBG 512 (oflags bit 3): add the probe's hits
+        (s[56:57]) and misses (the other lanes of exec) to the counters at
+        tenv[1] (interp.hip; read by bpftime_amd_dbg_counters).  Keeps SCC =
+        (hits != 0) for the branch that follows."""
+        off = self.label("lcc")
+        self.e("s_bitcmp1_b32 %[oflags], 3", f"s_cbranch_scc0 {off}",
+               "s_bcnt1_i32_b64 s52, s[56:57]", "s_bcnt1_i32_b64 s53, exec", "s_sub_u32 s53, s53, s52",
+               "s_mov_b64 s[54:55], exec", "s_mov_b64 exec, 1",
+               f"s_sub_u32 s69, %[comb], {TENV - 8}", "v_mov_b32 v41, s69",
+               "ds_read_b64 v[42:43], v41",
+               "v_mov_b32 v56, s52", "v_mov_b32 v57, 0",
+               "s_waitcnt lgkmcnt(0)",
+               "global_atomic_add_x2 v[42:43], v[56:57], off",
+               "v_mov_b32 v56, s53",
+               "global_atomic_add_x2 v[42:43], v[56:57], off offset:8",
+               "s_mov_b64 exec, s[54:55]",
+               f"{off}:",
+               "s_cmp_lg_u64 s[56:57], 0")
 
     def lcache_fill(self, vslot):
         """exec = lanes that found their key in slot v<vslot>: claim the
@@ -1140,12 +1171,17 @@ class Gen:
                "s_mov_b64 exec, s[52:53]",
                f"{skip}:")
 
-    def index_probe(self, kd, done):
+    def index_probe(self, kd, done, bail):
         """The map's lookup index (common.hpp ix_pos), if it has one: up to
         kIxProbes entries from ix_pos(h) until every lane has found its key
-        (r0 = that slot's value).  An empty entry in any lane, or too many
-        probes, hands the whole wave to the reference probe that follows
-        (h stays in v[48:49]; lanes that already hit are recomputed there)."""
+        (r0 = that slot's value).  The index holds exactly the keys the
+        reference probe reaches, so an empty entry in any lane (a miss, or a
+        line of this XCD's L2 an insert has not reached yet), an entry an
+        insert holds reserved (kIxRes), or too many probes hand the whole
+        wave to the C++ tier's lookup (dev_helpers.hpp hash_find_ix:
+        coherent reads, the miss record the lookup-or-init race rule needs)
+        instead of the reference probe's walk.  A map without an index goes
+        to the reference probe that follows (h stays in v[48:49])."""
         loop, fail = self.label("ixl"), self.label("ixf")
         self.e("s_cmp_eq_u64 s[74:75], 0", f"s_cbranch_scc1 {fail}",
                "s_mov_b32 s85, 0x85ebca6b", "v_mul_lo_u32 v41, v49, s85", "v_xor_b32 v41, v41, v48",
@@ -1157,7 +1193,8 @@ class Gen:
                "global_load_dword v50, v[42:43], off sc1",
                "s_waitcnt vmcnt(0)",
                "v_cmp_eq_u32 s[56:57], 0, v50",                                 # empty entry
-               "s_cmp_lg_u64 s[56:57], 0", f"s_cbranch_scc1 {fail}",
+               "v_cmp_eq_u32 vcc, -1, v50", "s_or_b64 s[56:57], s[56:57], vcc",  # ... or reserved
+               "s_cmp_lg_u64 s[56:57], 0", f"s_cbranch_scc1 {bail}",
                "v_add_u32 v50, -1, v50",
                "v_mov_b32 v51, s68",
                "v_mad_u64_u32 v[54:55], s[56:57], v50, v51, s[64:65]",           # slot
@@ -1173,7 +1210,7 @@ class Gen:
         self.e("s_andn2_b64 exec, s[62:63], s[56:57]",                          # exec = other keys
                f"s_cbranch_execz {done}",
                "v_add_u32 v41, 1, v41", "v_and_b32 v41, s67, v41",
-               "s_add_u32 s85, s85, 1", "s_cmp_ge_u32 s85, 8", f"s_cbranch_scc1 {fail}",
+               "s_add_u32 s85, s85, 1", "s_cmp_ge_u32 s85, 8", f"s_cbranch_scc1 {bail}",
                f"s_branch {loop}",
                f"{fail}:", "s_mov_b64 exec, s[60:61]")
 
@@ -1203,7 +1240,7 @@ class Gen:
                        "v_sub_co_u32 v48, vcc, v50, v48", "v_subb_co_u32 v49, vcc, v51, v49, vcc",
                        f"v_bfe_u32 v50, v{44 + i // 4}, {8 * (i % 4)}, 8",
                        "v_add_co_u32 v48, vcc, v48, v50", "v_addc_co_u32 v49, vcc, 0, v49, vcc")
-            self.index_probe(kd, done)
+            self.index_probe(kd, done, bail)
             # idx = h % nbuckets: h = ((hi * 2^16 + lo >> 16) * 2^16 + lo & 0xffff)
             self.e("v_cvt_f64_u32 v[58:59], s66", "v_rcp_f64 v[54:55], v[58:59]",
                    "v_cvt_f64_u32 v[50:51], v49")

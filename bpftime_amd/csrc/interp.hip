@@ -593,7 +593,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   SRP(err_count); SRV(n); SRV(stride); SRV(first_unit); SRV(data_lo); SRV(data_hi); SRV(arena_lo);
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
-  SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(flush_log); SRV(log_words); SRP(lane_scratch);
+  SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(dbg_counts); SRP(flush_log); SRV(log_words); SRP(lane_scratch);
   SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask); SRV(lcache); SRP(gregs); SRP(rb_stage); SRP(gctx);
   SRP(miss_log); SRP(miss_counts); SRV(miss_cap); SRP(tail_slots);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
@@ -650,7 +650,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   // counter v of the table (entry v / 4, counter v % 4 of its granule) as a
   // flush tag {address | (4-byte ? 1 : 0)} and delta
   auto comb_counter = [&](uint32_t v, uint64_t &tag, uint64_t &delta) {
-    const uint32_t e = v >> 2, j = v & 3, t = comb[e];
+    const uint32_t e = v >> 2, j = v & 3, t = comb[comb_tag_pos(e, p.comb_entries)];
     tag = delta = 0;
     if (!t) return;
     // 4-byte granules are 16-byte aligned; 8-byte ones 8-byte aligned (pairs)
@@ -670,7 +670,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const bool on = IMAGE && KIND == CTX_XDP && p.frames && p.tail_entry && !(p.dbg & 8);  // dbg 8: C++ frames
     const uint64_t stride = (uint64_t)gridDim.x * kBlock * 8;
     tenv[0] = on ? (uint64_t)(uintptr_t)p.frames : 0;
-    tenv[1] = (uint64_t)(uintptr_t)p.tail_entry;
+    // (other launches, BPFTIME_AMD_DBG 512: the lookup cache's hit / miss
+    // counters, gen_fast.py lcache_count)
+    tenv[1] = IMAGE ? (uint64_t)(uintptr_t)p.tail_entry : (uint64_t)(uintptr_t)p.dbg_counts;
     tenv[2] = stride | ((stride * p.frame_words) << 32);
     const uint32_t sw = p.stack_size / 8;  // (images in the asm tier: <= kLdsStackMax bytes)
     const uint32_t smask = p.tail_stack_mask & (sw >= 16 ? 0xffffu : (1u << sw) - 1);
@@ -724,7 +726,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   // (bit 2, BPFTIME_AMD_DBG 128: counter adds that miss the combining table
   // are dropped -- a timing experiment, never a result)
   fe.oflags = sreg((uint32_t)__builtin_amdgcn_readfirstlane((p.verdicts ? 1u : 0u) | (p.rets ? 2u : 0u) |
-                                                            ((p.dbg & 128) ? 4u : 0u)));
+                                                            ((p.dbg & 128) ? 4u : 0u) |
+                                                            ((p.dbg & 512) && p.dbg_counts ? 8u : 0u)));
   fe.dlo = sreg((uint64_t)(p.checked ? p.data_lo : 0));
   fe.dhi = sreg((uint64_t)(p.checked ? p.data_hi : ~(uint64_t)0));
   fe.alo = p.arena_lo;

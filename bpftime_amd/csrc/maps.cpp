@@ -860,8 +860,13 @@ static int ix_rebuild(int fd) {
     }
   r.ix_stale.erase(fd);
   if (e0 == nb) return 0;  // full table: no index (lookups take the reference probe)
-  const uint64_t isz = (uint64_t)m.d.ix_mask + 1;
-  std::vector<uint32_t> ix(isz, 0);
+  const uint64_t isz = (uint64_t)m.d.ix_mask + 1, words = ix_bitmap_words(nb);
+  // the index, then the bucket bitmap (common.hpp ix_bitmap): one upload
+  std::vector<uint32_t> ix(isz + 2 * words, 0);
+  uint64_t *bits = (uint64_t *)(ix.data() + isz);
+  for (uint64_t i = 0; i < nb; i++)
+    if (state(i) != 0) bits[i >> 6] |= 1ull << (i & 63);
+  if (nb % 64) bits[words - 1] |= ~0ull << (nb % 64);
   std::set<std::string> run_keys;
   uint64_t run_start = 1;  // distance from e0 of the current run's first bucket
   for (uint64_t k = 1; k < nb; k++) {
@@ -880,7 +885,7 @@ static int ix_rebuild(int fd) {
     while (ix[p]) p = (p + 1) & m.d.ix_mask;
     ix[p] = (uint32_t)i + 1;
   }
-  if (hipMemcpy((void *)m.ix_addr, ix.data(), 4 * isz, hipMemcpyHostToDevice) != hipSuccess) return -1;
+  if (hipMemcpy((void *)m.ix_addr, ix.data(), 4 * ix.size(), hipMemcpyHostToDevice) != hipSuccess) return -1;
   m.ix_valid = true;
   m.d.ix = m.ix_addr;
   return r.push_map(fd);
@@ -1091,11 +1096,17 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
   }
   if (extra && m.type != MT_LRU_HASH && !getenv("BPFTIME_AMD_NO_HASH_INDEX")) {
     // lookup index (common.hpp ix_pos): a power of two >= 2 x buckets, so
-    // it is at most half full; an empty table's index is empty and valid
+    // it is at most half full; an empty table's index is empty and valid.
+    // After it the bucket bitmap (common.hpp ix_bitmap), the bits past the
+    // last bucket set
     uint64_t isz = 64;
     while (isz < 2 * (uint64_t)d.nbuckets) isz <<= 1;
-    uint64_t ix = isz <= (1ull << 32) ? r.arena_alloc(4 * isz) : 0;
-    if (ix && hipMemset((void *)ix, 0, 4 * isz) == hipSuccess) {
+    const uint64_t words = ix_bitmap_words(d.nbuckets);
+    uint64_t ix = isz <= (1ull << 32) ? r.arena_alloc(4 * isz + 8 * words) : 0;
+    const uint64_t pad = d.nbuckets % 64 ? ~0ull << (d.nbuckets % 64) : 0;
+    if (ix && hipMemset((void *)ix, 0, 4 * isz + 8 * words) == hipSuccess &&
+        hipMemcpy((void *)(ix_bitmap(ix, (uint32_t)(isz - 1)) + 8 * (words - 1)), &pad, 8, hipMemcpyHostToDevice) ==
+            hipSuccess) {
       m.ix_addr = ix;
       m.ix_valid = true;
       d.ix = ix;

@@ -34,6 +34,19 @@ extern "C" hipError_t bpftime_amd_launch_miss_merge(const uint64_t *log, const u
                                                      uint32_t nblocks, const KParams *p, uint32_t *bad,
                                                      hipStream_t stream);
 
+// experiment counters (BPFTIME_AMD_DBG 512), a device buffer made on first use
+static std::mutex g_dbg_mu;
+static uint64_t *g_dbg = nullptr;  // lookup-cache hit / miss lanes (gen_fast.py lcache_count)
+static constexpr int kDbgCounts = 4;
+uint64_t *dbg_counts() {
+  std::lock_guard<std::mutex> g(g_dbg_mu);
+  if (!g_dbg && (hipMalloc((void **)&g_dbg, 8 * kDbgCounts) != hipSuccess ||
+                 hipMemset(g_dbg, 0, 8 * kDbgCounts) != hipSuccess))
+    g_dbg = nullptr;
+  return g_dbg;
+}
+
+
 struct HelperReg {
   std::string name;
   void *fn;
@@ -592,6 +605,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   p.head = b->head;
   p.checked = (b->flags & EBPF_BATCH_UNCHECKED) ? 0 : 1;
   if (const char *d = getenv("BPFTIME_AMD_DBG")) p.dbg = (uint32_t)strtoul(d, nullptr, 0);
+  if (p.dbg & 512) p.dbg_counts = dbg_counts();
   if (hipMemsetAsync(err, 0, 4, s) != hipSuccess) {
     error = "hipMemsetAsync failed";
     return -1;
@@ -1052,6 +1066,17 @@ int bpftime_amd_vm_counter_info(const struct ebpf_vm *vm, uint32_t ctx_kind, uin
 void bpftime_amd_set_step_limit(struct ebpf_vm *vm, uint64_t limit) { vm->impl->step_limit = limit; }
 
 const char *bpftime_amd_vm_error(const struct ebpf_vm *vm) { return vm->impl->error.c_str(); }
+
+// ---- experiment counters (BPFTIME_AMD_DBG 512) ----------------------------
+int bpftime_amd_dbg_counters(uint64_t *out, int n, int reset) {
+  uint64_t *d = bpftime_amd::dbg_counts();
+  if (!d || !out || n < 0) return -1;
+  if (n > kDbgCounts) n = kDbgCounts;
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(out, d, 8 * n, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  if (reset && hipMemset(d, 0, 8 * kDbgCounts) != hipSuccess) return -1;
+  return n;
+}
 
 // ---- device utilities ------------------------------------------------------
 int bpftime_amd_device_count(void) {

@@ -303,6 +303,9 @@ int bpftime_amd_merge_delta(void *acc, const void *init, const void *shard, uint
 /* ---- device utilities (HIP runtime plumbing for callers without one) ---- */
 int bpftime_amd_device_count(void);
 int bpftime_amd_hip_runtime_version(void);  /* hipRuntimeGetVersion of the runtime this library runs on, -1 on error */
+/* Experiment counters (BPFTIME_AMD_DBG=512: hash lookup-cache hit lanes, miss lanes): up to n
+ * u64 into out after the device is idle, zeroed when reset; the count or -1. */
+int bpftime_amd_dbg_counters(uint64_t *out, int n, int reset);
 int bpftime_amd_set_device(int dev);
 void *bpftime_amd_dev_alloc(uint64_t bytes);
 void bpftime_amd_dev_free(void *p);
