@@ -94,6 +94,7 @@ SIGNATURES = [
     ("bpftime_amd_register_default_helpers", C.c_int, [C.c_void_p]),
     ("bpftime_amd_vm_info", C.c_int, [C.c_void_p, u32p, C.POINTER(C.c_int), u32p, u32p]),
     ("bpftime_amd_set_step_limit", None, [C.c_void_p, C.c_uint64]),
+    ("bpftime_amd_last_batch_ms", C.c_float, [C.c_void_p]),
     ("bpftime_amd_vm_fast_info", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
     ("bpftime_amd_vm_counter_info", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32),
                                               C.POINTER(C.c_uint32)]),

@@ -225,7 +225,10 @@ __device__ uint64_t hash_find_ix(const DMap &m, uint64_t key, uint64_t h, bool i
   for (uint32_t t = 0; t <= m.ix_mask;) {
     const uint64_t ea = m.ix + 4ull * p;
     uint32_t e = ald32(ea);
-    if (e == 0 || e == kIxRes) e = acoh32(ea);
+    // an empty entry is confirmed at the coherence point; a reservation is
+    // polled with loads, confirmed every 16th trip (thousands of lanes may
+    // wait on a hot new key's: same-address atomics serialize)
+    if (e == 0 || (e == kIxRes && (spins & 15) == 15)) e = acoh32(ea);
     if (e == 0) {
       if (!insert) return 0;
       uint32_t z = 0;

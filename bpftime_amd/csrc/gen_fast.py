@@ -1152,6 +1152,21 @@ class Gen:
                f"{off}:",
                "s_cmp_lg_u64 s[56:57], 0")
 
+    def dbg_lanes(self, slot, mask):
+        """BPFTIME_AMD_DBG 512: add the lanes of `mask` (an SGPR pair, a
+        subset of exec) to counter `slot` at tenv[1] (index-probe exits);
+        uses s[52:53], s69, v[56:59]."""
+        off, back = self.label("dlo"), self.label("dlb")
+        self.e("s_bitcmp1_b32 %[oflags], 3", f"s_cbranch_scc0 {off}",
+               "s_mov_b64 s[52:53], exec", f"s_and_b64 exec, exec, {mask}", f"s_cbranch_execz {back}",
+               f"s_sub_u32 s69, %[comb], {TENV - 8}", "v_mov_b32 v56, s69",
+               "ds_read_b64 v[56:57], v56",
+               "v_mov_b32 v58, 1", "v_mov_b32 v59, 0",
+               "s_waitcnt lgkmcnt(0)",
+               f"global_atomic_add_x2 v[56:57], v[58:59], off offset:{8 * slot}",
+               f"{back}:", "s_mov_b64 exec, s[52:53]",
+               f"{off}:")
+
     def lcache_fill(self, vslot):
         """exec = lanes that found their key in slot v<vslot>: claim the
         probe's empty way (v83) and write the key, then the entry (a lane
@@ -1193,8 +1208,9 @@ class Gen:
                "global_load_dword v50, v[42:43], off sc1",
                "s_waitcnt vmcnt(0)",
                "v_cmp_eq_u32 s[56:57], 0, v50",                                 # empty entry
-               "v_cmp_eq_u32 vcc, -1, v50", "s_or_b64 s[56:57], s[56:57], vcc",  # ... or reserved
-               "s_cmp_lg_u64 s[56:57], 0", f"s_cbranch_scc1 {bail}",
+               "v_cmp_eq_u32 vcc, -1, v50", "s_or_b64 s[56:57], s[56:57], vcc")  # ... or reserved
+        self.dbg_lanes(2, "s[56:57]")
+        self.e("s_cmp_lg_u64 s[56:57], 0", f"s_cbranch_scc1 {bail}",
                "v_add_u32 v50, -1, v50",
                "v_mov_b32 v51, s68",
                "v_mad_u64_u32 v[54:55], s[56:57], v50, v51, s[64:65]",           # slot
@@ -1210,8 +1226,9 @@ class Gen:
         self.e("s_andn2_b64 exec, s[62:63], s[56:57]",                          # exec = other keys
                f"s_cbranch_execz {done}",
                "v_add_u32 v41, 1, v41", "v_and_b32 v41, s67, v41",
-               "s_add_u32 s85, s85, 1", "s_cmp_ge_u32 s85, 8", f"s_cbranch_scc1 {bail}",
-               f"s_branch {loop}",
+               "s_add_u32 s85, s85, 1", "s_cmp_lt_u32 s85, 8", f"s_cbranch_scc1 {loop}")
+        self.dbg_lanes(3, "exec")
+        self.e(f"s_branch {bail}",
                f"{fail}:", "s_mov_b64 exec, s[60:61]")
 
     def hash_lookup(self):

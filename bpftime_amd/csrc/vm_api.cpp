@@ -182,6 +182,8 @@ class Mi355xVm {
   std::string link_note;    // targets left out of the last image, and why
   // block-end flush logs (common.hpp kMergeGroup) and tail-call frames
   StreamBufs logs, frames, scratch, regs, misses;
+  // the kernels of the last EBPF_BATCH_TIMED batch
+  hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;
 
   Mi355xVm() {
     // bpftime_prog.cpp:126-127 defaults, pointed at the device registry
@@ -191,6 +193,8 @@ class Mi355xVm {
     if (sl) step_limit = strtoull(sl, nullptr, 0);
   }
   ~Mi355xVm() {
+    if (ev_t0) hipEventDestroy(ev_t0);
+    if (ev_t1) hipEventDestroy(ev_t1);
     unload();
     if (d_err) hipFree(d_err);
     if (d_stage) hipFree(d_stage);
@@ -771,6 +775,16 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
             "miss cap %u\n",
             (unsigned long long)b->count, grid, block, p.comb_entries, p.lcache, p.stage, (unsigned)prog.stack_size,
             p.gregs ? 1 : 0, p.gctx ? 1 : 0, p.unwind_idx, p.miss_cap);
+  // EBPF_BATCH_TIMED: events around this batch's kernels only (the host
+  // work above -- linking, buffers, index upkeep -- stays outside)
+  const bool timed = (b->flags & EBPF_BATCH_TIMED) != 0;
+  if (timed) {
+    if ((!ev_t0 && hipEventCreate(&ev_t0) != hipSuccess) || (!ev_t1 && hipEventCreate(&ev_t1) != hipSuccess) ||
+        hipEventRecord(ev_t0, s) != hipSuccess) {
+      error = "timing event failed";
+      return -1;
+    }
+  }
   hipError_t e = bpftime_amd_launch_interp(&p, b->ctx_kind, prog.big_stack, grid, ordered ? 1 : 0, block, s);
   // (BPFTIME_AMD_SYNC_EACH: synchronize after every launch, naming the one that failed)
   const bool sync_each = getenv("BPFTIME_AMD_SYNC_EACH") != nullptr;
@@ -789,6 +803,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     hipMemcpy(&bad, p.miss_counts + (uint64_t)grid * kMissParts, 4, hipMemcpyDeviceToHost);
     if (bad) fprintf(stderr, "bpftime_amd: k_miss_merge: %u records outside the windows\n", bad);
   }
+  if (e == hipSuccess && timed) e = hipEventRecord(ev_t1, s);
   if (e != hipSuccess) {
     error = std::string("kernel launch failed: ") + hipGetErrorString(e);
     return -1;
@@ -1064,6 +1079,15 @@ int bpftime_amd_vm_counter_info(const struct ebpf_vm *vm, uint32_t ctx_kind, uin
 }
 
 void bpftime_amd_set_step_limit(struct ebpf_vm *vm, uint64_t limit) { vm->impl->step_limit = limit; }
+
+float bpftime_amd_last_batch_ms(struct ebpf_vm *vm) {
+  Mi355xVm *v = vm ? vm->impl : nullptr;
+  float ms = -1.f;
+  if (!v || !v->ev_t0 || !v->ev_t1 || hipEventSynchronize(v->ev_t1) != hipSuccess ||
+      hipEventElapsedTime(&ms, v->ev_t0, v->ev_t1) != hipSuccess)
+    return -1.f;
+  return ms;
+}
 
 const char *bpftime_amd_vm_error(const struct ebpf_vm *vm) { return vm->impl->error.c_str(); }
 

@@ -17,7 +17,7 @@ from . import isa
 from ._lib import BpfLinkCreateArgs, BpfMapAttr, EbpfBatch, lib
 
 CTX_RAW, CTX_XDP, CTX_SYSCALL = 0, 1, 2
-BATCH_SYNC, BATCH_ORDERED, BATCH_UNCHECKED, BATCH_SYS_NR = 0x1, 0x2, 0x4, 0x8
+BATCH_SYNC, BATCH_ORDERED, BATCH_UNCHECKED, BATCH_SYS_NR, BATCH_TIMED = 0x1, 0x2, 0x4, 0x8, 0x10
 
 
 class EbpfError(RuntimeError):
@@ -266,6 +266,10 @@ class VM:
 
     def set_step_limit(self, n: int) -> None:
         lib().bpftime_amd_set_step_limit(C.c_void_p(self.h), n)
+
+    def last_batch_ms(self) -> float:
+        """Kernel time of this VM's last BATCH_TIMED batch (ms; -1 none)."""
+        return lib().bpftime_amd_last_batch_ms(self.h)
 
     def exec_batch(self, kind: int, data: DeviceBuffer, count: int, stride: int, fixed_len: int = 0,
                    lens: Optional[DeviceBuffer] = None, verdicts: Optional[DeviceBuffer] = None,

@@ -191,6 +191,8 @@ int bpftime_amd_register_default_helpers(struct ebpf_vm *vm);
 int bpftime_amd_vm_info(const struct ebpf_vm *vm, uint32_t *stack_size, int *big_stack,
                         uint32_t *fused_rmw, uint32_t *n_insns);
 void bpftime_amd_set_step_limit(struct ebpf_vm *vm, uint64_t limit);
+/* Kernel time (ms) of the vm's last EBPF_BATCH_TIMED batch, waiting for it; -1 when none. */
+float bpftime_amd_last_batch_ms(struct ebpf_vm *vm);
 /* loads/stores (and array-lookup keys) the loader typed statically for the
  * fast path under the given ctx kind (packet, slot, ctx or stack bases) */
 int bpftime_amd_vm_fast_info(const struct ebpf_vm *vm, uint32_t ctx_kind, uint32_t *specialized);

@@ -85,6 +85,7 @@ ebpf_jit_fn ebpf_load_aot_object(struct ebpf_vm *vm, const void *buf, size_t buf
 #define EBPF_BATCH_ORDERED 0x2 /* one lane, units in index order (exact sequential semantics) */
 #define EBPF_BATCH_UNCHECKED 0x4 /* skip the global-window confinement check */
 #define EBPF_BATCH_SYS_NR 0x8    /* EBPF_CTX_SYSCALL: only records whose id == sys_nr run (per-syscall attach) */
+#define EBPF_BATCH_TIMED 0x10    /* record events around the batch's kernels (bpftime_amd_last_batch_ms) */
 
 struct ebpf_batch {
 	uint32_t ctx_kind;       /* EBPF_CTX_* */
