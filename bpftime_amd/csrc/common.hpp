@@ -194,6 +194,9 @@ constexpr uint32_t CTX_SYSCALL = 2;  // r1 = 64-B trace_event_raw_sys_enter reco
 // Launches of at least this many units build the flat table of an IPv4 LPM
 // trie changed since the last one (maps.cpp prepare_ix); smaller ones walk
 constexpr uint64_t kLpmFlatMinUnits = 1ull << 16;
+// LPM replica header word 3: an ORDERED batch's update found the node pool
+// full (dev_helpers.hpp lpm_update; the host fails the batch, maps.cpp)
+constexpr uint32_t kLpmPoolOut = 0x80000000u;
 
 // Ring-buffer staging per block (dev_helpers.hpp RbStage)
 constexpr uint32_t kRbStageRec = 2048;                                // record bytes (a ring chunk) per block

@@ -579,7 +579,7 @@ __device__ uint64_t lpm_lookup(const DMap &m, uint64_t key) {
 // key_off, value at val_off}.  Errors return -1 like the reference helper.
 struct LpmHdr {
   int32_t root;
-  uint32_t nodes, entries, cap;
+  uint32_t nodes, entries, cap;  // (cap | kLpmPoolOut: an update found the pool full)
 };
 
 __device__ __forceinline__ uint32_t lpm_match(const DMap &m, uint64_t nb, const uint8_t *kd, uint32_t kp) {
@@ -606,7 +606,12 @@ __device__ uint64_t lpm_update(const DMap &m, uint64_t key, uint64_t val, uint64
   auto need_room = [&]() {
     if (flags == 2) return false;                    // ENOENT
     if (h->entries >= m.max_entries) return false;   // ENOSPC
-    return h->nodes + 2 <= h->cap;                   // the replica's node pool (maps.cpp)
+    // the replica's node pool (maps.cpp): running out of it is no answer
+    // the reference gives (its heap grows), so it is flagged in the
+    // header and the host fails the batch (maps.cpp lpm_pull)
+    if (h->nodes + 2 <= (h->cap & ~kLpmPoolOut)) return true;
+    h->cap |= kLpmPoolOut;
+    return false;
   };
   auto make = [&](uint32_t p, bool in) -> int32_t {
     const int32_t i = (int32_t)h->nodes++;
@@ -727,53 +732,85 @@ constexpr uint64_t kRbSlack = kRbMaxWaves * kRbWaveMax;    // 32 MiB
 // Block staging of ring-buffer records.  A block does not move the ring's
 // producer position per record (a same-address atomic at the memory side,
 // ~40 ns each under the whole chip's contention: it bounded the sampler at
-// 1.5 Gpps): its first reservation, when the ring has ample room (the fast
-// path's condition), reserves a chunk of kRbStageRec bytes of the ring with
-// one fetch-and-add, and the block's waves then claim records inside the
-// chunk with an LDS add, writing them to a per-block staging area.  When the
-// block ends it copies its records to their places in the chunk (with the
-// flags submit / discard gave them) and fills the chunk's unused tail with
-// one DISCARD record, which a consumer skips.  Every byte is reserved in the
-// ring before it is handed out, so no reservation of any other block or
-// path can overrun (the exact path below is unchanged); the difference to
-// the reference is the discarded tail, up to one chunk per block and launch
-// of ring space that a ring going from ample room to full inside one launch
-// can no longer give to records.  A wave whose records do not fit the chunk
-// reserves directly.  Right after the chunk's reservation its first header
-// reads BUSY (one record spanning the chunk), and rb_publish writes that
-// header last: a consumer polling while the block runs stops at the chunk as
-// it stops at any reserved record (the reference writes each BUSY header
-// before moving the position, under its spin lock; here the producer
-// position moves a few instructions before the BUSY header lands, and
-// bpftime_amd_ringbuf_fetch synchronizes the device before it reads).
+// 1.5 Gpps).  Its first reservation, when the ring has ample room (the fast
+// path's condition, counting promises), PROMISES itself kRbStageRec bytes:
+// an add to the ring's promise counter (at data + 192), no ring position.
+// The block's waves then claim records inside that budget with an LDS
+// compare-and-swap on the bytes used, writing them to a per-block staging
+// area.  When the block ends it reserves exactly the bytes it used with one
+// fetch-and-add of the producer position, copies its records there and
+// returns its promise: no ring byte is ever wasted, so a ring that goes from
+// ample room to full inside one launch accepts exactly what a serial run
+// accepts (the reference's ringbuf::reserve, ringbuf_map.cpp:262-295).
+// Every reservation counts the outstanding promises as taken
+// (rb_room), so a promised byte is always there at the block's end.  A
+// reservation that does not fit while promises are outstanding first closes
+// its own block's staging (the block's used bytes are reserved at once, its
+// promise returned: a closed block's waves reserve directly) and then waits
+// for the other blocks' promises to come back -- they do when those blocks
+// end or close; no new promise is made that close to full -- so it fails only
+// when the ring is really full, as a serial reservation would.  A wave whose
+// records do not fit the block's budget reserves directly.  The consumer,
+// bpftime_amd_ringbuf_fetch, synchronizes the device before it reads.
 // Consumers see the same records in another parallel order.
 // (sizes: common.hpp kRbStage*)
+constexpr uint32_t kRbClosed = 0x80000000u;  // RbStage::used: the block's staging is closed
 struct RbStage {
   uint8_t *buf = nullptr;  // this block's area: records, then u32 offsets (nullptr: no staging)
-  uint32_t *used = nullptr, *end = nullptr, *nrec = nullptr;  // LDS: bytes claimed, staged end, records
-  int32_t *fd = nullptr;   // LDS: the ring of the block's chunk (-1 undecided, -3 deciding, -2 none)
-  uint64_t *base = nullptr;  // LDS: the chunk's ring position
+  uint32_t *used = nullptr, *end = nullptr, *nrec = nullptr;  // LDS: bytes claimed (| kRbClosed), -, records
+  int32_t *fd = nullptr;   // LDS: the ring of the block's promise (-1 undecided, -3 deciding, -2 none)
+  uint64_t *base = nullptr;  // LDS: the ring position of the block's records (set when it closes)
 };
 
-__device__ __forceinline__ uint64_t rb_cas_reserve(const DMap &m, uint64_t total) {
+// the ring's room for a reservation: capacity - (producer - consumer) -
+// the bytes blocks have promised themselves (RbStage)
+__device__ __forceinline__ int64_t rb_room(const DMap &m, uint64_t *prod_out = nullptr) {
+  const uint64_t cons = __hip_atomic_load(G64(m.data), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t prod = __hip_atomic_load(G64(m.data + 128), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t prom = __hip_atomic_load(G64(m.data + 192), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (prod_out) *prod_out = prod;
+  return (int64_t)m.max_entries - (int64_t)(prod - cons) - (int64_t)prom;
+}
+
+// Close the block's staging (a reservation of the block needs the exact
+// path): no claim succeeds after this, the bytes claimed so far are
+// reserved in the ring now (rb_publish copies them there) and the promise
+// is returned.
+__device__ void rb_close(const DMap &m, const RbStage &st) {
+  if (!st.buf || *st.fd < 0) return;
+  const uint32_t u = __hip_atomic_fetch_or(st.used, kRbClosed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (u & kRbClosed) return;  // (closed by another wave of the block)
+  *st.base = u ? __hip_atomic_fetch_add(G64(m.data + 128), (uint64_t)u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+               : 0;
+  __hip_atomic_fetch_add(G64(m.data + 192), (uint64_t)0 - kRbStageRec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint64_t rb_cas_reserve(const DMap &m, uint64_t total, const RbStage &st, int32_t fd) {
   // returns the old producer position, or ~0 if total does not fit.  The
-  // loop always ends by a successful CAS or a failed room check, as the
+  // loop ends by a successful CAS or a failed room check, as the
   // reference's spin-locked reserve does: the consumer position does not
   // move while a launch runs (its only consumer, bpftime_amd_ringbuf_fetch,
-  // synchronizes the device first), and every lost CAS means another
-  // reservation moved the producer position by >= 8 bytes, so after at most
-  // max_entries / 8 lost CASes the room check fails.  The bound below is
-  // that count plus one and is never the reason the loop ends.
-  const uint64_t cons = __hip_atomic_load(G64(m.data), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  unsigned long long p = __hip_atomic_load(G64(m.data + 128), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // synchronizes the device first), every lost CAS means another
+  // reservation moved the producer position by >= 8 bytes, and promises
+  // only come back.  A room that only the outstanding promises take is
+  // waited for (this block's own promise returned first, rb_close).
   uint32_t backoff = 1;
-  const uint64_t bound = (uint64_t)m.max_entries / 8 + 2;
+  const uint64_t bound = (uint64_t)m.max_entries / 8 + (1u << 20);
   for (uint64_t spin = 0; spin < bound; spin++) {
-    if ((uint64_t)m.max_entries - (p - cons) < total) return ~0ull;
-    if (__hip_atomic_compare_exchange_strong(G64(m.data + 128), &p, p + total, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT))
-      return p;
-    // lost to another wave: back off (thousands of waves share this word)
+    uint64_t p;
+    const int64_t room = rb_room(m, &p);
+    if (room < (int64_t)total) {
+      const uint64_t prom = __hip_atomic_load(G64(m.data + 192), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!prom) return ~0ull;  // full, with nothing promised: the serial answer
+      if (*st.fd == fd) rb_close(m, st);
+    } else {
+      unsigned long long e = p;
+      if (__hip_atomic_compare_exchange_strong(G64(m.data + 128), &e, p + total, __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        return p;
+    }
+    // lost to another wave, or waiting for promises: back off (thousands of
+    // waves share these words)
     for (uint32_t i = 0; i < backoff; i++) __builtin_amdgcn_s_sleep(2);
     backoff = backoff < 64 ? 2 * backoff : 64;
   }
@@ -808,26 +845,15 @@ __device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size, con
           int32_t cur = -1;
           if (__hip_atomic_compare_exchange_strong(st.fd, &cur, -3, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_WORKGROUP)) {
-            const uint64_t cons = __hip_atomic_load(G64(m.data), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint64_t prod = __hip_atomic_load(G64(m.data + 128), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             int32_t got = -2;
-            // the fast path's condition (below), for a chunk
-            if (m.max_entries >= 2 * kRbSlack && (uint64_t)m.max_entries - (prod - cons) >= kRbStageRec + kRbSlack) {
-              *st.base = __hip_atomic_fetch_add(G64(m.data + 128), (uint64_t)kRbStageRec, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
+            // the fast path's condition (below), for a block's budget
+            if (m.max_entries >= 2 * kRbSlack && rb_room(m) >= (int64_t)(kRbStageRec + kRbSlack)) {
+              __hip_atomic_fetch_add(G64(m.data + 192), (uint64_t)kRbStageRec, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
               got = (int32_t)fd;
             }
             __hip_atomic_store(st.fd, got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             cur = got;
-            if (got >= 0) {
-              // the chunk reads as one reserved record until the block
-              // publishes (written once the block's other waves may use the
-              // chunk: inside the deciding window, where they reserve
-              // directly, the two stores cost the sampler 7 %)
-              const uint64_t h = m.data + 256 + (*st.base & (m.max_entries - 1));
-              *(int32_t *)(uintptr_t)(h + 4) = (int32_t)fd;
-              *(uint32_t *)(uintptr_t)h = (kRbStageRec - RB_HDR) | RB_BUSY;
-            }
           }
           sfd = cur;
         }
@@ -837,12 +863,20 @@ __device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size, con
         uint32_t base = ~0u, rbase = 0;
         const uint32_t cnt = (uint32_t)__builtin_popcountll(active);
         if (me == leader) {
-          base = __hip_atomic_fetch_add(st.used, (uint32_t)sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if ((uint64_t)base + sum <= kRbStageRec) {  // (then the record slots fit too: >= 8 B each)
-            rbase = __hip_atomic_fetch_add(st.nrec, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_max(st.end, base + (uint32_t)sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          } else {
-            base = ~0u;  // staging full: direct (the staged end stays below every later claim)
+          // claim sum bytes of the budget (a compare-and-swap, so the used
+          // count is exactly the claimed bytes: rb_close reserves them)
+          uint32_t u = __hip_atomic_load(st.used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          for (;;) {
+            if ((u & kRbClosed) || (uint64_t)u + sum > kRbStageRec) {
+              base = ~0u;  // closed, or the budget is spent: direct
+              break;
+            }
+            if (__hip_atomic_compare_exchange_strong(st.used, &u, u + (uint32_t)sum, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+              base = u;  // (then the record slots fit too: >= 8 B each)
+              rbase = __hip_atomic_fetch_add(st.nrec, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              break;
+            }
           }
         }
         base = __shfl(base, leader);
@@ -866,19 +900,17 @@ __device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size, con
       // Safe because at most kRbMaxWaves reservations of <= kRbWaveMax
       // bytes can be between their room check and their add, so an add
       // admitted with kRbSlack bytes to spare never overruns the consumer.
-      const uint64_t cons = __hip_atomic_load(G64(m.data), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t prod = __hip_atomic_load(G64(m.data + 128), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (sum <= kRbWaveMax && (uint64_t)m.max_entries - (prod - cons) >= sum + kRbSlack)
+      if (sum <= kRbWaveMax && rb_room(m) >= (int64_t)(sum + kRbSlack))
         base = __hip_atomic_fetch_add(G64(m.data + 128), sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else
-        base = rb_cas_reserve(m, sum);
+        base = rb_cas_reserve(m, sum, st, (int32_t)fd);
     }
     base = __shfl(base, leader);
     if (base != ~0ull) pos = base + before;
   }
   if (pos == ~0ull && fits) {  // lane by lane (full ring, mixed rings)
     for (uint64_t rest = __ballot(1); rest; rest &= rest - 1)
-      if ((uint32_t)__builtin_ctzll(rest) == me) pos = rb_cas_reserve(m, total);
+      if ((uint32_t)__builtin_ctzll(rest) == me) pos = rb_cas_reserve(m, total, st, (int32_t)fd);
   }
   if (pos == ~0ull) return 0;
   const uint64_t mask = m.max_entries - 1, d = m.data + 256;
@@ -921,48 +953,40 @@ __device__ uint64_t rb_output(const DMap *maps, uint64_t fd, uint64_t data, uint
   return 0;
 }
 
-// The block's staged records into its chunk of the ring (every wave of the
-// block is done; called by every thread of the block), one thread per
-// record, and the chunk's unused tail as one DISCARD record.  The chunk's
-// first header word (BUSY since the reservation) is written last, after the
-// block's barrier: a consumer polling the ring from this XCD stops at the
-// chunk until the block publishes.  (Ordering that store after the others
-// for every XCD would take an agent-scope release -- an L2 write-back per
-// block: 1.40 -> 2.09 ms per 2^24 sampled frames -- or write-through stores
-// of the whole chunk drained before it: 1.40 -> 1.51 ms.  The ring's
-// consumer here, bpftime_amd_ringbuf_fetch, synchronizes the device before
-// it reads, as the reference's consumer reads after its producers' spin
-// lock, so neither is paid.)
+// The block's staged records into the ring (every wave of the block is
+// done; called by every thread of the block): thread 0 reserves exactly the
+// bytes the block used (unless a wave closed the block's staging, which
+// reserved them then) and returns the block's promise; then one thread per
+// record copies it, with the flags submit / discard gave it.
 __device__ void rb_publish(const DMap *maps, const RbStage &st, uint32_t tid, uint32_t nthreads) {
   const int32_t fd = *st.fd;
   if (!st.buf || fd < 0) return;
   const DMap m = maps[fd];
+  const uint32_t used = *st.used & ~kRbClosed;
+  if (tid == 0 && !(*st.used & kRbClosed)) {
+    *st.base = used ? __hip_atomic_fetch_add(G64(m.data + 128), (uint64_t)used, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)
+                    : 0;
+    __hip_atomic_fetch_add(G64(m.data + 192), (uint64_t)0 - kRbStageRec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
   const uint64_t base = *st.base, mask = m.max_entries - 1, d = m.data + 256;
-  const uint32_t end = *st.end, n = min(*st.nrec, kRbStageMaxRec);
+  const uint32_t n = min(*st.nrec, kRbStageMaxRec);
   const uint32_t *offs = (const uint32_t *)(st.buf + kRbStageRec);
   for (uint32_t i = tid; i < n; i += nthreads) {
     const uint32_t off = offs[i];
     const uint32_t h = *(const uint32_t *)(st.buf + off);
     const uint32_t total = ((h & ~(RB_BUSY | RB_DISCARD)) + RB_HDR + 7) / 8 * 8;
     const uint64_t *src = (const uint64_t *)(st.buf + off);
-    uint64_t *dst = (uint64_t *)(uintptr_t)(d + ((base + off) & mask));
-    for (uint32_t w = off ? 0 : 1; w < total / 8; w++) dst[w] = src[w];
-    if (!off) ((uint32_t *)dst)[1] = ((const uint32_t *)src)[1];
+    // where a direct reservation puts them (rb_reserve): the header at the
+    // position, the data contiguous from the position after it -- at the
+    // ring's start when the header takes its last 8 bytes (the ring area is
+    // 2 x max_entries bytes, as the reference's is)
+    const uint64_t pos = base + off;
+    *(uint64_t *)(uintptr_t)(d + (pos & mask)) = src[0];
+    uint64_t *dst = (uint64_t *)(uintptr_t)(d + ((pos + RB_HDR) & mask));
+    for (uint32_t w = 1; w < total / 8; w++) dst[w - 1] = src[w];
   }
-  uint32_t first = 0;  // the chunk's first header word
-  if (end < kRbStageRec) {
-    const uint32_t tail = (kRbStageRec - end - RB_HDR) | RB_DISCARD;
-    if (end == 0) {
-      first = tail;
-    } else if (tid == 0) {
-      const uint64_t h = d + ((base + end) & mask);
-      *(uint32_t *)(uintptr_t)h = tail;
-      *(int32_t *)(uintptr_t)(h + 4) = fd;
-    }
-  }
-  if (end) first = *(const uint32_t *)st.buf;  // the record staged at offset 0
-  __syncthreads();
-  if (tid == 0) *(uint32_t *)(uintptr_t)(d + (base & mask)) = first;
 }
 
 struct LaneEnv {

@@ -768,6 +768,18 @@ int lpm_pull(int fd) {
   if (hipDeviceSynchronize() != hipSuccess) return -1;  // the batch that wrote it
   uint32_t hdr[4];
   if (hipMemcpy(hdr, (void *)m.d.data, 16, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (hdr[3] & kLpmPoolOut) {
+    // a program's update ran out of the replica's node pool (sized before
+    // the launch for two nodes per update site and unit, maps.cpp
+    // prepare_ix): the reference's trie would have grown, so the batch's
+    // results are not the reference's.  The host keeps its trie (the state
+    // before that batch) and reports it
+    lpm_touch(fd);
+    set_error("LPM_TRIE map fd " + std::to_string(fd) +
+              ": an ORDERED batch's program-side update ran out of the device node pool; the trie keeps its state "
+              "from before that batch");
+    return -1;
+  }
   const uint64_t bytes = 16 + (uint64_t)std::min(hdr[1], m.lpm->cap) * m.d.slot_size;
   std::vector<uint8_t> img(bytes);
   if (hipMemcpy(img.data(), (void *)m.d.data, bytes, hipMemcpyDeviceToHost) != hipSuccess) return -1;
@@ -1116,6 +1128,7 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
   r.maps[fd] = m;
   r.kind[fd] = HKind::MAP;
   if (m.type == MT_LRU_HASH) r.lru_maps.insert(fd);
+  if (m.lpm) r.lpm_maps++;
   if (r.push_map(fd) < 0) return -1;
   return fd;
 }
@@ -1257,6 +1270,9 @@ const void *bpftime_map_lookup_elem(int fd, const void *key) {
         errno = EINVAL;
         return nullptr;
       }
+      // (the runtime lock: a launch on another thread inserts into
+      // lpm_dev_dirty and allocates from the arena under it)
+      std::lock_guard<std::mutex> g(rt().mu);
       if (lpm_pull(fd) < 0) return nullptr;
       const LpmTrie::Node *n = m->lpm->lookup((const uint8_t *)key);
       if (!n) return nullptr;
@@ -1283,6 +1299,7 @@ long bpftime_map_update_elem(int fd, const void *key, const void *value, uint64_
       errno = EINVAL;
       return -1;
     }
+    std::lock_guard<std::mutex> g(rt().mu);  // (see bpftime_map_lookup_elem)
     if (lpm_pull(fd) < 0) return -1;
     if (m->lpm->nodes.size() + 2 > m->lpm->cap && lpm_grow(fd, m->lpm->nodes.size() + 2) < 0) return -1;
     const long rc = m->lpm->update((const uint8_t *)key, value, flags);
@@ -1388,6 +1405,7 @@ long bpftime_map_delete_elem(int fd, const void *key) {
       errno = EINVAL;
       return -1;
     }
+    std::lock_guard<std::mutex> g(rt().mu);
     if (lpm_pull(fd) < 0) return -1;
     const long rc = m->lpm->remove((const uint8_t *)key);
     if (rc == 0) lpm_touch(fd);
@@ -1438,6 +1456,7 @@ int bpftime_map_get_next_key(int fd, const void *key, void *next_key) {
       errno = next_key ? ENOENT : EINVAL;
       return -1;
     }
+    std::lock_guard<std::mutex> g(rt().mu);
     if (lpm_pull(fd) < 0) return -1;
     return m->lpm->first_key((uint8_t *)next_key);
   }
@@ -1511,6 +1530,7 @@ void bpftime_close(int fd) {
       drop_host_view(r, fd);
       r.lru_maps.erase(fd);
       r.lpm_dev_dirty.erase(fd);
+      if (r.maps[fd].lpm) r.lpm_maps--;
       r.maps[fd] = MapRec();
       r.push_map(fd);
     } else if (r.kind[fd] == HKind::PROG) {
@@ -1541,6 +1561,7 @@ void bpftime_amd_reset(void) {
     r.links[i] = LinkRec();
     r.perfs[i] = PerfRec();
   }
+  r.lpm_maps = 0;
   for (int id : detach) bpftime_amd_syscall_detach(id);
   if (r.d_maptab) hipMemset(r.d_maptab, 0, sizeof(DMap) * kMaxFds);
   r.arena_used = 0;
@@ -1664,7 +1685,10 @@ int64_t bpftime_amd_ringbuf_fetch(int fd, void *out, uint64_t cap, uint64_t *use
 
 uint64_t bpftime_amd_map_count(int fd) {
   MapRec *m = map_of(fd);
-  if (m && m->lpm) return lpm_pull(fd) < 0 ? 0 : m->lpm->entries;
+  if (m && m->lpm) {
+    std::lock_guard<std::mutex> g(rt().mu);
+    return lpm_pull(fd) < 0 ? 0 : m->lpm->entries;
+  }
   if (!m || !m->d.count_addr) return 0;
   return read_count(*m);
 }

@@ -111,6 +111,13 @@ struct Runtime {
   // (a program's, on any stream, or the host's): whichever comes second
   // waits for the device first (vm_api.cpp exec_batch, maps.cpp host delete)
   std::atomic<bool> lcache_inflight{false}, deleter_inflight{false};
+  // LPM tries (vm_api.cpp exec_batch): launches of a runtime holding any are
+  // prepared and launched under lpm_launch_mu; a launch that may write a
+  // trie (ORDERED) waits for every launch that may still touch one, and any
+  // launch after a writer waits for it
+  std::mutex lpm_launch_mu;
+  std::atomic<int> lpm_maps{0};
+  std::atomic<bool> lpm_inflight{false}, lpm_writer_inflight{false};
   std::set<int> lru_maps;                // LRU_HASH maps
   std::atomic<uint64_t> lru_seq{1};      // LRU stamp sequence: launches and host-side ops (common.hpp)
   uint32_t lru_launches = 0;             // launches since the last tombstone check

@@ -639,8 +639,26 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     r.lcache_inflight = false;
     r.deleter_inflight = false;
   }
+  // LPM tries: a launch of a program that writes one (ORDERED) never
+  // overlaps another launch that may touch one, on any stream -- whichever
+  // comes second waits for the device -- and the launch and its marking of
+  // the tries as device-written happen under one lock, so a concurrent
+  // launch's preparation sees them
+  std::unique_lock<std::mutex> lpm_lk(r.lpm_launch_mu, std::defer_lock);
+  const bool touches_lpm = r.lpm_maps.load() > 0;
+  if (touches_lpm) {
+    lpm_lk.lock();
+    if ((!lpm_w.empty() && r.lpm_inflight.load()) || r.lpm_writer_inflight.load()) {
+      if (hipDeviceSynchronize() != hipSuccess) {
+        error = "device synchronize failed";
+        return -1;
+      }
+      r.lpm_inflight = false;
+      r.lpm_writer_inflight = false;
+    }
+  }
   if (r.prepare_ix(prog.may_delete, b->count, lpm_w, lpm_updates) < 0) {
-    error = "hash lookup index rebuild failed";
+    error = lpm_w.empty() ? "hash lookup index rebuild failed" : std::string(bpftime_amd_last_error());
     return -1;
   }
   p.lru_seq = r.prepare_lru();
@@ -813,6 +831,11 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   if (!lpm_w.empty()) {
     std::lock_guard<std::mutex> g(r.mu);
     for (const int fd : lpm_w) r.lpm_dev_dirty.insert(fd);
+    r.lpm_writer_inflight = true;
+  }
+  if (touches_lpm) {
+    r.lpm_inflight = true;
+    lpm_lk.unlock();
   }
   if (b->flags & EBPF_BATCH_SYNC) {
     uint32_t failed = 0;
@@ -821,6 +844,16 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     if (he != hipSuccess || r.host_views_pull() < 0) {
       error = std::string("batch sync failed: ") + (he != hipSuccess ? hipGetErrorString(he) : "host view pull");
       return -1;
+    }
+    // a program-side LPM update that ran out of the device node pool fails
+    // the batch here (maps.cpp lpm_pull; asynchronous batches report it at
+    // the trie's next use)
+    for (const int fd : lpm_w) {
+      std::lock_guard<std::mutex> g(r.mu);
+      if (lpm_pull(fd) < 0) {
+        error = bpftime_amd_last_error();
+        return -1;
+      }
     }
     return (int)failed;
   }

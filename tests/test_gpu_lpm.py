@@ -218,3 +218,97 @@ def test_lpm_program_writes_refused_in_parallel(fresh_runtime):
     vm2 = dev.VM()
     vm2.load(a.assemble())
     assert vm2.exec_batch(dev.CTX_RAW, d, 64, 16, fixed_len=16) == 0
+
+
+def churn_prog(fd, per_unit=4):
+    """RAW units {u32 id}: per_unit times insert the /32 (id * 16 + i), then
+    delete it -- the trie's entries stay small while its nodes (logically
+    deleted, lpm_trie_map.cpp:490-541) keep growing."""
+    a = Asm().ldx(4, 6, 1, 0).alu64("lsh", 6, 4).mov64(7, 0)
+    a.label("loop")
+    a.st(4, 10, -8, 32).mov64(2, "r6").alu64("add", 2, "r7").stx(4, 10, -4, "r2").st(4, 10, -12, 1)
+    a.ld_map_fd(1, fd).mov64(2, "r10").add64(2, -8).mov64(3, "r10").add64(3, -12).mov64(4, 0).call(2)
+    a.ld_map_fd(1, fd).mov64(2, "r10").add64(2, -8).call(3)
+    a.add64(7, 1).jmp("jlt", 7, per_unit, "loop")
+    a.mov64(0, 0).exit()
+    return a.assemble()
+
+
+def test_lpm_device_pool_exhausted_fails_the_batch(fresh_oracle, fresh_runtime):
+    """An ORDERED batch whose program-side updates outgrow the replica's node
+    pool (sized before the launch for two nodes per update site and unit)
+    fails with an error naming the trie, where the reference's heap would
+    have grown; the host keeps the trie as it was before the batch (ADVICE
+    r03).  A batch within the pool gives the oracle's trie."""
+    po, dev = fresh_oracle, fresh_runtime
+    (om,), (dm,) = make_maps([(LPM, 8, 4, 16)], po, dev)
+    for m in (om, dm):
+        m.update(k4(8, "10.0.0.0"), struct.pack("<I", 7))
+    code = churn_prog(dm.fd, per_unit=1)   # two new nodes per unit at most: the pool holds them
+    vm = dev.VM()
+    vm.load(code)
+    small = np.arange(16, dtype=np.uint32).reshape(16, 1).view(np.uint8)
+    d = dev.DeviceBuffer.from_array(np.ascontiguousarray(small))
+    assert vm.exec_batch(dev.CTX_RAW, d, 16, 4, fixed_len=4, flags=dev.BATCH_SYNC | dev.BATCH_ORDERED) == 0
+    ovm = po.OracleVM()
+    ovm.load(code)
+    ovm.run_raw(np.ascontiguousarray(small).copy(), 4)
+    assert dm.count() == om.count() == 1 and dm.lookup(k4(8, "10.0.0.0")) == struct.pack("<I", 7)
+    n = 4096
+    big = np.arange(n, dtype=np.uint32).reshape(n, 1).view(np.uint8) + 0   # ids 0..4095: fresh /32s
+    d2 = dev.DeviceBuffer.from_array(np.ascontiguousarray(big))
+    vm4 = dev.VM()
+    vm4.load(churn_prog(dm.fd, per_unit=4))  # four inserts per unit behind one update site
+    with pytest.raises(dev.EbpfError, match=r"LPM_TRIE map fd %d: .*node pool" % dm.fd):
+        vm4.exec_batch(dev.CTX_RAW, d2, n, 4, fixed_len=4, flags=dev.BATCH_SYNC | dev.BATCH_ORDERED)
+    assert dm.count() == 1 and dm.lookup(k4(8, "10.0.0.0")) == struct.pack("<I", 7)
+    assert dm.lookup(k4(32, "0.0.1.0")) is None
+
+
+def test_lpm_writer_and_reader_on_two_streams(fresh_oracle, fresh_runtime):
+    """An ORDERED batch writing routes on one stream and a parallel routing
+    batch on another, launched back to back without waiting: the reader sees
+    every route the writer added (the second launch waits for the device),
+    as the serial order writer-then-reader gives."""
+    po, dev = fresh_oracle, fresh_runtime
+    L = dev.lib()
+    (om,), (dm,) = make_maps([(LPM, 8, 4, 4096)], po, dev)
+    rng = np.random.default_rng(21)
+    n = 2000
+    units = np.zeros((n, 16), np.uint8)
+    w = units.view(np.uint32)
+    plens = rng.choice([8, 16, 24, 32], n)
+    nets = rng.integers(0, 1 << 32, n, dtype=np.uint64) & ((np.uint64(0xFFFFFFFF) << (np.uint64(32) - plens.astype(np.uint64))) & np.uint64(0xFFFFFFFF))
+    w[:, 0] = 1                                                  # update, flags ANY
+    w[:, 1] = plens
+    units[:, 8:12] = nets.astype(np.uint32).astype(">u4").view(np.uint8).reshape(n, 4)
+    w[:, 3] = rng.integers(1, 4, n)                              # DROP / PASS / TX
+    wcode = learn_prog(dm.fd)
+    rcode = route_prog(dm.fd)
+    npk = 1 << 16
+    pk = gen.xdp_packets(npk, seed=22)
+    pk[:, 12:14] = [0x08, 0x00]
+    pk[: npk // 2, 30:34] = units[rng.integers(0, n, npk // 2), 8:12]
+    ow = po.OracleVM()
+    ow.load(wcode)
+    ow.run_raw(units.copy(), 16)
+    orr = po.OracleVM()
+    orr.load(rcode)
+    want = orr.run_xdp(pk.copy(), fixed_len=64)
+    vw, vr = dev.VM(), dev.VM()
+    vw.load(wcode)
+    vr.load(rcode)
+    s1, s2 = L.bpftime_amd_stream_create(), L.bpftime_amd_stream_create()
+    try:
+        du = dev.DeviceBuffer.from_array(units)
+        dp = dev.DeviceBuffer.from_array(pk)
+        dv = dev.DeviceBuffer(4 * npk)
+        vw.exec_batch(dev.CTX_RAW, du, n, 16, fixed_len=16, flags=dev.BATCH_ORDERED, stream=s1)
+        vr.exec_batch(dev.CTX_XDP, dp, npk, 64, fixed_len=64, verdicts=dv, flags=0, stream=s2)
+        L.bpftime_amd_stream_sync(s2)
+        np.testing.assert_array_equal(dv.download(np.uint32), want)
+        assert dm.count() == om.count()
+    finally:
+        L.bpftime_amd_sync()
+        L.bpftime_amd_stream_destroy(s1)
+        L.bpftime_amd_stream_destroy(s2)

@@ -71,8 +71,8 @@ def test_oracle_ringbuf_rules(fresh_oracle):
 @pytest.mark.parametrize("size,frac", [(1 << 20, None), (4096, 0), (1 << 26, None)])
 def test_device_ringbuf_sampler(fresh_oracle, fresh_runtime, size, frac):
     """(1 << 26: a ring large enough for block staging, dev_helpers.hpp
-    RbStage: records reach the ring through per-block chunks whose unused
-    tails are DISCARD records the consumer skips)"""
+    RbStage: records reach the ring when their block ends, in the bytes it
+    reserves for exactly them)"""
     po, dev = fresh_oracle, fresh_runtime
     dm = dev.Map(RB, 0, 0, size)
     om = po.OracleMap(RB, 0, 0, size, fd=dm.fd)
@@ -252,13 +252,11 @@ def test_device_ringbuf_fills_within_launch(fresh_oracle, fresh_runtime, ordered
 @pytest.mark.gpu
 def test_device_ringbuf_staged_ring_fills_within_launch(fresh_oracle, fresh_runtime):
     """A 64 MiB ring (large enough for block staging, dev_helpers.hpp RbStage)
-    filled part way through one parallel launch.  Staging stops once the
-    ring is within kRbSlack (32 MiB) of full, and the chunks reserved before
-    that may end with DISCARD tails the reference would have filled, so the
-    accepted count can fall short of the reference's by at most one chunk
-    (2 KiB) per block of the launch -- the documented difference of staged
-    rings; every accepted record is delivered and the verdicts
-    agree with the records."""
+    filled part way through one parallel launch: staged blocks reserve
+    exactly the bytes they used when they end and no ring byte is wasted, so
+    the ring accepts exactly what the reference's serial reservations
+    accept, room / record size (ringbuf_map.cpp:262-295); every accepted
+    record is delivered and the verdicts agree with the records."""
     po, dev = fresh_oracle, fresh_runtime
     size = 1 << 26
     dm = dev.Map(RB, 0, 0, size, fd=7)
@@ -275,4 +273,4 @@ def test_device_ringbuf_staged_ring_fills_within_launch(fresh_oracle, fresh_runt
     fit = size // 24
     ok = int((got == 2).sum())
     assert ok == len(drecs) and ok + int((got == 1).sum()) == n
-    assert fit - (4096 * 2048) // 24 <= ok <= fit
+    assert ok == fit
