@@ -13,9 +13,10 @@ never touches the GPU).  Three legs, SURVEY.md §8d:
 each worker over its own contiguous shard of the stream with private map
 copies, their map totals checked (the harness shape of
 tools/bpftimetool/main.cpp:42-58, steady clock around the packet loop only).
-Prints one JSON object: the nproc leg as value/cores (with the cgroup's CPU
-quota and the cores the workers kept busy on average, which a quota below
-nproc caps), the 16-core leg as cores_16, the 1-core leg as single_core.
+Prints one JSON object: the stronger of the 16-process and nproc legs as
+value/cores (the nproc leg's width is capped by a cgroup CPU quota below
+nproc: the GPU box has 256 cores in the affinity under a 16-CPU quota), both
+legs as cores_16 / cores_all, the 1-core leg as single_core.
 """
 import argparse
 import json
@@ -243,17 +244,26 @@ def main():
         vn, loopn, walln, okn, effn = v16, loop16, wall16, ok16, eff16
     ok = ok1 and ok16 and okn
     quota = cpu_quota()
+    # value: the stronger multi-process leg.  On the GPU box the affinity
+    # holds 256 cores under a 16-CPU cgroup quota, where the nproc leg keeps
+    # only ~15 cores busy and reports less than the 16-process leg (VERDICT
+    # r03); on an unthrottled host the nproc leg is the wider one
+    best16 = v16 >= vn
     out = {
-        "value": round(vn, 3), "unit": unit, "cores": nall, "kind": "port",
-        "sample": "%s: %d oracle processes pinned one per core (every core in this process's affinity; "
-                  "os.cpu_count() %d, cgroup CPU quota %s), each over its own contiguous 2^%d-unit shard of the "
-                  "same stream with private maps (%.1f s loops, %.1f s wall, %s cores busy on average, map totals "
-                  "%s), cpu %s" % (args.workload, nall, os.cpu_count() or 0, quota, bits, loopn, walln, effn,
-                                   "ok" if ok else "MISMATCH", cpu_model()),
-        "nproc": os.cpu_count(), "affinity_cores": len(cores), "cpu_quota_cores": quota, "effective_cores": effn,
+        "value": round(v16 if best16 else vn, 3), "unit": unit, "cores": n16 if best16 else nall, "kind": "port",
+        "sample": "%s: the stronger of two legs of oracle processes pinned one per core, each over its own "
+                  "contiguous 2^%d-unit shard of the same stream with private maps: %d processes (%.1f Munits/s) and "
+                  "%d processes = every core in this process's affinity (%.1f Munits/s; os.cpu_count() %d, cgroup "
+                  "CPU quota %s, %s cores busy on average); map totals %s; cpu %s"
+                  % (args.workload, bits, n16, v16, nall, vn, os.cpu_count() or 0, quota, effn,
+                     "ok" if ok else "MISMATCH", cpu_model()),
+        "nproc": os.cpu_count(), "affinity_cores": len(cores), "cpu_quota_cores": quota,
         "cores_16": {"value": round(v16, 3), "unit": unit, "cores": n16, "effective_cores": eff16,
                      "sample": "%d pinned oracle processes (the GPU box's CPU share per GPU), %.1f s loops"
                                % (n16, loop16)},
+        "cores_all": {"value": round(vn, 3), "unit": unit, "cores": nall, "effective_cores": effn,
+                      "sample": "one pinned oracle process per core in the affinity, %.1f s loops, %.1f s wall"
+                                % (loopn, walln)},
         "single_core": {"value": round(done1 / secs1 / 1e6, 3), "unit": unit, "cores": 1,
                         "sample": "1 oracle thread pinned to core %d, %.1f s" % (cores[0], secs1)},
         "ok": ok,
