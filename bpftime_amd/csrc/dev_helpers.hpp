@@ -145,12 +145,23 @@ __device__ __forceinline__ uint64_t ald64(uint64_t a) {
 // compare-and-swap on its state -- publish key and value, then the index
 // entry.  Never waits on another lane: a lane of the same wave that waits on
 // the reservation re-reads it on its next loop trip (hash_find_ix).
+#ifdef BPFTIME_AMD_INSERT_STATS
+// (experiment build only: insert-path counters, tools/insert_stats.py)
+__device__ unsigned long long g_istats[8];
+#define ISTAT(i, v) atomicAdd(&g_istats[i], (unsigned long long)(v))
+#define ISTAT_MAX(i, v) atomicMax(&g_istats[i], (unsigned long long)(v))
+#else
+#define ISTAT(i, v) ((void)0)
+#define ISTAT_MAX(i, v) ((void)0)
+#endif
 __device__ uint64_t ix_insert(const DMap &m, uint64_t key, uint64_t h, uint64_t ea, uint64_t init,
                               uint32_t init_bytes, bool *inserted, uint64_t part, uint32_t part_off,
                               uint32_t part_bytes) {
   const uint64_t nb = m.nbuckets, bm = ix_bitmap(m.ix, m.ix_mask);
   uint64_t b = h % nb, left = nb;
+  uint32_t words = 0;
   while (left) {
+    words++;
     const uint64_t w = b >> 6, o = b & 63;
     uint64_t span = 64 - o;
     if (span > left) span = left;
@@ -195,8 +206,12 @@ __device__ uint64_t ix_insert(const DMap &m, uint64_t key, uint64_t h, uint64_t 
       __hip_atomic_store(G32(s), ST_FILLED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(G32(ea), (uint32_t)b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       *inserted = true;
+      ISTAT(0, 1);
+      ISTAT(1, words);
+      ISTAT_MAX(4, words);
       return s;
     }
+    ISTAT(2, 1);
     // claimed by another insert: go on after it
     b = b + 1 == nb ? 0 : b + 1;
     left--;
@@ -222,7 +237,9 @@ __device__ uint64_t hash_find_ix(const DMap &m, uint64_t key, uint64_t h, bool i
                                  uint32_t init_bytes, bool *inserted, uint64_t part, uint32_t part_off,
                                  uint32_t part_bytes) {
   uint32_t p = ix_pos(h, m.ix_mask), spins = 0;
+  ISTAT(insert ? 5 : 6, 1);
   for (uint32_t t = 0; t <= m.ix_mask;) {
+    ISTAT(7, 1);
     const uint64_t ea = m.ix + 4ull * p;
     uint32_t e = ald32(ea);
     // an empty entry is confirmed at the coherence point; a reservation is
@@ -239,6 +256,7 @@ __device__ uint64_t hash_find_ix(const DMap &m, uint64_t key, uint64_t h, bool i
     }
     if (e == kIxRes) {
       if (insert) {  // maybe this key's: read the entry again on the next trip
+        ISTAT(3, 1);
         if (++spins > (1u << 22)) return 0;  // bounded: never hang the GPU
         __builtin_amdgcn_s_sleep(1);
         continue;
@@ -755,11 +773,18 @@ constexpr uint64_t kRbSlack = kRbMaxWaves * kRbWaveMax;    // 32 MiB
 // Consumers see the same records in another parallel order.
 // (sizes: common.hpp kRbStage*)
 constexpr uint32_t kRbClosed = 0x80000000u;  // RbStage::used: the block's staging is closed
+struct RbLds {       // LDS: the block's staging counters
+  uint32_t used;     // bytes claimed (| kRbClosed)
+  uint32_t nrec;     // records
+  int32_t fd;        // the ring of the block's promise (-1 undecided, -3 deciding, -2 none)
+  uint32_t pad;
+  uint64_t base;     // the ring position of the block's records (set when it closes)
+};
+// (two pointers, passed by value: a struct the helpers take by reference
+// lives in scratch, written by every lane of every launch)
 struct RbStage {
   uint8_t *buf = nullptr;  // this block's area: records, then u32 offsets (nullptr: no staging)
-  uint32_t *used = nullptr, *end = nullptr, *nrec = nullptr;  // LDS: bytes claimed (| kRbClosed), -, records
-  int32_t *fd = nullptr;   // LDS: the ring of the block's promise (-1 undecided, -3 deciding, -2 none)
-  uint64_t *base = nullptr;  // LDS: the ring position of the block's records (set when it closes)
+  RbLds *lds = nullptr;
 };
 
 // the ring's room for a reservation: capacity - (producer - consumer) -
@@ -776,16 +801,16 @@ __device__ __forceinline__ int64_t rb_room(const DMap &m, uint64_t *prod_out = n
 // path): no claim succeeds after this, the bytes claimed so far are
 // reserved in the ring now (rb_publish copies them there) and the promise
 // is returned.
-__device__ void rb_close(const DMap &m, const RbStage &st) {
-  if (!st.buf || *st.fd < 0) return;
-  const uint32_t u = __hip_atomic_fetch_or(st.used, kRbClosed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+__device__ void rb_close(const DMap &m, RbStage st) {
+  if (!st.buf || st.lds->fd < 0) return;
+  const uint32_t u = __hip_atomic_fetch_or(&st.lds->used, kRbClosed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (u & kRbClosed) return;  // (closed by another wave of the block)
-  *st.base = u ? __hip_atomic_fetch_add(G64(m.data + 128), (uint64_t)u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+  st.lds->base = u ? __hip_atomic_fetch_add(G64(m.data + 128), (uint64_t)u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                : 0;
   __hip_atomic_fetch_add(G64(m.data + 192), (uint64_t)0 - kRbStageRec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ uint64_t rb_cas_reserve(const DMap &m, uint64_t total, const RbStage &st, int32_t fd) {
+__device__ __forceinline__ uint64_t rb_cas_reserve(const DMap &m, uint64_t total, RbStage st, int32_t fd) {
   // returns the old producer position, or ~0 if total does not fit.  The
   // loop ends by a successful CAS or a failed room check, as the
   // reference's spin-locked reserve does: the consumer position does not
@@ -802,7 +827,7 @@ __device__ __forceinline__ uint64_t rb_cas_reserve(const DMap &m, uint64_t total
     if (room < (int64_t)total) {
       const uint64_t prom = __hip_atomic_load(G64(m.data + 192), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (!prom) return ~0ull;  // full, with nothing promised: the serial answer
-      if (*st.fd == fd) rb_close(m, st);
+      if (st.lds->fd == fd) rb_close(m, st);
     } else {
       unsigned long long e = p;
       if (__hip_atomic_compare_exchange_strong(G64(m.data + 128), &e, p + total, __ATOMIC_RELAXED,
@@ -817,7 +842,7 @@ __device__ __forceinline__ uint64_t rb_cas_reserve(const DMap &m, uint64_t total
   return ~0ull;
 }
 
-__device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size, const RbStage &st) {
+__device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size, RbStage st) {
   const bool ok = fd < kMaxFds && maps[fd < kMaxFds ? fd : 0].type == MT_RINGBUF &&
                   !(size & (RB_BUSY | RB_DISCARD));
   const DMap m = maps[ok ? fd : 0];
@@ -839,11 +864,11 @@ __device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size, con
     if (st.buf) {
       // block staging (RbStage): the block's first reservation reserves
       // its chunk (a wave arriving while another decides reserves directly)
-      int32_t sfd = __shfl(__hip_atomic_load(st.fd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), leader);
+      int32_t sfd = __shfl(__hip_atomic_load(&st.lds->fd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), leader);
       if (sfd == -1) {
         if (me == leader) {
           int32_t cur = -1;
-          if (__hip_atomic_compare_exchange_strong(st.fd, &cur, -3, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+          if (__hip_atomic_compare_exchange_strong(&st.lds->fd, &cur, -3, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_WORKGROUP)) {
             int32_t got = -2;
             // the fast path's condition (below), for a block's budget
@@ -852,7 +877,7 @@ __device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size, con
                                      __HIP_MEMORY_SCOPE_AGENT);
               got = (int32_t)fd;
             }
-            __hip_atomic_store(st.fd, got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(&st.lds->fd, got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             cur = got;
           }
           sfd = cur;
@@ -865,16 +890,16 @@ __device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size, con
         if (me == leader) {
           // claim sum bytes of the budget (a compare-and-swap, so the used
           // count is exactly the claimed bytes: rb_close reserves them)
-          uint32_t u = __hip_atomic_load(st.used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          uint32_t u = __hip_atomic_load(&st.lds->used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           for (;;) {
             if ((u & kRbClosed) || (uint64_t)u + sum > kRbStageRec) {
               base = ~0u;  // closed, or the budget is spent: direct
               break;
             }
-            if (__hip_atomic_compare_exchange_strong(st.used, &u, u + (uint32_t)sum, __ATOMIC_RELAXED,
+            if (__hip_atomic_compare_exchange_strong(&st.lds->used, &u, u + (uint32_t)sum, __ATOMIC_RELAXED,
                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
               base = u;  // (then the record slots fit too: >= 8 B each)
-              rbase = __hip_atomic_fetch_add(st.nrec, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              rbase = __hip_atomic_fetch_add(&st.lds->nrec, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
               break;
             }
           }
@@ -925,7 +950,7 @@ __device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size, con
 // the position area, fd 0, as the reference reads the zeroed end of its
 // producer page.  bpf_ringbuf_output passes the fd it reserved from
 // (bpf_helper.cpp:460-465).
-__device__ void rb_submit(const DMap *maps, uint64_t sample, bool discard, const RbStage &st, int32_t fd = -1) {
+__device__ void rb_submit(const DMap *maps, uint64_t sample, bool discard, RbStage st, int32_t fd = -1) {
   if (st.buf && sample >= (uint64_t)(uintptr_t)st.buf + RB_HDR &&
       sample < (uint64_t)(uintptr_t)st.buf + kRbStageRec) {  // a staged record: published at block end
     uint32_t *h = (uint32_t *)(uintptr_t)(sample - RB_HDR);
@@ -945,7 +970,7 @@ __device__ void rb_submit(const DMap *maps, uint64_t sample, bool discard, const
                         __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ uint64_t rb_output(const DMap *maps, uint64_t fd, uint64_t data, uint64_t size, const RbStage &st) {
+__device__ uint64_t rb_output(const DMap *maps, uint64_t fd, uint64_t data, uint64_t size, RbStage st) {
   const uint64_t buf = rb_reserve(maps, fd, size, st);
   if (!buf) return (uint64_t)-1;
   copy_bytes(buf, data, (uint32_t)size);
@@ -958,20 +983,21 @@ __device__ uint64_t rb_output(const DMap *maps, uint64_t fd, uint64_t data, uint
 // bytes the block used (unless a wave closed the block's staging, which
 // reserved them then) and returns the block's promise; then one thread per
 // record copies it, with the flags submit / discard gave it.
-__device__ void rb_publish(const DMap *maps, const RbStage &st, uint32_t tid, uint32_t nthreads) {
-  const int32_t fd = *st.fd;
-  if (!st.buf || fd < 0) return;
+__device__ void rb_publish(const DMap *maps, RbStage st, uint32_t tid, uint32_t nthreads) {
+  if (!st.buf) return;
+  const int32_t fd = st.lds->fd;
+  if (fd < 0) return;
   const DMap m = maps[fd];
-  const uint32_t used = *st.used & ~kRbClosed;
-  if (tid == 0 && !(*st.used & kRbClosed)) {
-    *st.base = used ? __hip_atomic_fetch_add(G64(m.data + 128), (uint64_t)used, __ATOMIC_RELAXED,
+  const uint32_t used = st.lds->used & ~kRbClosed;
+  if (tid == 0 && !(st.lds->used & kRbClosed)) {
+    st.lds->base = used ? __hip_atomic_fetch_add(G64(m.data + 128), (uint64_t)used, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT)
                     : 0;
     __hip_atomic_fetch_add(G64(m.data + 192), (uint64_t)0 - kRbStageRec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  const uint64_t base = *st.base, mask = m.max_entries - 1, d = m.data + 256;
-  const uint32_t n = min(*st.nrec, kRbStageMaxRec);
+  const uint64_t base = st.lds->base, mask = m.max_entries - 1, d = m.data + 256;
+  const uint32_t n = min(st.lds->nrec, kRbStageMaxRec);
   const uint32_t *offs = (const uint32_t *)(st.buf + kRbStageRec);
   for (uint32_t i = tid; i < n; i += nthreads) {
     const uint32_t off = offs[i];

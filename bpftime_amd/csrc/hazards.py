@@ -143,6 +143,8 @@ def parse(lines: List[str]) -> Tuple[List[Insn], Dict[str, int]]:
         if t.endswith(":"):
             labels[t[:-1]] = len(insns)
             continue
+        if t.startswith("."):  # a directive (.p2align: padding counts as no wait state)
+            continue
         if t.startswith("s_set_gpr_idx_on"):
             modes = t[t.index("gpr_idx(") + 8:t.index(")", t.index("gpr_idx("))]
             idx_dst, idx_src = "DST" in modes, "SRC0" in modes or "SRC1" in modes

@@ -631,21 +631,15 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   for (uint32_t i = tid; i < 5 * p.comb_entries; i += BS) comb[i] = 0;
   for (uint32_t i = tid; i < lcache_bytes(p.lcache) / 4; i += BS) lcache[i] = 0;
   // ring-buffer staging (dev_helpers.hpp RbStage): LDS counters of the block
-  __shared__ uint32_t rb_used, rb_end, rb_nrec;
-  __shared__ int32_t rb_fd;
-  __shared__ uint64_t rb_base;
+  __shared__ RbLds rb_lds;
   if (tid == 0) {
-    rb_used = rb_end = rb_nrec = 0;
-    rb_fd = -1;
+    rb_lds.used = rb_lds.nrec = 0;
+    rb_lds.fd = -1;
   }
   RbStage rbs;
   if (p.rb_stage) {
     rbs.buf = p.rb_stage + (uint64_t)blockIdx.x * kRbStageBytes;
-    rbs.used = &rb_used;
-    rbs.end = &rb_end;
-    rbs.nrec = &rb_nrec;
-    rbs.fd = &rb_fd;
-    rbs.base = &rb_base;
+    rbs.lds = &rb_lds;
   }
   // counter v of the table (entry v / 4, counter v % 4 of its granule) as a
   // flush tag {address | (4-byte ? 1 : 0)} and delta
@@ -1350,3 +1344,14 @@ extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_l
 }
 
 }  // namespace bpftime_amd
+
+#ifdef BPFTIME_AMD_INSERT_STATS
+extern "C" int bpftime_amd_insert_stats(uint64_t *out) {
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpyFromSymbol(out, HIP_SYMBOL(bpftime_amd::g_istats), 64) != hipSuccess)
+    return -1;
+  static const uint64_t z[8] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(bpftime_amd::g_istats), z, 64) == hipSuccess ? 0 : -1;
+}
+#endif
+
