@@ -157,26 +157,46 @@ __device__ unsigned long long g_istats[8];
 __device__ uint64_t ix_insert(const DMap &m, uint64_t key, uint64_t h, uint64_t ea, uint64_t init,
                               uint32_t init_bytes, bool *inserted, uint64_t part, uint32_t part_off,
                               uint32_t part_bytes) {
-  const uint64_t nb = m.nbuckets, bm = ix_bitmap(m.ix, m.ix_mask);
+  const uint64_t nb = m.nbuckets, bm = ix_bitmap(m.ix, m.ix_mask), nw = (nb + 63) >> 6;
   uint64_t b = h % nb, left = nb;
   uint32_t words = 0;
   while (left) {
-    words++;
-    const uint64_t w = b >> 6, o = b & 63;
-    uint64_t span = 64 - o;
-    if (span > left) span = left;
-    if (span > nb - b) span = nb - b;
-    uint64_t freeb = ~ald64(bm + 8 * w) >> o;
-    if (span < 64) freeb &= (1ull << span) - 1;
-    if (!freeb) {
+    // the next kScan bitmap words at once (one memory round trip for 64 *
+    // kScan buckets: the late inserts of a nearly full table scan far), then
+    // the first clear bit in probe order
+    constexpr uint32_t kScan = 8;
+    uint64_t wv[kScan];
+    {
+      uint64_t w = b >> 6;
+#pragma unroll
+      for (uint32_t k = 0; k < kScan; k++) {
+        wv[k] = ald64(bm + 8 * w);
+        w = w + 1 == nw ? 0 : w + 1;
+      }
+    }
+    bool found = false;
+#pragma unroll
+    for (uint32_t k = 0; k < kScan; k++) {
+      if (!left) break;
+      words++;
+      const uint64_t o = b & 63;
+      uint64_t span = 64 - o;
+      if (span > left) span = left;
+      if (span > nb - b) span = nb - b;
+      uint64_t freeb = ~wv[k] >> o;
+      if (span < 64) freeb &= (1ull << span) - 1;
+      if (freeb) {
+        const uint64_t i = (uint64_t)__builtin_ctzll(freeb);
+        b += i;
+        left -= i;
+        found = true;
+        break;
+      }
       b += span;
       left -= span;
       if (b == nb) b = 0;
-      continue;
     }
-    const uint64_t i = (uint64_t)__builtin_ctzll(freeb);
-    b += i;
-    left -= i;
+    if (!found) continue;
     const uint64_t s = m.data + b * (uint64_t)m.slot_size;
     const uint64_t bit = 1ull << (b & 63);
     uint32_t prev = ST_EMPTY;

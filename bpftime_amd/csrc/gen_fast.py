@@ -99,14 +99,6 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # handler entries aligned to 2^HANDLER_ALIGN bytes (0: packed); 64-B entries
 # measured 0.4406 -> 0.4366 ms on the headline (same box, best of 4)
 HANDLER_ALIGN = int(os.environ.get("BPFTIME_AMD_HANDLER_ALIGN", "6"))
-# a staged fresh unit also loads one dword of the lane's next chained unit
-# (build: the `pf` block) so that its window is in L2 when the chain reaches
-# it; that load is the newest memory operation of the unit's start, so the
-# staged handlers wait for their window with vmcnt(STAGE_WAIT) (loads return
-# in order: with <= 1 outstanding the window loads, issued before the
-# prefetch, have landed)
-PREFETCH = int(os.environ.get("BPFTIME_AMD_PREFETCH", "0"))
-STAGE_WAIT = f"s_waitcnt vmcnt({1 if PREFETCH else 0})"
 
 ALU_OPS = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "MOV", "LSH", "RSH", "ARSH"]
 JCC = ["EQ", "GT", "GE", "SET", "NE", "SGT", "SGE", "LT", "LE", "SLT", "SLE"]
@@ -550,7 +542,7 @@ class Gen:
 
     def staged_load(self, sz):
         """X = sz bytes at window offset s82 (zero-extended)."""
-        self.e(STAGE_WAIT,                                 # staging loads landed
+        self.e("s_waitcnt vmcnt(0)",                       # staging loads landed
                "s_lshr_b32 s70, s82, 2", "s_and_b32 s71, s82, 3", "s_lshl_b32 s71, s71, 3")
         self.idx("s70", "SRC0")
         self.e(f"v_mov_b32 v44, v{STG}", f"v_mov_b32 v45, v{STG + 1}", f"v_mov_b32 v46, v{STG + 2}")
@@ -571,7 +563,7 @@ class Gen:
             self.e("s_cmp_lg_u32 s71, 0", f"s_cbranch_scc1 {on_unaligned}")
         else:
             self.e(f"s_add_u32 s69, s71, {sz}", "s_cmp_gt_u32 s69, 4", f"s_cbranch_scc1 {on_unaligned}")
-        self.e(STAGE_WAIT, "s_lshr_b32 s70, s82, 2")
+        self.e("s_waitcnt vmcnt(0)", "s_lshr_b32 s70, s82, 2")
         if sz == 8:
             self.idx("s70", "DST")
             self.e(f"v_mov_b32 v{STG}, v44", f"v_mov_b32 v{STG + 1}, v45")
@@ -817,7 +809,7 @@ class Gen:
     def ldxs(self, name):
         fb = self.label("lfb")
         sz = int(name[4])
-        self.e("s_cmp_eq_u32 s80, 0", f"s_cbranch_scc1 {fb}", STAGE_WAIT)
+        self.e("s_cmp_eq_u32 s80, 0", f"s_cbranch_scc1 {fb}", "s_waitcnt vmcnt(0)")
         self.idx("s42", "SRC0")
         n = {"LDXS1": 1, "LDXS2": 1, "LDXS4": 1, "LDXS2X": 2, "LDXS4X": 2, "LDXS8A": 2, "LDXS8U": 3}[name]
         for j in range(n):
@@ -843,7 +835,7 @@ class Gen:
         imm = name.startswith("STS")
         sz = int(name[-1])
         fb = self.label("sfb")
-        self.e("s_cmp_eq_u32 s80, 0", f"s_cbranch_scc1 {fb}", STAGE_WAIT)
+        self.e("s_cmp_eq_u32 s80, 0", f"s_cbranch_scc1 {fb}", "s_waitcnt vmcnt(0)")
         if not imm:
             (self.rd if sz == 8 else self.rd_lo)("s45", 44)
         elif sz == 8:
@@ -1950,21 +1942,21 @@ class Gen:
         # lanes (nr = bytes 8..15, syscall_trace_attach_impl.cpp:25) finish
         # with r0 = 0 here, from the staged bytes, instead of a separate load
         # of nr before the staging loads (chain_routine: unstaged units)
-        fchk, pf = self.label("fchk"), self.label("pf")
+        fchk = self.label("fchk")
         e(f"{filt}:",
           # a chained unit's length load (chain_routine) completes with the
           # staging loads: one memory round trip per unit instead of two
           "s_bitcmp1_b32 %[entry], 5", f"s_cbranch_scc0 {fchk}",
           "s_waitcnt vmcnt(0)",
           f"{fchk}:",
-          "s_bitcmp1_b32 %[entry], 6", f"s_cbranch_scc0 {pf}",
+          "s_bitcmp1_b32 %[entry], 6", f"s_cbranch_scc0 {loaded}",
           "s_waitcnt vmcnt(0)",
           f"v_cmp_eq_u64 s[54:55], 60, v[{STG + 2}:{STG + 3}]",
           "s_movk_i32 s70, 0xe7", "s_mov_b32 s71, 0",
           f"v_cmp_eq_u64 s[56:57], s[70:71], v[{STG + 2}:{STG + 3}]",
           "s_or_b64 s[54:55], s[54:55], s[56:57]",
           "s_and_b64 s[54:55], s[54:55], exec",
-          f"s_cbranch_scc0 {pf}",
+          f"s_cbranch_scc0 {loaded}",
           "s_andn2_b64 s[60:61], exec, s[54:55]",
           "s_mov_b64 exec, s[54:55]",
           "v_mov_b32 v56, 0", "v_mov_b32 v57, 0",
@@ -1975,20 +1967,8 @@ class Gen:
           "global_store_dwordx2 %[raddr], v[56:57], off",
           f"{fsr}:",
           "s_mov_b64 exec, s[60:61]",
-          f"s_cbranch_execnz {pf}",
+          f"s_cbranch_execnz {loaded}",
           "s_mov_b32 s84, 0", f"s_branch {L('chain')}")                  # every lane an exit record
-        if PREFETCH:
-            # the next chained unit's first line (this unit's own when the
-            # chain ends here): v101 is never read for its value (the staged
-            # window's read-past-end register); the block's exit waits for it
-            e(f"{pf}:",
-              "s_mov_b32 s71, 0",
-              "s_cmp_eq_u32 %[chain], 0",
-              "s_cselect_b32 s70, 0, %[sstep]",
-              "v_lshl_add_u64 v[56:57], v[52:53], 0, s[70:71]",
-              "global_load_dword v101, v[56:57], off")
-        else:
-            e(f"{pf}:")
         e(f"{loaded}:",
           "s_getpc_b64 s[50:51]",          # = address of the s_branch below
           f"s_branch {L('start')}")
