@@ -1,0 +1,14 @@
+#!/bin/bash
+# one build, several environments, failures reported and skipped:
+#   bash tools/ab_env_k.sh build workload "ENV1" "ENV2" ...
+set -u
+v=$1; w=$2; shift 2
+for round in 1 2; do
+  for e in "$@"; do
+    if env $e BPFTIME_AMD_LIB=$PWD/ab/$v.so timeout -k 10 300 python bench.py --workload $w --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/abe.json 2> gpurun_out/abe.err; then
+      python -c "import json;d=json.load(open('gpurun_out/abe.json'));print('$round', '$e', '$w', d['value'], d['ms_per_step'], d.get('cold', {}).get('ms'), d.get('dbg_lcache'))"
+    else
+      echo "$round $e $w FAILED: $(tail -1 gpurun_out/abe.err)"
+    fi
+  done
+done
