@@ -847,7 +847,7 @@ __device__ __forceinline__ uint64_t rb_cas_reserve(const DMap &m, uint64_t total
     if (room < (int64_t)total) {
       const uint64_t prom = __hip_atomic_load(G64(m.data + 192), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (!prom) return ~0ull;  // full, with nothing promised: the serial answer
-      if (st.lds->fd == fd) rb_close(m, st);
+      if (st.buf && st.lds->fd == fd) rb_close(m, st);  // (a launch without staging waits only)
     } else {
       unsigned long long e = p;
       if (__hip_atomic_compare_exchange_strong(G64(m.data + 128), &e, p + total, __ATOMIC_RELAXED,
