@@ -57,6 +57,10 @@ def test_miss_log_store_without_its_nop_is_flagged():
     (["v_readfirstlane_b32 s52, v41", "s_nop 4", "global_load_dword v42, v41, s[52:53]"], None),
     (["v_cmp_eq_u32_e64 s[54:55], v41, 0", "global_atomic_add v41, v42, s[54:55]"], "sgpr-vmem"),
     (["v_readfirstlane_b32 s69, v41", "v_readlane_b32 s70, v42, s69"], "sgpr-lane"),
+    # alignment padding may be empty: a directive counts as no wait state
+    (["global_store_dwordx4 v42, v[56:59], off", ".p2align 6", ".Lh:", "v_mov_b32 v57, 0"], "store-data"),
+    (["v_readfirstlane_b32 s52, v41", "s_nop 3", ".p2align 6", "global_load_dword v42, v41, s[52:53]"],
+     "sgpr-vmem"),
     (["v_readfirstlane_b32 s69, v41", "s_nop 3", "v_readlane_b32 s70, v42, s69"], None),
     (["v_rcp_f64 v[44:45], v[46:47]", "v_mul_f64 v[48:49], v[44:45], v[50:51]"], "trans"),
     (["v_rcp_f64 v[44:45], v[46:47]", "s_nop 0", "v_mul_f64 v[48:49], v[44:45], v[50:51]"], None),
