@@ -856,9 +856,14 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     // group at the lowest pc runs as a uniform wave while the other lanes
     // are parked at their pcs (c.lpc), until the group exits, splits or
     // reaches a tail call / return; then the lowest group runs next, and
-    // groups that meet at one pc run together again.  (BPFTIME_AMD_DBG bit 2:
-    // the C++ divergent loop instead.)
-    const bool groups = IMAGE && p.fast_div && !(p.dbg & 4);
+    // groups that meet at one pc run together again: tail-call images, and
+    // the XDP launches with the register copy in global memory (G: hash
+    // tables), where a hash insert's lanes run their insert path in asm
+    // while the lanes that found their key wait (flow-hash's cold launch
+    // 8.0 -> 5.0 ms; for the syscall kind the extra live state costs its
+    // steady state 7 %, so it keeps the C++ divergent loop).
+    // (BPFTIME_AMD_DBG bit 2: the C++ divergent loop instead.)
+    const bool groups = (IMAGE || (G && KIND == CTX_XDP)) && p.fast_div && !(p.dbg & 4);
     bool parked = false;
     auto unpark = [&]() {
       c.alive = c.alive || parked;
@@ -876,7 +881,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     };
     while (__ballot(c.alive || parked) != 0) {
       uint32_t r;
-      if (IMAGE && uni && __ballot(c.alive) == 0) {  // the running group died (a helper error): the parked lanes go on
+      if (groups && uni && __ballot(c.alive) == 0) {  // the running group died (a helper error): the parked lanes go on
         unpark();
         continue;
       }
