@@ -1596,12 +1596,13 @@ class Gen:
         else:
             self.e(f"v_mad_u64_u32 v[58:59], s[62:63], {w}, s76, v[56:57]")
 
-    def stack_words(self, store):
-        """The stack words of the save mask (s85 & 0xffff; stack bytes
-        s85 >> 16) to (store) or from the frame (words 20..)."""
+    def stack_words(self, store, mask=None):
+        """The stack words of the save mask (s85 & 0xffff, or the SGPR
+        `mask`; stack bytes s85 >> 16) to (store) or from the frame (words
+        20..)."""
         loop, done = self.label("tsl"), self.label("tsd")
         self.e("s_lshr_b32 s69, s85, 16", "v_subrev_u32 v41, s69, %[stklo]",   # the stack bottom
-               "s_and_b32 s70, s85, 0xffff",
+               f"s_mov_b32 s70, {mask}" if mask else "s_and_b32 s70, s85, 0xffff",
                f"{loop}:", "s_cmp_eq_u32 s70, 0", f"s_cbranch_scc1 {done}",
                "s_ff1_i32_b32 s69, s70", "s_bitset0_b32 s70, s69",
                "s_lshl_b32 s71, s69, 3", "v_add_u32 v43, s71, v41",
@@ -1767,13 +1768,46 @@ class Gen:
             self.e(f"global_load_dwordx2 v[{R0 + 2 * r}:{R0 + 2 * r + 1}], v[58:59], off", f"{skip}:")
         self.e("s_mov_b64 exec, s[60:61]",
                f"v_mov_b32 v{R0 + 20}, %[r10lo]", f"v_mov_b32 v{R0 + 21}, %[r10hi]")
-        for k in range(6):
-            skip = self.label("trc")
-            self.e(f"s_bitcmp1_b32 s68, {k}", f"s_cbranch_scc0 {skip}")
-            self.word_addr(12 + k)
-            self.e("global_load_dwordx2 v[42:43], v[58:59], off", "s_waitcnt vmcnt(0)",
-                   f"ds_write_b64 %[r1lo], v[42:43] offset:{8 * k}", f"{skip}:")
-        self.stack_words(store=False)
+        # the first saved ctx word and the first saved stack word load with
+        # the registers (one memory round trip for the usual frame: a live
+        # register, a ctx field, a stack word); the others one at a time.
+        # s64 / s66: ctx / stack words left; s65: the first ctx word's byte
+        # offset, s67: the first stack word's index (-1: none)
+        c0, s0, cw, sw = self.label("trc0"), self.label("trs0"), self.label("trcw"), self.label("trsw")
+        self.e("s_and_b32 s64, s68, 0x3f", "s_mov_b32 s65, -1",
+               "s_cmp_eq_u32 s64, 0", f"s_cbranch_scc1 {c0}",
+               "s_ff1_i32_b32 s69, s64", "s_bitset0_b32 s64, s69",
+               "s_lshl_b32 s65, s69, 3",
+               "s_add_u32 s69, s69, 12", "s_mul_i32 s69, s69, s76",
+               "v_add_co_u32 v58, vcc, s69, v56", "v_addc_co_u32 v59, vcc, 0, v57, vcc",
+               "global_load_dwordx2 v[42:43], v[58:59], off",
+               f"{c0}:",
+               "s_and_b32 s66, s85, 0xffff", "s_mov_b32 s67, -1",
+               "s_cmp_eq_u32 s66, 0", f"s_cbranch_scc1 {s0}",
+               "s_ff1_i32_b32 s67, s66", "s_bitset0_b32 s66, s67",
+               "s_add_u32 s69, s67, 20", "s_mul_i32 s69, s69, s76",
+               "v_add_co_u32 v58, vcc, s69, v56", "v_addc_co_u32 v59, vcc, 0, v57, vcc",
+               "global_load_dwordx2 v[44:45], v[58:59], off",
+               f"{s0}:",
+               "s_waitcnt vmcnt(0)",
+               "s_cmp_lt_i32 s65, 0", f"s_cbranch_scc1 {cw}",
+               "v_add_u32 v41, s65, %[r1lo]", "ds_write_b64 v41, v[42:43]",
+               f"{cw}:",
+               "s_cmp_lt_i32 s67, 0", f"s_cbranch_scc1 {sw}",
+               "s_lshr_b32 s69, s85, 16", "v_subrev_u32 v41, s69, %[stklo]",  # the stack bottom
+               "s_lshl_b32 s69, s67, 3", "v_add_u32 v41, s69, v41",
+               "ds_write_b64 v41, v[44:45]",
+               f"{sw}:")
+        loop, done = self.label("trcl"), self.label("trcd")
+        self.e(f"{loop}:", "s_cmp_eq_u32 s64, 0", f"s_cbranch_scc1 {done}",
+               "s_ff1_i32_b32 s69, s64", "s_bitset0_b32 s64, s69",
+               "s_lshl_b32 s65, s69, 3",
+               "s_add_u32 s69, s69, 12", "s_mul_i32 s69, s69, s76",
+               "v_add_co_u32 v58, vcc, s69, v56", "v_addc_co_u32 v59, vcc, 0, v57, vcc",
+               "global_load_dwordx2 v[42:43], v[58:59], off", "s_waitcnt vmcnt(0)",
+               "v_add_u32 v41, s65, %[r1lo]", "ds_write_b64 v41, v[42:43]",
+               f"s_branch {loop}", f"{done}:")
+        self.stack_words(store=False, mask="s66")
         self.e("s_waitcnt vmcnt(0) lgkmcnt(0)")
         self.go_groups()
 

@@ -1,6 +1,7 @@
 #!/bin/bash
-# round-4 experiment batch: lane groups through the asm tier for XDP G launches
+# round-4 experiment batch: tail-call pops restore their first ctx and stack
+# words with the registers (one round trip); tail-call tests, A/B
 set -u
 mkdir -p gpurun_out
-WL="main flow-hash syscall-agg tail-call" ROUNDS=2 timeout -k 10 600 bash tools/ab.sh base grpX > gpurun_out/ab_grp.txt 2>&1 &&
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_suite.txt 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_tailcall.py tests/test_oracle_tailcall.py -x -q --timeout 120 --timeout-method thread > gpurun_out/tail_tests.txt 2>&1 &&
+WL="tail-call main" ROUNDS=3 timeout -k 10 400 bash tools/ab.sh grpX pop1 > gpurun_out/ab_pop.txt 2>&1
