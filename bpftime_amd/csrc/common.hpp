@@ -199,7 +199,10 @@ constexpr uint64_t kLpmFlatMinUnits = 1ull << 16;
 constexpr uint32_t kLpmPoolOut = 0x80000000u;
 
 // Ring-buffer staging per block (dev_helpers.hpp RbStage)
-constexpr uint32_t kRbStageRec = 2048;                                // record bytes (a ring chunk) per block
+// (8 KiB: a block at one wave per resident slot holds its units' samples;
+// ringbuf-sample 1.45 ms with 2 KiB at 4 waves per slot, 1.10 ms with 8 KiB
+// at one)
+constexpr uint32_t kRbStageRec = 8192;                                // record bytes (a ring budget) per block
 constexpr uint32_t kRbStageMaxRec = kRbStageRec / 8;                  // records per block (>= 8 B each)
 constexpr uint32_t kRbStageBytes = kRbStageRec + 4 * kRbStageMaxRec;  // + u32 record offsets
 

@@ -687,10 +687,10 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     // 61.0 B per packet at x 1 / 2 / 4 / 8; 0.467 / 0.479 / 0.496 / 0.484 ms;
     // lpm-route 0.467 / 0.479 / 0.506 ms at x 1 / 2 / 4); a combining table
     // is flushed once per block (flow-hash 0.60 -> 1.09 ms at x 4).  Ring
-    // staging keeps x 4: a block's 2-KiB ring chunk must hold the records of
-    // its units (ringbuf-sample 7.46 / 4.03 / 1.43 ms at x 1 / 2 / 4).
-    // BPFTIME_AMD_GRID_MULT overrides.
-    uint32_t mult = stage && !p.comb_entries ? 4 : 1;
+    // staging too, with an 8-KiB budget per block (common.hpp kRbStageRec;
+    // ringbuf-sample 1.10 / 1.21 / 1.47 ms at x 1 / 2 / 4; with the 2-KiB
+    // budget 7.46 / 4.03 / 1.43).  BPFTIME_AMD_GRID_MULT overrides.
+    uint32_t mult = 1;
     if (const char *g = getenv("BPFTIME_AMD_GRID_MULT"))
       if (atoi(g) > 0) mult = (uint32_t)atoi(g);
     uint64_t cap = (uint64_t)cus * (uint64_t)occ * mult;
