@@ -312,8 +312,11 @@ constexpr size_t kCuLds = 160 * 1024;  // LDS per CU (gfx950)
 // tenv; the asm finds them 48 B before the combining table), the combining
 // table (a u32 tag + a 16-byte delta granule per entry).
 // tenv: 8 u64 launch constants (tail calls, the register copy base, the
-// block's miss-log region and its capacity), then kMissParts u32 miss counters
-constexpr uint32_t kTenvBytes = 64 + 4 * kMissParts;  // gen_fast.py TENV
+// block's miss-log region and its capacity), then kMissParts u32 miss counters,
+// then the block's ring staging area (u64, 0 = none) and the LDS address of
+// its counters (dev_helpers.hpp RbLds; gen_fast.py call_rbout)
+constexpr uint32_t kTenvRb = 64 + 4 * kMissParts;     // (u64 index kTenvRb / 8)
+constexpr uint32_t kTenvBytes = kTenvRb + 16;          // gen_fast.py TENV
 // Hash-lookup cache of a block (programs whose hash lookups the loader marks
 // FW_LCACHE: no deletions): `sets` 2-way sets, the ways' 16-B keys
 // ([set][way]) then their u32 entries {(slot + 1) | fd << 22}, right below

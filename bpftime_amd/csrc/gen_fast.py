@@ -115,7 +115,18 @@ PM = ["s[88:89]", "s[90:91]", "s[94:95]"]
 KP = 3
 WAYS = 8  # combining-table associativity
 MISS_PARTS = 256  # miss-log partitions (common.hpp kMissParts)
-TENV = 64 + 4 * MISS_PARTS  # launch constants + miss counters below the combining table (common.hpp kTenvBytes)
+RB_TENV = 64 + 4 * MISS_PARTS  # the block's ring staging slots in the launch constants (common.hpp kTenvRb)
+TENV = RB_TENV + 16  # launch constants + miss counters + ring slots below the combining table (common.hpp kTenvBytes)
+
+
+def _common_const(name):
+    """A constexpr of common.hpp (kept in one place)."""
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "common.hpp")) as f:
+        m = re.search(r"constexpr uint32_t %s = (\d+);" % name, f.read())
+    return int(m.group(1))
+
+
+RB_STAGE_REC = _common_const("kRbStageRec")  # ring staging budget per block
 # hash-lookup cache: w4 of a FW_LCACHE lookup = its 2-way set count (common.hpp
 # lcache_bytes: the ways' 16-B keys, then their u32 entries)
 
@@ -145,7 +156,7 @@ def handler_ids():
             ids += [f"ATOM{sz}_{op}", f"ATOM{sz}_{op}_F"]
         ids += [f"ATOMMV{sz}_ADD"]
     ids += ["ATOMMV8_ADD2"]
-    ids += ["LDDW", "JA", "CALL_LOOKUP", "CALL_LOOKUP_STK", "CALL_LOOKUP_AK", "EXIT"]
+    ids += ["LDDW", "JA", "CALL_LOOKUP", "CALL_LOOKUP_STK", "CALL_LOOKUP_AK", "CALL_RBOUT", "EXIT"]
     for sz in (4, 8):
         for k in ("R", "I"):
             ids += [f"RMW{sz}_{k}", f"RMWMV{sz}_{k}", f"RMWK{sz}_{k}", f"RMWD{sz}_{k}"]
@@ -1568,6 +1579,87 @@ class Gen:
                "ds_read_b64 v[42:43], v41", "s_waitcnt lgkmcnt(0)",
                "v_readfirstlane_b32 s52, v42", "v_readfirstlane_b32 s53, v43", "s_nop 4")
 
+    def call_rbout(self):
+        """bpf_ringbuf_output(ring, data, size, flags) (bpf_helper.cpp:451-467)
+        on the block's ring staging (dev_helpers.hpp rb_reserve's staged path
+        and rb_submit), the data being the unit's staged bytes from window
+        dword w2 (loader.cpp link_staged: data = the packet at a constant
+        offset): with the unit staged, the block's staging holding a promise
+        from ring w6 (RbLds.fd), size (r3) wave-uniform, a multiple of 4 and
+        at most 16, the first lane claims the wave's records in the block's
+        budget with a compare-and-swap on RbLds.used and takes their record
+        indices from RbLds.nrec; each lane writes its record (final: the
+        block publishes its records when it ends, rb_publish) and its offset,
+        r0 = 0.  Anything else -- no staging, an undecided or other ring, a
+        closed or spent budget -- leaves for the C++ tier before any state
+        changes (bail: exec restored first)."""
+        slow = L("slow")
+        loop, bail, d0, d1, d2, d3, dd = (self.label(x) for x in ("rbl", "rbb", "rb0", "rb1", "rb2", "rb3", "rbd"))
+        e = self.e
+        e("s_cmp_eq_u32 s80, 0", f"s_cbranch_scc1 {slow}",                 # the unit's staging
+          f"s_sub_u32 s69, %[comb], {TENV - RB_TENV}", "v_mov_b32 v41, s69",
+          "ds_read_b64 v[42:43], v41", "ds_read_b32 v44, v41 offset:8",
+          f"v_mov_b32 v45, v{R0 + 6}", f"v_mov_b32 v46, v{R0 + 7}",          # r3 = size
+          "s_waitcnt lgkmcnt(0)",
+          "v_readfirstlane_b32 s52, v42", "v_readfirstlane_b32 s53, v43",  # the block's staging area
+          "v_readfirstlane_b32 s70, v44",                                  # its RbLds
+          "v_readfirstlane_b32 s44, v45",
+          "s_cmp_eq_u64 s[52:53], 0", f"s_cbranch_scc1 {slow}",
+          "v_cmp_ne_u32 s[54:55], s44, v45", "v_cmp_ne_u32 vcc, 0, v46",
+          "s_or_b64 vcc, vcc, s[54:55]", "s_and_b64 vcc, vcc, exec", f"s_cbranch_vccnz {slow}",
+          "s_and_b32 s69, s44, 3", "s_cmp_lg_u32 s69, 0", f"s_cbranch_scc1 {slow}",
+          "s_cmp_gt_u32 s44, 16", f"s_cbranch_scc1 {slow}",
+          "v_mov_b32 v41, s70",
+          "ds_read_b32 v45, v41 offset:8",                                 # RbLds.fd
+          "s_waitcnt lgkmcnt(0)", "v_readfirstlane_b32 s71, v45",
+          "s_cmp_lg_u32 s71, s46", f"s_cbranch_scc1 {slow}",
+          # the wave's bytes: lanes x total, total = (size + 8 + 7) & ~7
+          "s_add_u32 s45, s44, 15", "s_and_b32 s45, s45, -8",
+          "s_bcnt1_i32_b64 s69, exec", "s_mul_i32 s71, s69, s45",
+          "s_mov_b64 s[54:55], exec",
+          "s_ff1_i32_b64 s72, exec", "s_lshl_b64 exec, 1, s72",              # the first lane claims
+          f"{loop}:",
+          "ds_read_b32 v46, v41",                                          # RbLds.used
+          "s_waitcnt lgkmcnt(0)", "v_readfirstlane_b32 s72, v46",
+          "s_bitcmp1_b32 s72, 31", f"s_cbranch_scc1 {bail}",               # closed
+          "s_add_u32 s73, s72, s71", f"s_cmp_gt_u32 s73, {RB_STAGE_REC}", f"s_cbranch_scc1 {bail}",
+          "v_mov_b32 v46, s72", "v_mov_b32 v47, s73",
+          "ds_cmpst_rtn_b32 v48, v41, v46, v47",
+          "s_waitcnt lgkmcnt(0)", "v_readfirstlane_b32 s74, v48",
+          "s_cmp_lg_u32 s74, s72", f"s_cbranch_scc1 {loop}",
+          "v_mov_b32 v46, s69",
+          "ds_add_rtn_u32 v48, v41, v46 offset:4",                          # RbLds.nrec
+          "s_waitcnt lgkmcnt(0)", "v_readfirstlane_b32 s73, v48",
+          "s_mov_b64 exec, s[54:55]",
+          # each lane's record at base + rank * total: the header, then the data
+          "v_mbcnt_lo_u32_b32 v46, s54, 0", "v_mbcnt_hi_u32_b32 v46, s55, v46",
+          "v_mul_lo_u32 v47, v46, s45", "v_add_u32 v47, s72, v47",
+          "v_add_co_u32 v48, vcc, s52, v47", "v_mov_b32 v49, s53", "v_addc_co_u32 v49, vcc, 0, v49, vcc",
+          "v_mov_b32 v50, s44", "v_mov_b32 v51, s46",
+          "global_store_dwordx2 v[48:49], v[50:51], off")
+        self.idx("s42", "SRC0")
+        e(f"v_mov_b32 v42, v{STG}", f"v_mov_b32 v43, v{STG + 1}", f"v_mov_b32 v44, v{STG + 2}",
+          f"v_mov_b32 v45, v{STG + 3}")
+        self.idx_off()
+        e("s_cmp_eq_u32 s44, 4", f"s_cbranch_scc1 {d1}",
+          "s_cmp_eq_u32 s44, 8", f"s_cbranch_scc1 {d2}",
+          "s_cmp_eq_u32 s44, 12", f"s_cbranch_scc1 {d3}",
+          "s_cmp_eq_u32 s44, 16", f"s_cbranch_scc0 {dd}",
+          "global_store_dwordx4 v[48:49], v[42:45], off offset:8", f"s_branch {dd}",
+          f"{d3}:", "global_store_dwordx3 v[48:49], v[42:44], off offset:8", f"s_branch {dd}",
+          f"{d2}:", "global_store_dwordx2 v[48:49], v[42:43], off offset:8", f"s_branch {dd}",
+          f"{d1}:", "global_store_dword v[48:49], v42, off offset:8",
+          f"{dd}:",
+          # the record's offset at the block's table (after the budget)
+          "v_add_u32 v46, s73, v46", "v_lshlrev_b32 v46, 2, v46",
+          f"v_add_u32 v46, {RB_STAGE_REC}, v46",
+          "v_add_co_u32 v50, vcc, s52, v46", "v_mov_b32 v51, s53", "v_addc_co_u32 v51, vcc, 0, v51, vcc",
+          "global_store_dword v[50:51], v47, off",
+          f"v_mov_b32 v{R0}, 0", f"v_mov_b32 v{R0 + 1}, 0")
+        self.next_seq()
+        e(f"{bail}:", "s_mov_b64 exec, s[54:55]", f"s_branch {slow}")
+        del d0
+
     def tail_env(self):
         self.e(f"s_sub_u32 s69, %[comb], {TENV}", "v_mov_b32 v41, s69",
                "ds_read_b128 v[42:45], v41", "ds_read_b128 v[46:49], v41 offset:16",
@@ -2075,6 +2167,8 @@ class Gen:
                 self.call_lookup(stack_key=True)
             elif name == "CALL_LOOKUP_AK":
                 self.call_lookup_ak()
+            elif name == "CALL_RBOUT":
+                self.call_rbout()
             elif name == "EXIT":
                 self.exit_()
             elif name == "TAIL":

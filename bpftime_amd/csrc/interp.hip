@@ -681,6 +681,10 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     tenv[6] = p.miss_cap;
     // images: the slot -> entry pc table of the asm tier's bpf_tail_call
     tenv[7] = (uint64_t)(uintptr_t)p.tail_slots;
+    // the block's ring staging for the asm tier's bpf_ringbuf_output
+    // (gen_fast.py call_rbout): its area and the LDS address of its counters
+    tenv[kTenvRb / 8] = p.rb_stage ? (uint64_t)(uintptr_t)rbs.buf : 0;
+    tenv[kTenvRb / 8 + 1] = (uint32_t)(uintptr_t)&rb_lds;
   }
   uint32_t *const miss_cnt = (uint32_t *)((uint8_t *)tenv + 64);  // per partition: records claimed
   for (uint32_t i = tid; i < kMissParts; i += BS) miss_cnt[i] = 0;

@@ -1317,6 +1317,23 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
       }
     }
     if (d.op == X_CALL) {
+      // bpf_ringbuf_output of packet bytes at a constant offset into a ring
+      // bound at load: the asm tier writes the record from the staged
+      // window when the launch stages the ring (link_staged, gen_fast.py
+      // call_rbout; op 3 with the ring's fd in imm)
+      if (d.hi == 130) {
+        const MapRec *m = st[1].kind == P_MAPFD ? map_rec(st[1].id) : nullptr;
+        if (m && m->type == MT_RINGBUF && st[2].kind == P_PKT && st[2].k >= 0 &&
+            st[2].k + 16 <= (int64_t)kFastStageBytes && !getenv("BPFTIME_AMD_NO_ASM_RINGBUF")) {
+          FStatic &s = out.stat[i];
+          s.kind = 1;
+          s.op = 3;
+          s.sz = 16;  // (the window must hold the largest record the asm writes)
+          s.at = st[2].k;
+          s.imm = st[1].id;
+        }
+        continue;
+      }
       if (d.hi != 1) continue;
       // lookup with its key on the stack: key read straight from LDS; an
       // ARRAY map bound at load needs no map-table read at all
@@ -1539,6 +1556,14 @@ static void link_staged(const FastForm &f, uint32_t head, uint32_t stage, bool o
     FInsn g = out[i];
     g.imm = (int64_t)((uint64_t)(o >> 2) | ((uint64_t)sh << 32));  // w2 dword index, w3 bit shift
     g.target = o;                                                // fallback: slot + o
+    if (s.op == 3) {  // bpf_ringbuf_output's source: dword-aligned in the window
+      if (o & 3) continue;
+      g.hoff = 4 + 4 * F_CALL_RBOUT;
+      g.imm = (int64_t)(o >> 2);
+      g.target = (uint32_t)s.imm;  // the ring's fd
+      out[i] = g;
+      continue;
+    }
     if (s.op == 0) {
       uint32_t id;
       if (sz == 8) id = (o & 3) ? F_LDXS8U : F_LDXS8A;

@@ -31,11 +31,11 @@ struct LddwHelpers {
 // link_fast once the batch head and staged window are known).
 struct FStatic {
   uint8_t kind = 0;  // 0 none, 1 packet (ctx->data + at), 2 slot (+ at)
-  uint8_t op = 0;    // 0 LDX, 1 STX, 2 ST
+  uint8_t op = 0;    // 0 LDX, 1 STX, 2 ST, 3 bpf_ringbuf_output source (imm: the ring fd)
   uint8_t sz = 0;
   uint8_t pad = 0;
   int32_t at = 0;
-  int32_t imm = 0;   // ST immediate
+  int32_t imm = 0;   // ST immediate (op 3: the ring fd)
 };
 
 // Threaded-code form of a program for one entry convention.
