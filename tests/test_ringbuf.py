@@ -102,6 +102,46 @@ def test_device_ringbuf_sampler(fresh_oracle, fresh_runtime, size, frac):
     assert dm.ringbuf_fetch() == []                          # consumed
 
 
+def _output_program(rb_fd, size, off):
+    """byte0 % 8 == 0: bpf_ringbuf_output(data + off, size); verdict TX when
+    it succeeded, DROP when not, PASS for the others."""
+    a = Asm().ldx(8, 2, 1, 0).ldx(8, 3, 1, 8).mov64(0, 2)
+    a.mov64(4, "r2").add64(4, 32).jmp("jgt", 4, "r3", "out")
+    a.ldx(1, 8, 2, 0).alu64("and", 8, 7).jmp("jne", 8, 0, "out")
+    a.ld_map_fd(1, rb_fd).add64(2, off).mov64(3, size).mov64(4, 0).call(130)
+    a.mov64(1, "r0").mov64(0, 3).jmp("jeq", 1, 0, "out").mov64(0, 1)
+    a.label("out").exit()
+    return a.assemble()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size,off", [(4, 0), (8, 4), (12, 0), (16, 16), (12, 2), (0, 8), (20, 0)])
+def test_device_ringbuf_output_sizes(fresh_oracle, fresh_runtime, size, off):
+    """bpf_ringbuf_output of packet bytes [off, off + size) through a staged
+    ring: dword-aligned sources of up to 16 B are written by the asm tier
+    from the staged window (gen_fast.py call_rbout), the others (an odd
+    offset, 20 B) by the C++ tier; verdicts equal and the record multiset
+    equals the oracle's."""
+    po, dev = fresh_oracle, fresh_runtime
+    dm = dev.Map(RB, 0, 0, 1 << 26)
+    om = po.OracleMap(RB, 0, 0, 1 << 26, fd=dm.fd)
+    code = _output_program(dm.fd, size, off)
+    n = 1 << 17
+    pk = gen.xdp_packets(n, seed=40 + size + off)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    want = ovm.run_xdp(pk.copy(), fixed_len=64)
+    vm = dev.VM()
+    vm.load(code)
+    d = dev.DeviceBuffer.from_array(pk)
+    dv = dev.DeviceBuffer(4 * n)
+    assert vm.exec_batch(dev.CTX_XDP, d, n, 64, fixed_len=64, verdicts=dv) == 0
+    np.testing.assert_array_equal(dv.download(np.uint32), want)
+    drecs, orecs = dm.ringbuf_fetch(cap=1 << 24), om.ringbuf_fetch()
+    assert len(drecs) == int((pk[:, 0] % 8 == 0).sum()) > 1000
+    assert sorted(drecs) == sorted(orecs)
+
+
 def _wrap_stream(rounds, n, seed):
     """Per-round frames of a wrap test: every 16th frame outputs 12 B (a 24-B
     record), frames with byte0 % 16 == 1 reserve 16 B and submit or discard."""
