@@ -226,6 +226,11 @@ struct KParams {
   uint64_t n;
   uint64_t stride;
   uint64_t first_unit;    // global index of unit 0 (virtual-cpu assignment)
+  // (host-computed for the launch's grid, so the kernel divides nothing:
+  // (n - 64) / (grid x block) and its remainder -- a wave's chained
+  // iterations, interp.hip `full` -- and (grid x block / 64) % ncpu)
+  uint64_t full_q, full_r;
+  uint32_t step_cpu;
   uint64_t data_lo, data_hi;    // allowed global window #1 (the batch)
   uint64_t arena_lo, arena_hi;  // allowed global window #2 (map arena)
   uint64_t step_limit;    // max executed insns per unit

@@ -595,7 +595,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
   SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(dbg_counts); SRP(flush_log); SRV(log_words); SRP(lane_scratch);
   SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask); SRV(lcache); SRP(gregs); SRP(rb_stage); SRP(gctx);
-  SRP(miss_log); SRP(miss_counts); SRV(miss_cap); SRP(tail_slots);
+  SRP(miss_log); SRP(miss_counts); SRV(miss_cap); SRP(tail_slots); SRV(full_q); SRV(full_r); SRV(step_cpu);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
   p.unwind_idx = (int32_t)sreg((uint64_t)(uint32_t)pin.unwind_idx);
 #undef SRP
@@ -755,8 +755,10 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
                         ustep * p.stride < (1ull << 32) && !(p.dbg & 64);
   uint64_t full = 0;  // iterations in which every lane of this wave has a unit
   if (chain_ok) {
-    const uint64_t wb = (uint64_t)blockIdx.x * BS + (tid & ~63u);
-    full = p.n >= wb + 64 ? (p.n - 64 - wb) / ustep + 1 : 0;
+    // (n - 64 - wb) / ustep + 1 for the wave's first unit wb < ustep, from
+    // the host's quotient and remainder of (n - 64) / ustep
+    const uint64_t wb = (uint64_t)blockIdx.x * BS + __builtin_amdgcn_readfirstlane(tid & ~63u);
+    full = p.n >= wb + 64 ? p.full_q + (wb <= p.full_r ? 1 : 0) : 0;
   }
   fe.sstep = (uint32_t)(ustep * p.stride);
   fe.ustep = (uint32_t)ustep;
@@ -764,7 +766,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const bool ncpu_pow2 = (ncpu & (ncpu - 1)) == 0;
   const uint32_t chain_bits = (KIND != CTX_XDP ? 8u : 0u) | (KIND == CTX_RAW ? 16u : 0u) | (p.lens ? 32u : 0u) |
                               (KIND == CTX_SYSCALL ? 64u : 0u) | (IMAGE ? 128u : 0u) |
-                              ((uint32_t)((ustep / 64) % ncpu) << 16);
+                              (p.step_cpu << 16);
   uint64_t it = 0;
   for (uint64_t u0 = ordered ? 0 : (uint64_t)blockIdx.x * BS; u0 < p.n; u0 += ustep, it++) {
     uint64_t unit, slot, chunk, vcpu;

@@ -700,6 +700,12 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       if (atoi(g) > 0 && grid > (uint32_t)atoi(g)) grid = (uint32_t)atoi(g);
     if (im.d_tail_entry && grid > kTailGrid) grid = kTailGrid;  // one frame stack per lane of the grid
   }
+  {
+    const uint64_t ustep = (uint64_t)grid * block;
+    p.full_q = p.n >= 64 ? (p.n - 64) / ustep : 0;
+    p.full_r = p.n >= 64 ? (p.n - 64) % ustep : 0;
+    p.step_cpu = ordered ? 0 : (uint32_t)((ustep / 64) % (p.ncpu ? p.ncpu : 1));
+  }
   if (greg) {
     p.gregs = (uint64_t *)regs.get(s, (uint64_t)grid * 11 * block * 8);
     if (!p.gregs) {
