@@ -36,7 +36,8 @@ class EbpfBatch(C.Structure):  # include/ebpf-vm.h struct ebpf_batch
                 ("rx_queue_index", C.c_uint32), ("head", C.c_uint32), ("verdicts", C.c_void_p),
                 ("rets", C.c_void_p), ("data_off_out", C.c_void_p), ("len_out", C.c_void_p),
                 ("first_unit", C.c_uint64), ("stream", C.c_void_p), ("descs", C.c_void_p),
-                ("umem_bytes", C.c_uint64), ("sys_nr", C.c_int64)]
+                ("umem_bytes", C.c_uint64), ("sys_nr", C.c_int64), ("sys_state", C.c_void_p),
+                ("sys_ret", C.c_void_p), ("sys_phase", C.c_uint32), ("pid_tgid_off", C.c_int32)]
 
 
 class PerfEvent(C.Structure):
@@ -122,6 +123,9 @@ SIGNATURES = [
     ("bpftime_amd_syscall_attach", C.c_int, [C.c_int, C.c_int64]),
     ("bpftime_amd_syscall_detach", C.c_int, [C.c_int]),
     ("bpftime_amd_syscall_dispatch", C.c_int64, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]),
+    ("bpftime_amd_syscall_attach_ex", C.c_int, [C.c_int, C.c_int64, C.c_int]),
+    ("bpftime_amd_syscall_dispatch_records", C.c_int64, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p,
+                                                         C.c_uint32, C.c_void_p]),
     ("bpftime_amd_handle_sysbpf", C.c_long, [C.c_int, C.c_void_p, C.c_uint32]),
     ("bpftime_map_get_info", C.c_int, [C.c_int, C.POINTER(BpfMapAttr), C.POINTER(C.c_char_p),
                                         C.POINTER(C.c_int)]),
@@ -175,6 +179,11 @@ SIGNATURES = [
     ("bpftime_amd_event_record", C.c_int, [C.c_void_p, C.c_void_p]),
     ("bpftime_amd_event_elapsed_ms", C.c_float, [C.c_void_p, C.c_void_p]),
     ("bpftime_amd_last_error", C.c_char_p, []),
+    ("bpftime_amd_gen_syscall_full", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p,
+                                                C.c_uint32, C.c_void_p]),
+    ("bpftime_amd_static_lds", C.c_size_t, [C.c_uint32, C.c_bool, C.c_bool, C.c_uint32]),
+    ("bpftime_amd_lds_bytes", C.c_size_t, [C.c_uint32, C.c_bool, C.c_uint32, C.c_uint32, C.c_uint32, C.c_bool,
+                                           C.c_bool, C.c_uint32]),
     ("bpftime_amd_gen_xdp", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64,
                                        C.c_uint64, C.c_void_p]),
     ("bpftime_amd_gen_flow", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,

@@ -189,7 +189,8 @@ constexpr uint32_t kFrameLiveShift = 40;  // + r: the bit of register r (1..9)
 // Context kinds for a batch
 constexpr uint32_t CTX_RAW = 0;      // r1 = unit memory, r2 = length
 constexpr uint32_t CTX_XDP = 1;      // r1 = xdp_md_userspace (48 B, LDS)
-constexpr uint32_t CTX_SYSCALL = 2;  // r1 = 64-B trace_event_raw_sys_enter record
+constexpr uint32_t CTX_SYSCALL = 2;  // r1 = trace_event_raw_sys_enter (64 B) or, for
+                                     // EBPF_CTX_SYSCALL_EXIT batches, trace_event_raw_sys_exit (24 B)
 
 // Launches of at least this many units build the flat table of an IPv4 LPM
 // trie changed since the last one (maps.cpp prepare_ix); smaller ones walk
@@ -267,6 +268,15 @@ struct KParams {
   uint32_t *miss_counts;     // [grid][kMissParts] records each block wrote (k_miss_merge reads them)
   uint32_t miss_cap;         // records per block and partition (even)
   const int32_t *tail_slots; // images: per PROG_ARRAY fd the offset of its slots' entry pcs, then those (vm_api.cpp)
+  // syscall dispatch state (include/ebpf-vm.h struct ebpf_batch): per unit
+  // override flags and return value, the phase bit (1 enter, 2 exit), or null
+  uint32_t *sys_state;
+  int64_t *sys_ret;
+  uint32_t sys_phase;
+  // bpf_get_current_pid_tgid: a u64 at this offset from the unit (recorded
+  // syscalls), or (0) the launching thread's value
+  int32_t pid_off;
+  uint64_t pid_tgid;
 };
 
 // Combining-table misses.  A deferred counter add that finds no table entry

@@ -1045,7 +1045,27 @@ struct LaneEnv {
   int32_t miss_fd;
   uint64_t miss_hash;
   RbStage rb;        // the block's ring-buffer staging (RbStage)
+  // syscall dispatch state of this unit (KParams::sys_state / sys_ret), the
+  // bit this batch's phase sets; null outside a dispatch
+  uint32_t *ovr_state;
+  int64_t *ovr_val;
+  uint32_t ovr_bit;
+  uint64_t pid_tgid;  // bpf_get_current_pid_tgid's value for this unit
 };
+
+// bpftime_override_return / bpftime_set_retval (attach/base_attach_impl/
+// base_attach_impl.hpp:76-105): the dispatch's return callback records the
+// value (syscall_trace_attach_impl.cpp:35-40); with no callback set the
+// reference throws, which fails the unit here
+__device__ __forceinline__ uint64_t helper_set_retval(uint64_t v, LaneEnv &env, uint32_t *err) {
+  if (!env.ovr_state) {
+    *err = E_BADOP;
+    return 0;
+  }
+  *env.ovr_state |= env.ovr_bit;
+  if (env.ovr_val) *env.ovr_val = (int64_t)v;
+  return 0;
+}
 
 __device__ __forceinline__ uint64_t lru_next_stamp(LaneEnv &env) {
   const uint32_t op = env.lru_ops < 255 ? env.lru_ops : 255;

@@ -97,6 +97,34 @@ __global__ void k_gen_syscall(uint8_t *base, uint64_t n, uint64_t seed, uint64_t
   }
 }
 
+// 96-B replay records (gen.py syscall_records_full): the enter record of
+// k_gen_syscall (id -1 instead for 0.5 % of the records, the tracepoint's
+// interrupt marker syscount skips), then trace_event_raw_sys_exit {0, id,
+// ret}: ret a negative errno in [-133, -1] for 20 % of the records, else in
+// [0, 65535]; then the caller's pid_tgid: tgid 1000 + [0, 64), tid tgid + [0, 4)
+__global__ void k_gen_syscall_full(uint8_t *base, uint64_t n, uint64_t seed, uint64_t first, const double *cdf,
+                                   uint32_t support) {
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n * 12;
+       w += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t unit = w / 12, j = w % 12, g = first + unit;
+    uint64_t v = 0;
+    if (j == 1 || j == 9) {
+      const uint64_t r = sm64(seed ^ 0x5555, g);
+      v = (r % 100) == 0 ? (((r >> 9) & 1) ? 60 : 231) : zipf_pick(cdf, support, seed, g);
+      if ((r % 200) == 1) v = ~0ull;
+    } else if (j >= 2 && j < 8) {
+      v = sm64(seed ^ (0x6000 + (j - 2)), g) & 0xFFFFFFFFFFull;
+    } else if (j == 10) {
+      const uint64_t r = sm64(seed ^ 0x7777, g);
+      v = (r % 5) == 0 ? (uint64_t)(-(int64_t)(1 + (r >> 8) % 133)) : (r >> 16) & 0xFFFF;
+    } else if (j == 11) {
+      const uint64_t r = sm64(seed ^ 0x8888, g), tgid = 1000 + r % 64;
+      v = (tgid << 32) | (tgid + (r >> 8) % 4);
+    }
+    *(uint64_t *)(base + unit * 96 + j * 8) = v;
+  }
+}
+
 }  // namespace bpftime_amd
 
 static uint32_t gen_blocks(uint64_t total) {
@@ -118,6 +146,15 @@ extern "C" int bpftime_amd_gen_syscall(void *dev, uint64_t n, uint64_t seed, uin
   if (!cdf || !support) return -1;
   if (!n) return 0;
   hipLaunchKernelGGL(bpftime_amd::k_gen_syscall, dim3(gen_blocks(n * 8)), dim3(256), 0, (hipStream_t)stream,
+                     (uint8_t *)dev, n, seed, first, cdf, support);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int bpftime_amd_gen_syscall_full(void *dev, uint64_t n, uint64_t seed, uint64_t first, const double *cdf,
+                                            uint32_t support, void *stream) {
+  if (!cdf || !support) return -1;
+  if (!n) return 0;
+  hipLaunchKernelGGL(bpftime_amd::k_gen_syscall_full, dim3(gen_blocks(n * 12)), dim3(256), 0, (hipStream_t)stream,
                      (uint8_t *)dev, n, seed, first, cdf, support);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -54,6 +54,7 @@ __device__ __forceinline__ uint64_t call_helper(uint32_t id, uint64_t a1, uint64
       return (uint32_t)x;
     }
     case 8: return env.vcpu % ncpu;
+    case 14: return env.pid_tgid;  // bpf_get_current_pid_tgid (KParams::pid_off)
     case 28: return helper_csum_diff(a1, a2, a3, a4, a5);
     case 44: return helper_adjust_head(a1, a2);
     case 65: return helper_adjust_tail(a1, a2);
@@ -62,6 +63,8 @@ __device__ __forceinline__ uint64_t call_helper(uint32_t id, uint64_t a1, uint64
     case 131: return rb_reserve(maps, a1, a2, env.rb);
     case 132: rb_submit(maps, a1, false, env.rb); return 0;
     case 133: rb_submit(maps, a1, true, env.rb); return 0;
+    case 58: return helper_set_retval(a2, env, err);   // bpf_override_return(ctx, value)
+    case 187: return helper_set_retval(a1, env, err);  // bpf_set_retval(value)
   }
   *err = E_BADOP;
   return 0;
@@ -596,6 +599,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(dbg_counts); SRP(flush_log); SRV(log_words); SRP(lane_scratch);
   SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask); SRV(lcache); SRP(gregs); SRP(rb_stage); SRP(gctx);
   SRP(miss_log); SRP(miss_counts); SRV(miss_cap); SRP(tail_slots); SRV(full_q); SRV(full_r); SRV(step_cpu);
+  SRP(sys_state); SRP(sys_ret); SRV(sys_phase); SRV(pid_tgid);
+  p.pid_off = (int32_t)sreg((uint64_t)(uint32_t)pin.pid_off);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
   p.unwind_idx = (int32_t)sreg((uint64_t)(uint32_t)pin.unwind_idx);
 #undef SRP
@@ -751,7 +756,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   // outputs, no syscall-number filter; dbg 64 turns it off.  (Images: only
   // from a unit no lane group is parked in, and the depth is reset.)
   const bool chain_ok = !ordered && !p.descs && p.stride && !p.out_data_off && !p.out_len &&
-                        !(KIND == CTX_XDP && p.needs_ctx) && !(KIND == CTX_SYSCALL && p.sys_nr >= 0) &&
+                        !(KIND == CTX_XDP && p.needs_ctx) &&
+                        !(KIND == CTX_SYSCALL && (p.sys_nr >= 0 || p.sys_state)) &&
                         ustep * p.stride < (1ull << 32) && !(p.dbg & 64);
   uint64_t full = 0;  // iterations in which every lane of this wave has a unit
   if (chain_ok) {
@@ -843,15 +849,20 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
       fu.r2 = 48;
     } else {
       fu.r1 = slot;
-      fu.r2 = KIND == CTX_SYSCALL ? 64 : len;
+      fu.r2 = len;  // (syscall kinds: the ctx size, 64 or 24, as fixed_len)
     }
 
-    bool alive = active;
-    if (KIND == CTX_SYSCALL && active) {
-      // exit / exit_group bypass every callback (syscall_trace_attach_impl.cpp:25)
+    // syscall records this program does not run on: exit / exit_group
+    // bypass every callback (syscall_trace_attach_impl.cpp:25), a per-syscall
+    // program sees its nr only, and an exit program skips a record whose
+    // enter programs overrode the return (:70-72; the dispatch's state)
+    auto sys_skip = [&]() {
       const int64_t nr = *(const int64_t *)(slot + 8);
-      if (nr == 60 || nr == 231 || (p.sys_nr >= 0 && nr != p.sys_nr)) alive = false;
-    }
+      return nr == 60 || nr == 231 || (p.sys_nr >= 0 && nr != p.sys_nr) ||
+             (p.sys_state && p.sys_phase == 2 && (p.sys_state[unit] & 1));
+    };
+    bool alive = active;
+    if (KIND == CTX_SYSCALL && active && sys_skip()) alive = false;
     c.alive = alive && desc_ok;
     c.pc = 0;
     c.lpc = 0;
@@ -1046,6 +1057,10 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         env.lru_ops = lru_ops;
         env.exact = ordered;
         env.rb = rbs;
+        env.ovr_state = p.sys_state ? p.sys_state + unit : nullptr;
+        env.ovr_val = p.sys_ret ? p.sys_ret + unit : nullptr;
+        env.ovr_bit = p.sys_phase;
+        env.pid_tgid = p.pid_off ? *(const uint64_t *)(slot + (int64_t)p.pid_off) : p.pid_tgid;
         uint32_t cerr = E_OK;
         uint64_t *R = c.R;
         const uint64_t rv = call_helper(c.call_id, R[1 * kBlock], R[2 * kBlock], R[3 * kBlock], R[4 * kBlock],
@@ -1081,12 +1096,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         if (p.verdicts) p.verdicts[unit] = 0;
         if (p.rets) p.rets[unit] = (p.dbg & 32) ? (0xE0000000ull | c.err | ((uint64_t)c.pc << 8) | ((uint64_t)c.lpc << 36)) : 0;
         atomicAdd(p.err_count, 1u);
-      } else if (KIND == CTX_SYSCALL) {
-        const int64_t nr = *(const int64_t *)(slot + 8);
-        if (nr == 60 || nr == 231 || (p.sys_nr >= 0 && nr != p.sys_nr)) {
-          if (p.verdicts) p.verdicts[unit] = 0;
-          if (p.rets) p.rets[unit] = 0;
-        }
+      } else if (KIND == CTX_SYSCALL && sys_skip()) {
+        if (p.verdicts) p.verdicts[unit] = 0;
+        if (p.rets) p.rets[unit] = 0;
       }
       if (KIND == CTX_XDP) {
         const XdpCtx *x = (const XdpCtx *)my_ctx;
@@ -1329,10 +1341,46 @@ extern "C" hipError_t bpftime_amd_launch_miss_merge(const uint64_t *log, const u
   return hipGetLastError();
 }
 
+// Static LDS of a k_interp instance (Rf, rb_lds, wdelta, nlog): the
+// kernel's own attribute, or (no device) the same sum restated
+template <uint32_t KIND, bool BIGSTACK, bool IMAGE, bool G, uint32_t BS>
+static size_t static_lds_of() {
+  hipFuncAttributes a;
+  if (hipFuncGetAttributes(&a, (const void *)k_interp<KIND, BIGSTACK, IMAGE, G, BS>) == hipSuccess)
+    return a.sharedSizeBytes;
+  (void)hipGetLastError();
+  const size_t rf = (size_t)(IMAGE ? (G ? 3 : 14) : (G ? 1 : 12)) * BS * 8;
+  return rf + sizeof(RbLds) + (BS / 64) * 2 * 2 * 8 + 16;
+}
+
+extern "C" size_t bpftime_amd_static_lds(uint32_t kind, bool big_stack, bool gregs, uint32_t block) {
+#define S(K, B, G, BS) return static_lds_of<K, B, false, G, BS>()
+#define SK(K)                                          \
+  if (big_stack) S(K, true, false, kBlock);            \
+  else if (gregs && block == kBigBlock) S(K, false, true, kBigBlock); \
+  else if (gregs) S(K, false, true, kBlock);           \
+  else S(K, false, false, kBlock);
+  if (kind == CTX_XDP) {
+    SK(CTX_XDP)
+  } else if (kind == CTX_SYSCALL) {
+    SK(CTX_SYSCALL)
+  } else {
+    SK(CTX_RAW)
+  }
+#undef SK
+#undef S
+}
+
+extern "C" size_t bpftime_amd_lds_bytes(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
+                                        uint32_t lcache_sets, bool ctx_lds, bool gregs, uint32_t block) {
+  return dyn_lds_for(kind, big_stack, stack_size, comb_entries, lcache_sets, ctx_lds, block) +
+         bpftime_amd_static_lds(kind, big_stack, gregs, block);
+}
+
 extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds, bool gregs, uint32_t block) {
   // (a block asking for more LDS than a CU has never fits, whatever the
-  // occupancy query answers for it)
-  if (dyn_lds > kCuLds) return 0;
+  // occupancy query answers for it: dynamic plus the kernel's static LDS)
+  if (dyn_lds + bpftime_amd_static_lds(kind, big_stack, gregs, block) > kCuLds) return 0;
   int n = 0;
   hipError_t e;
 #define O(K, B, G) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_interp<K, B, false, G, kBlock>, kBlock, dyn_lds)

@@ -24,6 +24,8 @@ bool device_helper_supported(uint32_t id) {
   switch (id) {
     case 1: case 2: case 3: case 5: case 7: case 8: case 28: case 44: case 65: case 189:
     case 130: case 131: case 132: case 133:
+    case 58: case 187:  // bpf_override_return / bpf_set_retval (syscall dispatch state)
+    case 14:            // bpf_get_current_pid_tgid (recorded caller / launching thread)
     case kTailHelper:
       return true;
   }
@@ -479,6 +481,7 @@ int load_program(const RawInsn *code, size_t n, const std::map<size_t, size_t> &
         return -EINVAL;
       }
       if (cur.imm == 3) out.may_delete = true;
+      if (cur.imm == 58 || cur.imm == 187) out.sets_retval = true;
     } else if (cur.code == 0x18) {
       if (i + 1 == n) {
         err = "Unable to patch lddw instructions at " + std::to_string(i) + ", it's the last instruction";
@@ -1237,6 +1240,16 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
     kinds_ok = pointer_kinds(prog, lo.lddw_src, xdp, pkt_ok, in);
   }
   lpm_write_sites(prog, lo.lddw_src, kinds_ok ? &in : nullptr, out);
+  // may a store reach the memory r1 points to at entry (the unit: the
+  // syscall dispatch runs such a program on a copy of its records, as each
+  // reference callback gets its own ctx copy)
+  out.stores_unit = !kinds_ok;
+  for (size_t i = 0; kinds_ok && i < prog.size(); i++) {
+    const DInsn &d = prog[i];
+    if (d.op != X_ST && d.op != X_STX && d.op != X_RMW_ADD && d.op != X_ATOMIC) continue;
+    const uint8_t k = in[i][d.dst].kind;
+    if (k != P_UNDEF && k != P_STK && k != P_MAPVAL && k != P_CONST) out.stores_unit = true;
+  }
   if (!kinds_ok) {
     // ctx rewritten: generic handlers only, no pointer kinds to prove a
     // counter unobserved

@@ -63,6 +63,9 @@ struct FastForm {
   // LPM trie: {helper id, map fd}.  The device changes a trie only in ORDERED
   // batches (dev_helpers.hpp lpm_update); vm_api.cpp refuses other batches
   std::vector<std::pair<uint32_t, int32_t>> lpm_writes;
+  // a store may reach the unit r1 points to at entry (the pointer kinds
+  // cannot place every store on the stack, a map value or a constant)
+  bool stores_unit = true;
 };
 
 struct LoadOut {
@@ -74,6 +77,7 @@ struct LoadOut {
   uint32_t comb_entries = 0;  // per-block LDS combining entries (0 = none needed)
   bool may_delete = false;    // calls map_delete_elem: hash lookup indexes stop being valid
   bool tail_call = false;     // calls bpf_tail_call: linked with the prog arrays' targets at launch
+  bool sets_retval = false;   // calls bpf_override_return (58) / bpf_set_retval (187)
   bool multi_entry = false;   // a linked image (tail-call targets are extra entries)
   std::vector<uint32_t> entries;  // the linked targets' entry pcs
   std::vector<uint16_t> tail_live;  // per pc: registers r1..r9 live after a bpf_tail_call (bit r)

@@ -1562,7 +1562,8 @@ void bpftime_amd_reset(void) {
     r.perfs[i] = PerfRec();
   }
   r.lpm_maps = 0;
-  for (int id : detach) bpftime_amd_syscall_detach(id);
+  (void)detach;
+  syscall_detach_all();  // the link-made attachments and the direct ones
   if (r.d_maptab) hipMemset(r.d_maptab, 0, sizeof(DMap) * kMaxFds);
   r.arena_used = 0;
   r.prog_gen++;  // tail-call images linked before the reset relink
@@ -1709,7 +1710,7 @@ int bpftime_progs_create(int fd, const void *insns, size_t insn_cnt, const char 
   return fd;
 }
 
-static int link_perf(int fd, int prog_fd, int perf_fd, bool strict);
+static int link_perf(int fd, int prog_fd, int perf_fd, int bad_errno);
 
 // bpftime_shm_internal.cpp:566-607: only prog_fd is validated; the target of
 // an XDP link is an ifindex.
@@ -1718,16 +1719,8 @@ int bpftime_link_create(int fd, struct bpf_link_create_args *args) {
   if (args && args->attach_type == BPFTIME_AMD_BPF_PERF_EVENT) {
     // :578-600: a perf-event link's target must be a perf event (libbpf
     // probes with target_fd -1 and expects EBADF); it attaches like
-    // BPF_PROG_ATTACH
-    if (!bpftime_is_perf_event_fd((int)args->target_fd)) {
-      errno = EBADF;
-      return -1;
-    }
-    if (!bpftime_is_prog_fd((int)args->prog_fd)) {
-      errno = EBADF;
-      return -1;
-    }
-    return link_perf(fd, (int)args->prog_fd, (int)args->target_fd, true);
+    // BPF_PROG_ATTACH (both fds checked under the runtime lock, link_perf)
+    return link_perf(fd, (int)args->prog_fd, (int)args->target_fd, EBADF);
   }
   std::lock_guard<std::mutex> g(r.mu);
   if (!args) {
@@ -1989,49 +1982,48 @@ int bpftime_is_perf_event_fd(int fd) { return fd >= 0 && fd < (int)kMaxFds && rt
 // runs nothing on this path (sys_exit tracepoints: the replay holds enter
 // records only; uprobes, software events), -1 for a tracepoint id that does
 // not resolve (the reference's attach fails there too,
-// syscall_trace_attach_private_data.cpp:51-62)
-static int perf_drives(const PerfRec &p, int64_t *nr) {
+// syscall_trace_attach_private_data.cpp:51-62); *enter: the sys_enter (1) or
+// sys_exit (0) tracepoint
+static int perf_drives(const PerfRec &p, int64_t *nr, int *enter) {
   if (p.type != 2) return 0;
-  int enter = 1;
+  *enter = 1;
   *nr = p.sys_nr;
-  if (p.tracepoint_id >= 0 && bpftime_amd_tracepoint_resolve(p.tracepoint_id, nr, &enter) < 0) return -1;
-  return enter ? 1 : 0;
+  if (p.tracepoint_id >= 0 && bpftime_amd_tracepoint_resolve(p.tracepoint_id, nr, enter) < 0) return -1;
+  return 1;
 }
 
 // A link from prog_fd to perf_fd at `fd` (-1: a fresh one).  A link to a
-// sys_enter tracepoint attaches the program to the syscall dispatch (it is
-// instantiated: a program the device cannot load fails the link); any other
-// perf target gives a link record that runs nothing.  `strict`: a
-// tracepoint id that does not resolve fails the link (BPF_PROG_ATTACH,
-// BPF_LINK_CREATE) instead of leaving it inert (a JSON import, which the
-// reference accepts and resolves only when its agent attaches).
-static int link_perf(int fd, int prog_fd, int perf_fd, bool strict) {
+// sys_enter or sys_exit tracepoint attaches the program to the syscall
+// dispatch (it is instantiated: a program the device cannot load fails the
+// link); any other perf target, and a tracepoint id that does not resolve
+// here, gives a link record that runs nothing: the reference's
+// add_bpf_link / add_bpf_prog_attach_target (bpftime_shm_internal.cpp:293-315,
+// :566-607) check only the handler kinds and resolve the id when its agent
+// attaches.  bad_errno: what a non-perf perf_fd or non-program prog_fd sets
+// (ENOENT for BPF_PROG_ATTACH, EBADF for BPF_LINK_CREATE).
+static int link_perf(int fd, int prog_fd, int perf_fd, int bad_errno) {
   Runtime &r = rt();
   int64_t nr = -1;
-  int drives;
+  int drives, enter = 1;
   {
     std::lock_guard<std::mutex> g(r.mu);
     if (perf_fd < 0 || perf_fd >= (int)kMaxFds || r.kind[perf_fd] != HKind::PERF) {  // "Fd is not a perf fd"
-      errno = ENOENT;
+      errno = bad_errno;
       return -1;
     }
     if (prog_fd < 0 || prog_fd >= (int)kMaxFds || r.kind[prog_fd] != HKind::PROG) {
-      errno = ENOENT;
+      errno = bad_errno;
       return -1;
     }
     if (fd >= 0 && (fd >= (int)kMaxFds || r.kind[fd] != HKind::NONE)) {
       errno = EBADF;
       return -1;
     }
-    drives = perf_drives(r.perfs[perf_fd], &nr);
-  }
-  if (drives < 0 && strict) {
-    errno = EEXIST;
-    return -1;
+    drives = perf_drives(r.perfs[perf_fd], &nr, &enter);
   }
   int id = 0;
   if (drives > 0) {
-    id = bpftime_amd_syscall_attach(prog_fd, nr);  // instantiates the program (outside the lock)
+    id = bpftime_amd_syscall_attach_ex(prog_fd, nr, enter);  // instantiates the program (outside the lock)
     if (id < 0) return -1;
   }
   std::lock_guard<std::mutex> g(r.mu);
@@ -2051,9 +2043,9 @@ static int link_perf(int fd, int prog_fd, int perf_fd, bool strict) {
   return fd;
 }
 
-int bpftime_attach_perf_to_bpf(int perf_fd, int bpf_fd) { return link_perf(-1, bpf_fd, perf_fd, true); }
+int bpftime_attach_perf_to_bpf(int perf_fd, int bpf_fd) { return link_perf(-1, bpf_fd, perf_fd, ENOENT); }
 
-int bpftime_amd_link_perf(int fd, int prog_fd, int perf_fd) { return link_perf(fd, prog_fd, perf_fd, false); }
+int bpftime_amd_link_perf(int fd, int prog_fd, int perf_fd) { return link_perf(fd, prog_fd, perf_fd, ENOENT); }
 
 int bpftime_amd_link_attached(int fd) {
   Runtime &r = rt();

@@ -14,6 +14,8 @@
 
 #include "common.hpp"
 
+struct ebpf_vm;  // include/ebpf-vm.h
+
 namespace bpftime_amd {
 
 struct MapRec {
@@ -39,9 +41,9 @@ struct MapRec {
 
 // A perf event record (bpf_perf_event_handler, runtime/src/handler/
 // perf_event_handler.hpp:161-215): what a link's target_fd names.  Only a
-// syscall sys_enter tracepoint drives anything here (the syscall replay
-// dispatch); the other kinds are kept as records, so state that holds them
-// imports, exports and links unchanged.
+// syscall sys_enter / sys_exit tracepoint drives anything here (the syscall
+// replay dispatch); the other kinds are kept as records, so state that holds
+// them imports, exports and links unchanged.
 struct PerfRec {
   int type = 2;                // bpf_event_type (bpftime_shm.hpp:48-64); 2 = PERF_TYPE_TRACEPOINT
   int pid = -1;
@@ -64,7 +66,7 @@ struct ProgRec {
 struct LinkRec {
   uint32_t prog_fd = 0, target = 0, attach_type = 0, flags = 0;
   bool perf = false;  // target is a perf event record (maps.cpp link_perf)
-  int attach_id = 0;  // a perf link to a sys_enter tracepoint: its syscall attachment (syscall_dispatch.cpp)
+  int attach_id = 0;  // a perf link to a sys_enter / sys_exit tracepoint: its syscall attachment (syscall_dispatch.cpp)
 };
 
 enum class HKind : uint8_t { NONE, MAP, PROG, LINK, PERF };
@@ -135,5 +137,14 @@ int lpm_pull(int fd);
 
 Runtime &rt();
 void set_error(const std::string &e);
+
+// What the syscall dispatch needs to know of a loaded VM's program
+// (vm_api.cpp): bit 0 it calls bpf_override_return / bpf_set_retval (58 /
+// 187), bit 1 it may store into the memory r1 points to (its unit: the
+// dispatch then runs it on a copy of the records).  -1: no program loaded.
+constexpr int kProgSetsRetval = 1, kProgStoresCtx = 2;
+int vm_prog_flags(const ::ebpf_vm *vm);
+// Drops every syscall attachment (bpftime_amd_reset; syscall_dispatch.cpp).
+void syscall_detach_all();
 
 }  // namespace bpftime_amd

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime_api.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -28,6 +30,7 @@ namespace bpftime_amd {
 extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind, bool big_stack, uint32_t grid,
                                                 uint32_t ordered, uint32_t block, hipStream_t stream);
 extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds, bool gregs, uint32_t block);
+extern "C" size_t bpftime_amd_static_lds(uint32_t kind, bool big_stack, bool gregs, uint32_t block);
 extern "C" hipError_t bpftime_amd_launch_merge(const uint64_t *log, uint32_t log_words, uint32_t nblocks,
                                                 hipStream_t stream);
 extern "C" hipError_t bpftime_amd_launch_miss_merge(const uint64_t *log, const uint32_t *counts, uint32_t cap,
@@ -412,16 +415,39 @@ class Mi355xVm {
   int exec_one(void *mem, size_t mem_len, uint64_t *ret);
 };
 
+// The message of a launch whose block does not fit the CU's LDS: the parts
+// of its dynamic LDS (common.hpp dyn_lds_for) and the kernel's static LDS
+std::string lds_fit_error(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
+                          uint32_t lcache, bool ctx_lds, bool greg, uint32_t block) {
+  const size_t lanes = (size_t)block * ((kind == CTX_XDP && ctx_lds ? 48 : 0) + (big_stack ? 0 : stack_size));
+  const size_t dyn = dyn_lds_for(kind, big_stack, stack_size, comb_entries, lcache, ctx_lds, block);
+  const size_t stat = bpftime_amd_static_lds(kind, big_stack, greg, block);
+  return "launch does not fit the CU's LDS: " + std::to_string(dyn + stat) + " bytes per " +
+         std::to_string(block) + "-lane block (lanes' ctx and stacks " + std::to_string(lanes) +
+         ", lookup cache " + std::to_string(lcache) + " sets " + std::to_string(lcache_bytes(lcache)) +
+         ", launch constants " + std::to_string(kTenvBytes) + ", combining table " + std::to_string(comb_entries) +
+         " entries " + std::to_string(20 * (size_t)comb_entries) + ", static " + std::to_string(stat) + ") > " +
+         std::to_string(kCuLds) + " (check BPFTIME_AMD_COMB_ENTRIES / BPFTIME_AMD_LCACHE_SETS)";
+}
+
 int Mi355xVm::exec_batch(const ebpf_batch *b) {
   if (!loaded) {
     error = "no program loaded";
     return -1;
   }
-  if (!b || b->ctx_kind > CTX_SYSCALL || (b->count && !b->data) || (b->count && !b->stride && !b->descs)) {
+  if (!b || b->ctx_kind > EBPF_CTX_SYSCALL_EXIT || (b->count && !b->data) || (b->count && !b->stride && !b->descs)) {
     error = "invalid batch";
     return -1;
   }
-  if (b->descs && (b->ctx_kind == CTX_SYSCALL || !b->umem_bytes)) {
+  // the sys_exit ctx runs on the syscall kernel: only r2 (the ctx size) and
+  // the window differ (EBPF_CTX_SYSCALL_EXIT, include/ebpf-vm.h)
+  const bool sys_exit = b->ctx_kind == EBPF_CTX_SYSCALL_EXIT;
+  const uint32_t kind = sys_exit ? CTX_SYSCALL : b->ctx_kind;
+  if (b->sys_state && (kind != CTX_SYSCALL || (b->sys_phase != 1 && b->sys_phase != 2))) {
+    error = "sys_state needs a syscall batch with sys_phase 1 (enter) or 2 (exit)";
+    return -1;
+  }
+  if (b->descs && (kind == CTX_SYSCALL || !b->umem_bytes)) {
     error = "descriptor batches need an XDP / raw ctx and umem_bytes";
     return -1;
   }
@@ -455,7 +481,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     // staged window: what the static packet / slot accesses need, when every
     // slot is 16-B aligned and at least that long (a window never reaches
     // into the next unit)
-    const bool xdp = b->ctx_kind == CTX_XDP;
+    const bool xdp = kind == CTX_XDP;
     const uint32_t head = xdp ? b->head : 0;
     const uint32_t need = stage_need(xdp ? im.fx : im.fr, head);
     // (descriptor batches: the kernel checks each wave's frames)
@@ -468,7 +494,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   }
   p.maps = r.d_maptab;
   p.data = (uint8_t *)b->data;
-  p.lens = b->lens;
+  p.lens = kind == CTX_SYSCALL ? nullptr : b->lens;
   p.verdicts = b->verdicts;
   p.rets = b->rets;
   p.out_data_off = b->data_off_out;
@@ -479,14 +505,24 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   p.stride = b->stride;
   p.first_unit = b->first_unit;
   p.data_lo = (uint64_t)(uintptr_t)b->data;
-  p.data_hi = p.data_lo + (b->descs ? b->umem_bytes : b->count * b->stride);
+  // (a sys_exit unit is 24 B inside its record: the window ends with the
+  // last record's exit half, 32 B of a 96-B record)
+  p.data_hi = p.data_lo + (b->descs  ? b->umem_bytes
+                           : sys_exit ? (b->count - 1) * b->stride + (b->stride < 32 ? b->stride : 32)
+                                      : b->count * b->stride);
   p.descs = (const uint64_t *)b->descs;
   p.umem_bytes = b->umem_bytes;
-  p.sys_nr = (b->flags & EBPF_BATCH_SYS_NR) && b->ctx_kind == CTX_SYSCALL ? b->sys_nr : -1;
+  p.sys_nr = (b->flags & EBPF_BATCH_SYS_NR) && kind == CTX_SYSCALL ? b->sys_nr : -1;
+  p.sys_state = b->sys_state;
+  p.sys_ret = b->sys_ret;
+  p.sys_phase = b->sys_phase;
+  p.pid_off = b->pid_tgid_off;
+  p.pid_tgid = ((uint64_t)(uint32_t)getpid() << 32) | (uint32_t)syscall(SYS_gettid);
   p.arena_lo = (uint64_t)(uintptr_t)r.arena;
   p.arena_hi = p.arena_lo + r.arena_size;
   p.step_limit = step_limit;
-  p.fixed_len = b->fixed_len;
+  // (syscall kinds: r2 = sizeof the ctx, syscall_trace_attach_impl.cpp:46)
+  p.fixed_len = kind != CTX_SYSCALL ? b->fixed_len : sys_exit ? 24 : 64;
   p.stack_size = prog.stack_size;
   // ORDERED: every counter add goes straight to memory (link_fast), no table
   p.comb_entries = (b->flags & EBPF_BATCH_ORDERED) ? 0 : prog.comb_entries;
@@ -499,7 +535,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   // ... and an XDP program that reads its ctx only through the specialised
   // data / data_end loads (the loader's escape analysis) keeps the ctx there
   // too: only the C++ tier reads it (48 B of LDS per lane)
-  const bool gctx = greg && b->ctx_kind == CTX_XDP && !p.needs_ctx && !im.d_tail_entry &&
+  const bool gctx = greg && kind == CTX_XDP && !p.needs_ctx && !im.d_tail_entry &&
                     !getenv("BPFTIME_AMD_LDS_CTX");
   bool prog_arrays = false, rings = false;
   for (uint32_t fd = 0; fd < kMaxFds; fd++)
@@ -520,7 +556,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   // syscall-agg 0.645 -> 0.61 ms; flow-hash, whose table fills the CU, is
   // best at 1024: 2048 sets 1.08 ms, 512 0.93, 1024 0.89)
   {
-    const FastForm &ff = b->ctx_kind == CTX_XDP ? im.fx : im.fr;
+    const FastForm &ff = kind == CTX_XDP ? im.fx : im.fr;
     uint32_t want = 0;
     if (prog.comb_entries) {
       want = 2 * kComb;
@@ -536,8 +572,8 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     if (block == kBigBlock) {
       const uint32_t e_min = prog.comb_entries ? kComb : 0;
       auto fits = [&](uint32_t lc) {
-        return bpftime_amd_occupancy(b->ctx_kind, prog.big_stack,
-                                     dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, e_min, lc, !gctx,
+        return bpftime_amd_occupancy(kind, prog.big_stack,
+                                     dyn_lds_for(kind, prog.big_stack, prog.stack_size, e_min, lc, !gctx,
                                                  kBigBlock),
                                      greg, kBigBlock) >= 1;
       };
@@ -547,7 +583,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
         if (!getenv("BPFTIME_AMD_LCACHE_SETS")) p.lcache = p.lcache ? lcache_sets() : 0;
       }
     }
-    p.fast = im.linked(b->ctx_kind == CTX_XDP, b->ctx_kind == CTX_XDP ? b->head : 0, p.stage, ordered, unwind_helper,
+    p.fast = im.linked(kind == CTX_XDP, kind == CTX_XDP ? b->head : 0, p.stage, ordered, unwind_helper,
                        p.lcache);
     if (!p.fast) {
       error = "device upload failed";
@@ -555,7 +591,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     }
   }
   auto dyn_of = [&](uint32_t e) {
-    return dyn_lds_for(b->ctx_kind, prog.big_stack, prog.stack_size, e, p.lcache, !gctx, block);
+    return dyn_lds_for(kind, prog.big_stack, prog.stack_size, e, p.lcache, !gctx, block);
   };
   if (p.comb_entries) {
     // the table's reach: a counter that finds no entry is a device atomic
@@ -568,7 +604,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     // 4 0.68, 1024 at 3 0.74; tail-call (per-CPU counters) 256 and 512 at 4
     // 1.63, 1024 2.41.  So: hint / 32 granules, a power of two in
     // [512, kCombMax] (1024 when the loader cannot bound the addresses)
-    const uint32_t hint = (b->ctx_kind == CTX_XDP ? im.fx : im.fr).comb_hint;
+    const uint32_t hint = (kind == CTX_XDP ? im.fx : im.fr).comb_hint;
     uint32_t e = 2 * kComb;
     if (hint == ~0u)
       e = 1024;
@@ -580,7 +616,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     // blocks / CU 1.32 ms, 1792 at 3 1.57, 1536 at 3 1.42 -- nor does reach
     // beyond hint / 32 at the same residency: flow-hash 3072 1.29,
     // syscall-agg 768 / 984 0.672 / 0.677 against 512 0.664)
-    while (e > kComb && bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn_of(e), greg, block) < 1) e /= 2;
+    while (e > kComb && bpftime_amd_occupancy(kind, prog.big_stack, dyn_of(e), greg, block) < 1) e /= 2;
     // one 1024-lane block per CU: a table that wants 2048 entries or more
     // takes the rest of the CU's LDS (multiples of 8 ways), since every
     // counter it misses is a memory-side atomic.  Measured (flow-hash, one
@@ -590,15 +626,16 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       static std::mutex fill_mu;
       static std::map<size_t, uint32_t> fill;  // (dyn_of(0), ctx kind) -> the largest table that fits
       std::lock_guard<std::mutex> g(fill_mu);
-      const size_t key = dyn_of(0) * 4 + b->ctx_kind;
+      const size_t key = dyn_of(0) * 4 + kind;
       auto it = fill.find(key);
       if (it == fill.end()) {
         uint32_t f = kCombMax;
-        while (f > e && bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn_of(f), greg, block) < 1) f -= 32;
+        while (f > e && bpftime_amd_occupancy(kind, prog.big_stack, dyn_of(f), greg, block) < 1) f -= 32;
         it = fill.emplace(key, f).first;
       }
       e = it->second > e ? it->second : e;
     }
+    // (an override that does not fit the CU fails the batch below, named)
     if (const char *ce = getenv("BPFTIME_AMD_COMB_ENTRIES")) e = (uint32_t)atoi(ce) & ~7u;
     p.comb_entries = e;
   }
@@ -610,16 +647,29 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   p.checked = (b->flags & EBPF_BATCH_UNCHECKED) ? 0 : 1;
   if (const char *d = getenv("BPFTIME_AMD_DBG")) p.dbg = (uint32_t)strtoul(d, nullptr, 0);
   if (p.dbg & 512) p.dbg_counts = dbg_counts();
-  if (hipMemsetAsync(err, 0, 4, s) != hipSuccess) {
-    error = "hipMemsetAsync failed";
+  // every block of the launch must fit the CU's LDS (env overrides of the
+  // table / cache sizes included): a launch that needs more fails, named,
+  // instead of running at an occupancy of zero
+  const size_t lds_need = dyn_of(p.comb_entries);
+  const int occ_fit = bpftime_amd_occupancy(kind, prog.big_stack, lds_need, greg, block);
+  if (occ_fit < 1) {
+    error = lds_fit_error(kind, prog.big_stack, prog.stack_size, p.comb_entries, p.lcache, !gctx, greg, block);
     return -1;
+  }
+  {
+    const hipError_t me = hipMemsetAsync(err, 0, 4, s);
+    if (me != hipSuccess) {
+      error = std::string("hipMemsetAsync failed: ") + hipGetErrorString(me) +
+              " (an earlier operation on this stream or device may have failed)";
+      return -1;
+    }
   }
   // program-side LPM trie updates / deletes: the device changes a trie only
   // in ORDERED batches (one lane, the reference's order: dev_helpers.hpp
   // lpm_update), the host takes the replica back afterwards (lpm_pull)
   std::vector<int> lpm_w;
   uint32_t lpm_updates = 0;
-  for (const auto &w : (b->ctx_kind == CTX_XDP ? im.fx : im.fr).lpm_writes) {
+  for (const auto &w : (kind == CTX_XDP ? im.fx : im.fr).lpm_writes) {
     lpm_updates += w.first == 2;
     if (!(b->flags & EBPF_BATCH_ORDERED)) {
       error = std::string(w.first == 2 ? "bpf_map_update_elem" : "bpf_map_delete_elem") +
@@ -676,9 +726,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       hipGetDeviceProperties(&prop, dev);
       cus = prop.multiProcessorCount;
     }
-    const size_t dyn = dyn_of(p.comb_entries);
-    int occ = bpftime_amd_occupancy(b->ctx_kind, prog.big_stack, dyn, greg, block);
-    if (occ < 1) occ = 1;
+    const int occ = occ_fit;
     uint64_t want = (b->count + block - 1) / block;
     // one wave per resident wave slot (x 1): every wave launch writes the
     // kernel's register spills (ScratchSize ~200 B / lane) once, and at x 4
@@ -809,7 +857,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       return -1;
     }
   }
-  hipError_t e = bpftime_amd_launch_interp(&p, b->ctx_kind, prog.big_stack, grid, ordered ? 1 : 0, block, s);
+  hipError_t e = bpftime_amd_launch_interp(&p, kind, prog.big_stack, grid, ordered ? 1 : 0, block, s);
   // (BPFTIME_AMD_SYNC_EACH: synchronize after every launch, naming the one that failed)
   const bool sync_each = getenv("BPFTIME_AMD_SYNC_EACH") != nullptr;
   auto step = [&](const char *what, hipError_t le) {
@@ -959,6 +1007,15 @@ struct ebpf_vm {
   Mi355xVm *impl;
 };
 
+namespace bpftime_amd {
+int vm_prog_flags(const ::ebpf_vm *vm) {
+  if (!vm || !vm->impl->loaded) return -1;
+  auto im = vm->impl->image();
+  if (!im) return -1;
+  return (im->prog.sets_retval ? kProgSetsRetval : 0) | (im->fr.stores_unit ? kProgStoresCtx : 0);
+}
+}  // namespace bpftime_amd
+
 extern "C" {
 
 struct ebpf_vm *ebpf_create(const char *vm_name) {
@@ -1047,7 +1104,7 @@ int ebpf_exec_batch(const struct ebpf_vm *vm, const struct ebpf_batch *batch) {
 }
 
 int ebpf_set_ctx_kind(struct ebpf_vm *vm, uint32_t ctx_kind) {
-  if (ctx_kind > CTX_SYSCALL) return -1;
+  if (ctx_kind > EBPF_CTX_SYSCALL_EXIT) return -1;
   vm->impl->ctx_kind = ctx_kind;
   return 0;
 }
@@ -1062,7 +1119,9 @@ int bpftime_amd_register_default_helpers(struct ebpf_vm *vm) {
            {65, "bpf_xdp_adjust_tail"},      {5, "bpf_ktime_get_ns"}, {7, "bpf_get_prandom_u32"},
            {131, "bpf_ringbuf_reserve"},     {132, "bpf_ringbuf_submit"}, {133, "bpf_ringbuf_discard"},
            {130, "bpf_ringbuf_output"},      {12, "bpf_tail_call"},
-           {1, "bpf_map_lookup_elem"},       {2, "bpf_map_update_elem"}, {3, "bpf_map_delete_elem"}};
+           {1, "bpf_map_lookup_elem"},       {2, "bpf_map_update_elem"}, {3, "bpf_map_delete_elem"},
+           {58, "bpf_override_return"},      {187, "bpf_set_retval"},
+           {14, "bpf_get_current_pid_tgid"}};
   int err = 0;
   for (auto &e : h) err |= ebpf_register(vm, e.id, e.name, nullptr);
   return err ? -1 : 0;

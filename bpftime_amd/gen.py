@@ -100,6 +100,31 @@ def syscall_records(n: int, seed: int = SEED_CFG5, first: int = 0) -> np.ndarray
     return recs.view(np.uint8).reshape(n, 64)
 
 
+def syscall_records_full(n: int, seed: int = SEED_CFG5, first: int = 0) -> np.ndarray:
+    """96-B replay records (include/bpftime_amd.h BPFTIME_AMD_SYSCALL_RECORD_FULL):
+    the config 5 enter record (id -1 instead for 0.5 %: the tracepoint's
+    interrupt marker), then trace_event_raw_sys_exit {ent 0, id, ret} with
+    ret a negative errno in [-133, -1] for 20 % of the records, else in
+    [0, 65535], then the caller's pid_tgid (tgid 1000 + [0, 64) << 32 | tid
+    tgid + [0, 4))."""
+    idx = np.arange(first, first + n, dtype=np.uint64)
+    enter = syscall_records(n, seed, first).view(np.uint64).reshape(n, 8).copy()
+    r = sm64(seed ^ 0x5555, idx)
+    ids = np.where((r % np.uint64(200)) == np.uint64(1), np.uint64(0xFFFFFFFFFFFFFFFF), enter[:, 1])
+    enter[:, 1] = ids
+    rr = sm64(seed ^ 0x7777, idx)
+    neg = (np.uint64(0) - (np.uint64(1) + (rr >> np.uint64(8)) % np.uint64(133)))
+    ret = np.where((rr % np.uint64(5)) == np.uint64(0), neg, (rr >> np.uint64(16)) & np.uint64(0xFFFF))
+    recs = np.zeros((n, 12), dtype=np.uint64)
+    recs[:, :8] = enter
+    recs[:, 9] = ids
+    recs[:, 10] = ret
+    rp = sm64(seed ^ 0x8888, idx)
+    tgid = np.uint64(1000) + rp % np.uint64(64)
+    recs[:, 11] = (tgid << np.uint64(32)) | (tgid + (rp >> np.uint64(8)) % np.uint64(4))
+    return recs.view(np.uint8).reshape(n, 96)
+
+
 # ---------------------------------------------------------------------------
 # config 1: 1k-packet pcap (990 x 64 B Eth/IPv4/UDP + 10 runts, seed 1)
 # ---------------------------------------------------------------------------

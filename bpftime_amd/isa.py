@@ -59,6 +59,9 @@ BPF_FUNC_trace_printk = 6
 BPF_FUNC_get_prandom_u32 = 7
 BPF_FUNC_get_smp_processor_id = 8
 BPF_FUNC_tail_call = 12
+BPF_FUNC_get_current_pid_tgid = 14
+BPF_FUNC_override_return = 58
+BPF_FUNC_set_retval = 187
 BPF_FUNC_csum_diff = 28
 BPF_FUNC_xdp_adjust_head = 44
 BPF_FUNC_xdp_adjust_tail = 65

@@ -16,7 +16,10 @@ semantics after libbpf relocation / CO-RE, not byte-identical clang output.
 """
 from __future__ import annotations
 
-from .isa import (Asm, BPF_ANY, BPF_FUNC_map_lookup_elem, BPF_FUNC_map_update_elem,
+import struct
+
+from .isa import (Asm, BPF_ANY, BPF_FUNC_get_current_pid_tgid, BPF_FUNC_map_lookup_elem,
+                  BPF_FUNC_map_update_elem, BPF_FUNC_override_return, BPF_FUNC_set_retval,
                   BPF_FUNC_ringbuf_output, BPF_NOEXIST, ATOMIC_ADD, XDP_DROP, XDP_PASS, XDP_TX, XDP_ABORTED)
 
 ETH_P_IP_LE = 0x0008  # htons(0x0800) as read by a little-endian ldxh
@@ -194,6 +197,123 @@ def syscall_agg(counts_fd: int) -> bytes:
     a.ldx(8, 2, 0, 8)                     # val->total_ns += args[2]
     a.add64(2, "r7")
     a.stx(8, 0, 8, "r2")
+    a.label("ret")
+    a.mov64(0, 0)
+    a.exit()
+    return a.assemble()
+
+
+# syscount's const volatile options (example/tracing/syscount/syscount.bpf.c:
+# 12-17) as its .rodata: bool filter_cg @0, count_by_process @1,
+# measure_latency @2, filter_failed @3, int filter_errno @4, pid_t
+# filter_pid @8 (12 B, an ARRAY map of one value, read through lddw map_val)
+SYSCOUNT_RODATA = 12
+EEXIST = 17
+
+
+def syscount_rodata(count_by_process: bool = False, filter_failed: bool = False, filter_errno: int = 0,
+                    filter_pid: int = 0) -> bytes:
+    return struct.pack("<BBBBii", 0, int(count_by_process), 0, int(filter_failed), filter_errno, filter_pid)
+
+
+def syscount_exit(data_fd: int, rodata_fd: int) -> bytes:
+    """syscount's sys_exit program (example/tracing/syscount/syscount.bpf.c:
+    49-87) over ``trace_event_raw_sys_exit`` {ent, id@8, ret@16}: skip id == -1
+    (an interrupt), filter_pid on the caller's pid, filter_failed (ret >= 0
+    skipped) and filter_errno (ret != -filter_errno skipped) from .rodata;
+    key = count_by_process ? pid : id; ``bpf_map_lookup_or_try_init`` of
+    data (maps.bpf.h: lookup, NOEXIST update of a zeroed data_t, an error
+    other than -EEXIST gives up, lookup again); ``count = count + 1``.
+    measure_latency (ktime, the start map) is not compiled in: SURVEY.md
+    Appendix B.11.  data: HASH u32 -> data_t 32 B {u64 count, u64 total_ns,
+    char comm[16]}.  Returns 0."""
+    a = Asm()
+    a.mov64(6, "r1")
+    a.call(BPF_FUNC_get_current_pid_tgid)
+    a.mov64(8, "r0").alu64("rsh", 8, 32)  # pid = id >> 32
+    a.ldx(8, 7, 6, 8)                     # args->id
+    a.jmp("jeq", 7, -1, "ret")
+    a.ld_map_value(9, rodata_fd, 0)
+    a.ldx(4, 2, 9, 8)                     # filter_pid
+    a.jmp("jeq", 2, 0, "nopid")
+    a.jmp32("jne", 8, "r2", "ret")        # (pid_t) pid != filter_pid
+    a.label("nopid")
+    a.ldx(8, 3, 6, 16)                    # args->ret
+    a.ldx(1, 2, 9, 3)                     # filter_failed
+    a.jmp("jeq", 2, 0, "nofail")
+    a.jmp("jsge", 3, 0, "ret")
+    a.label("nofail")
+    a.ldx(4, 2, 9, 4)                     # filter_errno
+    a.jmp("jeq", 2, 0, "noerr")
+    a.alu64("lsh", 2, 32).alu64("arsh", 2, 32).neg64(2)  # (long) -filter_errno
+    a.jmp("jne", 3, "r2", "ret")
+    a.label("noerr")
+    a.ldx(1, 2, 9, 1)                     # count_by_process
+    a.mov64(1, "r7")
+    a.jmp("jeq", 2, 0, "key")
+    a.mov64(1, "r8")
+    a.label("key")
+    a.stx(4, 10, -4, "r1")                # u32 key
+    a.ld_map_fd(1, data_fd)
+    a.mov64(2, "r10").add64(2, -4)
+    a.call(BPF_FUNC_map_lookup_elem)
+    a.jmp("jne", 0, 0, "have")
+    a.st(8, 10, -40, 0)                   # static const struct data_t zero
+    a.st(8, 10, -32, 0)
+    a.st(8, 10, -24, 0)
+    a.st(8, 10, -16, 0)
+    a.ld_map_fd(1, data_fd)
+    a.mov64(2, "r10").add64(2, -4)
+    a.mov64(3, "r10").add64(3, -40)
+    a.mov64(4, BPF_NOEXIST)
+    a.call(BPF_FUNC_map_update_elem)
+    a.jmp("jeq", 0, 0, "again")
+    a.jmp("jne", 0, -EEXIST, "ret")       # err && err != -EEXIST: give up
+    a.label("again")
+    a.ld_map_fd(1, data_fd)
+    a.mov64(2, "r10").add64(2, -4)
+    a.call(BPF_FUNC_map_lookup_elem)
+    a.jmp("jeq", 0, 0, "ret")
+    a.label("have")
+    a.ldx(8, 1, 0, 0)                     # val->count = val->count + 1
+    a.add64(1, 1)
+    a.stx(8, 0, 0, "r1")
+    a.label("ret")
+    a.mov64(0, 0)
+    a.exit()
+    return a.assemble()
+
+
+def inject_enter(mod: int, value: int = -1) -> bytes:
+    """error-inject's sys_enter program (example/error-inject/
+    error_inject_syscall.bpf.c:12-22) made deterministic for replays (B.11):
+    ``bpf_override_return(ctx, value)`` when args[2] % mod == 0 instead of on
+    an even ``bpf_get_prandom_u32``.  Returns 0."""
+    a = Asm()
+    a.ldx(8, 2, 1, 32)                    # args[2]
+    a.alu64("mod", 2, mod)
+    a.jmp("jne", 2, 0, "ret")
+    a.mov64(2, value)
+    a.call(BPF_FUNC_override_return)
+    a.label("ret")
+    a.mov64(0, 0)
+    a.exit()
+    return a.assemble()
+
+
+def exit_clamp(value: int = 0) -> bytes:
+    """A sys_exit program that turns a failed call's return into ``value``
+    with ``bpf_set_retval`` (bpf_helper.cpp:1282-1286) when ret < 0 and id
+    is odd.  Returns 0."""
+    a = Asm()
+    a.ldx(8, 3, 1, 16)                    # args->ret
+    a.jmp("jsge", 3, 0, "ret")
+    a.ldx(8, 2, 1, 8)
+    a.jmp("jset", 2, 1, "set")
+    a.ja("ret")
+    a.label("set")
+    a.mov64(1, value)
+    a.call(BPF_FUNC_set_retval)
     a.label("ret")
     a.mov64(0, 0)
     a.exit()

@@ -16,7 +16,8 @@ import numpy as np
 from . import isa
 from ._lib import BpfLinkCreateArgs, BpfMapAttr, EbpfBatch, lib
 
-CTX_RAW, CTX_XDP, CTX_SYSCALL = 0, 1, 2
+CTX_RAW, CTX_XDP, CTX_SYSCALL, CTX_SYSCALL_EXIT = 0, 1, 2, 3
+SYSCALL_RECORD, SYSCALL_RECORD_FULL = 64, 96  # include/bpftime_amd.h replay records
 BATCH_SYNC, BATCH_ORDERED, BATCH_UNCHECKED, BATCH_SYS_NR, BATCH_TIMED = 0x1, 0x2, 0x4, 0x8, 0x10
 
 
@@ -322,6 +323,30 @@ def prog_create(code: bytes, name: str, prog_type: int, fd: int = -1) -> int:
 def link_create(prog_fd: int, target: int, attach_type: int, fd: int = -1) -> int:
     a = BpfLinkCreateArgs(prog_fd=prog_fd, target_fd=target, attach_type=attach_type)
     return lib().bpftime_link_create(fd, C.byref(a))
+
+
+def syscall_attach(prog_fd: int, sys_nr: int, enter: bool = True) -> int:
+    """A program on the sys_enter / sys_exit tracepoint of sys_nr (-1: every
+    syscall; syscall_trace_attach_impl.cpp:121-166): the attach id."""
+    i = lib().bpftime_amd_syscall_attach_ex(prog_fd, sys_nr, 1 if enter else 0)
+    if i < 0:
+        raise EbpfError(f"syscall attach failed: {_err()}")
+    return i
+
+
+def syscall_detach(i: int) -> int:
+    return lib().bpftime_amd_syscall_detach(i)
+
+
+def syscall_dispatch(records: DeviceBuffer, n: int, record_size: int = SYSCALL_RECORD_FULL,
+                     out: Optional[DeviceBuffer] = None, flags: int = BATCH_SYNC, stream: int = 0) -> int:
+    """dispatch_syscall over n recorded calls (64-B enter or 96-B enter + exit
+    records); out (i64 per record) receives what each call returns."""
+    rc = lib().bpftime_amd_syscall_dispatch_records(records.ptr, n, record_size, out.ptr if out else None,
+                                                     flags, stream or None)
+    if rc < 0:
+        raise EbpfError(f"syscall dispatch failed: {_err()}")
+    return rc
 
 
 def xdp_links() -> list:

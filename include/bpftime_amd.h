@@ -87,10 +87,10 @@ int bpftime_progs_create(int fd, const void *insns, size_t insn_cnt, const char 
 int bpftime_link_create(int fd, struct bpf_link_create_args *args);
 /* ---- perf events (bpftime_shm.hpp:351-380; bpf_perf_event_handler,
  * runtime/src/handler/perf_event_handler.hpp:161-215) ----
- * The targets a link or BPF_PROG_ATTACH names.  A syscall sys_enter
- * tracepoint drives the replay dispatch (bpftime_amd_syscall_dispatch); the
- * other kinds (sys_exit tracepoints, uprobes, software events) are kept as
- * records so the reference's state imports, exports and links unchanged.
+ * The targets a link or BPF_PROG_ATTACH names.  A syscall sys_enter or
+ * sys_exit tracepoint drives the replay dispatch (bpftime_amd_syscall_dispatch);
+ * the other kinds (uprobes, software events) are kept as records so the
+ * reference's state imports, exports and links unchanged.
  *
  * A syscall sys_enter tracepoint perf event by syscall number (what
  * perf_event_open of syscalls:sys_enter_<nr>, or raw_syscalls:sys_enter for
@@ -258,15 +258,47 @@ void bpftime_object_close(struct bpftime_object *obj);
 int64_t bpftime_amd_ringbuf_fetch(int fd, void *out, uint64_t cap, uint64_t *used);
 
 /* ---- syscall tracepoint dispatch (csrc/syscall_dispatch.cpp) ----
- * syscall_trace_attach_impl.cpp:18-95: attach a program to the sys_enter
- * tracepoint of `sys_nr` (-1: every syscall); a replay batch of n 64-B
- * trace_event_raw_sys_enter records (device memory) runs the per-syscall
- * programs on their records, then the global ones, skipping exit /
- * exit_group; r0 is ignored.  Returns the failed-unit count with
- * EBPF_BATCH_SYNC in flags, else 0; -1 on errors. */
+ * syscall_trace_attach_impl.cpp:18-95 over recorded syscalls in device memory.
+ *
+ * attach (create_attach_with_ebpf_callback, :121-166): a program on the
+ * sys_enter (is_enter = 1) or sys_exit (0) tracepoint of `sys_nr` in
+ * [0, 512), or of every syscall (-1); an attach id, or -1 with errno EINVAL
+ * (not a program, sys_nr out of range) or the load error.
+ * bpftime_amd_syscall_attach(prog, nr) = bpftime_amd_syscall_attach_ex(prog, nr, 1).
+ *
+ * Replay records: BPFTIME_AMD_SYSCALL_RECORD (64 B) = trace_event_raw_sys_enter
+ * {ent = 0, id, args[6]}; BPFTIME_AMD_SYSCALL_RECORD_FULL (96 B) = that, then
+ * trace_event_raw_sys_exit {ent = 0, id, ret} (24 B) at +64, then the
+ * calling thread's u64 pid_tgid (tgid << 32 | tid) at +88: the enter ctx and
+ * the exit ctx as dispatch_syscall builds them (:57-66, :80-85), each the unit
+ * its programs run on in place, and what bpf_get_current_pid_tgid returns to
+ * them (bpf_helper.cpp:330-348; 64-B records: the dispatching thread's).  Per record
+ * (dispatch_syscall :18-95): exit (60) / exit_group (231) run nothing and
+ * return ret; the per-syscall enter programs, then the global ones; if one of
+ * them called bpf_override_return / bpf_set_retval the record returns that
+ * value and its exit programs do not run; else the per-syscall exit programs,
+ * then the global ones, and the record returns ret, or the value an exit
+ * program set.  Ids outside [0, 512) (the reference indexes its callback
+ * arrays with them, undefined there) run only global programs.  Each program
+ * runs once over the batch (records are not interleaved across programs:
+ * equal to the per-record order whenever the programs' map effects commute);
+ * a program that may store into its ctx runs on a copy of the records, as
+ * each reference callback runs on its own copy (:43-45).
+ *
+ * dispatch_records: `out_rets` (device i64 per record, nullable) receives the
+ * value dispatch_syscall would return (64-B records have no ret: 0 unless
+ * overridden).  64-B records with sys_exit programs attached are refused
+ * (EINVAL).  Returns the failed-unit count summed over the programs with
+ * EBPF_BATCH_SYNC, else 0; -1 on errors (bpftime_amd_last_error).
+ * bpftime_amd_syscall_dispatch(r, n, f, s) = dispatch_records(r, n, 64, NULL, f, s). */
+#define BPFTIME_AMD_SYSCALL_RECORD 64
+#define BPFTIME_AMD_SYSCALL_RECORD_FULL 96
 int bpftime_amd_syscall_attach(int prog_fd, int64_t sys_nr);   /* attach id or -1 */
+int bpftime_amd_syscall_attach_ex(int prog_fd, int64_t sys_nr, int is_enter);
 int bpftime_amd_syscall_detach(int id);
 int64_t bpftime_amd_syscall_dispatch(const void *records, uint64_t n, uint32_t flags, void *stream);
+int64_t bpftime_amd_syscall_dispatch_records(const void *records, uint64_t n, uint32_t record_size,
+                                             int64_t *out_rets, uint32_t flags, void *stream);
 
 /* ---- attach plugins (attach/base_attach_impl/base_attach_impl.hpp:24-71,
  * attach/simple_attach_impl/simple_attach_impl.cpp:7-55; csrc/attach.cpp) ----
@@ -345,6 +377,20 @@ int bpftime_amd_gen_flow(void *dev, uint32_t *lens, uint64_t n, uint64_t stride,
 /* config 5 records (gen.py syscall_records), 64 B each. */
 int bpftime_amd_gen_syscall(void *dev, uint64_t n, uint64_t seed, uint64_t first, const double *cdf,
                             uint32_t support, void *stream);
+/* 96-B replay records (gen.py syscall_records_full): config 5's enter record
+ * (id -1 for 0.5 %), then the exit ctx {0, id, ret}, then a pid_tgid. */
+int bpftime_amd_gen_syscall_full(void *dev, uint64_t n, uint64_t seed, uint64_t first, const double *cdf,
+                                 uint32_t support, void *stream);
+/* Static LDS bytes of the interpreter kernel for a launch shape (its
+ * attribute; the restated sum without a device): with the dynamic part
+ * (common.hpp dyn_lds_for) what a block needs of the CU's 160 KiB. */
+size_t bpftime_amd_static_lds(uint32_t kind, bool big_stack, bool gregs, uint32_t block);
+/* Dynamic + static LDS bytes of an interpreter block (ctx kind, 512-B scratch
+ * stack, per-lane stack bytes, combining-table entries, lookup-cache sets,
+ * ctx in LDS, register copy in global memory, lanes): a launch whose block
+ * needs more than 160 KiB fails with a named error (vm_api.cpp). */
+size_t bpftime_amd_lds_bytes(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
+                             uint32_t lcache_sets, bool ctx_lds, bool gregs, uint32_t block);
 
 #ifdef __cplusplus
 }

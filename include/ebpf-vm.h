@@ -80,6 +80,11 @@ ebpf_jit_fn ebpf_load_aot_object(struct ebpf_vm *vm, const void *buf, size_t buf
 #define EBPF_CTX_RAW 0     /* r1 = unit memory, r2 = length */
 #define EBPF_CTX_XDP 1     /* r1 = struct xdp_md_userspace (runtime/extension/userspace_xdp.h:6-17) */
 #define EBPF_CTX_SYSCALL 2 /* r1 = 64-B trace_event_raw_sys_enter; nr 60/231 skipped */
+/* r1 = 24-B trace_event_raw_sys_exit {ent = 0, id, ret} (syscall_trace_attach_impl.hpp:31-36,
+ * built at syscall_trace_attach_impl.cpp:80-85), r2 = 24; nr 60/231 skipped.  The unit is the
+ * exit half of a 96-B replay record (data = records + 64, stride 96) or any record with
+ * that layout at `stride`. */
+#define EBPF_CTX_SYSCALL_EXIT 3
 
 #define EBPF_BATCH_SYNC 0x1    /* wait for completion; return the failed-unit count */
 #define EBPF_BATCH_ORDERED 0x2 /* one lane, units in index order (exact sequential semantics) */
@@ -112,6 +117,23 @@ struct ebpf_batch {
 	const struct ebpf_xdp_desc *descs;
 	uint64_t umem_bytes;
 	int64_t sys_nr;          /* with EBPF_BATCH_SYS_NR: the syscall nr a per-syscall program is attached to */
+	/* Syscall dispatch state (bpftime_amd_syscall_dispatch_records sets these; NULL / 0
+	 * otherwise).  Per unit a u32 of flags -- bit 0: an enter program overrode the
+	 * syscall's return (bpf_override_return 58 / bpf_set_retval 187,
+	 * base_attach_impl.hpp:76-105), bit 1: an exit program did -- and the i64 the
+	 * dispatch returns for the record (the override value when one was set).
+	 * sys_phase 1 (enter) / 2 (exit) is the bit those helpers set; an exit batch skips
+	 * units whose bit 0 is set (syscall_trace_attach_impl.cpp:70-72).  Without
+	 * sys_state helpers 58 / 187 fail the unit (the reference throws when no return
+	 * callback is set). */
+	uint32_t *sys_state;
+	int64_t *sys_ret;
+	uint32_t sys_phase;
+	/* bpf_get_current_pid_tgid (14, bpf_helper.cpp:330-348) is the calling thread's
+	 * tgid << 32 | tid: in a syscall replay the recorded caller's, a u64 at this
+	 * offset from each unit (96-B records: +88 of the record); 0: the thread that
+	 * launches the batch */
+	int32_t pid_tgid_off;
 };
 
 /* linux/if_xdp.h struct xdp_desc */

@@ -108,6 +108,127 @@ int orc_run_syscall(struct orc_vm *vm, const uint8_t *recs, uint64_t n, uint64_t
 	return 0;
 }
 
+struct trace_event_raw_sys_exit { /* syscall_trace_attach_impl.hpp:31-36 */
+	uint16_t type;
+	uint8_t flags, preempt_count;
+	int32_t pid;
+	int64_t id;
+	int64_t ret;
+};
+
+/* syscall_trace_attach_impl.hpp:92-98: attach entries by id; the callback
+ * sets are std::set of entry pointers, kept here in attach order */
+#define ORC_SYS_MAX 256
+static struct {
+	int id;
+	struct orc_vm *vm;
+	int64_t sys_nr;
+	int enter;
+} g_sys[ORC_SYS_MAX];
+static int g_sys_n, g_sys_next = 1;
+
+int orc_sys_attach(struct orc_vm *vm, int64_t sys_nr, int is_enter)
+{
+	if (sys_nr >= 512 || sys_nr < -1 || g_sys_n == ORC_SYS_MAX) /* :134-139 */
+		return -22;
+	g_sys[g_sys_n].id = g_sys_next;
+	g_sys[g_sys_n].vm = vm;
+	g_sys[g_sys_n].sys_nr = sys_nr;
+	g_sys[g_sys_n].enter = is_enter != 0;
+	g_sys_n++;
+	return g_sys_next++;
+}
+
+int orc_sys_detach(int id) /* :96-119 */
+{
+	for (int i = 0; i < g_sys_n; i++)
+		if (g_sys[i].id == id) {
+			memmove(&g_sys[i], &g_sys[i + 1], (size_t)(g_sys_n - i - 1) * sizeof(g_sys[0]));
+			g_sys_n--;
+			return 0;
+		}
+	return -2;
+}
+
+void orc_sys_reset(void)
+{
+	g_sys_n = 0;
+	g_sys_next = 1;
+}
+
+/* run_callbacks (:41-53) over one callback set: each on its own ctx copy,
+ * exec failures ignored */
+static void run_set(int enter, int global, int64_t nr, const void *ctx, size_t len)
+{
+	for (int i = 0; i < g_sys_n; i++) {
+		if (g_sys[i].enter != enter || (global ? g_sys[i].sys_nr != -1 : g_sys[i].sys_nr != nr))
+			continue;
+		uint8_t copy[64];
+		memcpy(copy, ctx, len);
+		uint64_t v;
+		(void)orc_vm_exec(g_sys[i].vm, copy, len, &v);
+	}
+}
+
+static int any_set(int enter, int64_t nr)
+{
+	for (int i = 0; i < g_sys_n; i++)
+		if (g_sys[i].enter == enter && (g_sys[i].sys_nr == -1 || (nr >= 0 && g_sys[i].sys_nr == nr)))
+			return 1;
+	return 0;
+}
+
+int orc_sys_dispatch(const uint8_t *recs, uint64_t n, uint32_t rec_size, int64_t *out)
+{
+	if (rec_size != 64 && rec_size != 96)
+		return -22;
+	for (uint64_t i = 0; i < n; i++) {
+		const uint8_t *r = recs + i * rec_size;
+		const struct trace_event_raw_sys_enter *er = (const void *)r;
+		const int64_t nr = er->id;
+		/* the "original syscall" is the recorded one: its ret */
+		const int64_t ret = rec_size == 96 ? ((const struct trace_event_raw_sys_exit *)(r + 64))->ret : 0;
+		if (nr == 231 /*__NR_exit_group*/ || nr == 60 /*__NR_exit*/) { /* :25-26 */
+			if (out)
+				out[i] = ret;
+			continue;
+		}
+		const int64_t pnr = nr >= 0 && nr < 512 ? nr : -2; /* no per-syscall set */
+		if (rec_size == 96) /* the recorded caller (bpf_helper.cpp:330-348) */
+			orc_pid_tgid_recorded(1, *(const uint64_t *)(r + 88));
+		orc_retval.active = 1; /* :35-40 */
+		orc_retval.overridden = 0;
+		if (any_set(1, pnr)) { /* :55-67 */
+			struct trace_event_raw_sys_enter ctx;
+			memset(&ctx, 0, sizeof(ctx));
+			ctx.id = nr;
+			memcpy(ctx.args, er->args, sizeof(ctx.args));
+			run_set(1, 0, pnr, &ctx, sizeof(ctx));
+			run_set(1, 1, pnr, &ctx, sizeof(ctx));
+		}
+		orc_retval.active = 0; /* :68-72 */
+		if (orc_retval.overridden) {
+			if (out)
+				out[i] = orc_retval.value;
+			continue;
+		}
+		orc_retval.active = 1; /* :73-78 */
+		if (any_set(0, pnr)) { /* :80-89 */
+			struct trace_event_raw_sys_exit ctx;
+			memset(&ctx, 0, sizeof(ctx));
+			ctx.id = nr;
+			ctx.ret = ret;
+			run_set(0, 0, pnr, &ctx, sizeof(ctx));
+			run_set(0, 1, pnr, &ctx, sizeof(ctx));
+		}
+		orc_retval.active = 0; /* :90-94 */
+		if (out)
+			out[i] = orc_retval.overridden ? orc_retval.value : ret;
+	}
+	orc_pid_tgid_recorded(0, 0);
+	return 0;
+}
+
 double orc_time_xdp(struct orc_vm *vm, uint8_t *base, uint64_t n, uint64_t stride, uint32_t fixed_len,
 		    uint32_t *verdicts, int pin_cpu)
 {

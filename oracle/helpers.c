@@ -13,6 +13,9 @@
  *   6 trace_printk                    :64-76   (orc_vm_register_trace_helpers;
  *   14 get_current_pid_tgid           :330-348  the host-process helpers of
  *                                               tools/aot/example/malloc.json)
+ *   58 override_return, 187 set_retval attach/base_attach_impl/
+ *                                     base_attach_impl.hpp:76-105 (the thread's
+ *                                     return callback; orc_sys_dispatch sets it)
  * Registration order follows the kernel + shm-maps helper groups
  * (bpf_helper.cpp:1177-1401).
  */
@@ -234,8 +237,20 @@ void orc_set_pid_tgid(uint64_t v)
 	g_pid_set = 1;
 }
 
+/* a replayed call's recorded caller (orc_sys_dispatch, 96-B records) */
+static int g_pid_rec_on;
+static uint64_t g_pid_rec;
+
+void orc_pid_tgid_recorded(int on, uint64_t v)
+{
+	g_pid_rec_on = on;
+	g_pid_rec = v;
+}
+
 static uint64_t h_pid_tgid(uint64_t a, uint64_t b, uint64_t c, uint64_t d, uint64_t e)
 {
+	if (g_pid_rec_on)
+		return g_pid_rec;
 	if (g_pid_set)
 		return g_pid_tgid;
 	return ((uint64_t)getpid() << 32) | (uint32_t)syscall(SYS_gettid);
@@ -356,6 +371,37 @@ static uint64_t h_tail_call(uint64_t ctx, uint64_t prog_array, uint64_t index, u
 	return rv;
 }
 
+/* base_attach_impl.hpp:18-19 curr_thread_override_return_callback: set by
+ * orc_sys_dispatch around each phase (syscall_trace_attach_impl.cpp:35-40,
+ * :73-78); the callback records {overridden, value}.  Unset, the helpers
+ * throw (:86-90, :99-103), which ends the program: orc_helper_abort makes
+ * the interpreter fail the exec. */
+struct orc_retval_cb orc_retval = {0, 0, 0};
+int orc_helper_abort;
+
+static uint64_t set_retval(uint64_t v)
+{
+	if (!orc_retval.active) {
+		orc_helper_abort = 1;
+		return 0;
+	}
+	orc_retval.overridden = 1;
+	orc_retval.value = (int64_t)v;
+	return 0;
+}
+
+static uint64_t h_override_return(uint64_t ctx, uint64_t v, uint64_t a, uint64_t b, uint64_t c)
+{
+	(void)ctx, (void)a, (void)b, (void)c;
+	return set_retval(v);
+}
+
+static uint64_t h_set_retval(uint64_t v, uint64_t a, uint64_t b, uint64_t c, uint64_t d)
+{
+	(void)a, (void)b, (void)c, (void)d;
+	return set_retval(v);
+}
+
 int orc_vm_register_default_helpers(struct orc_vm *vm)
 {
 	int err = 0;
@@ -375,5 +421,9 @@ int orc_vm_register_default_helpers(struct orc_vm *vm)
 	err |= orc_vm_register(vm, 1, "bpf_map_lookup_elem", h_lookup);
 	err |= orc_vm_register(vm, 2, "bpf_map_update_elem", h_update);
 	err |= orc_vm_register(vm, 3, "bpf_map_delete_elem", h_delete);
+	/* kernel helper group, bpf_helper.cpp:1264-1286 */
+	err |= orc_vm_register(vm, 58, "bpf_override_return", h_override_return);
+	err |= orc_vm_register(vm, 187, "bpf_set_retval", h_set_retval);
+	err |= orc_vm_register(vm, 14, "bpf_get_current_pid_tgid", h_pid_tgid);
 	return err ? -1 : 0;
 }

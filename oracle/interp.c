@@ -495,6 +495,11 @@ int orc_vm_exec(struct orc_vm *vm, void *mem, size_t mem_len, uint64_t *ret)
 		case 0x85: {
 			orc_helper_fn fn = vm->ext[d.imm];
 			reg[0] = fn(reg[1], reg[2], reg[3], reg[4], reg[5]);
+			if (orc_helper_abort) { /* the helper threw (helpers.c set_retval) */
+				orc_helper_abort = 0;
+				vm->insn_count += count;
+				return -1;
+			}
 			if (d.imm == vm->unwind_idx && reg[0] == 0) {
 				vm->insn_count += count;
 				*ret = reg[0];

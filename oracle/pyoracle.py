@@ -72,6 +72,10 @@ def lib():
             "orc_run_raw": (C.c_int, [vp, vp, u64, u64, u32, vp]),
             "orc_run_syscall": (C.c_int, [vp, vp, u64, vp, vp]),
             "orc_time_xdp": (C.c_double, [vp, vp, u64, u64, u32, vp, C.c_int]),
+            "orc_sys_attach": (C.c_int, [vp, C.c_int64, C.c_int]),
+            "orc_sys_detach": (C.c_int, [C.c_int]),
+            "orc_sys_reset": (None, []),
+            "orc_sys_dispatch": (C.c_int, [vp, u64, u32, vp]),
         }
         for k, (r, a) in sig.items():
             f = getattr(l, k)
@@ -243,6 +247,40 @@ class OracleMap:
 
 def reset() -> None:
     lib().orc_maps_reset()
+    lib().orc_sys_reset()
+
+
+class OracleSyscallDispatch:
+    """syscall_trace_attach_impl (attach/syscall_trace_attach_impl/src/
+    syscall_trace_attach_impl.cpp:18-166) over recorded calls: programs on
+    sys_enter / sys_exit tracepoints, dispatched record by record."""
+
+    def __init__(self):
+        self.vms = {}
+
+    def attach(self, code: bytes, sys_nr: int, enter: bool = True) -> int:
+        v = OracleVM()
+        v.load(code)
+        i = lib().orc_sys_attach(v.h, sys_nr, 1 if enter else 0)
+        if i > 0:
+            self.vms[i] = v  # keeps the VM alive while attached
+        return i
+
+    def detach(self, i: int) -> int:
+        rc = lib().orc_sys_detach(i)
+        self.vms.pop(i, None)
+        return rc
+
+    def dispatch(self, recs: np.ndarray) -> np.ndarray:
+        """recs: (n, 64) or (n, 96) uint8; returns what dispatch_syscall
+        returns per record (int64)."""
+        n, rs = recs.shape
+        recs = np.ascontiguousarray(recs)
+        out = np.zeros(n, dtype=np.int64)
+        rc = lib().orc_sys_dispatch(recs.ctypes.data, n, rs, out.ctypes.data)
+        if rc < 0:
+            raise ValueError(f"orc_sys_dispatch: {rc}")
+        return out
 
 
 def prog_create(fd: int, code: bytes) -> int:

@@ -7,9 +7,10 @@
 #include <random>
 
 // maps.cpp's only references outside itself (the perf-event attach path)
-extern "C" int bpftime_amd_syscall_attach(int, int64_t) { return -1; }
+extern "C" int bpftime_amd_syscall_attach_ex(int, int64_t, int) { return -1; }
 extern "C" int bpftime_amd_syscall_detach(int) { return -1; }
 extern "C" int bpftime_amd_tracepoint_resolve(int32_t, int64_t *, int *) { return -1; }
+void bpftime_amd::syscall_detach_all() {}
 
 using bpftime_amd::LpmTrie;
 

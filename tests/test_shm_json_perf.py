@@ -143,7 +143,8 @@ def test_malloc_program_on_the_oracle(tmp_path):
     assert len(code) == 8 * ref["5"]["attr"]["cnt"] == 8 * 55
     vm = po.OracleVM()
     rc, msg = vm.try_load(code)
-    assert rc < 0 and msg == "call to nonexistent function 14 at PC 0"   # compat_ubpf.cpp:83-94
+    # bpf_get_current_pid_tgid (14) is a default helper; bpf_trace_printk is not
+    assert rc < 0 and msg == "call to nonexistent function 6 at PC 20"   # compat_ubpf.cpp:83-94
     vm = po.OracleVM()
     vm.register_trace_helpers()
     vm.load(code)
@@ -162,8 +163,9 @@ def test_malloc_program_on_the_oracle(tmp_path):
 def test_perf_event_kinds_roundtrip(clean, tmp_path):
     """Every perf event kind the reference imports (:130-180) re-created
     with its fields and exported as the reference exports it (:66-95);
-    links to them stay records (a sys_exit tracepoint: the replay holds
-    enter records only); an unsupported type fails the file."""
+    links to the non-tracepoint kinds stay records (a sys_exit tracepoint
+    link attaches to the dispatch: tests/test_gpu_syscall_exit.py); an
+    unsupported type fails the file."""
     l = clean
     code = programs.kat_mul()
     prog = {"type": "bpf_prog_handler", "name": "p", "attr": {"type": 5, "insns": code.hex(), "cnt": len(code) // 8}}
@@ -177,7 +179,7 @@ def test_perf_event_kinds_roundtrip(clean, tmp_path):
               "attr": {"type": 1008, "pid": -1, "offset": 64, "_module_name": "/bin/y"}},
         "7": {"type": "bpf_perf_event_handler", "enabled": True,
               "attr": {"type": 1, "pid": -1, "cpu": 3, "sample_type": 1024, "config": 10}},
-        "8": {"type": "bpf_link_handler", "attr": {"prog_fd": 3, "target_fd": 4}},
+        "8": {"type": "bpf_link_handler", "attr": {"prog_fd": 3, "target_fd": 7}},
         "9": {"type": "bpf_link_handler", "attr": {"prog_fd": 3, "target_fd": 5}},
     }
     p = tmp_path / "in.json"
@@ -227,7 +229,7 @@ def test_attach_fds_become_links(clean, tmp_path):
         "4": {"type": "bpf_perf_event_handler", "enabled": False,
               "attr": {"type": 6, "pid": -1, "offset": 8, "ref_ctr_off": 0, "_module_name": "m"}},
         "5": {"type": "bpf_perf_event_handler", "enabled": False,
-              "attr": {"type": 2, "pid": -1, "tracepoint_id": TP_EXIT}},
+              "attr": {"type": 2, "pid": -1, "tracepoint_id": 99999}},   # (no such id here: a record)
     }
     p = tmp_path / "in.json"
     p.write_text(json.dumps(state))
@@ -248,7 +250,9 @@ def test_perf_link_checks(clean):
     """bpftime_shm_internal.cpp:566-600 / :282-315: a BPF_PERF_EVENT link
     needs a perf event target (EBADF, also libbpf's target_fd -1 probe);
     BPF_PROG_ATTACH needs a perf fd and a prog fd (ENOENT); an unresolvable
-    tracepoint id fails the attach (EEXIST)."""
+    tracepoint id leaves the link a record that runs nothing, as the
+    reference's add_bpf_prog_attach_target / add_bpf_link, which check the
+    handler kinds only and resolve the id when the agent attaches."""
     l = clean
     code = programs.kat_mul()
     pfd = l.bpftime_progs_create(-1, code, len(code) // 8, b"p", 5)
@@ -256,8 +260,14 @@ def test_perf_link_checks(clean):
     assert l.bpftime_link_create(-1, C.byref(a)) < 0 and C.get_errno() in (0, errno.EBADF)
     tfd = l.bpftime_tracepoint_create(-1, -1, 5555)
     assert tfd > 0 and l.bpftime_is_perf_event_fd(tfd)
-    assert l.bpftime_attach_perf_to_bpf(tfd, pfd) < 0                  # id 5555 does not resolve
-    assert l.bpftime_attach_perf_to_bpf(pfd, pfd) < 0                  # not a perf fd
+    lfd = l.bpftime_attach_perf_to_bpf(tfd, pfd)                       # id 5555 does not resolve here
+    assert lfd > 0 and l.bpftime_amd_link_attached(lfd) == 0
+    assert l.bpftime_attach_perf_to_bpf(pfd, pfd) < 0 and C.get_errno() == errno.ENOENT  # not a perf fd
+    a = _lib.BpfLinkCreateArgs(prog_fd=pfd, target_fd=tfd, attach_type=41)
+    lfd2 = l.bpftime_link_create(-1, C.byref(a))
+    assert lfd2 > 0 and l.bpftime_amd_link_attached(lfd2) == 0
+    a = _lib.BpfLinkCreateArgs(prog_fd=tfd, target_fd=tfd, attach_type=41)
+    assert l.bpftime_link_create(-1, C.byref(a)) < 0 and C.get_errno() == errno.EBADF  # not a program
     assert l.bpftime_amd_link_perf(-1, pfd, tfd) > 0                   # the JSON import's record
 
 
@@ -289,7 +299,7 @@ def test_reference_export_imports_on_device(clean, tmp_path):
     assert l.bpftime_is_map_fd(3) and l.bpftime_is_map_fd(4) and l.bpftime_is_prog_fd(5)
     assert l.bpftime_is_perf_event_fd(6) and l.bpftime_amd_link_attached(7) == 0
     assert export(l, tmp_path) == ref
-    with pytest.raises(dev.EbpfError, match="function 14 at PC 0"):
+    with pytest.raises(dev.EbpfError, match="function 6 at PC 20"):
         dev.prog_instantiate(5)
 
 
@@ -297,9 +307,10 @@ def test_reference_export_imports_on_device(clean, tmp_path):
 def test_tracepoint_state_runs_the_dispatch(fresh_oracle, fresh_runtime, clean, tmp_path):
     """A syscall-agg state attached to raw_syscalls:sys_enter (global) and a
     read counter attached to sys_enter_read, imported from JSON by
-    tracepoint id, replayed through bpftime_amd_syscall_dispatch bit-exact
-    against the oracle; the export round-trips and re-imports into the same
-    attachments; a sys_exit link stays a record."""
+    tracepoint id, and the read counter also attached to sys_exit_read,
+    replayed through bpftime_amd_syscall_dispatch_records over 96-B records
+    bit-exact against the oracle's dispatch; the export round-trips and
+    re-imports into the same attachments."""
     po, dev, l = fresh_oracle, fresh_runtime, clean
     l.bpftime_amd_set_tracefs_events(str(tmp_path / "events").encode())
     code = programs.syscall_agg(3)
@@ -323,24 +334,27 @@ def test_tracepoint_state_runs_the_dispatch(fresh_oracle, fresh_runtime, clean, 
     p = tmp_path / "state.json"
     p.write_text(json.dumps(state))
     n = 60000
-    recs = gen.syscall_records(n)
-    ids_col = recs.view(np.uint64).reshape(n, 8)[:, 1]
+    recs = gen.syscall_records_full(n)
+    ids_col = recs.view(np.int64).reshape(n, 12)[:, 1]
 
     def run_and_check():
-        assert l.bpftime_amd_link_attached(7) == 1 and l.bpftime_amd_link_attached(12) == 1
-        assert l.bpftime_amd_link_attached(14) == 0
+        assert [l.bpftime_amd_link_attached(f) for f in (7, 12, 14)] == [1, 1, 1]
         po.reset()
         om = po.OracleMap(isa.BPF_MAP_TYPE_HASH, 4, 32, 8192, fd=3)
         orm = po.OracleMap(isa.BPF_MAP_TYPE_ARRAY, 4, 8, 1, fd=9)
         d = dev.DeviceBuffer.from_array(recs)
-        assert l.bpftime_amd_syscall_dispatch(d.ptr, n, dev.BATCH_SYNC, None) == 0
-        for c, sel in ((rd, recs[ids_col == 0]), (code, recs)):
-            v = po.OracleVM()
-            v.load(c)
-            v.run_syscall(sel.copy())
+        # a sys_exit program is attached: 64-B records hold no exit ctx
+        assert l.bpftime_amd_syscall_dispatch(d.ptr, n, dev.BATCH_SYNC, None) == -1
+        assert dev.syscall_dispatch(d, n) == 0
+        od = po.OracleSyscallDispatch()
+        od.attach(code, -1, enter=True)
+        od.attach(rd, 0, enter=True)
+        od.attach(rd, 0, enter=False)
+        od.dispatch(recs)
         assert dev.Map.from_fd(3).hash_items() == om.items()
         assert dev.Map.from_fd(9).lookup(b"\0\0\0\0") == orm.lookup(b"\0\0\0\0")
-        assert struct.unpack("<Q", orm.lookup(b"\0\0\0\0"))[0] == int((ids_col == 0).sum()) > 0
+        # the read counter runs at sys_enter_read and at sys_exit_read
+        assert struct.unpack("<Q", orm.lookup(b"\0\0\0\0"))[0] == 2 * int((ids_col == 0).sum()) > 0
         assert len(om.items()) > 100
 
     assert l.bpftime_import_global_shm_from_json(str(p).encode()) == 0, l.bpftime_amd_last_error()
@@ -362,5 +376,5 @@ def test_tracepoint_state_runs_the_dispatch(fresh_oracle, fresh_runtime, clean, 
     _lib.lib().bpftime_close(7)
     d = dev.DeviceBuffer.from_array(recs)
     before = dev.Map.from_fd(3).hash_items()
-    assert l.bpftime_amd_syscall_dispatch(d.ptr, n, dev.BATCH_SYNC, None) == 0
+    assert dev.syscall_dispatch(d, n) == 0
     assert dev.Map.from_fd(3).hash_items() == before
