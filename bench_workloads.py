@@ -3,6 +3,7 @@ size, device-resident, one GPU:
 
   python bench.py --workload flow-hash     # 2^24 frames in 2048-B slots, HASH map
   python bench.py --workload syscall-agg   # 2^25 trace_event_raw_sys_enter records
+  python bench.py --workload syscount      # 2^25 96-B records, sys_exit through the dispatch
 
 The headline line (xdp-counter) stays in bench.py.  Inputs are generated on
 the device by csrc/gen.hip from the same seeded streams as bpftime_amd/gen.py;
@@ -227,6 +228,68 @@ def syscall_agg(args, dev, gen, isa, programs):
     }
 
 
+def syscount(args, dev, gen, isa, programs):
+    """syscount's sys_exit program (example/tracing/syscount/syscount.bpf.c:
+    49-87) attached to raw_syscalls:sys_exit, replayed through the dispatch
+    (bpftime_amd_syscall_dispatch_records) over 2^25 device-resident 96-B
+    records (enter ctx, trace_event_raw_sys_exit, caller pid_tgid)."""
+    n = 1 << (args.log2n if args.log2n_set else 25)
+    dev.reset_runtime()
+    data = dev.Map(isa.BPF_MAP_TYPE_HASH, 4, 32, 8192, name="data")
+    ro = dev.Map(isa.BPF_MAP_TYPE_ARRAY, 4, programs.SYSCOUNT_RODATA, 1, name="syscount.rodata")
+    ro.update(b"\0" * 4, programs.syscount_rodata())
+    code = programs.syscount_exit(data.fd, ro.fd)
+    pfd = dev.prog_create(code, "sys_exit", 5)
+    dev.syscall_attach(pfd, -1, enter=False)
+    cdf = gen.zipf_cdf(335, 1.2)
+    dcdf = dev.DeviceBuffer.from_array(cdf)
+    recs = dev.DeviceBuffer(n * 96)
+    if dev.lib().bpftime_amd_gen_syscall_full(recs.ptr, n, gen.SEED_CFG5, 0, dcdf.ptr, 335, None):
+        raise SystemExit("syscall generator failed")
+
+    def step():
+        dev.syscall_dispatch(recs, n, flags=0)
+
+    wall, kern_s = _timed(dev, step, args.steps, args.warmup)
+    runs = args.steps + args.warmup
+    # host recomputation of the histogram from the same seeded stream
+    idx = np.arange(n, dtype=np.uint64)
+    ids = gen.zipf_ids(gen.SEED_CFG5, 0, n, 335, 1.2).astype(np.int64)
+    r = gen.sm64(gen.SEED_CFG5 ^ 0x5555, idx)
+    ids = np.where((r % np.uint64(100)) == np.uint64(0), np.where((r >> np.uint64(9)) & np.uint64(1), 60, 231), ids)
+    ids = np.where((r % np.uint64(200)) == np.uint64(1), -1, ids)
+    del r
+    live = ~np.isin(ids, [60, 231, -1])
+    hist = np.bincount(ids[live], minlength=335).astype(np.uint64)
+    got = data.hash_items()
+    ok_map = len(got) == int((hist > 0).sum()) and all(
+        struct.unpack("<Q", got.get(struct.pack("<I", int(k)), b"\0" * 32)[:8])[0] == int(hist[k]) * runs
+        for k in np.nonzero(hist)[0])
+    algo = 24.0  # SURVEY.md §8d per record: id + ret of the exit ctx, the caller's pid_tgid
+    cpu = None
+    if not args.no_cpu_baseline:
+        from bench import cpu_baseline
+        cpu = cpu_baseline(args.cpu_seconds, "syscount")
+    value = n * args.steps / wall / 1e6
+    achieved = algo * n / kern_s / 1e9
+    return {
+        "metric": "device-resident Mrec/s, syscount sys_exit prog through the syscall dispatch",
+        "value": round(value, 3), "unit": "Mrec/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic (seeded splitmix64 96-B records: id Zipf(1.2) over 0..334 + 1% exit/exit_group + "
+                "0.5% id -1, 20% negative rets, 64 callers; seed 0x5EED0005)",
+        "config": {"workload": "syscount sys_exit (BASELINE configs[4]'s attach point) over 2^%d device-resident "
+                               "96-B records, HASH map max 8192" % int(np.log2(n)), "records": n},
+        "parity": {"per_id_totals_exact": ok_map, "keys": len(got), "ok": ok_map},
+        **_dbg_lcache(dev),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic("syscount", n),
+                     "kernel_avg_ms": round(kern_s * 1e3, 4), "algo_bytes_per_rec": algo},
+        "cpu_baseline": cpu,
+    }
+
+
 def _lpm_routes(rng, nroutes):
     """Every /8 (so each address has a route) plus random /12../28 prefixes;
     values 1..3 = DROP / PASS / TX."""
@@ -435,5 +498,5 @@ def run(args):
     from bpftime_amd import gen, isa, programs
     from bpftime_amd import vm as dev
     fn = {"flow-hash": flow_hash, "syscall-agg": syscall_agg, "lpm-route": lpm_route,
-          "ringbuf-sample": ringbuf_sample, "tail-call": tail_call}[args.workload]
+          "ringbuf-sample": ringbuf_sample, "tail-call": tail_call, "syscount": syscount}[args.workload]
     print(json.dumps(fn(args, dev, gen, isa, programs)))

@@ -165,7 +165,7 @@ def handler_ids():
         for cc in JCC:
             for k in ("R", "I"):
                 ids.append(f"J{w}_{cc}_{k}")
-    ids += ["TAIL", "TRET"]  # rare: after the hot handlers
+    ids += ["TAIL", "TRET", "CALL_PID", "KLDX"]  # rare / new: after the hot handlers
     return ids
 
 
@@ -891,6 +891,34 @@ class Gen:
         else:
             self.e("v_add_co_u32_e32 v60, vcc, %[head], v52")
         self.e("v_addc_co_u32_e32 v61, vcc, 0, v53, vcc")
+        self.idx_off()
+        self.next_seq()
+
+    def call_pid(self):
+        """bpf_get_current_pid_tgid (bpf_helper.cpp:330-348) of a recorded
+        syscall: r0 = the u64 at slot + w7 (link_fast: KParams pid_off, the
+        caller's pid_tgid in the replay record).  r1-r5 are left as they
+        are, as the C++ tier's helper call leaves them."""
+        self.e("v_add_co_u32_e32 v48, vcc, s47, v52",
+               "v_addc_co_u32_e32 v49, vcc, 0, v53, vcc",
+               f"global_load_dwordx2 v[{R0}:{R0 + 1}], v[48:49], off",
+               "s_waitcnt vmcnt(0)")
+        self.next_seq()
+
+    def ldxk(self):
+        """dst = a load from a constant address nothing in the program
+        writes (loader.cpp const_loads: inside an ARRAY map's storage, e.g.
+        a .rodata value), through the scalar cache: w[2:3] the address
+        rounded down to 4 bytes, w7 0 (8 bytes at a 4-aligned address) or
+        width << 16 | bit offset (s_bfe_u64)."""
+        k = self.label("ldxk")
+        self.e("s_load_dwordx2 s[52:53], s[42:43], 0x0",
+               "s_waitcnt lgkmcnt(0)",
+               "s_cmp_eq_u32 s47, 0", f"s_cbranch_scc1 {k}",
+               "s_bfe_u64 s[52:53], s[52:53], s47",
+               f"{k}:")
+        self.idx("s44", "DST")
+        self.e(f"v_mov_b32_e32 v{R0}, s52", f"v_mov_b32_e32 v{R0 + 1}, s53")
         self.idx_off()
         self.next_seq()
 
@@ -2175,6 +2203,10 @@ class Gen:
                 self.tail_call()
             elif name == "TRET":
                 self.tail_ret()
+            elif name == "CALL_PID":
+                self.call_pid()
+            elif name == "KLDX":
+                self.ldxk()
             elif name.startswith("RMWD"):
                 self.rmwd(int(name[4]), name[6])
             elif name.startswith("RMWMV"):

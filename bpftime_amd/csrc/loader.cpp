@@ -1053,6 +1053,69 @@ static std::vector<bool> counter_nodefer(const std::vector<DInsn> &p, const std:
   return nodefer;
 }
 
+// Loads at a constant address (an lddw map_val immediate + offsets) inside
+// an ARRAY / PER-CPU ARRAY map's storage that nothing in the program may
+// write -- no store, atomic or counter add that may alias it, no helper that
+// writes that map -- are the same for every unit of a launch (host writes
+// reach the device between launches, and the kernel starts with a fresh
+// scalar cache): they read through the scalar cache (F_KLDX).  A .rodata
+// value (libbpf's const volatile globals) is the common case: syscount's
+// filters.  kimm[i] = the 4-aligned address, kaux[i] = 0 (8 bytes) or
+// width << 16 | bit offset.
+static void const_loads(const std::vector<DInsn> &p, const std::vector<uint8_t> &lddw_src,
+                        const std::vector<std::vector<PVal>> &in, std::vector<int64_t> &kimm,
+                        std::vector<int32_t> &kaux) {
+  const uint32_t n = (uint32_t)p.size();
+  kimm.assign(n, 0);
+  kaux.assign(n, -1);
+  auto reached = [&](uint32_t i) { return !(in[i][0].kind == P_UNDEF && in[i][1].kind == P_UNDEF); };
+  std::vector<Loc> writes;
+  for (uint32_t i = 0; i < n; i++) {
+    if (!reached(i)) continue;
+    const DInsn &d = p[i];
+    const int64_t sz = 1 << ((d.aux >> A_SIZE_SHIFT) & 3);
+    const std::vector<PVal> &st = in[i];
+    switch (d.op) {
+      case X_ST: case X_STX: case X_ATOMIC: case X_RMW_ADD:
+        writes.push_back(loc_of(p, st[d.dst], d.off, sz));
+        break;
+      case X_CALL:
+        switch (d.hi) {
+          case 1: case 5: case 7: case 8: case 14: case 28: case 58: case 187: case 130:
+          case 131: case 132: case 133: case 44: case 65:
+            break;  // no array-map writes (ring memory, the unit's ctx, dispatch state)
+          case 2: case 3:  // the values of the map in r1
+            if (st[1].kind == P_MAPFD) writes.push_back(Loc{Loc::MAPVAL, st[1].id, 0, kUnknownLen});
+            else writes.push_back(Loc{Loc::ANY, -1, 0, 0});
+            break;
+          case 189:
+            writes.push_back(loc_of(p, st[3], 0, kUnknownLen));
+            break;
+          default:
+            if (d.hi != kRetHelper) writes.push_back(Loc{Loc::ANY, -1, 0, 0});
+        }
+        break;
+      default:
+        break;
+    }
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    const DInsn &d = p[i];
+    if (d.op != X_LDX || !reached(i)) continue;
+    const PVal b = in[i][d.src];
+    if (b.kind != P_CONST || b.id < 0 || (size_t)b.id >= lddw_src.size() || lddw_src[b.id] != 2) continue;
+    const int64_t sz = 1 << ((d.aux >> A_SIZE_SHIFT) & 3);
+    const Loc me = loc_of(p, b, d.off, sz);
+    const uint64_t a = (uint64_t)me.lo;
+    if (a % sz != 0 || (sz == 8 && a % 4 != 0) || !in_array_storage(a, (uint32_t)sz)) continue;
+    bool hit = false;
+    for (const Loc &w : writes) hit = hit || may_alias(me, w);
+    if (hit) continue;
+    kimm[i] = (int64_t)(a & ~3ull);
+    kaux[i] = sz == 8 ? 0 : (int32_t)(((8 * sz) << 16) | (8 * (a & 3)));
+  }
+}
+
 // A hash element's bucket can change owner while a launch runs: LRU inserts
 // evict, and a deleted key's bucket is reused.  A counter add held until its
 // block ends could then land in another key's value, so adds into such maps
@@ -1297,6 +1360,9 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
     out.comb_hint = hint >= ~0u ? ~0u : (uint32_t)hint;
   }
   if (lo.multi_entry && xdp) tail_save_masks(prog, in, lo.stack_size, out);
+  std::vector<int64_t> kimm;
+  std::vector<int32_t> kaux;
+  if (!getenv("BPFTIME_AMD_NO_KLDX")) const_loads(prog, lo.lddw_src, in, kimm, kaux);
   uint32_t nspec = 0;
   bool ctx_escapes = false;
   const bool big_stack = lo.big_stack;
@@ -1435,6 +1501,11 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
         f.hoff = 4 + 4 * (d.op == X_LDX ? ldm[si] : stxm[si]);
         nspec++;
       }
+    } else if (d.op == X_LDX && i < kaux.size() && kaux[i] >= 0) {
+      f.hoff = 4 + 4 * F_KLDX;
+      f.imm = kimm[i];
+      f.aux = kaux[i];
+      nspec++;
     }
   }
   // adjacent 8-byte atomic adds through one map-value base at off / off + 8
@@ -1532,8 +1603,15 @@ static void link_staged(const FastForm &f, uint32_t head, uint32_t stage, bool o
                         const std::vector<DInsn> &prog, std::vector<FInsn> &out);
 
 void link_fast(const FastForm &f, uint32_t head, uint32_t stage, bool ordered, const std::vector<DInsn> &prog,
-               std::vector<FInsn> &out, int32_t unwind_idx, uint32_t lc_sets) {
+               std::vector<FInsn> &out, int32_t unwind_idx, uint32_t lc_sets, uint32_t pid_off) {
   link_staged(f, head, stage, ordered, prog, out);
+  // bpf_get_current_pid_tgid of a recorded syscall: a load from the unit
+  if (pid_off && pid_off < 256)
+    for (size_t i = 0; i < prog.size() && i < out.size(); i++)
+      if (prog[i].op == X_CALL && prog[i].hi == 14 && unwind_idx != 14) {
+        out[i].hoff = 4 + 4 * F_CALL_PID;
+        out[i].aux = (int32_t)pid_off;
+      }
   // the launch's lookup-cache set count (vm_api.cpp) into the lookups that use it
   for (FInsn &x : out)
     if ((x.w1 & FW_LCACHE) && lc_sets) x.dst_x2 = lc_sets;

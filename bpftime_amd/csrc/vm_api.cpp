@@ -84,15 +84,19 @@ struct Image {
     if (d_tail_slots) hipFree(d_tail_slots);
     for (auto &kv : links) hipFree(kv.second);
   }
-  const FInsn *linked(bool xdp, uint32_t head, uint32_t stage, bool ordered, int32_t unwind_idx, uint32_t lc_sets) {
+  const FInsn *linked(bool xdp, uint32_t head, uint32_t stage, bool ordered, int32_t unwind_idx, uint32_t lc_sets,
+                      int32_t pid_off) {
     std::lock_guard<std::mutex> g(link_mu);
-    const bool uw = unwind_idx == 1;  // the only helper with asm handlers an unwind index changes
+    // (the helpers with asm handlers an unwind index changes: lookup, pid_tgid)
+    const bool uw = unwind_idx == 1, uwp = unwind_idx == 14;
+    const uint32_t po = pid_off > 0 && pid_off < 256 && !uwp ? (uint32_t)pid_off : 0;
     const uint64_t key = ((uint64_t)xdp << 63) | ((uint64_t)ordered << 62) | ((uint64_t)uw << 61) |
-                         ((uint64_t)(lc_sets & 0x1fff) << 47) | ((uint64_t)stage << 40) | (stage ? head : 0);
+                         ((uint64_t)(lc_sets & 0x1fff) << 47) | ((uint64_t)stage << 40) | ((uint64_t)po << 32) |
+                         (stage ? head : 0);
     auto it = links.find(key);
     if (it != links.end()) return it->second;
     std::vector<FInsn> out;
-    link_fast(xdp ? fx : fr, head, stage, ordered, prog.prog, out, uw ? 1 : -1, lc_sets);
+    link_fast(xdp ? fx : fr, head, stage, ordered, prog.prog, out, uw ? 1 : -1, lc_sets, po);
     FInsn *d = nullptr;
     const size_t bytes = out.size() * sizeof(FInsn);
     if (hipMalloc((void **)&d, bytes) != hipSuccess) return nullptr;
@@ -584,7 +588,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       }
     }
     p.fast = im.linked(kind == CTX_XDP, kind == CTX_XDP ? b->head : 0, p.stage, ordered, unwind_helper,
-                       p.lcache);
+                       p.lcache, b->pid_tgid_off);
     if (!p.fast) {
       error = "device upload failed";
       return -1;

@@ -33,3 +33,38 @@ def test_cpu_baseline_ringbuf_leg_wraps():
     assert r.returncode == 0, r.stderr
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["ok"], out
+
+
+def test_union_of_timed_intervals():
+    sys.path.insert(0, ROOT)
+    import bench_cpu
+    assert bench_cpu.union_seconds([]) == 0.0
+    assert bench_cpu.union_seconds([(0, 1), (0.5, 2), (3, 4)]) == pytest.approx(3.0)
+    assert bench_cpu.union_seconds([(2, 3), (0, 1)]) == pytest.approx(2.0)
+
+
+def test_serialized_leg_is_not_counted_as_parallel():
+    """under the GPU box's CPU quota the workers of a leg did
+    not run side by side, and units / the longest single loop made serial
+    loops look parallel (2,108 Mpps on 15.6 busy cores).  Two workers whose
+    loops never overlap (the second starts after the first ended) must give
+    about one worker's rate, with concurrency about 1."""
+    sys.path.insert(0, ROOT)
+    import bench_cpu
+    cores = sorted(os.sched_getaffinity(0))
+    c = cores[:2] if len(cores) > 1 else cores * 2
+    v1, _, _, ok1, _, conc1 = bench_cpu.leg("xdp-counter", c[:1], 0.5)
+    v2, union2, _, ok2, _, conc2 = bench_cpu.leg("xdp-counter", c, 0.5, stagger=3.0)
+    assert ok1 and ok2
+    assert conc2 < 1.15 and union2 > 0.9
+    assert v2 < 1.3 * v1
+
+
+def test_syscount_leg():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench_cpu.py"), "--workload", "syscount",
+                        "--seconds", "0.3", "--cores", "2"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["ok"] and out["unit"] == "Mrec/s" and out["value"] > 0
+    # the chosen leg never claims more per usable CPU than 1.1 x one core
+    assert out["value"] / out["cores"] <= 1.1 * out["single_core"]["value"] or out["cores"] == 1
