@@ -897,9 +897,21 @@ class Gen:
     def call_pid(self):
         """bpf_get_current_pid_tgid (bpf_helper.cpp:330-348) of a recorded
         syscall: r0 = the u64 at slot + w7 (link_fast: KParams pid_off, the
-        caller's pid_tgid in the replay record).  r1-r5 are left as they
-        are, as the C++ tier's helper call leaves them."""
-        self.e("v_add_co_u32_e32 v48, vcc, s47, v52",
+        caller's pid_tgid in the replay record), from the unit's staged
+        bytes when the window holds it (w3 = 1, w2 = its dword index), else
+        a load.  r1-r5 are left as they are, as the C++ tier's helper call
+        leaves them."""
+        glb = self.label("pidg")
+        self.e("s_cmp_eq_u32 s80, 0", f"s_cbranch_scc1 {glb}",
+               "s_cmp_eq_u32 s43, 0", f"s_cbranch_scc1 {glb}",
+               "s_waitcnt vmcnt(0)")
+        self.idx("s42", "SRC0")
+        self.e(f"v_mov_b32 v44, v{STG}", f"v_mov_b32 v45, v{STG + 1}")
+        self.idx_off()
+        self.e(f"v_mov_b32 v{R0}, v44", f"v_mov_b32 v{R0 + 1}, v45")
+        self.next_seq()
+        self.e(f"{glb}:",
+               "v_add_co_u32_e32 v48, vcc, s47, v52",
                "v_addc_co_u32_e32 v49, vcc, 0, v53, vcc",
                f"global_load_dwordx2 v[{R0}:{R0 + 1}], v[48:49], off",
                "s_waitcnt vmcnt(0)")

@@ -1611,6 +1611,9 @@ void link_fast(const FastForm &f, uint32_t head, uint32_t stage, bool ordered, c
       if (prog[i].op == X_CALL && prog[i].hi == 14 && unwind_idx != 14) {
         out[i].hoff = 4 + 4 * F_CALL_PID;
         out[i].aux = (int32_t)pid_off;
+        // (inside the staged window: its dword index, and a flag)
+        const bool staged = pid_off % 4 == 0 && pid_off + 8 <= stage;
+        out[i].imm = staged ? (int64_t)(pid_off / 4) | (1ll << 32) : 0;
       }
   // the launch's lookup-cache set count (vm_api.cpp) into the lookups that use it
   for (FInsn &x : out)
