@@ -177,6 +177,7 @@ SIGNATURES = [
     ("bpftime_amd_event_create", C.c_void_p, []),
     ("bpftime_amd_event_destroy", None, [C.c_void_p]),
     ("bpftime_amd_event_record", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("bpftime_amd_stream_wait_event", C.c_int, [C.c_void_p, C.c_void_p]),
     ("bpftime_amd_event_elapsed_ms", C.c_float, [C.c_void_p, C.c_void_p]),
     ("bpftime_amd_last_error", C.c_char_p, []),
     ("bpftime_amd_gen_syscall_full", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p,

@@ -830,7 +830,8 @@ __device__ void rb_close(const DMap &m, RbStage st) {
   __hip_atomic_fetch_add(G64(m.data + 192), (uint64_t)0 - kRbStageRec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ uint64_t rb_cas_reserve(const DMap &m, uint64_t total, RbStage st, int32_t fd) {
+__device__ __forceinline__ uint64_t rb_cas_reserve(const DMap *maps, const DMap &m, uint64_t total, RbStage st,
+                                                   int32_t fd) {
   // returns the old producer position, or ~0 if total does not fit.  The
   // loop ends by a successful CAS or a failed room check, as the
   // reference's spin-locked reserve does: the consumer position does not
@@ -838,7 +839,10 @@ __device__ __forceinline__ uint64_t rb_cas_reserve(const DMap &m, uint64_t total
   // synchronizes the device first), every lost CAS means another
   // reservation moved the producer position by >= 8 bytes, and promises
   // only come back.  A room that only the outstanding promises take is
-  // waited for (this block's own promise returned first, rb_close).
+  // waited for, this block's own promise returned first (rb_close) -- on
+  // whichever ring it is: a block waiting on ring B while it holds a
+  // promise on ring A could otherwise wait for a block that waits on A
+  // (ADVICE r04), so no block waits holding a promise.
   uint32_t backoff = 1;
   const uint64_t bound = (uint64_t)m.max_entries / 8 + (1u << 20);
   for (uint64_t spin = 0; spin < bound; spin++) {
@@ -847,7 +851,11 @@ __device__ __forceinline__ uint64_t rb_cas_reserve(const DMap &m, uint64_t total
     if (room < (int64_t)total) {
       const uint64_t prom = __hip_atomic_load(G64(m.data + 192), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (!prom) return ~0ull;  // full, with nothing promised: the serial answer
-      if (st.buf && st.lds->fd == fd) rb_close(m, st);  // (a launch without staging waits only)
+      // (a launch without staging waits only)
+      if (st.buf) {
+        const int32_t pfd = __hip_atomic_load(&st.lds->fd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (pfd >= 0 && pfd < (int32_t)kMaxFds) rb_close(pfd == fd ? m : maps[pfd], st);
+      }
     } else {
       unsigned long long e = p;
       if (__hip_atomic_compare_exchange_strong(G64(m.data + 128), &e, p + total, __ATOMIC_RELAXED,
@@ -862,7 +870,8 @@ __device__ __forceinline__ uint64_t rb_cas_reserve(const DMap &m, uint64_t total
   return ~0ull;
 }
 
-__device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size, RbStage st) {
+// The calling lanes that reserve from one ring (rb_reserve groups them).
+__device__ uint64_t rb_reserve_ring(const DMap *maps, uint64_t fd, uint64_t size, RbStage st) {
   const bool ok = fd < kMaxFds && maps[fd < kMaxFds ? fd : 0].type == MT_RINGBUF &&
                   !(size & (RB_BUSY | RB_DISCARD));
   const DMap m = maps[ok ? fd : 0];
@@ -948,20 +957,35 @@ __device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size, RbS
       if (sum <= kRbWaveMax && rb_room(m) >= (int64_t)(sum + kRbSlack))
         base = __hip_atomic_fetch_add(G64(m.data + 128), sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else
-        base = rb_cas_reserve(m, sum, st, (int32_t)fd);
+        base = rb_cas_reserve(maps, m, sum, st, (int32_t)fd);
     }
     base = __shfl(base, leader);
     if (base != ~0ull) pos = base + before;
   }
   if (pos == ~0ull && fits) {  // lane by lane (full ring, mixed rings)
     for (uint64_t rest = __ballot(1); rest; rest &= rest - 1)
-      if ((uint32_t)__builtin_ctzll(rest) == me) pos = rb_cas_reserve(m, total, st, (int32_t)fd);
+      if ((uint32_t)__builtin_ctzll(rest) == me) pos = rb_cas_reserve(maps, m, total, st, (int32_t)fd);
   }
   if (pos == ~0ull) return 0;
   const uint64_t mask = m.max_entries - 1, d = m.data + 256;
   __hip_atomic_store(G32(d + (pos & mask)), (uint32_t)size | RB_BUSY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(G32(d + (pos & mask) + 4), (uint32_t)fd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return d + ((pos + RB_HDR) & mask);
+}
+
+// bpf_ringbuf_reserve (bpf_helper.cpp:468-474) for the calling lanes: one
+// group per distinct ring fd, each reserved the wave way (a wave whose lanes
+// write two rings took the lane-by-lane path for all of them: one
+// contended compare-and-swap per record)
+__device__ uint64_t rb_reserve(const DMap *maps, uint64_t fd, uint64_t size, RbStage st) {
+  const uint64_t all = __ballot(1);
+  uint64_t done = 0, out = 0;
+  while (all & ~done) {
+    const uint64_t f0 = __shfl(fd, (uint32_t)__builtin_ctzll(all & ~done));
+    if (fd == f0) out = rb_reserve_ring(maps, fd, size, st);
+    done |= __ballot(fd == f0);
+  }
+  return out;
 }
 
 // fd < 0: the ring named by the record header's fd, ptr[-1]

@@ -42,7 +42,7 @@ int Runtime::ensure_device() {
   }
   device = dev;
   const char *mb = getenv("BPFTIME_AMD_ARENA_MB");
-  arena_size = (uint64_t)(mb ? atoll(mb) : 256) << 20;
+  arena_size = (uint64_t)(mb ? atoll(mb) : 1024) << 20;  // (288 GB of HBM: two 64-MiB staged rings and more fit)
   if (hipMalloc((void **)&arena, arena_size) != hipSuccess) {
     set_error("hipMalloc(arena) failed");
     arena = nullptr;

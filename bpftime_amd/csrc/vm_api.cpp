@@ -1267,6 +1267,9 @@ void bpftime_amd_event_destroy(void *ev) {
 int bpftime_amd_event_record(void *ev, void *stream) {
   return hipEventRecord((hipEvent_t)ev, (hipStream_t)stream) == hipSuccess ? 0 : -1;
 }
+int bpftime_amd_stream_wait_event(void *stream, void *ev) {
+  return hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0) == hipSuccess ? 0 : -1;
+}
 float bpftime_amd_event_elapsed_ms(void *start, void *stop) {
   float ms = -1;
   if (hipEventSynchronize((hipEvent_t)stop) != hipSuccess) return -1;

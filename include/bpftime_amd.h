@@ -359,6 +359,8 @@ void bpftime_amd_host_free(void *p);
 void *bpftime_amd_event_create(void);
 void bpftime_amd_event_destroy(void *ev);
 int bpftime_amd_event_record(void *ev, void *stream);
+/* work queued on `stream` after this waits for the event's last record */
+int bpftime_amd_stream_wait_event(void *stream, void *ev);
 float bpftime_amd_event_elapsed_ms(void *start, void *stop);
 const char *bpftime_amd_last_error(void);
 

@@ -314,3 +314,50 @@ def test_device_ringbuf_staged_ring_fills_within_launch(fresh_oracle, fresh_runt
     ok = int((got == 2).sum())
     assert ok == len(drecs) and ok + int((got == 1).sum()) == n
     assert ok == fit
+
+
+def two_ring_sampler(fd_a, fd_b):
+    """bpf_ringbuf_output of the first 16 bytes to ring A when byte1 is odd,
+    else ring B; verdict PASS on success, DROP when the ring had no room."""
+    a = Asm().ldx(8, 2, 1, 0).ldx(8, 3, 1, 8).mov64(0, 2)
+    a.mov64(4, "r2").add64(4, 16).jmp("jgt", 4, "r3", "out")
+    a.mov64(6, "r2").ldx(1, 8, 6, 1).alu64("and", 8, 1)
+    a.jmp("jeq", 8, 0, "b")
+    a.ld_map_fd(1, fd_a).ja("go")
+    a.label("b").ld_map_fd(1, fd_b)
+    a.label("go").mov64(2, "r6").mov64(3, 16).mov64(4, 0).call(130)
+    a.mov64(1, "r0").mov64(0, 2).jmp("jeq", 1, 0, "out").mov64(0, 1)
+    a.label("out").exit()
+    return a.assemble()
+
+
+@pytest.mark.gpu
+def test_device_two_staged_rings_fill_within_launch(fresh_oracle, fresh_runtime):
+    """a block holding its staging promise on one ring and
+    waiting for room on another could wait for a block doing the reverse.
+    One program fills two 64 MiB staged rings in one parallel launch: the
+    launch ends, and each ring accepts exactly room / record size, every
+    accepted record delivered (ringbuf_map.cpp:262-295)."""
+    po, dev = fresh_oracle, fresh_runtime
+    size = 1 << 26
+    ra = dev.Map(RB, 0, 0, size, fd=7)
+    rb = dev.Map(RB, 0, 0, size, fd=8)
+    n = 3 << 21                                              # ~75 MB of 24-B records per ring
+    pk = gen.xdp_packets(n, seed=33)
+    vm = dev.VM()
+    vm.load(two_ring_sampler(ra.fd, rb.fd))
+    d = dev.DeviceBuffer.from_array(pk)
+    dv = dev.DeviceBuffer(4 * n)
+    assert vm.exec_batch(dev.CTX_XDP, d, n, 64, fixed_len=64, verdicts=dv) == 0
+    got = dv.download(np.uint32)
+    fit = size // 24
+    odd = (pk[:, 1] & 1) == 1
+    assert odd.sum() > fit and (~odd).sum() > fit
+    ra_recs = ra.ringbuf_fetch(cap=1 << 27)
+    rb_recs = rb.ringbuf_fetch(cap=1 << 27)
+    assert len(ra_recs) == fit and len(rb_recs) == fit
+    assert int((got[odd] == 2).sum()) == fit and int((got[~odd] == 2).sum()) == fit
+    assert int((got == 1).sum()) == n - 2 * fit
+    # every delivered record is the first 16 bytes of an accepted frame of its ring
+    acc_a = {bytes(pk[i, :16]) for i in np.flatnonzero(odd & (got == 2))}
+    assert all(r in acc_a for r in ra_recs[:1000])
