@@ -87,6 +87,7 @@ SIGNATURES = [
     ("bpftime_amd_map_restore", C.c_int, [C.c_int, C.c_void_p, C.c_uint64]),
     ("bpftime_amd_map_geometry", C.c_int, [C.c_int, u64p, u32p, u32p, u32p, u32p]),
     ("bpftime_amd_map_count", C.c_uint64, [C.c_int]),
+    ("bpftime_amd_map_ack_error", C.c_int, [C.c_int]),
     ("bpftime_amd_set_ncpu", None, [C.c_uint32]),
     ("bpftime_amd_get_ncpu", C.c_uint32, []),
     ("bpftime_amd_reset", None, []),

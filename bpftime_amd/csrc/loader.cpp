@@ -1148,6 +1148,7 @@ static void lpm_write_sites(const std::vector<DInsn> &p, const std::vector<uint8
     const MapRec *m = v < kMaxFds ? map_rec((int64_t)v) : nullptr;
     if (m && m->type == MT_LPM_TRIE) named.push_back((int32_t)v);
   }
+  out.names_lpm = !named.empty();
   auto add = [&](uint32_t h, int32_t fd) {
     if (std::find(out.lpm_writes.begin(), out.lpm_writes.end(), std::make_pair(h, fd)) == out.lpm_writes.end())
       out.lpm_writes.emplace_back(h, fd);

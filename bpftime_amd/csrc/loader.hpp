@@ -63,6 +63,7 @@ struct FastForm {
   // LPM trie: {helper id, map fd}.  The device changes a trie only in ORDERED
   // batches (dev_helpers.hpp lpm_update); vm_api.cpp refuses other batches
   std::vector<std::pair<uint32_t, int32_t>> lpm_writes;
+  bool names_lpm = false;  // an lddw names an LPM trie (its launches take the LPM launch lock)
   // a store may reach the unit r1 points to at entry (the pointer kinds
   // cannot place every store on the stack, a map value or a constant)
   bool stores_unit = true;

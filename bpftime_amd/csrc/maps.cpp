@@ -759,8 +759,17 @@ static int lpm_grow(int fd, uint64_t want_nodes) {
   return 0;
 }
 
+static int lpm_pool_out_error(int fd) {
+  set_error("LPM_TRIE map fd " + std::to_string(fd) +
+            ": an ORDERED batch's program-side update ran out of the device node pool; the trie keeps its state "
+            "from before that batch (bpftime_amd_map_ack_error clears this report)");
+  errno = ENOMEM;
+  return -1;
+}
+
 int lpm_pull(int fd) {
   Runtime &r = rt();
+  if (r.kind[fd] == HKind::MAP && r.maps[fd].lpm_pool_out) return lpm_pool_out_error(fd);
   if (!r.lpm_dev_dirty.count(fd)) return 0;
   MapRec &m = r.maps[fd];
   r.lpm_dev_dirty.erase(fd);
@@ -775,10 +784,8 @@ int lpm_pull(int fd) {
     // results are not the reference's.  The host keeps its trie (the state
     // before that batch) and reports it
     lpm_touch(fd);
-    set_error("LPM_TRIE map fd " + std::to_string(fd) +
-              ": an ORDERED batch's program-side update ran out of the device node pool; the trie keeps its state "
-              "from before that batch");
-    return -1;
+    m.lpm_pool_out = true;
+    return lpm_pool_out_error(fd);
   }
   const uint64_t bytes = 16 + (uint64_t)std::min(hdr[1], m.lpm->cap) * m.d.slot_size;
   std::vector<uint8_t> img(bytes);
@@ -904,10 +911,23 @@ static int ix_rebuild(int fd) {
 }
 
 int Runtime::prepare_ix(bool may_delete, uint64_t units, const std::vector<int> &lpm_written,
-                        uint32_t lpm_update_sites) {
+                        uint32_t lpm_update_sites, bool lpm) {
   std::lock_guard<std::mutex> g(mu);
-  // every launch reads the current LPM tries (whatever else it does)
-  while (!lpm_stale.empty()) {
+  // a trie whose device update ran out of its pool fails every launch of a
+  // program naming a trie until acknowledged
+  // (a trie a writer left on the device: its header's pool flag, 16 bytes)
+  for (int fd = 0; lpm && fd < (int)kMaxFds; fd++) {
+    if (kind[fd] != HKind::MAP || !maps[fd].lpm) continue;
+    if (maps[fd].lpm_pool_out) return lpm_pool_out_error(fd);
+    if (!lpm_dev_dirty.count(fd)) continue;
+    uint32_t hdr[4];
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(hdr, (void *)maps[fd].d.data, 16, hipMemcpyDeviceToHost) != hipSuccess)
+      return -1;
+    if ((hdr[3] & kLpmPoolOut) && lpm_pull(fd) < 0) return -1;
+  }
+  // every launch of a program that names a trie reads the current LPM tries
+  while (lpm && !lpm_stale.empty()) {
     const int fd = *lpm_stale.begin();
     if (kind[fd] != HKind::MAP || !maps[fd].lpm) {
       lpm_stale.erase(fd);
@@ -935,7 +955,7 @@ int Runtime::prepare_ix(bool may_delete, uint64_t units, const std::vector<int> 
     }
     if (maps[fd].lpm->dsz == 4) lpm_flat_pending.insert(fd);
   }
-  if (units >= kLpmFlatMinUnits) {
+  if (lpm && units >= kLpmFlatMinUnits) {
     std::vector<int> pending(lpm_flat_pending.begin(), lpm_flat_pending.end());
     for (const int fd : pending) {
       if (kind[fd] != HKind::MAP || !maps[fd].lpm) {
@@ -1544,6 +1564,15 @@ void bpftime_close(int fd) {
     r.kind[fd] = HKind::NONE;
   }
   if (detach) bpftime_amd_syscall_detach(detach);  // a perf link: its syscall attachment
+}
+
+int bpftime_amd_map_ack_error(int fd) {
+  Runtime &r = rt();
+  std::lock_guard<std::mutex> g(r.mu);
+  if (fd < 0 || fd >= (int)kMaxFds || r.kind[fd] != HKind::MAP) return -1;
+  const bool had = r.maps[fd].lpm_pool_out;
+  r.maps[fd].lpm_pool_out = false;
+  return had ? 1 : 0;
 }
 
 void bpftime_amd_reset(void) {

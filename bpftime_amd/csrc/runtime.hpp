@@ -27,6 +27,10 @@ struct MapRec {
   uint64_t ix_addr = 0;    // hash lookup index storage (common.hpp ix_pos), 0 = none
   bool ix_valid = false;   // d.ix = ix_addr while the index holds exactly the reachable keys
   std::shared_ptr<struct LpmTrie> lpm;  // LPM_TRIE: the authoritative host trie
+  // LPM_TRIE: an ORDERED batch's device update ran out of the node pool;
+  // every host op on the trie and every launch naming a trie reports it
+  // (ENOMEM) until bpftime_amd_map_ack_error
+  bool lpm_pool_out = false;
   // BPF_MAP_CREATE attributes as given (BPF_OBJ_GET_INFO_BY_FD reports them)
   uint32_t ifindex = 0, btf_vmlinux_value_type_id = 0, btf_id = 0, btf_key_type_id = 0, btf_value_type_id = 0;
   uint64_t map_extra = 0;
@@ -105,8 +109,11 @@ struct Runtime {
   // lookup index; any other rebuilds the stale ones.  `lpm_written`: the LPM
   // tries the launch's program may update / delete (ORDERED batches only):
   // their lookups walk the replica (no flat table) while they change
+  // `lpm`: the program names an LPM trie (loader.cpp lpm_write_sites); a
+  // launch of one that does not leaves the tries as they are (their next
+  // user uploads them, under the LPM launch lock)
   int prepare_ix(bool may_delete, uint64_t units, const std::vector<int> &lpm_written = {},
-                 uint32_t lpm_update_sites = 0);
+                 uint32_t lpm_update_sites = 0, bool lpm = true);
   // launches that may still run: one whose hash lookups use the block LDS
   // lookup cache (a found slot is trusted for the rest of the launch), one of
   // a program that can delete.  A cached launch never overlaps a deletion

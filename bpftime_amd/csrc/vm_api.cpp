@@ -699,7 +699,10 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   // the tries as device-written happen under one lock, so a concurrent
   // launch's preparation sees them
   std::unique_lock<std::mutex> lpm_lk(r.lpm_launch_mu, std::defer_lock);
-  const bool touches_lpm = r.lpm_maps.load() > 0;
+  // (only launches of programs that name a trie: others need
+  // neither the lock nor the in-flight marks, and a writer waits for them)
+  const bool names_lpm = (kind == CTX_XDP ? im.fx : im.fr).names_lpm;
+  const bool touches_lpm = r.lpm_maps.load() > 0 && names_lpm;
   if (touches_lpm) {
     lpm_lk.lock();
     if ((!lpm_w.empty() && r.lpm_inflight.load()) || r.lpm_writer_inflight.load()) {
@@ -711,8 +714,10 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       r.lpm_writer_inflight = false;
     }
   }
-  if (r.prepare_ix(prog.may_delete, b->count, lpm_w, lpm_updates) < 0) {
-    error = lpm_w.empty() ? "hash lookup index rebuild failed" : std::string(bpftime_amd_last_error());
+  if (r.prepare_ix(prog.may_delete, b->count, lpm_w, lpm_updates, names_lpm) < 0) {
+    // (an LPM trie's report names itself; else the index rebuild failed)
+    const std::string le = bpftime_amd_last_error() ? bpftime_amd_last_error() : "";
+    error = le.rfind("LPM_TRIE", 0) == 0 ? le : "hash lookup index rebuild failed";
     return -1;
   }
   p.lru_seq = r.prepare_lru();

@@ -12,9 +12,14 @@ runtime.
 
 Ranks meet in a directory under /tmp named after the launch: torchrun's
 elastic agent is the parent of every worker of one launch, so its pid and
-start time (from /proc) plus MASTER_PORT identify the launch, and a later
+start time (from /proc), MASTER_PORT and the agent's run id
+(TORCHELASTIC_RUN_ID) identify the launch, with the user's uid; a later
 launch never sees an earlier one's files.  `BPFTIME_AMD_RDZV_DIR` names the
-directory instead.  Each message is a file written under a temporary name
+directory instead; ranks started outside torchrun must name one (their
+parent, a shell, would give every run from it the same directory).  The
+directory is made 0700 and refused when it is not a directory of this user
+that only this user can write, or when it holds a finished launch's files
+(a predictable /tmp path another user could plant).  Each message is a file written under a temporary name
 and renamed into place (atomic on one filesystem); waiting is polling with
 a sleep that grows to 1 ms.
 """
@@ -41,9 +46,21 @@ def launch_dir() -> str:
     d = os.environ.get("BPFTIME_AMD_RDZV_DIR")
     if d:
         return d
+    run = os.environ.get("TORCHELASTIC_RUN_ID")
+    if run is None:
+        raise RuntimeError("ranks started outside torchrun need BPFTIME_AMD_RDZV_DIR (a directory for this launch)")
+    run = "".join(c if c.isalnum() or c in "-_" else "_" for c in run)[:64]
     ppid = os.getppid()
     port = os.environ.get("MASTER_PORT", "0")
-    return os.path.join("/tmp", f"bpftime_amd_rdzv_{ppid}_{_proc_start(ppid)}_{port}")
+    return os.path.join("/tmp", f"bpftime_amd_rdzv_{os.getuid()}_{ppid}_{_proc_start(ppid)}_{port}_{run}")
+
+
+def _check_dir(path: str) -> None:
+    import stat
+    st = os.lstat(path)
+    if not stat.S_ISDIR(st.st_mode) or st.st_uid != os.getuid() or st.st_mode & 0o077:
+        raise PermissionError(f"refusing rendezvous directory {path}: it must be a directory of uid {os.getuid()} "
+                              f"with mode 0700 (found uid {st.st_uid}, mode {oct(st.st_mode & 0o7777)})")
 
 
 def _enc(obj: Any) -> Any:
@@ -73,7 +90,10 @@ class Rendezvous:
         self.rank, self.world, self.timeout = rank, world, timeout
         self.path = path or launch_dir()
         self.seq = 0
-        os.makedirs(self.path, exist_ok=True)
+        os.makedirs(self.path, mode=0o700, exist_ok=True)
+        _check_dir(self.path)
+        if rank == 0 and any(n.startswith("exit.") for n in os.listdir(self.path)):
+            raise RuntimeError(f"rendezvous directory {self.path} holds a finished launch's files")
 
     def _put(self, name: str, data: bytes) -> None:
         tmp = os.path.join(self.path, f".{name}.{self.rank}.tmp")

@@ -174,6 +174,11 @@ int bpftime_amd_map_restore(int fd, const void *in, uint64_t bytes);
 int bpftime_amd_map_geometry(int fd, uint64_t *nbuckets, uint32_t *slot_size, uint32_t *key_off,
                              uint32_t *val_off, uint32_t *ncpu);
 uint64_t bpftime_amd_map_count(int fd);
+/* An LPM trie whose device update (ORDERED batch) ran out of the node pool
+ * keeps the state from before that batch and reports ENOMEM on every host op
+ * and every launch of a program naming a trie until this acknowledges it:
+ * 1 when a report was cleared, 0 when there was none, -1 not a map. */
+int bpftime_amd_map_ack_error(int fd);
 /* virtual CPU count for per-CPU maps and helper 8 (default 64) */
 void bpftime_amd_set_ncpu(uint32_t ncpu);
 uint32_t bpftime_amd_get_ncpu(void);

@@ -261,6 +261,14 @@ def test_lpm_device_pool_exhausted_fails_the_batch(fresh_oracle, fresh_runtime):
     vm4.load(churn_prog(dm.fd, per_unit=4))  # four inserts per unit behind one update site
     with pytest.raises(dev.EbpfError, match=r"LPM_TRIE map fd %d: .*node pool" % dm.fd):
         vm4.exec_batch(dev.CTX_RAW, d2, n, 4, fixed_len=4, flags=dev.BATCH_SYNC | dev.BATCH_ORDERED)
+    # the report sticks: host ops fail with ENOMEM, and so does
+    # any launch of a program naming a trie, until it is acknowledged
+    import ctypes as C
+    L = dev.lib()
+    assert dm.lookup(k4(8, "10.0.0.0")) is None and C.get_errno() == 12
+    with pytest.raises(dev.EbpfError, match=r"LPM_TRIE map fd %d: .*node pool" % dm.fd):
+        vm.exec_batch(dev.CTX_RAW, d, 16, 4, fixed_len=4, flags=dev.BATCH_SYNC | dev.BATCH_ORDERED)
+    assert L.bpftime_amd_map_ack_error(dm.fd) == 1 and L.bpftime_amd_map_ack_error(dm.fd) == 0
     assert dm.count() == 1 and dm.lookup(k4(8, "10.0.0.0")) == struct.pack("<I", 7)
     assert dm.lookup(k4(32, "0.0.1.0")) is None
 

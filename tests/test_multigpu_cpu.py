@@ -145,7 +145,7 @@ def test_bench_control_plane_two_ranks(tmp_path):
 
 def _rdzv_worker(rank, world, q):
     sys.path.insert(0, ROOT)
-    os.environ.update(MASTER_PORT="29533")
+    os.environ.update(MASTER_PORT="29533", TORCHELASTIC_RUN_ID="test-run")
     import time
     from bpftime_amd.rendezvous import Rendezvous, launch_dir
     rz = Rendezvous(rank, world, timeout=120)
@@ -203,3 +203,26 @@ def test_merge_at_counter_width():
     assert shard.counter_width(12) == 4 and shard.counter_width(16) == 8
     with pytest.raises(ValueError):
         shard.counter_width(6)
+
+
+def test_rendezvous_refuses_planted_or_unnamed_dirs(tmp_path, monkeypatch):
+    """the directory must be this user's, mode 0700, and not a
+    finished launch's; ranks outside torchrun must name their directory."""
+    from bpftime_amd import rendezvous as rv
+    planted = tmp_path / "planted"
+    planted.mkdir(mode=0o777)
+    os.chmod(planted, 0o777)
+    with pytest.raises(PermissionError):
+        rv.Rendezvous(0, 2, path=str(planted))
+    old = tmp_path / "old"
+    old.mkdir(mode=0o700)
+    (old / "exit.1").write_bytes(b"")
+    with pytest.raises(RuntimeError):
+        rv.Rendezvous(0, 2, path=str(old))
+    monkeypatch.delenv("BPFTIME_AMD_RDZV_DIR", raising=False)
+    monkeypatch.delenv("TORCHELASTIC_RUN_ID", raising=False)
+    with pytest.raises(RuntimeError):
+        rv.launch_dir()
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "r/../x")
+    d = rv.launch_dir()
+    assert "/" not in os.path.basename(d) and f"_{os.getuid()}_" in d
