@@ -99,6 +99,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # handler entries aligned to 2^HANDLER_ALIGN bytes (0: packed); 64-B entries
 # measured 0.4406 -> 0.4366 ms on the headline (same box, best of 4)
 HANDLER_ALIGN = int(os.environ.get("BPFTIME_AMD_HANDLER_ALIGN", "6"))
+# cache policy of the unit-slot staging loads and write-backs (" nt": the
+# streamed slots as non-temporal, so they do not push hash tables, indexes
+# and tail-call frames out of the XCD's L2; "" default policy)
+SLOT_POLICY = os.environ.get("BPFTIME_AMD_GEN_SLOT_POLICY", "")
+SLOT_STORE_POLICY = os.environ.get("BPFTIME_AMD_GEN_SLOT_STORE_POLICY", "")
 
 ALU_OPS = ["ADD", "SUB", "MUL", "OR", "AND", "XOR", "MOV", "LSH", "RSH", "ARSH"]
 JCC = ["EQ", "GT", "GE", "SET", "NE", "SGT", "SGE", "LT", "LE", "SLT", "SLE"]
@@ -504,7 +509,8 @@ class Gen:
         for c in range(4):
             skip = self.label("fl")
             self.e(f"s_bitcmp1_b32 s84, {c}", f"s_cbranch_scc0 {skip}",
-                   f"global_store_dwordx4 v[52:53], v[{STG + 4 * c}:{STG + 4 * c + 3}], off offset:{16 * c}",
+                   f"global_store_dwordx4 v[52:53], v[{STG + 4 * c}:{STG + 4 * c + 3}], off offset:{16 * c}"
+                   + SLOT_STORE_POLICY,
                    f"{skip}:")
         if clear:
             self.e("s_mov_b32 s84, 0")
@@ -2100,10 +2106,11 @@ class Gen:
         filt, fsv, fsr = self.label("filt"), self.label("fsv"), self.label("fsr")
         e("s_bitcmp1_b32 %[entry], 1", f"s_cbranch_scc0 {loaded}",
           "s_mov_b32 s80, %[stage]",
-          f"global_load_dwordx4 v[{STG}:{STG + 3}], v[52:53], off")
+          f"global_load_dwordx4 v[{STG}:{STG + 3}], v[52:53], off" + SLOT_POLICY)
         for c in range(1, 4):
             e(f"s_cmp_lt_u32 %[stage], {16 * (c + 1)}", f"s_cbranch_scc1 {filt}",
-              f"global_load_dwordx4 v[{STG + 4 * c}:{STG + 4 * c + 3}], v[52:53], off offset:{16 * c}")
+              f"global_load_dwordx4 v[{STG + 4 * c}:{STG + 4 * c + 3}], v[52:53], off offset:{16 * c}"
+              + SLOT_POLICY)
         # syscall records (entry bit 6) of a staged unit: exit / exit_group
         # lanes (nr = bytes 8..15, syscall_trace_attach_impl.cpp:25) finish
         # with r0 = 0 here, from the staged bytes, instead of a separate load
