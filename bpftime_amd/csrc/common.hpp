@@ -185,6 +185,17 @@ constexpr uint32_t kFrameBytes = kFrameHdr + kFrameCtx + kStackSize;
 // stack top again after the return
 constexpr uint64_t kFrameMasked = 1ull << 40;
 constexpr uint32_t kFrameLiveShift = 40;  // + r: the bit of register r (1..9)
+// ... and bit kFrameRematShift + r: register r held the lane's own ctx
+// pointer at the call (not saved; the return sets it again)
+constexpr uint32_t kFrameRematShift = 50;
+// LDS frames (XDP images, depth < KParams tail_lds & 0xff): a masked frame of
+// a lane at depth d is the words [d][w][lane] of the block's LDS frame area
+// (after the combining table): w = 0 the header (as word 11; 0 = the frame is
+// in global memory, a full frame the C++ tier pushed), then the live
+// registers in order, the ctx words of the ctx mask, the stack words of the
+// stack mask (vm_api.cpp sizes words = 1 + the most live registers of a tail
+// call + both masks' words, and the depths to keep the block's residency)
+constexpr uint32_t kTailLdsMax = 4;  // depths held in LDS at most
 
 // Context kinds for a batch
 constexpr uint32_t CTX_RAW = 0;      // r1 = unit memory, r2 = length
@@ -260,6 +271,9 @@ struct KParams {
   uint64_t lru_seq;       // this launch's LRU stamp sequence (common.hpp kLruSeqShift)
   uint32_t tail_ctx_mask;    // XDP images: ctx words / stack words a frame keeps (loader.cpp tail_save_masks)
   uint32_t tail_stack_mask;
+  // XDP images: frames of the first (tail_lds & 0xff) depths pushed by the asm
+  // tier live in LDS, (tail_lds >> 8) u64 words each (common.hpp kFrameLds*)
+  uint32_t tail_lds;
   uint32_t lcache;           // the block's hash-lookup cache: its sets (0 = none; lcache_sets())
   uint64_t *gregs;           // r0..r10 copies for the C++ tier: [grid][11][kBlock] u64 (k_interp G), or nullptr (LDS)
   uint8_t *rb_stage;         // ring-buffer staging: [grid][kRbStageBytes] right after lane_scratch's words, or nullptr
@@ -331,7 +345,11 @@ constexpr size_t kCuLds = 160 * 1024;  // LDS per CU (gfx950)
 // then the block's ring staging area (u64, 0 = none) and the LDS address of
 // its counters (dev_helpers.hpp RbLds; gen_fast.py call_rbout)
 constexpr uint32_t kTenvRb = 64 + 4 * kMissParts;     // (u64 index kTenvRb / 8)
-constexpr uint32_t kTenvBytes = kTenvRb + 16;          // gen_fast.py TENV
+// then (XDP images) the LDS tail-call frames: their LDS address minus the
+// lane columns' (interp.hip Rf), the depths they hold | words per frame << 8
+// (KParams tail_lds; gen_fast.py tail_env)
+constexpr uint32_t kTenvLf = kTenvRb + 16;
+constexpr uint32_t kTenvBytes = kTenvLf + 16;          // gen_fast.py TENV
 // Hash-lookup cache of a block (programs whose hash lookups the loader marks
 // FW_LCACHE: no deletions): `sets` 2-way sets, the ways' 16-B keys
 // ([set][way]) then their u32 entries {(slot + 1) | fd << 22}, right below
@@ -340,9 +358,14 @@ constexpr uint32_t kTenvBytes = kTenvRb + 16;          // gen_fast.py TENV
 // the rest of a launch when nothing deletes.
 constexpr uint32_t kLcacheSets = 1024;  // default set count (BPFTIME_AMD_LCACHE_SETS: vm_api.cpp lcache_sets)
 BA_HD inline size_t lcache_bytes(uint32_t sets) { return (size_t)(32 + 8) * sets; }
+// ... and after the table, the LDS tail-call frames of an XDP image
+// (tail_lds: depths | words per frame << 8; [depth][word][lane] u64)
+BA_HD constexpr uint32_t tail_lds_lane_bytes(uint32_t tail_lds) { return (tail_lds & 0xff) * (tail_lds >> 8) * 8; }
 inline size_t dyn_lds_for(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
-                          uint32_t lcache_sets = 0, bool ctx_lds = true, uint32_t block = kBlock) {
-  return (size_t)block * ((kind == CTX_XDP && ctx_lds ? 48 : 0) + (big_stack ? 0 : stack_size)) +
+                          uint32_t lcache_sets = 0, bool ctx_lds = true, uint32_t block = kBlock,
+                          uint32_t tail_lds = 0) {
+  return (size_t)block * ((kind == CTX_XDP && ctx_lds ? 48 : 0) + (big_stack ? 0 : stack_size) +
+                          tail_lds_lane_bytes(tail_lds)) +
          lcache_bytes(lcache_sets) + kTenvBytes + 20 * (size_t)comb_entries;
 }
 

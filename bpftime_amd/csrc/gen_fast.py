@@ -121,7 +121,8 @@ KP = 3
 WAYS = 8  # combining-table associativity
 MISS_PARTS = 256  # miss-log partitions (common.hpp kMissParts)
 RB_TENV = 64 + 4 * MISS_PARTS  # the block's ring staging slots in the launch constants (common.hpp kTenvRb)
-TENV = RB_TENV + 16  # launch constants + miss counters + ring slots below the combining table (common.hpp kTenvBytes)
+LF_TENV = RB_TENV + 16  # the LDS tail-call frames' offset and shape (common.hpp kTenvLf)
+TENV = LF_TENV + 16  # launch constants + miss counters + ring slots + LDS frames below the combining table (common.hpp kTenvBytes)
 
 
 def _common_const(name):
@@ -187,7 +188,6 @@ class Gen:
         self.uid = 0
         self.greg = greg
         self.depth_off = 2048 if greg else 12 * 2048  # the lane's tail-call depth slot
-        self.hdr_off = self.depth_off + 2048          # ... and its depth-0 frame header (interp.hip kHdr0)
 
     def e(self, *lines):
         self.out.extend(lines)
@@ -1707,16 +1707,42 @@ class Gen:
         del d0
 
     def tail_env(self):
+        """The launch constants of tail calls; s46 / s47 = the LDS frames'
+        offset from v40 and depths | words << 8 (FInsn w6 / w7 are not
+        needed by TAIL / TRET)."""
         self.e(f"s_sub_u32 s69, %[comb], {TENV}", "v_mov_b32 v41, s69",
                "ds_read_b128 v[42:45], v41", "ds_read_b128 v[46:49], v41 offset:16",
+               f"ds_read_b64 v[58:59], v41 offset:{LF_TENV}",
                f"ds_read_b64 v[54:55], v40 offset:{self.depth_off}",          # depth, grid lane
                "s_waitcnt lgkmcnt(0)",
+               "v_readfirstlane_b32 s46, v58", "v_readfirstlane_b32 s47, v59",  # LDS frames
                "v_readfirstlane_b32 s72, v42", "v_readfirstlane_b32 s73, v43",  # frames
                "v_readfirstlane_b32 s74, v44", "v_readfirstlane_b32 s75, v45",  # entry table
                "v_readfirstlane_b32 s76, v46", "v_readfirstlane_b32 s77, v47",  # word / depth stride
                "v_readfirstlane_b32 s85, v48",                 # stack save mask | stack bytes << 16
                "v_readfirstlane_b32 s68, v49",                 # ctx save mask (s68: free until an exit)
                "s_cmp_eq_u64 s[72:73], 0", f"s_cbranch_scc1 {L('slow')}")
+
+    def lds_frame_ptr(self, v="v41"):
+        """v = the LDS address of this lane's word 0 at depth v54 (an LDS
+        frame: v40 + s46 + depth * words * 2048)."""
+        self.e("s_lshr_b32 s69, s47, 8", "s_lshl_b32 s69, s69, 11",
+               f"v_mul_lo_u32 {v}, v54, s69", f"v_add3_u32 {v}, {v}, v40, s46")
+
+    def lds_stack_words(self, store, mask):
+        """The stack words of the SGPR `mask` to (store) or from the LDS
+        frame words at v48 on (v48 advances a word each)."""
+        loop, done = self.label("tll"), self.label("tld")
+        self.e("s_lshr_b32 s69, s85, 16", "v_subrev_u32 v43, s69, %[stklo]",   # the stack bottom
+               f"s_mov_b32 s70, {mask}",
+               f"{loop}:", "s_cmp_eq_u32 s70, 0", f"s_cbranch_scc1 {done}",
+               "s_ff1_i32_b32 s69, s70", "s_bitset0_b32 s70, s69",
+               "s_lshl_b32 s71, s69, 3", "v_add_u32 v49, s71, v43")
+        if store:
+            self.e("ds_read_b64 v[44:45], v49", "s_waitcnt lgkmcnt(0)", "ds_write_b64 v48, v[44:45]")
+        else:
+            self.e("ds_read_b64 v[44:45], v48", "s_waitcnt lgkmcnt(0)", "ds_write_b64 v49, v[44:45]")
+        self.e("v_add_u32 v48, 0x800, v48", f"s_branch {loop}", f"{done}:")
 
     def frame_ptr(self):
         """v[56:57] = this lane's word 0 at depth v54."""
@@ -1830,7 +1856,16 @@ class Gen:
                "s_and_b64 exec, exec, s[54:55]", f"s_cbranch_execz {noval}")
         # ---- push (a masked frame, common.hpp kFrameMasked): the caller's
         # live registers (FInsn imm), the header, the ctx / stack words the
-        # image's targets may write (tenv masks) ----
+        # image's targets may write (tenv masks); the lanes at a depth below
+        # s47 & 0xff into their LDS frame (common.hpp kTailLdsMax), the others
+        # into global memory ----
+        nog, nol = self.label("tng"), self.label("tnl")
+        self.e("s_lshl_b32 s69, s42, 8", "s_or_b32 s69, s69, 0x100",              # masked | live << 8
+               "v_mov_b32 v44, s49", "v_mov_b32 v45, s69",
+               "s_and_b32 s69, s47, 0xff",
+               "v_cmp_gt_u32 s[64:65], s69, v54", "s_and_b64 s[64:65], s[64:65], exec",
+               "s_andn2_b64 s[66:67], exec, s[64:65]",
+               "s_mov_b64 exec, s[66:67]", f"s_cbranch_execz {nog}")
         self.frame_ptr()
         for r in range(1, 10):
             skip = self.label("tpr")
@@ -1838,14 +1873,7 @@ class Gen:
             self.word_addr(r - 1)
             self.e(f"global_store_dwordx2 v[58:59], v[{R0 + 2 * r}:{R0 + 2 * r + 1}], off", f"{skip}:")
         self.word_addr(11)
-        self.e("s_lshl_b32 s69, s42, 8", "s_or_b32 s69, s69, 0x100",              # masked | live << 8
-               "v_mov_b32 v44, s49", "v_mov_b32 v45, s69",
-               "global_store_dwordx2 v[58:59], v[44:45], off",
-               # depth 0: the header in LDS as well (the pop reads it there)
-               "s_mov_b64 s[64:65], exec",
-               "v_cmp_eq_u32 vcc, 0, v54", "s_and_b64 exec, exec, vcc",
-               f"ds_write_b64 v40, v[44:45] offset:{self.hdr_off}",
-               "s_mov_b64 exec, s[64:65]")
+        self.e("global_store_dwordx2 v[58:59], v[44:45], off")
         for k in range(6):
             skip = self.label("tpc")
             self.e(f"s_bitcmp1_b32 s68, {k}", f"s_cbranch_scc0 {skip}",
@@ -1853,6 +1881,21 @@ class Gen:
             self.word_addr(12 + k)
             self.e("global_store_dwordx2 v[58:59], v[42:43], off", f"{skip}:")
         self.stack_words(store=True)
+        self.e(f"{nog}:", "s_mov_b64 exec, s[64:65]", f"s_cbranch_execz {nol}")
+        self.lds_frame_ptr()
+        self.e("ds_write_b64 v41, v[44:45]", "v_add_u32 v48, 0x800, v41")
+        for r in range(1, 10):
+            skip = self.label("tlr")
+            self.e(f"s_bitcmp1_b32 s42, {r}", f"s_cbranch_scc0 {skip}",
+                   f"ds_write_b64 v48, v[{R0 + 2 * r}:{R0 + 2 * r + 1}]", "v_add_u32 v48, 0x800, v48", f"{skip}:")
+        for k in range(6):
+            skip = self.label("tlc")
+            self.e(f"s_bitcmp1_b32 s68, {k}", f"s_cbranch_scc0 {skip}",
+                   f"ds_read_b64 v[42:43], v{R0 + 2} offset:{8 * k}", "s_waitcnt lgkmcnt(0)",
+                   "ds_write_b64 v48, v[42:43]", "v_add_u32 v48, 0x800, v48", f"{skip}:")
+        self.e("s_and_b32 s71, s85, 0xffff")
+        self.lds_stack_words(store=True, mask="s71")
+        self.e(f"{nol}:", "s_mov_b64 exec, s[54:55]")
         self.e("v_add_u32 v54, 1, v54", f"ds_write_b32 v40, v54 offset:{self.depth_off}",
                f"v_mov_b32 v{R0}, 0", f"v_mov_b32 v{R0 + 1}, 0",
                f"v_mov_b32 v{R0 + 4}, 64", f"v_mov_b32 v{R0 + 5}, 0",
@@ -1877,35 +1920,39 @@ class Gen:
                "v_cmp_eq_u32 s[54:55], 0, v54", "s_and_b64 s[54:55], s[54:55], exec",
                f"s_cbranch_scc1 {L('slow')}",                                # no frame: C++ fails the lane
                "v_add_u32 v54, -1, v54",
+               # s[52:53]: lanes whose frame is in LDS (depth < s47 & 0xff;
+               # its header 0: a full frame in global memory, left for C++),
+               # s[56:57]: the others
+               "s_and_b32 s69, s47, 0xff",
+               "v_cmp_gt_u32 s[52:53], s69, v54", "s_and_b64 s[52:53], s[52:53], exec",
+               "s_andn2_b64 s[56:57], exec, s[52:53]")
+        h1, h2 = self.label("trh1"), self.label("trh2")
+        self.e("s_mov_b64 exec, s[52:53]", f"s_cbranch_execz {h1}")
+        self.lds_frame_ptr()
+        self.e("ds_read_b64 v[46:47], v41",
+               f"{h1}:", "s_mov_b64 exec, s[56:57]", f"s_cbranch_execz {h2}",
                "s_waitcnt vmcnt(0)")
         self.frame_ptr()
         self.word_addr(11)
-        # frames of depth 0: the header from LDS when every lane has it
-        # there (a C++ push zeroes the copy), else from the frame
-        glb, got = self.label("trg"), self.label("trh")
-        self.e("v_cmp_ne_u32 vcc, 0, v54", "s_and_b64 vcc, vcc, exec", f"s_cbranch_vccnz {glb}",
-               f"ds_read_b64 v[46:47], v40 offset:{self.hdr_off}",
-               "s_waitcnt lgkmcnt(0)",
-               "v_and_b32 v41, 0x100, v47", "v_cmp_eq_u32 vcc, 0, v41", "s_and_b64 vcc, vcc, exec",
-               f"s_cbranch_vccz {got}",
-               f"{glb}:",
-               "global_load_dwordx2 v[46:47], v[58:59], off",                 # return pc | flags
-               "s_waitcnt vmcnt(0)",
-               f"{got}:",
-               "v_and_b32 v41, 0x100, v47", "v_cmp_ne_u32 vcc, 0, v41",
+        self.e("global_load_dwordx2 v[46:47], v[58:59], off",                 # return pc | flags
+               f"{h2}:", "s_or_b64 exec, s[52:53], s[56:57]",
+               "s_waitcnt vmcnt(0) lgkmcnt(0)",
+               "v_and_b32 v49, 0x100, v47", "v_cmp_ne_u32 vcc, 0, v49",
                "s_andn2_b64 s[54:55], exec, vcc", f"s_cbranch_scc1 {L('slow')}",
                f"ds_write_b32 v40, v54 offset:{self.depth_off}",
-               "v_lshlrev_b32 v50, 5, v46",                                  # return IP
-               "s_mov_b64 s[60:61], exec")
+               "v_lshlrev_b32 v50, 5, v46")                                  # return IP
+        # ---- global frames: the live registers the header names, the
+        # image's ctx / stack words ----
+        ng = self.label("trng")
+        self.e("s_mov_b64 exec, s[56:57]", f"s_cbranch_execz {ng}", "s_mov_b64 s[60:61], exec")
         for r in range(1, 10):
             skip = self.label("trr")
             self.e("s_mov_b64 exec, s[60:61]",
-                   f"v_and_b32 v41, {1 << (8 + r)}, v47", "v_cmp_ne_u32 vcc, 0, v41",
+                   f"v_and_b32 v49, {1 << (8 + r)}, v47", "v_cmp_ne_u32 vcc, 0, v49",
                    "s_and_b64 exec, s[60:61], vcc", f"s_cbranch_execz {skip}")
             self.word_addr(r - 1)
             self.e(f"global_load_dwordx2 v[{R0 + 2 * r}:{R0 + 2 * r + 1}], v[58:59], off", f"{skip}:")
-        self.e("s_mov_b64 exec, s[60:61]",
-               f"v_mov_b32 v{R0 + 20}, %[r10lo]", f"v_mov_b32 v{R0 + 21}, %[r10hi]")
+        self.e("s_mov_b64 exec, s[60:61]")
         # the first saved ctx word and the first saved stack word load with
         # the registers (one memory round trip for the usual frame: a live
         # register, a ctx field, a stack word); the others one at a time.
@@ -1947,6 +1994,37 @@ class Gen:
                f"s_branch {loop}", f"{done}:")
         self.stack_words(store=False, mask="s66")
         self.e("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        # ---- LDS frames: the same words in order from word 1 ----
+        nl = self.label("trnl")
+        self.e(f"{ng}:", "s_mov_b64 exec, s[52:53]", f"s_cbranch_execz {nl}",
+               "v_add_u32 v48, 0x800, v41")
+        for r in range(1, 10):
+            skip = self.label("tlr")
+            self.e("s_mov_b64 exec, s[52:53]",
+                   f"v_and_b32 v49, {1 << (8 + r)}, v47", "v_cmp_ne_u32 vcc, 0, v49",
+                   "s_and_b64 exec, s[52:53], vcc", f"s_cbranch_execz {skip}",
+                   f"ds_read_b64 v[{R0 + 2 * r}:{R0 + 2 * r + 1}], v48", "v_add_u32 v48, 0x800, v48", f"{skip}:")
+        self.e("s_mov_b64 exec, s[52:53]")
+        for k in range(6):
+            skip = self.label("tlc")
+            self.e(f"s_bitcmp1_b32 s68, {k}", f"s_cbranch_scc0 {skip}",
+                   "ds_read_b64 v[42:43], v48", "v_add_u32 v48, 0x800, v48", "s_waitcnt lgkmcnt(0)",
+                   f"ds_write_b64 %[r1lo], v[42:43] offset:{8 * k}", f"{skip}:")
+        self.e("s_and_b32 s71, s85, 0xffff")
+        self.lds_stack_words(store=False, mask="s71")
+        self.e("s_waitcnt lgkmcnt(0)",
+               f"{nl}:", "s_or_b64 exec, s[52:53], s[56:57]",
+               f"v_mov_b32 v{R0 + 20}, %[r10lo]", f"v_mov_b32 v{R0 + 21}, %[r10hi]")
+        # registers that held the lane's own ctx pointer at the call
+        # (header bits 50 + r, common.hpp kFrameRematShift): set again
+        nr = self.label("trnr")
+        self.e("v_and_b32 v49, 0x0ff80000, v47", "v_cmp_ne_u32 vcc, 0, v49", "s_and_b64 vcc, vcc, exec",
+               f"s_cbranch_vccz {nr}", "s_mov_b64 s[60:61], exec")
+        for r in range(1, 10):
+            self.e("s_mov_b64 exec, s[60:61]",
+                   f"v_and_b32 v49, {1 << (18 + r)}, v47", "v_cmp_ne_u32 vcc, 0, v49", "s_and_b64 exec, s[60:61], vcc",
+                   f"v_mov_b32 v{R0 + 2 * r}, %[r1lo]", f"v_mov_b32 v{R0 + 2 * r + 1}, %[r1hi]")
+        self.e("s_mov_b64 exec, s[60:61]", f"{nr}:")
         self.go_groups()
 
     # ---- divergence: min-pc scheduling of lane groups ----

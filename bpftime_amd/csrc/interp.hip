@@ -597,7 +597,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   SRV(arena_hi); SRV(step_limit); SRV(fixed_len); SRV(stack_size); SRV(ncpu); SRV(ifindex); SRV(rxq);
   SRV(checked); SRV(head); SRV(ordered); SRV(fast_div); SRV(comb_entries); SRV(stage); SRV(needs_ctx);
   SRP(descs); SRV(umem_bytes); SRP(tail_entry); SRP(frames); SRV(frame_words); SRV(dbg); SRP(dbg_counts); SRP(flush_log); SRV(log_words); SRP(lane_scratch);
-  SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask); SRV(lcache); SRP(gregs); SRP(rb_stage); SRP(gctx);
+  SRV(lru_seq); SRV(tail_ctx_mask); SRV(tail_stack_mask); SRV(tail_lds); SRV(lcache); SRP(gregs); SRP(rb_stage); SRP(gctx);
   SRP(miss_log); SRP(miss_counts); SRV(miss_cap); SRP(tail_slots); SRV(full_q); SRV(full_r); SRV(step_cpu);
   SRP(sys_state); SRP(sys_ret); SRV(sys_phase); SRV(pid_tgid);
   p.pid_off = (int32_t)sreg((uint64_t)(uint32_t)pin.pid_off);
@@ -609,10 +609,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   // grid lane index << 32 (gen_fast.py tail_env).  (2 KiB of LDS decide
   // between 3 and 4 resident blocks of the headline program: images only.)
   // (G: the dummy and depth slots only)
-  // (images: then the header word of the lane's depth-0 frame as the asm
-  // tier pushed it, 0 = none: gen_fast.py tail_call / tail_ret)
-  constexpr uint32_t kDummy = G ? 0 : 11, kDepth = G ? 1 : 12, kHdr0 = kDepth + 1;
-  __shared__ uint64_t Rf[(IMAGE ? kHdr0 + 1 : kDummy + 1) * BS];
+  constexpr uint32_t kDummy = G ? 0 : 11, kDepth = G ? 1 : 12;
+  __shared__ uint64_t Rf[(IMAGE ? kDepth + 1 : kDummy + 1) * BS];
   // r0..r10 columns: [register][lane] per 256 lanes (kBlock), so a block of
   // BS > kBlock lanes (G launches only) holds BS / kBlock such column sets
   uint64_t *const Rg = G ? p.gregs + (uint64_t)blockIdx.x * 11 * BS : Rf;
@@ -633,6 +631,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   uint64_t *tenv = (uint64_t *)((uint8_t *)lcache + lcache_bytes(p.lcache));
   uint32_t *comb = (uint32_t *)((uint8_t *)tenv + kTenvBytes);
   uint64_t *comb_d = (uint64_t *)(comb + p.comb_entries);
+  // XDP images: the LDS tail-call frames of the first depths (common.hpp
+  // kTailLdsMax), [depth][word][lane]
+  uint64_t *const lfr = (uint64_t *)((uint8_t *)comb + 20 * (size_t)p.comb_entries);
   for (uint32_t i = tid; i < 5 * p.comb_entries; i += BS) comb[i] = 0;
   for (uint32_t i = tid; i < lcache_bytes(p.lcache) / 4; i += BS) lcache[i] = 0;
   // ring-buffer staging (dev_helpers.hpp RbStage): LDS counters of the block
@@ -690,6 +691,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     // (gen_fast.py call_rbout): its area and the LDS address of its counters
     tenv[kTenvRb / 8] = p.rb_stage ? (uint64_t)(uintptr_t)rbs.buf : 0;
     tenv[kTenvRb / 8 + 1] = (uint32_t)(uintptr_t)&rb_lds;
+    // the LDS frames (gen_fast.py tail_env): their address relative to the
+    // lane columns (v40 + this = the lane's word 0 at depth 0), depths | words << 8
+    tenv[kTenvLf / 8] = IMAGE ? (uint64_t)(uint32_t)((uintptr_t)lfr - (uintptr_t)&Rf[0]) | ((uint64_t)p.tail_lds << 32) : 0;
   }
   uint32_t *const miss_cnt = (uint32_t *)((uint8_t *)tenv + 64);  // per partition: records claimed
   for (uint32_t i = tid; i < kMissParts; i += BS) miss_cnt[i] = 0;
@@ -976,6 +980,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
           auto FW = [&](uint32_t d, uint32_t w) -> uint64_t & {
             return fbase[((uint64_t)d * p.frame_words + w) * kLanes];
           };
+          // the LDS frames (depth < ldep): word w of the lane's frame at depth d
+          const uint32_t ldep = p.tail_lds & 0xff, lwords = p.tail_lds >> 8;
+          auto LF = [&](uint32_t d, uint32_t w) -> uint64_t & { return lfr[(d * lwords + w) * kBlock + tid]; };
           const uint32_t sbytes = BIGSTACK ? kStackSize : p.stack_size;
           if (cid == kTailHelper) {
             next = c.call_pc + 1;
@@ -997,7 +1004,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
             const bool in_stack = a1 + 64 > stack_top - sbytes && a1 < stack_top;
             if (entry >= 0 && tdep[0] < kTailDepth && a1 != 0 && !in_stack) {
               const uint32_t d = tdep[0];
-              if (d == 0) Rf[kHdr0 * kBlock + tid] = 0;  // (the asm's LDS copy of a depth-0 header)
+              if (d < ldep) LF(d, 0) = 0;  // a full frame: in global memory
               for (int r = 1; r <= 10; r++) FW(d, r - 1) = R[r * kBlock];
               FW(d, 10) = a1;
               FW(d, 11) = (uint64_t)next | ((uint64_t)cb << 32);
@@ -1021,12 +1028,26 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
             const uint32_t d = tdep[0] - 1;
             tdep[0] = d;
             const uint64_t rv = R[0];
-            const uint64_t w11 = FW(d, 11);
+            const bool lds = d < ldep && (LF(d, 0) & kFrameMasked);
+            const uint64_t w11 = lds ? LF(d, 0) : FW(d, 11);
             next = (uint32_t)w11;
             const uint64_t sb = stack_top - sbytes;
-            if (w11 & kFrameMasked) {  // pushed by the asm tier (common.hpp kFrameMasked)
-              for (int r = 1; r <= 9; r++)
+            if (lds) {  // an LDS frame (common.hpp kTailLdsMax): the words in order
+              uint32_t w = 1;
+              for (int r = 1; r <= 9; r++) {
+                if ((w11 >> (kFrameLiveShift + r)) & 1) R[r * kBlock] = LF(d, w++);
+                if ((w11 >> (kFrameRematShift + r)) & 1) R[r * kBlock] = (uint64_t)(uintptr_t)my_ctx;
+              }
+              R[10 * kBlock] = stack_top;
+              for (uint32_t k = 0; k < 6; k++)
+                if ((p.tail_ctx_mask >> k) & 1) mem_store((uint64_t)(uintptr_t)my_ctx + 8 * k, 8, LF(d, w++));
+              for (uint32_t j = 0; 8 * j < sbytes && j < 16; j++)
+                if ((p.tail_stack_mask >> j) & 1) *(uint64_t *)(sb + 8 * j) = LF(d, w++);
+            } else if (w11 & kFrameMasked) {  // pushed by the asm tier (common.hpp kFrameMasked)
+              for (int r = 1; r <= 9; r++) {
                 if ((w11 >> (kFrameLiveShift + r)) & 1) R[r * kBlock] = FW(d, r - 1);
+                if ((w11 >> (kFrameRematShift + r)) & 1) R[r * kBlock] = (uint64_t)(uintptr_t)my_ctx;
+              }
               R[10 * kBlock] = stack_top;
               for (uint32_t k = 0; k < 6; k++)
                 if ((p.tail_ctx_mask >> k) & 1) mem_store((uint64_t)(uintptr_t)my_ctx + 8 * k, 8, FW(d, kFrameHdr / 8 + k));
@@ -1305,7 +1326,7 @@ extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind,
   const bool image = q.tail_entry && !big_stack;
   const bool g_regs = q.gregs && !big_stack;
   if (block != kBlock && (block != kBigBlock || !g_regs || image || ordered)) return hipErrorInvalidValue;
-  const size_t dyn = dyn_lds_for(kind, big_stack, p->stack_size, p->comb_entries, p->lcache, !p->gctx, block);
+  const size_t dyn = dyn_lds_for(kind, big_stack, p->stack_size, p->comb_entries, p->lcache, !p->gctx, block, p->tail_lds);
   dim3 g(grid), b(block);
 #define L(K, B, I, G) hipLaunchKernelGGL((k_interp<K, B, I, G, kBlock>), g, b, dyn, stream, q)
 #define LK(K)                                                          \
@@ -1349,14 +1370,16 @@ static size_t static_lds_of() {
   if (hipFuncGetAttributes(&a, (const void *)k_interp<KIND, BIGSTACK, IMAGE, G, BS>) == hipSuccess)
     return a.sharedSizeBytes;
   (void)hipGetLastError();
-  const size_t rf = (size_t)(IMAGE ? (G ? 3 : 14) : (G ? 1 : 12)) * BS * 8;
+  const size_t rf = (size_t)(IMAGE ? (G ? 2 : 13) : (G ? 1 : 12)) * BS * 8;
   return rf + sizeof(RbLds) + (BS / 64) * 2 * 2 * 8 + 16;
 }
 
-extern "C" size_t bpftime_amd_static_lds(uint32_t kind, bool big_stack, bool gregs, uint32_t block) {
+// (image: the kernel of a tail-call image, interp.hip bpftime_amd_launch_interp)
+extern "C" size_t bpftime_amd_static_lds_image(uint32_t kind, bool big_stack, bool gregs, uint32_t block, bool image) {
 #define S(K, B, G, BS) return static_lds_of<K, B, false, G, BS>()
 #define SK(K)                                          \
   if (big_stack) S(K, true, false, kBlock);            \
+  else if (image) { if (gregs) return static_lds_of<K, false, true, true, kBlock>(); else return static_lds_of<K, false, true, false, kBlock>(); } \
   else if (gregs && block == kBigBlock) S(K, false, true, kBigBlock); \
   else if (gregs) S(K, false, true, kBlock);           \
   else S(K, false, false, kBlock);
@@ -1371,21 +1394,28 @@ extern "C" size_t bpftime_amd_static_lds(uint32_t kind, bool big_stack, bool gre
 #undef S
 }
 
+extern "C" size_t bpftime_amd_static_lds(uint32_t kind, bool big_stack, bool gregs, uint32_t block) {
+  return bpftime_amd_static_lds_image(kind, big_stack, gregs, block, false);
+}
+
 extern "C" size_t bpftime_amd_lds_bytes(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
                                         uint32_t lcache_sets, bool ctx_lds, bool gregs, uint32_t block) {
   return dyn_lds_for(kind, big_stack, stack_size, comb_entries, lcache_sets, ctx_lds, block) +
          bpftime_amd_static_lds(kind, big_stack, gregs, block);
 }
 
-extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds, bool gregs, uint32_t block) {
+extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds, bool gregs, uint32_t block,
+                                    bool image) {
   // (a block asking for more LDS than a CU has never fits, whatever the
   // occupancy query answers for it: dynamic plus the kernel's static LDS)
-  if (dyn_lds + bpftime_amd_static_lds(kind, big_stack, gregs, block) > kCuLds) return 0;
+  if (dyn_lds + bpftime_amd_static_lds_image(kind, big_stack, gregs, block, image) > kCuLds) return 0;
   int n = 0;
   hipError_t e;
 #define O(K, B, G) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_interp<K, B, false, G, kBlock>, kBlock, dyn_lds)
+#define OI(K, G) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_interp<K, false, true, G, kBlock>, kBlock, dyn_lds)
 #define OK(K)                         \
   if (big_stack) O(K, true, false);   \
+  else if (image) { if (gregs) OI(K, true); else OI(K, false); } \
   else if (gregs && block == kBigBlock) \
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_interp<K, false, false, true, kBigBlock>, kBigBlock, dyn_lds); \
   else if (gregs) O(K, false, true);  \
@@ -1398,6 +1428,7 @@ extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_l
     OK(CTX_RAW)
   }
 #undef OK
+#undef OI
 #undef O
   return e == hipSuccess ? n : 1;
 }

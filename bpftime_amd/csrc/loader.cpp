@@ -1258,6 +1258,7 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
   out.specialized = 0;
   out.needs_comb = true;
   out.needs_ctx = xdp;
+  out.tail_max_live = 0;
   out.join.assign(prog.size(), 1);  // (filled in below when the pointer kinds hold)
   for (size_t i = 0; i < prog.size(); i++) {
     const DInsn &d = prog[i];
@@ -1277,6 +1278,7 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
     if (xdp && d.op == X_CALL && d.hi == (int32_t)kTailHelper) {
       f.hoff = 4 + 4 * F_TAIL;
       f.imm = i < lo.tail_live.size() ? lo.tail_live[i] : 0x3fe;  // registers the frame keeps
+      out.tail_max_live = std::max<uint32_t>(out.tail_max_live, (uint32_t)__builtin_popcount((uint32_t)f.imm & 0x3fe));
     }
     if (xdp && d.op == X_CALL && d.hi == kRetHelper) f.hoff = 4 + 4 * F_TRET;
   }
@@ -1360,7 +1362,21 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
     }
     out.comb_hint = hint >= ~0u ? ~0u : (uint32_t)hint;
   }
-  if (lo.multi_entry && xdp) tail_save_masks(prog, in, lo.stack_size, out);
+  if (lo.multi_entry && xdp) {
+    tail_save_masks(prog, in, lo.stack_size, out);
+    // a live register holding the lane's own ctx pointer at a tail call is
+    // not saved: the return sets it again (FInsn imm bit 10 + r, header bit
+    // kFrameRematShift + r; gen_fast.py tail_call / tail_ret)
+    const PVal ctx0{P_CTX, 0, 0};
+    out.tail_max_live = 0;
+    for (size_t i = 0; i < prog.size(); i++) {
+      FInsn &f = out.fast[i];
+      if (f.hoff != 4 + 4 * F_TAIL) continue;
+      for (int r = 1; r <= 9; r++)
+        if (((uint64_t)f.imm >> r) & 1 && in[i][r] == ctx0) f.imm = (int64_t)(((uint64_t)f.imm & ~(1ull << r)) | (1ull << (10 + r)));
+      out.tail_max_live = std::max<uint32_t>(out.tail_max_live, (uint32_t)__builtin_popcountll((uint64_t)f.imm & 0x3fe));
+    }
+  }
   std::vector<int64_t> kimm;
   std::vector<int32_t> kaux;
   if (!getenv("BPFTIME_AMD_NO_KLDX")) const_loads(prog, lo.lddw_src, in, kimm, kaux);

@@ -59,6 +59,7 @@ struct FastForm {
   // LDS stack words (bit j = the j-th 8 bytes from the stack bottom) that a
   // tail-call target may write -- what a frame must save for its caller
   uint32_t tail_ctx_mask = 0x3f, tail_stack_mask = 0xffffffffu;
+  uint32_t tail_max_live = 9;  // the most registers a tail call's frame keeps (FInsn imm popcount)
   // map_update_elem (2) / map_delete_elem (3) call sites that may reach an
   // LPM trie: {helper id, map fd}.  The device changes a trie only in ORDERED
   // batches (dev_helpers.hpp lpm_update); vm_api.cpp refuses other batches

@@ -29,8 +29,9 @@
 namespace bpftime_amd {
 extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind, bool big_stack, uint32_t grid,
                                                 uint32_t ordered, uint32_t block, hipStream_t stream);
-extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds, bool gregs, uint32_t block);
-extern "C" size_t bpftime_amd_static_lds(uint32_t kind, bool big_stack, bool gregs, uint32_t block);
+extern "C" int bpftime_amd_occupancy(uint32_t kind, bool big_stack, size_t dyn_lds, bool gregs, uint32_t block,
+                                    bool image);
+extern "C" size_t bpftime_amd_static_lds_image(uint32_t kind, bool big_stack, bool gregs, uint32_t block, bool image);
 extern "C" hipError_t bpftime_amd_launch_merge(const uint64_t *log, uint32_t log_words, uint32_t nblocks,
                                                 hipStream_t stream);
 extern "C" hipError_t bpftime_amd_launch_miss_merge(const uint64_t *log, const uint32_t *counts, uint32_t cap,
@@ -422,12 +423,13 @@ class Mi355xVm {
 // The message of a launch whose block does not fit the CU's LDS: the parts
 // of its dynamic LDS (common.hpp dyn_lds_for) and the kernel's static LDS
 std::string lds_fit_error(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
-                          uint32_t lcache, bool ctx_lds, bool greg, uint32_t block) {
-  const size_t lanes = (size_t)block * ((kind == CTX_XDP && ctx_lds ? 48 : 0) + (big_stack ? 0 : stack_size));
-  const size_t dyn = dyn_lds_for(kind, big_stack, stack_size, comb_entries, lcache, ctx_lds, block);
-  const size_t stat = bpftime_amd_static_lds(kind, big_stack, greg, block);
+                          uint32_t lcache, bool ctx_lds, bool greg, uint32_t block, bool image, uint32_t tail_lds) {
+  const size_t lanes = (size_t)block * ((kind == CTX_XDP && ctx_lds ? 48 : 0) + (big_stack ? 0 : stack_size) +
+                                        tail_lds_lane_bytes(tail_lds));
+  const size_t dyn = dyn_lds_for(kind, big_stack, stack_size, comb_entries, lcache, ctx_lds, block, tail_lds);
+  const size_t stat = bpftime_amd_static_lds_image(kind, big_stack, greg, block, image);
   return "launch does not fit the CU's LDS: " + std::to_string(dyn + stat) + " bytes per " +
-         std::to_string(block) + "-lane block (lanes' ctx and stacks " + std::to_string(lanes) +
+         std::to_string(block) + "-lane block (lanes' ctx, stacks and tail-call frames " + std::to_string(lanes) +
          ", lookup cache " + std::to_string(lcache) + " sets " + std::to_string(lcache_bytes(lcache)) +
          ", launch constants " + std::to_string(kTenvBytes) + ", combining table " + std::to_string(comb_entries) +
          " entries " + std::to_string(20 * (size_t)comb_entries) + ", static " + std::to_string(stat) + ") > " +
@@ -553,6 +555,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   // blocks (common.hpp): one table and lookup cache per 16 waves
   // (BPFTIME_AMD_BLOCK=256 keeps 4-wave blocks)
   uint32_t block = greg && !im.d_tail_entry && !stage ? kBigBlock : kBlock;
+  const bool image = im.d_tail_entry != nullptr && !prog.big_stack;  // (bpftime_amd_launch_interp)
   if (const char *bs = getenv("BPFTIME_AMD_BLOCK"))
     if (atoi(bs) == (int)kBlock) block = kBlock;
   // the lookup cache: 1024 sets, or 2048 in a 1024-lane block whose
@@ -579,7 +582,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
         return bpftime_amd_occupancy(kind, prog.big_stack,
                                      dyn_lds_for(kind, prog.big_stack, prog.stack_size, e_min, lc, !gctx,
                                                  kBigBlock),
-                                     greg, kBigBlock) >= 1;
+                                     greg, kBigBlock, image) >= 1;
       };
       if (!fits(p.lcache) && p.lcache > kLcacheSets && !getenv("BPFTIME_AMD_LCACHE_SETS")) p.lcache = kLcacheSets;
       if (!fits(p.lcache)) {
@@ -595,7 +598,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     }
   }
   auto dyn_of = [&](uint32_t e) {
-    return dyn_lds_for(kind, prog.big_stack, prog.stack_size, e, p.lcache, !gctx, block);
+    return dyn_lds_for(kind, prog.big_stack, prog.stack_size, e, p.lcache, !gctx, block, p.tail_lds);
   };
   if (p.comb_entries) {
     // the table's reach: a counter that finds no entry is a device atomic
@@ -620,7 +623,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     // blocks / CU 1.32 ms, 1792 at 3 1.57, 1536 at 3 1.42 -- nor does reach
     // beyond hint / 32 at the same residency: flow-hash 3072 1.29,
     // syscall-agg 768 / 984 0.672 / 0.677 against 512 0.664)
-    while (e > kComb && bpftime_amd_occupancy(kind, prog.big_stack, dyn_of(e), greg, block) < 1) e /= 2;
+    while (e > kComb && bpftime_amd_occupancy(kind, prog.big_stack, dyn_of(e), greg, block, image) < 1) e /= 2;
     // one 1024-lane block per CU: a table that wants 2048 entries or more
     // takes the rest of the CU's LDS (multiples of 8 ways), since every
     // counter it misses is a memory-side atomic.  Measured (flow-hash, one
@@ -634,7 +637,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
       auto it = fill.find(key);
       if (it == fill.end()) {
         uint32_t f = kCombMax;
-        while (f > e && bpftime_amd_occupancy(kind, prog.big_stack, dyn_of(f), greg, block) < 1) f -= 32;
+        while (f > e && bpftime_amd_occupancy(kind, prog.big_stack, dyn_of(f), greg, block, image) < 1) f -= 32;
         it = fill.emplace(key, f).first;
       }
       e = it->second > e ? it->second : e;
@@ -654,10 +657,44 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   // every block of the launch must fit the CU's LDS (env overrides of the
   // table / cache sizes included): a launch that needs more fails, named,
   // instead of running at an occupancy of zero
+  // XDP images: the asm tier's frames of the first depths in LDS, as many
+  // depths (kTailLdsMax at most) as keep the block's residency
+  // (BPFTIME_AMD_TAIL_LDS: at most that many; 0 = every frame in global memory)
+  if (image && kind == CTX_XDP && !(p.dbg & 8)) {
+    const FastForm &ff = im.fx;
+    const uint32_t sw = prog.stack_size / 8;
+    const uint32_t words = 1 + ff.tail_max_live + (uint32_t)__builtin_popcount(ff.tail_ctx_mask & 0x3f) +
+                           (uint32_t)__builtin_popcount(ff.tail_stack_mask & (sw >= 16 ? 0xffffu : (1u << sw) - 1));
+    uint32_t most = kTailLdsMax;
+    if (const char *t = getenv("BPFTIME_AMD_TAIL_LDS")) most = std::min<uint32_t>((uint32_t)atoi(t), kTailLdsMax);
+    p.tail_lds = 0;
+    const int occ0 = bpftime_amd_occupancy(kind, prog.big_stack, dyn_of(p.comb_entries), greg, block, image);
+    auto depths = [&](uint32_t e) -> uint32_t {
+      for (uint32_t dl = most; dl >= 1 && occ0 >= 1; dl--) {
+        p.tail_lds = dl | words << 8;
+        const bool ok = bpftime_amd_occupancy(kind, prog.big_stack, dyn_of(e), greg, block, image) >= occ0;
+        p.tail_lds = 0;
+        if (ok) return dl;
+      }
+      return 0;
+    };
+    uint32_t dl = depths(p.comb_entries);
+    // a combining table above the size its counters need (the loader's hint:
+    // kComb entries hold them) gives way to a deeper LDS frame stack
+    if (dl < most && p.comb_entries > kComb && 32ull * kComb >= ff.comb_hint && !getenv("BPFTIME_AMD_COMB_ENTRIES")) {
+      const uint32_t dl2 = depths(kComb);
+      if (dl2 > dl) {
+        dl = dl2;
+        p.comb_entries = kComb;
+      }
+    }
+    p.tail_lds = dl ? dl | words << 8 : 0;
+  }
   const size_t lds_need = dyn_of(p.comb_entries);
-  const int occ_fit = bpftime_amd_occupancy(kind, prog.big_stack, lds_need, greg, block);
+  const int occ_fit = bpftime_amd_occupancy(kind, prog.big_stack, lds_need, greg, block, image);
   if (occ_fit < 1) {
-    error = lds_fit_error(kind, prog.big_stack, prog.stack_size, p.comb_entries, p.lcache, !gctx, greg, block);
+    error = lds_fit_error(kind, prog.big_stack, prog.stack_size, p.comb_entries, p.lcache, !gctx, greg, block, image,
+                          p.tail_lds);
     return -1;
   }
   {
@@ -853,9 +890,9 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   if (getenv("BPFTIME_AMD_VERBOSE"))
     fprintf(stderr,
             "bpftime_amd: launch units %llu grid %u block %u comb %u lcache %u stage %u stack %u gregs %d gctx %d unwind %d "
-            "miss cap %u\n",
+            "miss cap %u tail lds %u x %u words occ %d\n",
             (unsigned long long)b->count, grid, block, p.comb_entries, p.lcache, p.stage, (unsigned)prog.stack_size,
-            p.gregs ? 1 : 0, p.gctx ? 1 : 0, p.unwind_idx, p.miss_cap);
+            p.gregs ? 1 : 0, p.gctx ? 1 : 0, p.unwind_idx, p.miss_cap, p.tail_lds & 0xff, p.tail_lds >> 8, occ_fit);
   // EBPF_BATCH_TIMED: events around this batch's kernels only (the host
   // work above -- linking, buffers, index upkeep -- stays outside)
   const bool timed = (b->flags & EBPF_BATCH_TIMED) != 0;

@@ -18,7 +18,7 @@ import _tailcall as tc
 pytestmark = pytest.mark.gpu
 
 I32 = lambda v: struct.pack("<i", v)  # noqa: E731
-PA_FD, TARGET_FD = 1001, 1002
+PA_FD, TARGET_FD, PA2_FD = 1001, 1002, 1003
 
 
 def test_device_prog_array_map_kat(fresh_runtime):
@@ -104,6 +104,63 @@ def test_xdp_tailcall_parity(fresh_oracle, fresh_runtime, n):
     ov, opk = _run_both(po, dev, ovm, dvm, n, 11 + n, cnt_o, cnt_d)
     idx = opk[:, 0] & 3
     assert (ov[idx == 3] == 31 + 1005).all() and (ov[idx == 2] == (0xFFFFFFFF + 1005) & 0xFFFFFFFF).all()
+
+
+# frame tiers: the asm tier's frames of the first depths in LDS (default:
+# as many depths as keep the residency), none (TAIL_LDS 0), one depth; C++
+# pops of asm-pushed frames (DBG 16) and C++ frames only (DBG 8)
+@pytest.mark.parametrize("env", [{"BPFTIME_AMD_TAIL_LDS": "0"}, {"BPFTIME_AMD_TAIL_LDS": "1"},
+                                 {"BPFTIME_AMD_DBG": "16"}, {"BPFTIME_AMD_DBG": "8"}])
+def test_xdp_tailcall_frame_tiers(fresh_oracle, fresh_runtime, monkeypatch, env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    test_xdp_tailcall_parity(fresh_oracle, fresh_runtime, 70000)
+
+
+def _mixed_array_caller():
+    """Like xdp_caller, but lanes with data[1] odd tail-call through a second
+    prog array (same slots): the map fd is not wave-uniform, so the C++ tier
+    pushes those waves' depth-0 frames (full frames, in global memory) and
+    the asm tier pops them at the targets' exits only through C++, while the
+    recursion target pushes its own frames in the asm tier."""
+    a = Asm()
+    a.mov64(6, "r1")
+    a.ldx(8, 2, 6, 0).ldx(8, 3, 6, 8)
+    a.mov64(4, "r2").add64(4, 2).jmp("jgt", 4, "r3", "short")
+    a.ldx(1, 7, 2, 0).alu64("and", 7, 3)
+    a.ldx(1, 8, 2, 1).alu64("and", 8, 1)
+    a.lddw(9, 0x1111222233334444).stx(8, 10, -8, 9)
+    a.ld_map_fd(2, PA_FD)
+    a.jmp("jeq", 8, 0, "one")
+    a.ld_map_fd(2, PA2_FD)
+    a.label("one")
+    a.mov64(1, "r6").mov64(3, "r7").call(tc.TAIL)
+    a.ldx(8, 1, 10, -8).lddw(2, 0x1111222233334444).jmp("jne", 1, "r2", "bad")
+    a.add64(0, 1000)
+    a.label("bad")
+    a.ldx(4, 1, 6, 20).alu64("add", 0, "r1")
+    a.exit()
+    a.label("short").mov64(0, 1).exit()
+    return a.assemble()
+
+
+@pytest.mark.parametrize("lds", ["0", "4"])
+def test_xdp_tailcall_full_and_masked_frames(fresh_oracle, fresh_runtime, monkeypatch, lds):
+    monkeypatch.setenv("BPFTIME_AMD_TAIL_LDS", lds)
+    po, dev = fresh_oracle, fresh_runtime
+    (pa_o, cnt_o), (pa_d, cnt_d) = _xdp_pair(po, dev)
+    pa2_o = po.OracleMap(isa.BPF_MAP_TYPE_PROG_ARRAY, 4, 4, 4, fd=PA2_FD)
+    pa2_d = dev.Map(isa.BPF_MAP_TYPE_PROG_ARRAY, 4, 4, 4, fd=PA2_FD)
+    for k, fd in ((0, 900), (1, 901), (3, 903)):
+        assert pa2_o.update(I32(k), I32(fd)) == 0 and pa2_d.update(I32(k), I32(fd)) == 0
+    code = _mixed_array_caller()
+    ovm = po.OracleVM()
+    ovm.load(code)
+    dvm = dev.VM()
+    dvm.load(code)
+    ov, opk = _run_both(po, dev, ovm, dvm, 70000, 5, cnt_o, cnt_d)
+    idx = opk[:, 0] & 3
+    assert (ov[idx == 3] == 31 + 1005).all() and (ov[idx == 1] == 2 + 1005).all()
 
 
 def test_xdp_tailcall_relink(fresh_oracle, fresh_runtime):
