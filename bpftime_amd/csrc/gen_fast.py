@@ -1884,15 +1884,22 @@ class Gen:
         self.e(f"{nog}:", "s_mov_b64 exec, s[64:65]", f"s_cbranch_execz {nol}")
         self.lds_frame_ptr()
         self.e("ds_write_b64 v41, v[44:45]", "v_add_u32 v48, 0x800, v41")
-        for r in range(1, 10):
-            skip = self.label("tlr")
-            self.e(f"s_bitcmp1_b32 s42, {r}", f"s_cbranch_scc0 {skip}",
-                   f"ds_write_b64 v48, v[{R0 + 2 * r}:{R0 + 2 * r + 1}]", "v_add_u32 v48, 0x800, v48", f"{skip}:")
-        for k in range(6):
-            skip = self.label("tlc")
-            self.e(f"s_bitcmp1_b32 s68, {k}", f"s_cbranch_scc0 {skip}",
-                   f"ds_read_b64 v[42:43], v{R0 + 2} offset:{8 * k}", "s_waitcnt lgkmcnt(0)",
-                   "ds_write_b64 v48, v[42:43]", "v_add_u32 v48, 0x800, v48", f"{skip}:")
+        # the live registers (s42 bits 1..9), then the ctx words of the mask
+        # (s68 bits 0..5), one loop trip per word
+        lr, ld, lc, lcd = self.label("tlr"), self.label("tlrd"), self.label("tlc"), self.label("tlcd")
+        self.e("s_and_b32 s70, s42, 0x3fe",
+               f"{lr}:", "s_cmp_eq_u32 s70, 0", f"s_cbranch_scc1 {ld}",
+               "s_ff1_i32_b32 s69, s70", "s_bitset0_b32 s70, s69", "s_lshl_b32 s71, s69, 1")
+        self.rd("s71", 42)
+        self.e("ds_write_b64 v48, v[42:43]", "v_add_u32 v48, 0x800, v48", f"s_branch {lr}",
+               f"{ld}:",
+               "s_and_b32 s70, s68, 0x3f",
+               f"{lc}:", "s_cmp_eq_u32 s70, 0", f"s_cbranch_scc1 {lcd}",
+               "s_ff1_i32_b32 s69, s70", "s_bitset0_b32 s70, s69", "s_lshl_b32 s71, s69, 3",
+               f"v_add_u32 v49, s71, v{R0 + 2}",
+               "ds_read_b64 v[42:43], v49", "s_waitcnt lgkmcnt(0)",
+               "ds_write_b64 v48, v[42:43]", "v_add_u32 v48, 0x800, v48", f"s_branch {lc}",
+               f"{lcd}:")
         self.e("s_and_b32 s71, s85, 0xffff")
         self.lds_stack_words(store=True, mask="s71")
         self.e(f"{nol}:", "s_mov_b64 exec, s[54:55]")
@@ -1998,18 +2005,32 @@ class Gen:
         nl = self.label("trnl")
         self.e(f"{ng}:", "s_mov_b64 exec, s[52:53]", f"s_cbranch_execz {nl}",
                "v_add_u32 v48, 0x800, v41")
+        # the live registers the header names: one loop trip each when every
+        # lane's header is the same (one call site), else per register
+        gen_, uni, ur, urd, regs_done = (self.label(x) for x in ("tlg", "tlu", "tlur", "tlurd", "tlrd"))
+        self.e("v_readfirstlane_b32 s70, v47", "v_cmp_ne_u32 vcc, s70, v47", "s_and_b64 vcc, vcc, exec",
+               f"s_cbranch_vccnz {gen_}",
+               f"{uni}:", "s_lshr_b32 s70, s70, 8", "s_and_b32 s70, s70, 0x3fe",
+               f"{ur}:", "s_cmp_eq_u32 s70, 0", f"s_cbranch_scc1 {urd}",
+               "s_ff1_i32_b32 s69, s70", "s_bitset0_b32 s70, s69", "s_lshl_b32 s71, s69, 1",
+               "ds_read_b64 v[42:43], v48", "v_add_u32 v48, 0x800, v48", "s_waitcnt lgkmcnt(0)")
+        self.wr("s71", 42)
+        self.e(f"s_branch {ur}", f"{urd}:", f"s_branch {regs_done}", f"{gen_}:")
         for r in range(1, 10):
             skip = self.label("tlr")
             self.e("s_mov_b64 exec, s[52:53]",
                    f"v_and_b32 v49, {1 << (8 + r)}, v47", "v_cmp_ne_u32 vcc, 0, v49",
                    "s_and_b64 exec, s[52:53], vcc", f"s_cbranch_execz {skip}",
                    f"ds_read_b64 v[{R0 + 2 * r}:{R0 + 2 * r + 1}], v48", "v_add_u32 v48, 0x800, v48", f"{skip}:")
-        self.e("s_mov_b64 exec, s[52:53]")
-        for k in range(6):
-            skip = self.label("tlc")
-            self.e(f"s_bitcmp1_b32 s68, {k}", f"s_cbranch_scc0 {skip}",
-                   "ds_read_b64 v[42:43], v48", "v_add_u32 v48, 0x800, v48", "s_waitcnt lgkmcnt(0)",
-                   f"ds_write_b64 %[r1lo], v[42:43] offset:{8 * k}", f"{skip}:")
+        lc, lcd = self.label("tlc"), self.label("tlcd")
+        self.e(f"{regs_done}:", "s_mov_b64 exec, s[52:53]",
+               "s_and_b32 s70, s68, 0x3f",
+               f"{lc}:", "s_cmp_eq_u32 s70, 0", f"s_cbranch_scc1 {lcd}",
+               "s_ff1_i32_b32 s69, s70", "s_bitset0_b32 s70, s69", "s_lshl_b32 s71, s69, 3",
+               "ds_read_b64 v[42:43], v48", "v_add_u32 v48, 0x800, v48",
+               "v_add_u32 v49, s71, %[r1lo]", "s_waitcnt lgkmcnt(0)",
+               "ds_write_b64 v49, v[42:43]", f"s_branch {lc}",
+               f"{lcd}:")
         self.e("s_and_b32 s71, s85, 0xffff")
         self.lds_stack_words(store=False, mask="s71")
         self.e("s_waitcnt lgkmcnt(0)",
@@ -2099,7 +2120,6 @@ class Gen:
                    "v_mov_b32 %[lpc], s52", "s_or_b64 s[60:61], s[60:61], exec", f"{skip}:")
 
     def divergence_routines(self):
-        n4 = 4 * len(handler_ids())
         back, spush, ahead = self.label("sback"), self.label("spush"), self.label("dahead")
         # split branch: vcc = taken lanes, W = the branch
         self.e(f"{L('split')}:",
@@ -2119,12 +2139,9 @@ class Gen:
                f"{spush}:")
         self.push()
         self.dispatch()
-        # divergent dispatch check (s[52:53] = divergent table entry)
-        self.e(f"{L('dcheck')}:",
-               "s_cmp_ge_u32 s48, s86", f"s_cbranch_scc1 {L('dswitch')}",
-               f"s_sub_u32 s52, s52, {n4}", "s_subb_u32 s53, s53, 0",
-               "s_setpc_b64 s[52:53]",
-               f"{L('dswitch')}:",
+        # divergent dispatch (build: the divergent table's per-handler
+        # stubs): the running group reached the first pending IP
+        self.e(f"{L('dswitch')}:",
                "s_waitcnt lgkmcnt(0)",       # the fall-through fetch lands before another
                "s_cmp_eq_u32 s48, s86", f"s_cbranch_scc0 {ahead}",
                "s_or_b64 exec, exec, s[88:89]")                # reconvergence
@@ -2226,7 +2243,12 @@ class Gen:
         for name in ids:                   # table: entry i at TB + 4 + 4*i
             e(f"s_branch {L('h_' + name)}")
         for name in ids:                   # divergent table: TB + 4N + 4 + 4*i
-            e(f"s_branch {L('dcheck')}")
+            e(f"s_branch {L('d_' + name)}")
+        # divergent dispatch: the running group has reached the first
+        # pending group's IP (s86) -> dswitch; else straight to the handler
+        for name in ids:
+            e(f"{L('d_' + name)}:", "s_cmp_ge_u32 s48, s86", f"s_cbranch_scc1 {L('dswitch')}",
+              f"s_branch {L('h_' + name)}")
         e(f"{L('start')}:")
         self.dispatch()
         # ---- handlers ----
@@ -2421,6 +2443,11 @@ def main():
         for i, name in enumerate(ids):
             f.write(f"  F_{name} = {i},\n")
         f.write(f"  F_COUNT = {len(ids)}\n}};\n\n")
+        f.write("// their names (BPFTIME_AMD_DUMP_FAST: vm_api.cpp prints a linked form)\n"
+                "inline const char *fop_name(uint32_t id) {\n  static const char *const k[] = {\n")
+        for name in ids:
+            f.write(f'      "{name}",\n')
+        f.write("  };\n  return id < F_COUNT ? k[id] : \"?\";\n}\n\n")
         f.write("// 32-byte threaded instruction (gen_fast.py register map, word for word):\n"
                 "//   dst_x2 / src_x2 are eBPF register numbers times two (VGPR pair index);\n"
                 "//   the staged / map-bound handlers reuse the fields as documented there\n"

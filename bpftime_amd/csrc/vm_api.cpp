@@ -98,6 +98,11 @@ struct Image {
     if (it != links.end()) return it->second;
     std::vector<FInsn> out;
     link_fast(xdp ? fx : fr, head, stage, ordered, prog.prog, out, uw ? 1 : -1, lc_sets, po);
+    if (getenv("BPFTIME_AMD_DUMP_FAST"))  // the linked threaded form, one FInsn a line
+      for (size_t i = 0; i < out.size(); i++)
+        fprintf(stderr, "bpftime_amd: fast %3zu %-18s w1 %08x imm %llx dst %u src %u tgt %u aux %x\n", i,
+                fop_name((out[i].hoff - 4) / 4), out[i].w1, (unsigned long long)out[i].imm, out[i].dst_x2 / 2,
+                out[i].src_x2 / 2, out[i].target / kFastInsnBytes, (unsigned)out[i].aux);
     FInsn *d = nullptr;
     const size_t bytes = out.size() * sizeof(FInsn);
     if (hipMalloc((void **)&d, bytes) != hipSuccess) return nullptr;
