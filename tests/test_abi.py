@@ -105,3 +105,29 @@ def test_sysbpf_errors_before_device_work():
     assert vm.sys_bpf(vm.BPF_MAP_FREEZE, bytearray(128))[0] == 0
     assert _lib.lib().bpftime_amd_handle_sysbpf(vm.BPF_MAP_CREATE, None, 0) == -1
     assert struct.calcsize("<IIQQQ") == 32
+
+
+def test_lds_sizing_of_launch_shapes():
+    """The LDS a block asks for (bpftime_amd_lds_bytes: common.hpp
+    dyn_lds_for + the kernel's static LDS, restated without a device): the
+    override shape that failed in round 4 (flow-hash with
+    BPFTIME_AMD_COMB_ENTRIES=2000 BPFTIME_AMD_LCACHE_SETS=2048, 1024-lane
+    blocks) exceeds the CU's 160 KiB and is refused by name before a launch
+    (vm_api.cpp lds_fit_error); the default flow-hash and headline shapes
+    fit."""
+    l = _lib.lib()
+    cu = 160 * 1024
+    xdp, syscall = 1, 2
+    # kind, big_stack, stack, comb entries, lcache sets, ctx in LDS, gregs, block
+    bad = l.bpftime_amd_lds_bytes(xdp, False, 32, 2000, 2048, False, True, 1024)
+    assert bad > cu
+    flow = l.bpftime_amd_lds_bytes(xdp, False, 32, 4000, 1024, False, True, 1024)
+    assert flow <= cu
+    head = l.bpftime_amd_lds_bytes(xdp, False, 8, 0, 0, False, False, 256)
+    assert head <= cu // 4           # four headline blocks per CU
+    # the parts add up: each entry of the combining table 20 B, each lookup
+    # set 40 B, each lane's stack its bytes
+    assert l.bpftime_amd_lds_bytes(xdp, False, 32, 2008, 2048, False, True, 1024) - bad == 8 * 20
+    assert l.bpftime_amd_lds_bytes(xdp, False, 32, 2000, 2049, False, True, 1024) - bad == 40
+    assert l.bpftime_amd_lds_bytes(xdp, False, 40, 2000, 2048, False, True, 1024) - bad == 8 * 1024
+    assert l.bpftime_amd_lds_bytes(syscall, False, 32, 512, 2048, True, True, 1024) < cu
