@@ -145,7 +145,21 @@ constexpr uint32_t kIxProbes = 8;  // asm tier: index probes before the C++ tier
 // index: bit b = bucket b is not EMPTY (bits past nbuckets set), kept by
 // device inserts while the index is valid and rebuilt with it (maps.cpp)
 constexpr uint32_t kIxRes = 0xffffffffu;
-inline BA_HD uint64_t ix_bitmap(uint64_t ix, uint32_t mask) { return ix + 4ull * ((uint64_t)mask + 1); }
+// Keyed indexes (keys of at most 16 B): beside the u32 entries, the key of
+// each entry at the same position in an array of 8-B (keys <= 8 B) or 16-B
+// slots, so a probe loads entry and key together and never reads the bucket
+// (one round trip per probe instead of entry, then bucket: flow-hash 0.83 ->
+// 0.67 ms; config 3's index of 262,144 positions is 5 MiB, a lookup touching
+// one key line as the reference probe touches one bucket line; at 131,072
+// positions the waves' longest probes made it slower, 0.85 ms).  Longer keys
+// keep only the entries and compare in the bucket.  An
+// insert writes the key before it publishes the entry (dev_helpers.hpp
+// ix_insert).  Layout: entries, keys, then the bucket bitmap.
+BA_HD constexpr uint32_t ix_key_stride(uint32_t key_size) { return key_size <= 8 ? 8 : key_size <= 16 ? 16 : 0; }
+inline BA_HD uint64_t ix_keys(uint64_t ix, uint32_t mask) { return ix + 4ull * ((uint64_t)mask + 1); }
+inline BA_HD uint64_t ix_bitmap(uint64_t ix, uint32_t mask, uint32_t key_size) {
+  return ix + (4ull + ix_key_stride(key_size)) * ((uint64_t)mask + 1);
+}
 inline BA_HD uint64_t ix_bitmap_words(uint64_t nbuckets) { return (nbuckets + 63) / 64; }
 
 // LRU_HASH recency (lru_var_hash_map.cpp keeps a doubly linked list, head =

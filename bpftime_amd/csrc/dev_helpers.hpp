@@ -157,7 +157,7 @@ __device__ unsigned long long g_istats[8];
 __device__ uint64_t ix_insert(const DMap &m, uint64_t key, uint64_t h, uint64_t ea, uint64_t init,
                               uint32_t init_bytes, bool *inserted, uint64_t part, uint32_t part_off,
                               uint32_t part_bytes) {
-  const uint64_t nb = m.nbuckets, bm = ix_bitmap(m.ix, m.ix_mask), nw = (nb + 63) >> 6;
+  const uint64_t nb = m.nbuckets, bm = ix_bitmap(m.ix, m.ix_mask, m.key_size), nw = (nb + 63) >> 6;
   uint64_t b = h % nb, left = nb;
   uint32_t words = 0;
   while (left) {
@@ -221,6 +221,21 @@ __device__ uint64_t ix_insert(const DMap &m, uint64_t key, uint64_t h, uint64_t 
         for (uint32_t k = 0; k < init_bytes; k += 4)
           __hip_atomic_store(G32(s + m.val_off + k), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (part) copy_bytes_publish(s + m.val_off + part_off, part, part_bytes);
+      // a keyed index (common.hpp ix_key_stride): the key at the entry's
+      // position before the entry is published
+      // (one 8- or 16-B store: a reader's line holds all of it or none, so a
+      // stale key line reads zero, gen_fast.py index_probe)
+      if (const uint32_t ks = ix_key_stride(m.key_size)) {
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (uint32_t i = 0; i < m.key_size; i++) ((uint8_t *)w)[i] = *(const volatile uint8_t *)(key + i);
+        const uint64_t ka = ix_keys(m.ix, m.ix_mask) + (ea - m.ix) / 4 * ks;
+        typedef __attribute__((ext_vector_type(2))) uint32_t v2u;
+        typedef __attribute__((ext_vector_type(4))) uint32_t v4u;
+        if (ks == 8)
+          *(__attribute__((address_space(1))) v2u *)(uintptr_t)ka = v2u{w[0], w[1]};
+        else
+          *(__attribute__((address_space(1))) v4u *)(uintptr_t)ka = v4u{w[0], w[1], w[2], w[3]};
+      }
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // key/value stores drained first
       __hip_atomic_store(G32(s), ST_FILLED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -257,6 +272,7 @@ __device__ uint64_t hash_find_ix(const DMap &m, uint64_t key, uint64_t h, bool i
                                  uint32_t init_bytes, bool *inserted, uint64_t part, uint32_t part_off,
                                  uint32_t part_bytes) {
   uint32_t p = ix_pos(h, m.ix_mask), spins = 0;
+  const uint32_t ks = ix_key_stride(m.key_size);
   ISTAT(insert ? 5 : 6, 1);
   for (uint32_t t = 0; t <= m.ix_mask;) {
     ISTAT(7, 1);
@@ -281,6 +297,11 @@ __device__ uint64_t hash_find_ix(const DMap &m, uint64_t key, uint64_t h, bool i
         __builtin_amdgcn_s_sleep(1);
         continue;
       }
+    } else if (ks) {
+      // a keyed index: the entry's key was published before the entry (read
+      // coherently when the entry was: ix_insert)
+      if (key_eq(ix_keys(m.ix, m.ix_mask) + (uint64_t)p * ks, key, m.key_size, true))
+        return m.data + (uint64_t)(e - 1) * m.slot_size;
     } else {
       const uint64_t s = m.data + (uint64_t)(e - 1) * m.slot_size;
       uint32_t st = ald32(s);

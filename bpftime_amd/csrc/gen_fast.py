@@ -1215,15 +1215,16 @@ class Gen:
     def dbg_lanes(self, slot, mask):
         """BPFTIME_AMD_DBG 512: add the lanes of `mask` (an SGPR pair, a
         subset of exec) to counter `slot` at tenv[1] (index-probe exits);
-        uses s[52:53], s69, v[56:59]."""
+        uses s[52:53], s69, v[42:43], v[58:59] (the probe's entry in v56
+        and key in v[48:51] stay)."""
         off, back = self.label("dlo"), self.label("dlb")
         self.e("s_bitcmp1_b32 %[oflags], 3", f"s_cbranch_scc0 {off}",
                "s_mov_b64 s[52:53], exec", f"s_and_b64 exec, exec, {mask}", f"s_cbranch_execz {back}",
-               f"s_sub_u32 s69, %[comb], {TENV - 8}", "v_mov_b32 v56, s69",
-               "ds_read_b64 v[56:57], v56",
+               f"s_sub_u32 s69, %[comb], {TENV - 8}", "v_mov_b32 v42, s69",
+               "ds_read_b64 v[42:43], v42",
                "v_mov_b32 v58, 1", "v_mov_b32 v59, 0",
                "s_waitcnt lgkmcnt(0)",
-               f"global_atomic_add_x2 v[56:57], v[58:59], off offset:{8 * slot}",
+               f"global_atomic_add_x2 v[42:43], v[58:59], off offset:{8 * slot}",
                f"{back}:", "s_mov_b64 exec, s[52:53]",
                f"{off}:")
 
@@ -1249,38 +1250,67 @@ class Gen:
     def index_probe(self, kd, done, bail):
         """The map's lookup index (common.hpp ix_pos), if it has one: up to
         kIxProbes entries from ix_pos(h) until every lane has found its key
-        (r0 = that slot's value).  The index holds exactly the keys the
+        (r0 = that slot's value).  The index is keyed (common.hpp
+        ix_key_stride: the key of each entry at the same position in an
+        array beside the entries), so a probe loads entry and key together
+        and the bucket is never read.  The index holds exactly the keys the
         reference probe reaches, so an empty entry in any lane (a miss, or a
         line of this XCD's L2 an insert has not reached yet), an entry an
         insert holds reserved (kIxRes), or too many probes hand the whole
-        wave to the C++ tier's lookup (dev_helpers.hpp hash_find_ix:
-        coherent reads, the miss record the lookup-or-init race rule needs)
-        instead of the reference probe's walk.  A map without an index goes
-        to the reference probe that follows (h stays in v[48:49])."""
+        wave to the C++ tier's lookup (dev_helpers.hpp hash_find_ix: coherent
+        reads, the miss record the lookup-or-init race rule needs) instead of
+        the reference probe's walk.  A map without an index goes to the
+        reference probe that follows (h stays in v[48:49]).  A published
+        entry's key was written (one store) before the entry: a key line this
+        XCD's L2 holds from before can only read zero, so a hit on the
+        all-zero key is confirmed in its bucket."""
         loop, fail = self.label("ixl"), self.label("ixf")
+        ks = 8 if kd <= 2 else 16
         self.e("s_cmp_eq_u64 s[74:75], 0", f"s_cbranch_scc1 {fail}",
                "s_mov_b32 s85, 0x85ebca6b", "v_mul_lo_u32 v41, v49, s85", "v_xor_b32 v41, v41, v48",
                "s_mov_b32 s85, 0x9e3779b1", "v_mul_lo_u32 v41, v41, s85",
                "v_lshrrev_b32 v50, 16, v41", "v_xor_b32 v41, v41, v50", "v_and_b32 v41, s67, v41",
                "s_mov_b32 s85, 0",
                f"{loop}:",
+               # the keys: 4 * (ix_mask + 1) bytes after the entries
+               "s_add_u32 s52, s67, 1", "s_mov_b32 s53, 0", "s_lshl_b64 s[52:53], s[52:53], 2",
+               "s_add_u32 s52, s52, s74", "s_addc_u32 s53, s53, s75",
                "v_mad_u64_u32 v[42:43], s[56:57], v41, 4, s[74:75]",
-               "global_load_dword v50, v[42:43], off sc1",
+               f"v_mad_u64_u32 v[54:55], s[56:57], v41, {ks}, s[52:53]",
+               "global_load_dword v56, v[42:43], off sc1",                      # bucket + 1
+               "global_load_dwordx2 v[48:49], v[54:55], off sc1" if ks == 8 else
+               "global_load_dwordx4 v[48:51], v[54:55], off sc1",               # its key
                "s_waitcnt vmcnt(0)",
-               "v_cmp_eq_u32 s[56:57], 0, v50",                                 # empty entry
-               "v_cmp_eq_u32 vcc, -1, v50", "s_or_b64 s[56:57], s[56:57], vcc")  # ... or reserved
+               "v_cmp_eq_u32 s[56:57], 0, v56",                                 # empty entry
+               "v_cmp_eq_u32 vcc, -1, v56", "s_or_b64 s[56:57], s[56:57], vcc")  # ... or reserved
         self.dbg_lanes(2, "s[56:57]")
         self.e("s_cmp_lg_u64 s[56:57], 0", f"s_cbranch_scc1 {bail}",
-               "v_add_u32 v50, -1, v50",
+               "v_cmp_eq_u32 s[56:57], v48, v44", "v_mov_b32 v57, v44")
+        for j in range(1, kd):
+            self.e(f"v_cmp_eq_u32 vcc, v{48 + j}, v{44 + j}", "s_and_b64 s[56:57], s[56:57], vcc",
+                   f"v_or_b32 v57, v57, v{44 + j}")
+        nz = self.label("ixnz")
+        self.e("v_add_u32 v50, -1, v56",
                "v_mov_b32 v51, s68",
-               "v_mad_u64_u32 v[54:55], s[56:57], v50, v51, s[64:65]",           # slot
-               "global_load_dword v51, v[54:55], off sc1",
-               "global_load_dwordx4 v[56:59], v[54:55], off offset:8 sc1",
-               "s_waitcnt vmcnt(0)",
-               "v_cmp_eq_u32 s[56:57], 1, v51")                                 # FILLED
-        for j in range(kd):
-            self.e(f"v_cmp_eq_u32 vcc, v{56 + j}, v{44 + j}", "s_and_b64 s[56:57], s[56:57], vcc")
-        self.e("s_and_saveexec_b64 s[62:63], s[56:57]",                         # exec = hits
+               "v_mad_u64_u32 v[54:55], vcc, v50, v51, s[64:65]",               # slot
+               # hits on the all-zero key: confirmed in the bucket (state
+               # FILLED and the key, as an index without keys does)
+               "v_cmp_eq_u32 vcc, 0, v57", "s_and_b64 vcc, vcc, s[56:57]", "s_and_b64 s[62:63], vcc, exec",
+               f"s_cbranch_scc0 {nz}",
+               "s_mov_b64 s[52:53], exec", "s_mov_b64 exec, s[62:63]",
+               # (v50 = the bucket stays for the lookup cache's fill)
+               "global_load_dword v57, v[54:55], off sc1",
+               "global_load_dwordx2 v[58:59], v[54:55], off offset:8 sc1")
+        if kd > 2:
+            self.e("global_load_dwordx2 v[42:43], v[54:55], off offset:16 sc1")
+        self.e("s_waitcnt vmcnt(0)",
+               "v_cmp_ne_u32 vcc, 1, v57")
+        for j, v in zip(range(kd), (58, 59, 42, 43)):
+            self.e(f"v_cmp_ne_u32 s[62:63], v{v}, v{44 + j}", "s_or_b64 vcc, vcc, s[62:63]")
+        self.e("s_and_b64 vcc, vcc, exec", "s_andn2_b64 s[56:57], s[56:57], vcc",
+               "s_mov_b64 exec, s[52:53]",
+               f"{nz}:",
+               "s_and_saveexec_b64 s[62:63], s[56:57]",                         # exec = hits
                f"v_add_co_u32 v{R0}, vcc, s70, v54", f"v_addc_co_u32 v{R0 + 1}, vcc, 0, v55, vcc")
         self.lcache_fill(50)
         self.e("s_andn2_b64 exec, s[62:63], s[56:57]",                          # exec = other keys

@@ -880,9 +880,10 @@ static int ix_rebuild(int fd) {
   r.ix_stale.erase(fd);
   if (e0 == nb) return 0;  // full table: no index (lookups take the reference probe)
   const uint64_t isz = (uint64_t)m.d.ix_mask + 1, words = ix_bitmap_words(nb);
-  // the index, then the bucket bitmap (common.hpp ix_bitmap): one upload
-  std::vector<uint32_t> ix(isz + 2 * words, 0);
-  uint64_t *bits = (uint64_t *)(ix.data() + isz);
+  const uint32_t ks = ix_key_stride(m.key_size);  // key bytes per position (keyed indexes)
+  // the index (entries, keys), then the bucket bitmap (common.hpp ix_bitmap): one upload
+  std::vector<uint32_t> ix(isz * (4 + ks) / 4 + 2 * words, 0);
+  uint64_t *bits = (uint64_t *)(ix.data() + isz * (4 + ks) / 4);
   for (uint64_t i = 0; i < nb; i++)
     if (state(i) != 0) bits[i >> 6] |= 1ull << (i & 63);
   if (nb % 64) bits[words - 1] |= ~0ull << (nb % 64);
@@ -903,6 +904,7 @@ static int ix_rebuild(int fd) {
     uint32_t p = ix_pos(h, m.d.ix_mask);
     while (ix[p]) p = (p + 1) & m.d.ix_mask;
     ix[p] = (uint32_t)i + 1;
+    if (ks) memcpy((uint8_t *)ix.data() + 4 * isz + (uint64_t)p * ks, key, m.key_size);
   }
   if (hipMemcpy((void *)m.ix_addr, ix.data(), 4 * ix.size(), hipMemcpyHostToDevice) != hipSuccess) return -1;
   m.ix_valid = true;
@@ -1131,14 +1133,19 @@ int bpftime_maps_create(int fd, const char *name, struct bpf_map_attr attr) {
     // it is at most half full; an empty table's index is empty and valid.
     // After it the bucket bitmap (common.hpp ix_bitmap), the bits past the
     // last bucket set
+    // (keyed indexes, common.hpp ix_key_stride: the keys beside the
+    // entries; config 3's 65,536 flows take 262,144 positions, 5 MiB with
+    // their keys, of which a lookup touches one key line as the reference
+    // probe touches one bucket line)
+    const uint32_t ks = ix_key_stride(m.key_size);
     uint64_t isz = 64;
     while (isz < 2 * (uint64_t)d.nbuckets) isz <<= 1;
     const uint64_t words = ix_bitmap_words(d.nbuckets);
-    uint64_t ix = isz <= (1ull << 32) ? r.arena_alloc(4 * isz + 8 * words) : 0;
+    uint64_t ix = isz <= (1ull << 32) ? r.arena_alloc((4 + ks) * isz + 8 * words) : 0;
     const uint64_t pad = d.nbuckets % 64 ? ~0ull << (d.nbuckets % 64) : 0;
-    if (ix && hipMemset((void *)ix, 0, 4 * isz + 8 * words) == hipSuccess &&
-        hipMemcpy((void *)(ix_bitmap(ix, (uint32_t)(isz - 1)) + 8 * (words - 1)), &pad, 8, hipMemcpyHostToDevice) ==
-            hipSuccess) {
+    if (ix && hipMemset((void *)ix, 0, (4 + ks) * isz + 8 * words) == hipSuccess &&
+        hipMemcpy((void *)(ix_bitmap(ix, (uint32_t)(isz - 1), m.key_size) + 8 * (words - 1)), &pad, 8,
+                  hipMemcpyHostToDevice) == hipSuccess) {
       m.ix_addr = ix;
       m.ix_valid = true;
       d.ix = ix;

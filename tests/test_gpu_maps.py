@@ -476,3 +476,63 @@ def test_ctx_stack_lookup_fits_cu(fresh_oracle, fresh_runtime, nflows):
     tot = sum(struct.unpack("<QQ", v)[0] for v in om.items().values())
     ip = (slots[:, 12] == 0x08) & (slots[:, 13] == 0)
     assert tot == 7 * int(ip.sum())
+
+
+def _keyed_counter_prog(map_fd, ksz):
+    """The flow-hash idiom over a key of ksz bytes copied from the packet's
+    first bytes: lookup, else insert zero (BPF_NOEXIST) and look up again,
+    then add 1 to the value."""
+    a = Asm()
+    a.mov64(6, "r1")
+    a.ldx(8, 2, 6, 0).ldx(8, 3, 6, 8)
+    a.mov64(4, "r2").add64(4, 32).mov64(0, isa.XDP_DROP).jmp("jgt", 4, "r3", "out")
+    for i in range(ksz // 4):
+        a.ldx(4, 5, 2, 4 * i).stx(4, 10, -32 + 4 * i, "r5")
+    a.st(8, 10, -48, 0)
+    a.ld_map_fd(1, map_fd).mov64(2, "r10").add64(2, -32).call(BPF_FUNC_map_lookup_elem)
+    a.jmp("jne", 0, 0, "have")
+    a.ld_map_fd(1, map_fd).mov64(2, "r10").add64(2, -32).mov64(3, "r10").add64(3, -48)
+    a.mov64(4, BPF_NOEXIST).call(BPF_FUNC_map_update_elem)
+    a.ld_map_fd(1, map_fd).mov64(2, "r10").add64(2, -32).call(BPF_FUNC_map_lookup_elem)
+    a.mov64(1, "r0").mov64(0, isa.XDP_ABORTED).jmp("jeq", 1, 0, "out")
+    a.mov64(0, "r1")
+    a.label("have")
+    a.mov64(1, 1).atomic(8, ATOMIC_ADD, 0, 0, "r1")
+    a.mov64(0, isa.XDP_PASS)
+    a.label("out")
+    a.exit()
+    return a.assemble()
+
+
+@pytest.mark.parametrize("ksz", [4, 8, 12, 16, 20])
+def test_keyed_index_inserts_and_lookups(fresh_oracle, fresh_runtime, ksz):
+    """Hash lookups through the keyed lookup index (common.hpp ix_key_stride:
+    keys of at most 16 B compare in the index, longer ones in the bucket)
+    while the same launch inserts: 300 keys that share all but their last
+    dword, the all-zero key among them (a key line an XCD's L2 holds from
+    before the insert reads zero: gen_fast.py index_probe confirms zero-key
+    hits in the bucket), a Zipf-like mix over 2^18 frames, one cold launch
+    then a warm one, against the oracle's counts."""
+    po, dev = fresh_oracle, fresh_runtime
+    (om,), (dm,) = make_maps([(isa.BPF_MAP_TYPE_HASH, ksz, 8, 512)], po, dev)
+    code = _keyed_counter_prog(dm.fd, ksz)
+    rng = np.random.default_rng(ksz)
+    keys = np.zeros((300, 32), np.uint8)
+    keys[1:, :ksz] = rng.integers(0, 256, ksz, dtype=np.uint8)   # a shared prefix
+    keys[1:, ksz - 4:ksz] = rng.integers(0, 256, (299, 4), dtype=np.uint8)
+    n = 1 << 18
+    pick = np.minimum((rng.pareto(1.2, n) * 10).astype(np.int64), 299)
+    pk = np.zeros((n, 64), np.uint8)
+    pk[:, :32] = keys[pick]
+    ovm = po.OracleVM()
+    ovm.load(code)
+    vm = dev.VM()
+    vm.load(code)
+    d = dev.DeviceBuffer.from_array(pk)
+    dv = dev.DeviceBuffer(4 * n)
+    for _ in range(2):
+        want = ovm.run_xdp(pk.copy(), fixed_len=64)
+        assert vm.exec_batch(dev.CTX_XDP, d, n, 64, fixed_len=64, verdicts=dv) == 0
+        np.testing.assert_array_equal(dv.download(np.uint32), want)
+        assert dm.hash_items() == om.items()
+    assert len(om.items()) == len(set(pick.tolist())) and (pick == 0).sum() > 1000
