@@ -7,13 +7,14 @@
 set -o pipefail
 TAG=${1:?tag}
 export TMPDIR=/tmp
-WS="xdp-counter flow-hash syscall-agg syscount tail-call lpm-route ringbuf-sample"
+WS=${WS:-"xdp-counter flow-hash syscall-agg syscount tail-call lpm-route ringbuf-sample"}
 mkdir -p gpurun_out/${TAG}_pmc
-bash tools/prof_all.sh $TAG || exit 1
+WS="$WS" bash tools/prof_all.sh $TAG || exit 1
 for w in $WS; do
   cp gpurun_out/pmc_$w.json profiles/pmc_$w.json
   cp gpurun_out/prof_${TAG}_$w.summary.txt gpurun_out/${TAG}_pmc/$w.txt
   cp gpurun_out/prof_${TAG}_$w/kt_kernel_stats.csv gpurun_out/${TAG}_pmc/${w}_kernel_stats.csv 2>/dev/null || true
 done
+[ -n "${NO_BENCH:-}" ] && exit 0
 bash tools/bench_all.sh || exit 1
 for w in $WS; do cat gpurun_out/bench_$w.json; done > gpurun_out/${TAG}_bench_lines.jsonl
