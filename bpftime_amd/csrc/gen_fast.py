@@ -1736,15 +1736,18 @@ class Gen:
         e(f"{bail}:", "s_mov_b64 exec, s[54:55]", f"s_branch {slow}")
         del d0
 
-    def tail_env(self):
+    def tail_env(self, slots=False):
         """The launch constants of tail calls; s46 / s47 = the LDS frames'
         offset from v40 and depths | words << 8 (FInsn w6 / w7 are not
-        needed by TAIL / TRET)."""
+        needed by TAIL / TRET); slots: also s[70:71] = the image's slot ->
+        entry table (tenv[7]), read in the same LDS round trip."""
         self.e(f"s_sub_u32 s69, %[comb], {TENV}", "v_mov_b32 v41, s69",
                "ds_read_b128 v[42:45], v41", "ds_read_b128 v[46:49], v41 offset:16",
                f"ds_read_b64 v[58:59], v41 offset:{LF_TENV}",
-               f"ds_read_b64 v[54:55], v40 offset:{self.depth_off}",          # depth, grid lane
-               "s_waitcnt lgkmcnt(0)",
+               f"ds_read_b64 v[54:55], v40 offset:{self.depth_off}")          # depth, grid lane
+        if slots:
+            self.e("ds_read_b64 v[56:57], v41 offset:56")
+        self.e("s_waitcnt lgkmcnt(0)",
                "v_readfirstlane_b32 s46, v58", "v_readfirstlane_b32 s47, v59",  # LDS frames
                "v_readfirstlane_b32 s72, v42", "v_readfirstlane_b32 s73, v43",  # frames
                "v_readfirstlane_b32 s74, v44", "v_readfirstlane_b32 s75, v45",  # entry table
@@ -1752,6 +1755,8 @@ class Gen:
                "v_readfirstlane_b32 s85, v48",                 # stack save mask | stack bytes << 16
                "v_readfirstlane_b32 s68, v49",                 # ctx save mask (s68: free until an exit)
                "s_cmp_eq_u64 s[72:73], 0", f"s_cbranch_scc1 {L('slow')}")
+        if slots:
+            self.e("v_readfirstlane_b32 s70, v56", "v_readfirstlane_b32 s71, v57", "s_nop 4")
 
     def lds_frame_ptr(self, v="v41"):
         """v = the LDS address of this lane's word 0 at depth v54 (an LDS
@@ -1847,21 +1852,17 @@ class Gen:
         PROG_ARRAY, and every lane that can call must pass its own ctx;
         anything else leaves for C++ before changing state."""
         noval, ni = self.label("tnv"), self.label("tni")
-        self.tail_env()
         self.rd_fixed(2, 44)
         self.uniform64((44, 45), (62, 63))
         self.e("s_cmp_lg_u32 s63, 0", f"s_cbranch_scc1 {L('slow')}",
                "s_cmpk_ge_u32 s62, 0x400", f"s_cbranch_scc1 {L('slow')}",
                "s_lshl_b32 s69, s62, 6",
-               "s_load_dwordx4 s[64:67], %[maps], s69",                       # type, ksz, vsz, max
-               # the image's slot -> entry pc table (tenv[7], vm_api.cpp
-               # d_tail_slots): one load per lane instead of the slot's prog
-               # fd and then that fd's entry
-               f"s_sub_u32 s69, %[comb], {TENV - 56}", "v_mov_b32 v41, s69",
-               "ds_read_b64 v[48:49], v41",
-               "s_waitcnt lgkmcnt(0)",
-               "v_readfirstlane_b32 s70, v48", "v_readfirstlane_b32 s71, v49", "s_nop 4",
-               "s_cmp_lg_u32 s64, 3", f"s_cbranch_scc1 {L('slow')}",         # BPF_MAP_TYPE_PROG_ARRAY
+               "s_load_dwordx4 s[64:67], %[maps], s69")                      # type, ksz, vsz, max
+        # the launch constants, and the image's slot -> entry pc table
+        # (tenv[7], vm_api.cpp d_tail_slots: one load per lane instead of the
+        # slot's prog fd and then that fd's entry), under the map's load
+        self.tail_env(slots=True)
+        self.e("s_cmp_lg_u32 s64, 3", f"s_cbranch_scc1 {L('slow')}",         # BPF_MAP_TYPE_PROG_ARRAY
                "s_cmp_eq_u64 s[70:71], 0", f"s_cbranch_scc1 {L('slow')}",
                "s_lshl_b32 s69, s62, 2",
                "s_load_dword s69, s[70:71], s69",                            # the array's offset
