@@ -172,6 +172,8 @@ def handler_ids():
             for k in ("R", "I"):
                 ids.append(f"J{w}_{cc}_{k}")
     ids += ["TAIL", "TRET", "CALL_PID", "KLDX"]  # rare / new: after the hot handlers
+    for sz in (1, 2, 4, 8):  # the lane's own LDS XDP ctx at a static offset
+        ids += [f"LDX{sz}_CTX", f"STX{sz}_CTX", f"ST{sz}_CTX"]
     return ids
 
 
@@ -800,21 +802,23 @@ class Gen:
         self.next_seq()
 
     # ---- stack (loader: r10 + constant, in the lane's LDS stack) ----
-    def ldx_stk(self, sz):
+    def ldx_stk(self, sz, base="%[stklo]"):
+        """dst = the sz bytes at static offset w6 from the stack top (base
+        %[r1lo]: from the lane's own LDS XDP ctx, loader.cpp *_CTX)."""
         ds = {1: "ds_read_u8", 2: "ds_read_u16", 4: "ds_read_b32", 8: "ds_read_b64"}[sz]
-        self.e("v_add_u32 v41, s46, %[stklo]",
+        self.e(f"v_add_u32 v41, s46, {base}",
                f"{ds} {'v[44:45]' if sz == 8 else 'v44'}, v41",
                "s_waitcnt lgkmcnt(0)")
         self.wr("s44", 44, hi=None if sz == 8 else "0")
         self.next_seq()
 
-    def store_stk(self, sz, from_reg):
+    def store_stk(self, sz, from_reg, base="%[stklo]"):
         if from_reg:
             (self.rd if sz == 8 else self.rd_lo)("s45", 44)
         else:
             self.imm32_x()
         ds = {1: "ds_write_b8", 2: "ds_write_b16", 4: "ds_write_b32", 8: "ds_write_b64"}[sz]
-        self.e("v_add_u32 v41, s46, %[stklo]",
+        self.e(f"v_add_u32 v41, s46, {base}",
                f"{ds} v41, {'v[44:45]' if sz == 8 else 'v44'}")
         self.next_seq()
 
@@ -2315,14 +2319,15 @@ class Gen:
                 self.ldxs(name)
             elif name in STAGED_ST:
                 self.stxs(name)
-            elif name.endswith("_STK") and not name.startswith("CALL"):
+            elif (name.endswith("_STK") or name.endswith("_CTX")) and not name.startswith("CALL"):
                 op = name.split("_")[0]
+                base = "%[r1lo]" if name.endswith("_CTX") else "%[stklo]"
                 if op.startswith("LDX"):
-                    self.ldx_stk(int(op[3:]))
+                    self.ldx_stk(int(op[3:]), base)
                 elif op.startswith("STX"):
-                    self.store_stk(int(op[3:]), True)
+                    self.store_stk(int(op[3:]), True, base)
                 else:
-                    self.store_stk(int(op[2:]), False)
+                    self.store_stk(int(op[2:]), False, base)
             elif name.endswith("_MV"):
                 op = name.split("_")[0]
                 if op.startswith("LDX"):

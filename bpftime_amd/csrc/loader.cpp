@@ -1512,6 +1512,16 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
       // ctx->data = slot + head, ctx->data_end = data + len (interp.hip setup)
       f.hoff = 4 + 4 * (at == 0 ? F_LDX_CTXDATA : F_LDX_CTXEND);
       nspec++;
+    } else if (xdp && b.kind == P_CTX && at >= 0 && at + sz <= 48 && at % sz == 0) {
+      // another field of the lane's own XDP ctx (userspace_xdp.h:6-17): in
+      // LDS whenever the program reads or writes it this way (the escape
+      // analysis below sets needs_ctx), at a static offset from r1
+      static const uint32_t ldc[4] = {F_LDX1_CTX, F_LDX2_CTX, F_LDX4_CTX, F_LDX8_CTX};
+      static const uint32_t stxc[4] = {F_STX1_CTX, F_STX2_CTX, F_STX4_CTX, F_STX8_CTX};
+      static const uint32_t stc[4] = {F_ST1_CTX, F_ST2_CTX, F_ST4_CTX, F_ST8_CTX};
+      f.hoff = 4 + 4 * (d.op == X_LDX ? ldc : d.op == X_STX ? stxc : stc)[si];
+      f.target = (uint32_t)at;
+      nspec++;
     } else if (b.kind == P_MAPVAL && d.op != X_ST) {
       const MapRec *m = map_rec(b.id);
       if (m && at >= 0 && at + sz <= m->value_size) {

@@ -367,7 +367,7 @@ def _staged_mix():
     a.stx(8, 10, -8, "r0").stx(4, 10, -12, "r5").st(1, 10, -13, 9).st(2, 10, -16, 300)
     a.ldx(4, 5, 10, -8).alu64("add", 0, "r5").ldx(1, 5, 10, -13).alu64("add", 0, "r5")
     a.ldx(2, 5, 10, -16).alu64("add", 0, "r5").ldx(8, 5, 10, -16).alu64("xor", 0, "r5")
-    a.ldx(4, 5, 6, 20).alu64("add", 0, "r5")          # ifindex: generic ctx load
+    a.ldx(4, 5, 6, 20).alu64("add", 0, "r5")          # ifindex: the LDS ctx field load (LDX4_CTX)
     a.alu64("and", 0, 0xffff).exit()
     a.label("short").mov64(0, 1).exit()
     return a.assemble()
@@ -382,7 +382,7 @@ def test_staged_typed_accesses(fresh_oracle, fresh_runtime, stride, n):
     lens[::7] = 40                                     # short units take the other path
     ov, os_, dv, ds, failed, vm = run_xdp_both(po, dev, code, slots, lens=lens, fixed_len=0)
     assert failed == 0
-    assert vm.fast_specialized(dev.CTX_XDP) == 29
+    assert vm.fast_specialized(dev.CTX_XDP) == 30
     np.testing.assert_array_equal(dv, ov)
     np.testing.assert_array_equal(ds, os_)
 
