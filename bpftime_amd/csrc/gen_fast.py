@@ -1005,8 +1005,19 @@ class Gen:
                "s_lshl_b32 s85, s62, 6",
                "s_load_dwordx4 s[72:75], %[maps], s85",                      # type, ksz, vsz, max
                "s_add_u32 s85, s85, 16",
-               "s_load_dwordx2 s[76:77], %[maps], s85",                     # data
-               "s_waitcnt lgkmcnt(0)")
+               "s_load_dwordx2 s[76:77], %[maps], s85")                     # data
+        if stack_key:
+            # a hash table's words and its key, in the same round trip
+            # (hash_lookup; harmless reads for the other map types): the
+            # lookup index at s[52:53], DMap words 4-11 at s[64:71], the
+            # stack key's four dwords at v[44:47]
+            self.e("s_add_u32 s69, s85, 40",
+                   "s_load_dwordx2 s[52:53], %[maps], s69",
+                   "s_load_dwordx8 s[64:71], %[maps], s85",
+                   "v_add_u32 v41, s46, %[stklo]",
+                   "ds_read_b32 v44, v41", "ds_read_b32 v45, v41 offset:4",
+                   "ds_read_b32 v46, v41 offset:8", "ds_read_b32 v47, v41 offset:12")
+        self.e("s_waitcnt lgkmcnt(0)")
         if stack_key:
             hsh, lpm = self.label("hash"), self.label("lpm")
             self.e("s_cmp_eq_u32 s72, 1", f"s_cbranch_scc1 {hsh}",          # BPF_MAP_TYPE_HASH
@@ -1327,19 +1338,12 @@ class Gen:
 
     def hash_lookup(self):
         done, bail = self.label("hdone"), self.label("hbail")
-        # DMap words 4-11: data, nbuckets, ix_mask, slot_size, key_off,
-        # val_off, ncpu; words 14-15: lookup index (0 = none)
-        self.e("s_lshl_b32 s85, s62, 6", "s_add_u32 s85, s85, 16",
-               "s_load_dwordx8 s[64:71], %[maps], s85",
-               "s_add_u32 s85, s85, 40",
-               "s_load_dwordx2 s[74:75], %[maps], s85",
-               "s_waitcnt lgkmcnt(0)",
-               "v_add_u32 v41, s46, %[stklo]",
-               "ds_read_b32 v44, v41", "ds_read_b32 v45, v41 offset:4",
-               "ds_read_b32 v46, v41 offset:8", "ds_read_b32 v47, v41 offset:12",
+        # DMap words 4-11 (s[64:71], loaded by call_lookup): data,
+        # nbuckets, ix_mask, slot_size, key_off, val_off, ncpu; words 14-15
+        # (s[52:53] there): lookup index (0 = none); the key in v[44:47]
+        self.e("s_mov_b64 s[74:75], s[52:53]",
                "s_mov_b64 s[60:61], exec", "s_mov_b64 s[76:77], exec",     # lanes still looking / all of them
-               "s_mov_b32 s49, s62",                                          # the map fd
-               "s_waitcnt lgkmcnt(0)")
+               "s_mov_b32 s49, s62")                                          # the map fd
         for kd in (1, 2, 3, 4):
             nxt = self.label("kdn")
             self.e(f"s_cmp_lg_u32 s73, {4 * kd}", f"s_cbranch_scc1 {nxt}")
