@@ -172,6 +172,9 @@ def handler_ids():
             for k in ("R", "I"):
                 ids.append(f"J{w}_{cc}_{k}")
     ids += ["TAIL", "TRET", "CALL_PID", "KLDX"]  # rare / new: after the hot handlers
+    # a map lookup with its argument set-up (lddw r1 = map; r2 = r10 + k;
+    # call 1) as one dispatch (loader.cpp fuse_pairs)
+    ids += ["CALL_LOOKUP_STK3", "CALL_LOOKUP_AK3"]
     for sz in (1, 2, 4, 8):  # the lane's own LDS XDP ctx at a static offset
         ids += [f"LDX{sz}_CTX", f"STX{sz}_CTX", f"ST{sz}_CTX"]
     return ids
@@ -190,6 +193,7 @@ class Gen:
         self.uid = 0
         self.greg = greg
         self.depth_off = 2048 if greg else 12 * 2048  # the lane's tail-call depth slot
+        self.span = 1  # FInsn slots a sequential next_seq steps over (fused lookups: 5)
 
     def e(self, *lines):
         self.out.extend(lines)
@@ -208,11 +212,12 @@ class Gen:
                "s_addc_u32 s53, s51, 0",
                "s_setpc_b64 s[52:53]")
 
-    def next_seq(self, slots=1):
+    def next_seq(self, slots=None):
         """Fall through: the handler offset of the next FInsn is w1 >> 8 of
         this one (link_fast), so the jump does not wait for the fetch; the
         handler waits for it on entry (lgkmcnt), overlapping the scalar load
         with the two control transfers."""
+        slots = self.span if slots is None else slots
         self.e(f"s_add_u32 s48, s48, {INSN * slots}",
                "s_lshr_b32 s52, s41, 8",
                "s_load_dwordx8 s[40:47], s[78:79], s48",
@@ -2350,6 +2355,20 @@ class Gen:
                 self.jump_taken()
             elif name == "CALL_LOOKUP":
                 self.call_lookup()
+            elif name in ("CALL_LOOKUP_STK3", "CALL_LOOKUP_AK3"):
+                # r1 = the map fd (w7), r2 = r10 + the key's stack offset (w6),
+                # then the lookup; the next FInsn is 5 slots on
+                self.e(f"v_mov_b32 v{R0 + 2}, s47", f"v_mov_b32 v{R0 + 3}, 0",
+                       "s_ashr_i32 s69, s46, 31",
+                       f"v_add_co_u32 v{R0 + 4}, vcc, s46, v{R0 + 20}",
+                       f"v_mov_b32 v{R0 + 5}, s69",
+                       f"v_addc_co_u32 v{R0 + 5}, vcc, v{R0 + 5}, v{R0 + 21}, vcc")
+                self.span = 5
+                if name == "CALL_LOOKUP_AK3":
+                    self.call_lookup_ak()
+                else:
+                    self.call_lookup(stack_key=True)
+                self.span = 1
             elif name == "CALL_LOOKUP_STK":
                 self.call_lookup(stack_key=True)
             elif name == "CALL_LOOKUP_AK":

@@ -1572,8 +1572,10 @@ uint32_t stage_need(const FastForm &f, uint32_t head) {
   return (uint32_t)((ext + 15) & ~15);
 }
 
-// FInsn slots an entry covers: lddw, and the pairs run as one dispatch
+// FInsn slots an entry covers: lddw, and the pairs run as one dispatch;
+// a fused lookup (its lddw, lea and call) five
 static size_t fspan(const std::vector<DInsn> &prog, const std::vector<FInsn> &out, size_t i) {
+  if (out[i].hoff == 4 + 4 * F_CALL_LOOKUP_STK3 || out[i].hoff == 4 + 4 * F_CALL_LOOKUP_AK3) return 5;
   return (i < prog.size() && prog[i].op == X_LDDW) || out[i].hoff == 4 + 4 * F_ATOMMV8_ADD2 ||
                  out[i].hoff == 4 + 4 * F_LEA || (out[i].w1 & FW_MOVI)
              ? 2
@@ -1612,6 +1614,26 @@ static void fuse_pairs(const std::vector<DInsn> &prog, const std::vector<uint8_t
       out[i] = g;
       i++;
     }
+  }
+  // a map lookup's argument set-up and call, `lddw r1, map; r2 = r10 + k;
+  // call 1` in either order of the first two, as one dispatch at the first
+  // (the call's FInsn with the map fd in w7: gen_fast.py CALL_LOOKUP_*3); the
+  // other two keep their FInsns for jumps into the sequence and the C++
+  // tier's re-entry
+  for (size_t i = 0; i + 4 < prog.size(); i++) {
+    const size_t c = i + 4;
+    if (!is(c, F_CALL_LOOKUP_STK) && !is(c, F_CALL_LOOKUP_AK)) continue;
+    size_t ld = i, le = i + 2;
+    if (is(i, F_LEA)) std::swap(ld, le);
+    if (!is(ld, F_LDDW) || prog[ld].op != X_LDDW || out[ld].dst_x2 != 2 || (uint64_t)out[ld].imm >= kMaxFds) continue;
+    if (!is(le, F_LEA) || out[le].dst_x2 != 4 || out[le].src_x2 != 20 ||
+        out[le].imm != (int64_t)(int32_t)out[c].target)
+      continue;
+    if (join[i + 2] || join[c]) continue;  // (sequential flow only: a jump into the middle runs the originals)
+    FInsn g = out[c];
+    g.hoff = 4 + 4 * (is(c, F_CALL_LOOKUP_STK) ? F_CALL_LOOKUP_STK3 : F_CALL_LOOKUP_AK3);
+    g.aux = (int32_t)out[ld].imm;
+    out[i] = g;
   }
 }
 
