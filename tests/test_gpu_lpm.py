@@ -91,6 +91,65 @@ def test_lpm_routing_program(fresh_oracle, fresh_runtime):
     assert not np.array_equal(want, want2)
 
 
+def route_prog_null_check(fd, taken_on_hit):
+    """route_prog with the lookup's result tested directly (`if r0 == 0` /
+    `if r0 != 0` right after the call: the loader fuses the lookup, its
+    argument set-up and that check into one dispatch, gen_fast.py
+    CALL_LOOKUP_STK3_Z / _NZ)."""
+    a = Asm().ldx(8, 2, 1, 0).ldx(8, 3, 1, 8).mov64(6, 2)
+    a.mov64(4, "r2").add64(4, 34).jmp("jgt", 4, "r3", "out")
+    a.ldx(2, 4, 2, 12).jmp("jne", 4, 0x0008, "out")
+    a.st(4, 10, -8, 32).ldx(4, 4, 2, 30).stx(4, 10, -4, "r4")
+    a.ld_map_fd(1, fd).mov64(2, "r10").add64(2, -8).call(1)
+    if taken_on_hit:
+        a.jmp("jne", 0, 0, "hit").mov64(6, 4).ja("out")
+        a.label("hit").ldx(4, 6, 0, 0)
+    else:
+        a.jmp("jeq", 0, 0, "out").ldx(4, 6, 0, 0)
+    a.label("out").mov64(0, "r6").exit()
+    return a.assemble()
+
+
+@pytest.mark.parametrize("taken_on_hit", [False, True])
+@pytest.mark.parametrize("hit_rate", [0.0, 0.8, 1.0])
+def test_lpm_lookup_fused_null_check(fresh_oracle, fresh_runtime, taken_on_hit, hit_rate):
+    """Waves whose lanes all miss, all hit, or split between the two after
+    the fused lookup + null check, bit-exact against the oracle."""
+    po, dev = fresh_oracle, fresh_runtime
+    rng = np.random.default_rng(11)
+    (om,), (dm,) = make_maps([(LPM, 8, 4, 1024)], po, dev)
+    nets = []
+    for i in range(500):
+        plen = int(rng.choice([16, 20, 24, 32]))
+        net = int(rng.integers(1 << 31, 1 << 32)) & ((0xFFFFFFFF << (32 - plen)) & 0xFFFFFFFF)
+        nets.append((plen, net))
+        for m in (om, dm):
+            m.update(struct.pack("<I", plen) + struct.pack(">I", net), struct.pack("<I", 1 + i % 3))
+    n = 1 << 15
+    pk = gen.xdp_packets(n, seed=12)
+    pk[:, 12:14] = [0x08, 0x00]
+    picks = rng.integers(0, len(nets), n)
+    hit = np.array([nets[i][1] for i in picks], np.uint64)
+    miss = rng.integers(0, 1 << 31, n, dtype=np.uint64)          # below every route
+    addr = np.where(rng.random(n) < hit_rate, hit, miss).astype(np.uint32)
+    pk[:, 30:34] = addr.astype(">u4").view(np.uint8).reshape(n, 4)
+    code = route_prog_null_check(dm.fd, taken_on_hit)
+    ovm = po.OracleVM()
+    ovm.load(code)
+    want = ovm.run_xdp(pk.copy(), fixed_len=64)
+    vm = dev.VM()
+    vm.load(code)
+    d = dev.DeviceBuffer.from_array(pk)
+    dv = dev.DeviceBuffer(4 * n)
+    assert vm.exec_batch(dev.CTX_XDP, d, n, 64, fixed_len=64, verdicts=dv) == 0
+    got = dv.download(np.uint32)
+    np.testing.assert_array_equal(got, want)
+    if hit_rate == 0.0:
+        assert set(got.tolist()) == {4 if taken_on_hit else 2}
+    else:
+        assert len(set(got.tolist())) >= 3
+
+
 def learn_prog(fd):
     """Route learning over 16-B raw units {u32 op, u32 prefixlen, 4 address
     bytes (network order), u32 value}: op & 0xff = 0 lookup (r0 = the value,
