@@ -93,9 +93,9 @@ def test_lpm_routing_program(fresh_oracle, fresh_runtime):
 
 def route_prog_null_check(fd, taken_on_hit):
     """route_prog with the lookup's result tested directly (`if r0 == 0` /
-    `if r0 != 0` right after the call: the loader fuses the lookup, its
-    argument set-up and that check into one dispatch, gen_fast.py
-    CALL_LOOKUP_STK3_Z / _NZ)."""
+    `if r0 != 0` right after the call, the LPM lookup running in the fused
+    CALL_LOOKUP_STK3 dispatch and the check in the jump handler that
+    follows)."""
     a = Asm().ldx(8, 2, 1, 0).ldx(8, 3, 1, 8).mov64(6, 2)
     a.mov64(4, "r2").add64(4, 34).jmp("jgt", 4, "r3", "out")
     a.ldx(2, 4, 2, 12).jmp("jne", 4, 0x0008, "out")
@@ -112,9 +112,10 @@ def route_prog_null_check(fd, taken_on_hit):
 
 @pytest.mark.parametrize("taken_on_hit", [False, True])
 @pytest.mark.parametrize("hit_rate", [0.0, 0.8, 1.0])
-def test_lpm_lookup_fused_null_check(fresh_oracle, fresh_runtime, taken_on_hit, hit_rate):
-    """Waves whose lanes all miss, all hit, or split between the two after
-    the fused lookup + null check, bit-exact against the oracle."""
+def test_lpm_lookup_direct_null_check(fresh_oracle, fresh_runtime, taken_on_hit, hit_rate):
+    """Waves whose lanes all miss, all hit, or split between the two at the
+    null check right after an asm-tier LPM lookup, bit-exact against the
+    oracle."""
     po, dev = fresh_oracle, fresh_runtime
     rng = np.random.default_rng(11)
     (om,), (dm,) = make_maps([(LPM, 8, 4, 1024)], po, dev)
