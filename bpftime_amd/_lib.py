@@ -37,7 +37,8 @@ class EbpfBatch(C.Structure):  # include/ebpf-vm.h struct ebpf_batch
                 ("rets", C.c_void_p), ("data_off_out", C.c_void_p), ("len_out", C.c_void_p),
                 ("first_unit", C.c_uint64), ("stream", C.c_void_p), ("descs", C.c_void_p),
                 ("umem_bytes", C.c_uint64), ("sys_nr", C.c_int64), ("sys_state", C.c_void_p),
-                ("sys_ret", C.c_void_p), ("sys_phase", C.c_uint32), ("pid_tgid_off", C.c_int32)]
+                ("sys_ret", C.c_void_p), ("sys_phase", C.c_uint32), ("pid_tgid_off", C.c_int32),
+                ("ktime_off", C.c_int32)]
 
 
 class PerfEvent(C.Structure):
@@ -127,6 +128,7 @@ SIGNATURES = [
     ("bpftime_amd_syscall_attach_ex", C.c_int, [C.c_int, C.c_int64, C.c_int]),
     ("bpftime_amd_syscall_dispatch_records", C.c_int64, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p,
                                                          C.c_uint32, C.c_void_p]),
+    ("bpftime_amd_syscall_dispatch_plan", C.c_int, [C.c_uint32]),
     ("bpftime_amd_handle_sysbpf", C.c_long, [C.c_int, C.c_void_p, C.c_uint32]),
     ("bpftime_map_get_info", C.c_int, [C.c_int, C.POINTER(BpfMapAttr), C.POINTER(C.c_char_p),
                                         C.POINTER(C.c_int)]),

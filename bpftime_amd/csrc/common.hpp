@@ -211,6 +211,11 @@ constexpr uint32_t kFrameRematShift = 50;
 // call + both masks' words, and the depths to keep the block's residency)
 constexpr uint32_t kTailLdsMax = 4;  // depths held in LDS at most
 
+// Map effects of a program (loader.hpp FastForm::map_fx): loads (and lookups), counter adds whose order no
+// one observes (fused ld/add/st and atomic adds without fetch), every other
+// write (stores, fetching or non-add atomics, update / delete / ring calls)
+constexpr uint8_t FX_READ = 1, FX_ADD = 2, FX_WRITE = 4;
+
 // Context kinds for a batch
 constexpr uint32_t CTX_RAW = 0;      // r1 = unit memory, r2 = length
 constexpr uint32_t CTX_XDP = 1;      // r1 = xdp_md_userspace (48 B, LDS)
@@ -305,7 +310,49 @@ struct KParams {
   // syscalls), or (0) the launching thread's value
   int32_t pid_off;
   uint64_t pid_tgid;
+  // bpf_ktime_get_ns: a u64 at this offset from the unit (the recorded clock
+  // of a syscall replay), or (0) the device clock
+  int32_t kt_off;
 };
+
+// Thread-ordered syscall dispatch (interp.hip k_sys_seq, syscall_dispatch.cpp):
+// one lane per recorded thread walks that thread's records in record order
+// and, per record, runs the attached programs the way dispatch_syscall does
+// (attach/syscall_trace_attach_impl/src/syscall_trace_attach_impl.cpp:18-95).
+// The programs in the reference's order: per-syscall enter programs, global
+// enter, per-syscall exit, global exit (attach order inside each group).
+struct SeqProg {
+  const DInsn *prog;
+  const FInsn *fast;    // its ORDERED link (every counter add reaches memory at once)
+  int64_t sys_nr;       // -1: every syscall
+  uint32_t enter;       // 1 sys_enter, 0 sys_exit
+  uint32_t pad;
+};
+static_assert(sizeof(SeqProg) == 32, "SeqProg is read with scalar loads");
+constexpr uint32_t kSeqMaxProgs = 64;  // attached programs a thread-ordered dispatch runs (kernel arguments)
+struct SeqParams {
+  uint32_t nprogs;
+  uint32_t rec_size;      // 64, 96 or 128 (include/bpftime_amd.h)
+  const uint8_t *recs;
+  uint64_t n;
+  // thread t's records: perm[seg[t] .. seg[t + 1]) (record indexes in record
+  // order); null perm: the identity; null seg: one thread over [0, n)
+  const uint32_t *perm;
+  const uint32_t *seg;
+  uint64_t nseg;
+  int64_t *out;           // what dispatch_syscall returns per record (nullable)
+  const DMap *maps;
+  uint32_t ncpu;
+  uint32_t checked;
+  uint64_t arena_lo, arena_hi;
+  uint64_t step_limit;
+  uint64_t lru_seq;
+  uint64_t pid_tgid;      // 64-B records: the dispatching thread's
+  uint32_t *err_count;    // failed callbacks
+  uint32_t exact;         // one lane over every record (EBPF_BATCH_ORDERED)
+  SeqProg progs[kSeqMaxProgs];  // in the kernel arguments: scalar loads, no upload
+};
+static_assert(sizeof(SeqParams) <= 4096, "kernel arguments");
 
 // Combining-table misses.  A deferred counter add that finds no table entry
 // (the set is full of other granules) does not become a memory-side atomic

@@ -1096,6 +1096,8 @@ struct LaneEnv {
   int64_t *ovr_val;
   uint32_t ovr_bit;
   uint64_t pid_tgid;  // bpf_get_current_pid_tgid's value for this unit
+  uint64_t ktime;     // bpf_ktime_get_ns's value for this unit (a replay's recorded clock) ...
+  bool kt_on;         // ... when set, else the device clock
 };
 
 // bpftime_override_return / bpftime_set_retval (attach/base_attach_impl/

@@ -1,7 +1,7 @@
 // bpftime_amd: device side of the syscall dispatch's per-record state
 // (csrc/syscall_dispatch.cpp): before the programs run, every record's
 // override flags are cleared and its return value is what dispatch_syscall
-// returns when no program overrides it -- the recorded ret of a 96-B record
+// returns when no program overrides it -- the recorded ret of a 96- or 128-B record
 // (trace_event_raw_sys_exit.ret at +80, syscall_trace_attach_impl.cpp:78-93),
 // 0 for a 64-B enter record, which holds none.
 #include <hip/hip_runtime.h>
@@ -12,7 +12,7 @@ namespace bpftime_amd {
 __global__ void k_sys_init(const uint8_t *records, uint64_t n, uint32_t record_size, int64_t *out,
                            uint32_t *state) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    state[i] = 0;
+    if (state) state[i] = 0;
     if (out) out[i] = record_size >= 88 ? *(const int64_t *)(records + i * record_size + 80) : 0;
   }
 }

@@ -45,7 +45,7 @@ __device__ __forceinline__ uint64_t call_helper(uint32_t id, uint64_t a1, uint64
     case 1: return helper_lookup(maps, a1, a2, env);
     case 2: return helper_update(maps, a1, a2, a3, a4, env);
     case 3: return helper_delete(maps, a1, a2, env);
-    case 5: return (uint64_t)__builtin_amdgcn_s_memrealtime() * 10ull;
+    case 5: return env.kt_on ? env.ktime : (uint64_t)__builtin_amdgcn_s_memrealtime() * 10ull;
     case 7: {
       uint64_t x = seed * 0x9E3779B97F4A7C15ull;
       x ^= x >> 31;
@@ -601,6 +601,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   SRP(miss_log); SRP(miss_counts); SRV(miss_cap); SRP(tail_slots); SRV(full_q); SRV(full_r); SRV(step_cpu);
   SRP(sys_state); SRP(sys_ret); SRV(sys_phase); SRV(pid_tgid);
   p.pid_off = (int32_t)sreg((uint64_t)(uint32_t)pin.pid_off);
+  p.kt_off = (int32_t)sreg((uint64_t)(uint32_t)pin.kt_off);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
   p.unwind_idx = (int32_t)sreg((uint64_t)(uint32_t)pin.unwind_idx);
 #undef SRP
@@ -1082,6 +1083,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         env.ovr_val = p.sys_ret ? p.sys_ret + unit : nullptr;
         env.ovr_bit = p.sys_phase;
         env.pid_tgid = p.pid_off ? *(const uint64_t *)(slot + (int64_t)p.pid_off) : p.pid_tgid;
+        env.kt_on = p.kt_off != 0;
+        env.ktime = p.kt_off ? *(const uint64_t *)(slot + (int64_t)p.kt_off) : 0;
         uint32_t cerr = E_OK;
         uint64_t *R = c.R;
         const uint64_t rv = call_helper(c.call_id, R[1 * kBlock], R[2 * kBlock], R[3 * kBlock], R[4 * kBlock],
@@ -1315,6 +1318,153 @@ __global__ __launch_bounds__(kBigBlock) void k_miss_merge(const uint64_t *log, c
   for (uint32_t i = tid; i < kMissEntries; i += kBigBlock) flush_delta_tag(mt[i], mt[kMissEntries + i]);
 }
 
+// Thread-ordered syscall dispatch (common.hpp SeqParams; the host side is
+// syscall_dispatch.cpp / vm_api.cpp seq_dispatch).  dispatch_syscall
+// (attach/syscall_trace_attach_impl/src/syscall_trace_attach_impl.cpp:18-95)
+// runs a call's callbacks on the calling thread, one call after another:
+// here lane t walks thread t's records in record order and, per record, runs
+// the attached programs as that function does -- exit / exit_group run
+// nothing; the enter programs (per-syscall, then global) each on a fresh
+// zeroed ctx {id, args}; if one overrode the return (58 / 187) the record
+// returns it and no exit program runs; else the exit programs each on a
+// fresh {id, ret}; the record returns ret or an exit override.  A wave runs
+// one attached program at a time over the lanes it applies to, through the
+// C++ tier (run_loop: uniform and divergent loops, helpers in between); every
+// counter add reaches memory at once (the ORDERED links), so a thread's
+// later callbacks see its earlier ones.  Threads are as independent as the
+// reference's: different lanes, no order between them.
+__global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
+  __shared__ uint64_t Rf[12 * kBlock];   // r0..r10 columns, the dummy slot
+  __shared__ uint64_t cx[8 * kBlock];    // the lane's ctx copy (64 B)
+  __shared__ uint32_t ovr_st[kBlock];    // override bits of the lane's record (1 enter, 2 exit)
+  __shared__ int64_t ovr_v[kBlock];      // ... and the value
+  const uint32_t tid = threadIdx.x;
+  const uint64_t t = (uint64_t)blockIdx.x * kBlock + tid;
+  uint64_t stk[kStackSize / 8];          // 512-B stack (private memory)
+  const uint64_t stack_top = (uint64_t)(uintptr_t)(stk + kStackSize / 8);
+  uint64_t *const ctx = &cx[8 * tid];
+  Ctx c;
+  c.R = &Rf[tid];
+  // the programs see their ctx copy (LDS), their stack and the map arena
+  c.win = Win{0, 0, p.arena_lo, p.arena_hi, 0, 0, p.checked != 0};
+  c.dummy = (uint64_t)(uintptr_t)&Rf[11 * kBlock + tid];
+  c.verdicts = nullptr;
+  c.rets = nullptr;
+  c.step_limit = p.step_limit > 0xffffffffull ? 0xffffffffu : (uint32_t)p.step_limit;
+  c.c0a = c.c0d = c.c1a = c.c1d = 0;
+  c.c0s = c.c1s = 0;
+  uint64_t k = 0, end = 0;
+  if (t < p.nseg) {
+    k = p.seg ? p.seg[t] : 0;
+    end = p.seg ? p.seg[t + 1] : p.n;
+  }
+  const uint32_t nprogs = __builtin_amdgcn_readfirstlane(p.nprogs);
+  auto rfl64 = [](uint64_t v) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+  };
+  while (__ballot(k < end) != 0) {
+    const bool has = k < end;
+    const uint64_t idx = has ? (p.perm ? (uint64_t)p.perm[k] : k) : 0;
+    const uint8_t *rec = p.recs + idx * p.rec_size;
+    const int64_t nr = has ? *(const int64_t *)(rec + 8) : 0;
+    const int64_t ret = has && p.rec_size >= 96 ? *(const int64_t *)(rec + 80) : 0;
+    const uint64_t pid = has && p.rec_size >= 96 ? *(const uint64_t *)(rec + 88) : p.pid_tgid;
+    const bool live = has && nr != 60 && nr != 231;  // :23-26
+    ovr_st[tid] = 0;
+    ovr_v[tid] = 0;
+    for (uint32_t a = 0; a < nprogs; a++) {
+      const SeqProg *sp = &p.progs[a];
+      const uint32_t enter = __builtin_amdgcn_readfirstlane(sp->enter);
+      const int64_t snr = (int64_t)rfl64((uint64_t)sp->sys_nr);
+      // an exit program skips a record whose enter programs overrode (:68-72)
+      const bool run = live && (snr < 0 || snr == nr) && !(!enter && (ovr_st[tid] & 1));
+      if (__ballot(run) == 0) continue;
+      // each callback on its own copy of a zeroed ctx (:41-53, :57-66, :80-85)
+      if (run) {
+        ctx[0] = 0;
+        ctx[1] = (uint64_t)nr;
+        if (enter) {
+          for (int w = 2; w < 8; w++) ctx[w] = *(const uint64_t *)(rec + 8 * w);
+        } else {
+          ctx[2] = (uint64_t)ret;
+          for (int w = 3; w < 8; w++) ctx[w] = 0;
+        }
+      }
+      c.prog = (prog_ptr)rfl64((uint64_t)(uintptr_t)sp->prog);
+      c.fast = (const FInsn *)rfl64((uint64_t)(uintptr_t)sp->fast);
+      for (int r = 0; r <= 10; r++) c.R[r * kBlock] = 0;
+      c.R[1 * kBlock] = (uint64_t)(uintptr_t)ctx;
+      c.R[2 * kBlock] = enter ? 64 : 24;  // sizeof the ctx (:46)
+      c.R[10 * kBlock] = stack_top;
+      c.alive = run;
+      c.err = E_OK;
+      c.pc = 0;
+      c.lpc = 0;
+      c.steps = 0;
+      c.unit = idx;
+      int32_t miss_fd = -1;
+      uint64_t miss_hash = 0;
+      uint32_t lru_ops = 0;
+      bool uni = true;
+      while (__ballot(c.alive) != 0) {
+        const uint32_t r = uni ? run_loop<true>(c) : run_loop<false>(c);
+        if (r == R_DONE) break;
+        if (r == R_DIVERGE) {
+          uni = false;
+          continue;
+        }
+        if (r == R_RECONV) {
+          uni = true;
+          continue;
+        }
+        // R_CALL: the helper (dev_helpers.hpp) for the lanes at the call
+        const bool csel = uni ? c.alive : (c.alive && c.lpc == c.call_pc);
+        if (csel) {
+          LaneEnv env;
+          env.vcpu = idx / 64;
+          env.scratch = 0;
+          env.miss_fd = miss_fd;
+          env.miss_hash = miss_hash;
+          env.lru_stamp = (p.lru_seq << kLruSeqShift) | ((idx & 0xffffffffull) << kLruUnitShift);
+          env.lru_ops = lru_ops;
+          env.exact = p.exact != 0;
+          env.ovr_state = &ovr_st[tid];
+          env.ovr_val = &ovr_v[tid];
+          env.ovr_bit = enter ? 1 : 2;
+          env.pid_tgid = pid;
+          env.kt_on = p.rec_size == 128;
+          env.ktime = p.rec_size == 128 ? *(const uint64_t *)(rec + (enter ? 96 : 104)) : 0;
+          uint32_t cerr = E_OK;
+          uint64_t *R = c.R;
+          const uint32_t cid = __builtin_amdgcn_readfirstlane(c.call_id);
+          const uint64_t rv = cid == kTailHelper ? 0
+                              : call_helper(cid, R[1 * kBlock], R[2 * kBlock], R[3 * kBlock], R[4 * kBlock],
+                                            R[5 * kBlock], p.maps, p.ncpu, idx ^ ((uint64_t)c.steps << 40), env,
+                                            &cerr);
+          if (cid == kTailHelper) cerr = E_BADOP;  // (the host refuses such programs)
+          R[0] = rv;
+          miss_fd = env.miss_fd;
+          miss_hash = env.miss_hash;
+          lru_ops = env.lru_ops;
+          if (cerr != E_OK) {
+            c.err = cerr;
+            c.alive = false;
+          }
+        }
+        if (uni)
+          c.pc = c.call_pc + 1;
+        else
+          c.lpc = csel ? c.call_pc + 1 : c.lpc;
+      }
+      // a failed callback is ignored by the dispatch (:47-52) and counted
+      if (run && c.err != E_OK) atomicAdd(p.err_count, 1u);
+    }
+    if (has && p.out) p.out[idx] = ovr_st[tid] ? ovr_v[tid] : ret;
+    if (has) k++;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Host-side launch wrappers
 // ---------------------------------------------------------------------------
@@ -1343,6 +1493,13 @@ extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind,
   }
 #undef LK
 #undef L
+  return hipGetLastError();
+}
+
+extern "C" hipError_t bpftime_amd_launch_sys_seq(const SeqParams *p, hipStream_t stream) {
+  const uint64_t grid = (p->nseg + kBlock - 1) / kBlock;
+  if (grid == 0 || grid > 0x7fffffffull || p->nprogs > kSeqMaxProgs) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_sys_seq, dim3((uint32_t)grid), dim3(kBlock), 0, stream, *p);
   return hipGetLastError();
 }
 

@@ -763,6 +763,18 @@ static const MapRec *map_rec(int64_t fd) {
   return &r.maps[fd];
 }
 
+// the array map whose storage holds [a, a+sz) (map_val addresses), or -1
+static int32_t array_fd_of(uint64_t a, uint32_t sz) {
+  Runtime &r = rt();
+  for (uint32_t fd = 0; fd < kMaxFds; fd++) {
+    if (r.kind[fd] != HKind::MAP) continue;
+    const MapRec &m = r.maps[fd];
+    if (m.type != MT_ARRAY && m.type != MT_PERCPU_ARRAY) continue;
+    if (a >= m.d.data && a + sz <= m.d.data + m.bytes) return (int32_t)fd;
+  }
+  return -1;
+}
+
 // [a, a+sz) inside the storage of an array map (map_val addresses)
 static bool in_array_storage(uint64_t a, uint32_t sz) {
   Runtime &r = rt();
@@ -1249,6 +1261,77 @@ uint32_t lcache_sets() {
   return sets;
 }
 
+// FastForm::map_fx from the pointer kinds: which maps each load, store,
+// atomic and map helper call reaches.  Accesses of the unit's own memory (its
+// stack, its ctx copy, packet / slot bytes) are not map effects; an access
+// whose base the kinds cannot place, or a helper that is not modelled, may
+// reach any map (any_fx).
+static void map_effects(const std::vector<DInsn> &prog, const std::vector<std::vector<PVal>> &in, FastForm &out) {
+  out.map_fx.clear();
+  out.any_fx = 0;
+  auto mark = [&](int32_t fd, uint8_t bits) {
+    if (fd >= 0) out.map_fx[fd] |= bits;
+    else out.any_fx |= bits;
+  };
+  // the map a memory access through base kind b (+ off) reaches: fd, -1 any
+  // map, -2 the unit's own memory
+  auto target = [&](size_t i, const PVal &b, int64_t off, uint32_t sz) -> int32_t {
+    switch (b.kind) {
+      case P_STK: case P_CTX: case P_PKT: case P_SLOT:
+        return -2;
+      case P_MAPVAL: case P_MVNULL:
+        return b.id;
+      case P_CONST: {
+        const DInsn &l = prog[(size_t)b.id];
+        const uint64_t a = ((uint64_t)(uint32_t)l.imm | ((uint64_t)(uint32_t)l.hi << 32)) + (int64_t)b.k + off;
+        return array_fd_of(a, sz);
+      }
+      default:
+        (void)i;
+        return -1;
+    }
+  };
+  for (size_t i = 0; i < prog.size(); i++) {
+    const DInsn &d = prog[i];
+    const std::vector<PVal> &st = in[i];
+    if (st[10].kind == P_UNDEF) continue;  // unreachable
+    const uint32_t sz = 1u << ((d.aux >> A_SIZE_SHIFT) & 3);
+    switch (d.op) {
+      case X_LDX: {
+        const int32_t t = target(i, st[d.src], d.off, sz);
+        if (t != -2) mark(t, FX_READ);
+        break;
+      }
+      case X_ST: case X_STX: {
+        const int32_t t = target(i, st[d.dst], d.off, sz);
+        if (t != -2) mark(t, FX_WRITE);
+        break;
+      }
+      case X_RMW_ADD: case X_ATOMIC: {
+        const uint32_t asz = d.op == X_ATOMIC ? (((d.aux >> A_SIZE_SHIFT) & 3) == 3 ? 8 : 4) : sz;
+        const int32_t t = target(i, st[d.dst], d.off, asz);
+        const bool add = d.op == X_RMW_ADD ? !(d.aux & A_FETCH) : d.hi == 0x00;
+        if (t != -2) mark(t, add ? FX_ADD : FX_WRITE);
+        break;
+      }
+      case X_CALL: {
+        const PVal &m = st[1];
+        const int32_t fd = m.kind == P_MAPFD ? m.id : -1;
+        switch (d.hi) {
+          case 1: mark(fd, FX_READ); break;                             // map_lookup_elem
+          case 2: case 3: case 130: case 131: mark(fd, FX_WRITE); break;  // update, delete, ringbuf output / reserve
+          case 5: case 7: case 8: case 14: case 28: case 44: case 58: case 65: case 132: case 133: case 187: case 189:
+            break;  // no map effects (132 / 133 finish a reservation 131 marked)
+          default: mark(-1, FX_READ | FX_WRITE); break;                 // bpf_tail_call, anything else
+        }
+        break;
+      }
+      default:
+        break;
+    }
+  }
+}
+
 void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
   const std::vector<DInsn> &prog = lo.prog;
   out.fast.assign(prog.size(), FInsn{});
@@ -1310,6 +1393,7 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
   // syscall dispatch runs such a program on a copy of its records, as each
   // reference callback gets its own ctx copy)
   out.stores_unit = !kinds_ok;
+  if (kinds_ok) map_effects(prog, in, out);  // (else any_fx stays: every map, read and written)
   for (size_t i = 0; kinds_ok && i < prog.size(); i++) {
     const DInsn &d = prog[i];
     if (d.op != X_ST && d.op != X_STX && d.op != X_RMW_ADD && d.op != X_ATOMIC) continue;

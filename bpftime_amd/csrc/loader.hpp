@@ -68,6 +68,12 @@ struct FastForm {
   // a store may reach the unit r1 points to at entry (the pointer kinds
   // cannot place every store on the stack, a map value or a constant)
   bool stores_unit = true;
+  // What the program does to each map it can reach (the syscall dispatch
+  // decides from it whether attached programs commute, syscall_dispatch.cpp):
+  // per map fd FX_* bits, and the bits of accesses the pointer kinds cannot
+  // attribute to one map (they may reach any)
+  std::map<int32_t, uint8_t> map_fx;
+  uint8_t any_fx = FX_READ | FX_WRITE;
 };
 
 struct LoadOut {

@@ -11,23 +11,37 @@
 // callback) it returns that value without running the syscall; else it runs
 // the syscall and the exit callbacks (per-syscall, then global) on
 // trace_event_raw_sys_exit {id, ret}, returning ret or an exit override.
+// dispatch_syscall runs on the calling thread: a thread's calls one after
+// another, threads side by side.
 //
-// Here the calls are recorded (include/bpftime_amd.h, 64-B enter records or
-// 96-B enter + exit records in device memory) and each attached program runs
-// once over the whole batch on the device, in the reference's program order:
-// per-syscall enter programs (filtered to their nr, EBPF_BATCH_SYS_NR), global
-// enter programs, per-syscall exit programs, global exit programs.  The
-// override state lives in a per-record u32 beside the records (set by helpers
-// 58 / 187 on the device; an exit batch skips records whose enter phase
-// overrode), the returned value in the caller's out_rets.  For one record
-// that is the reference's order; across records the programs are not
-// interleaved, which is equivalent whenever their map effects commute.
-// Host-side bookkeeping only; the work is ebpf_exec_batch.
+// Here the calls are recorded (include/bpftime_amd.h: 64-B enter records,
+// 96-B enter + exit records with the caller's pid_tgid, 128-B records with
+// the recorded clocks too, in device memory) and one of two plans runs them:
+//  * program-major: each attached program runs once over the whole batch on
+//    the device (ebpf_exec_batch), in the reference's program order:
+//    per-syscall enter programs (filtered to their nr, EBPF_BATCH_SYS_NR),
+//    global enter programs, per-syscall exit programs, global exit programs.
+//    The override state lives in a per-record u32 beside the records (set by
+//    helpers 58 / 187 on the device; an exit batch skips records whose enter
+//    phase overrode), the returned value in the caller's out_rets.  For one
+//    record that is the reference's order; across records the programs are
+//    not interleaved, which is equivalent whenever their map effects commute;
+//  * thread-ordered: records grouped by their recorded thread (group.hip),
+//    one lane per thread walking its records in record order, each record's
+//    callbacks run back to back as dispatch_syscall runs them (interp.hip
+//    k_sys_seq; vm_api.cpp seq_dispatch) -- the reference's schedule.
+// The dispatch takes thread-ordered when two attachments may not commute
+// (the loader's map effects, loader.hpp FastForm::map_fx): one writes a map
+// the other reads or writes, or adds to a map the other reads.  syscount's
+// latency pair is the case (example/tracing/syscount/syscount.bpf.c:33-47,
+// 71-76: sys_enter stores start[tid], sys_exit reads it).
+// Host-side bookkeeping only; the work is on the device.
 #include <errno.h>
 #include <stdlib.h>
 
 #include <algorithm>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -38,6 +52,10 @@
 
 extern "C" hipError_t bpftime_amd_launch_sys_init(const void *records, uint64_t n, uint32_t record_size,
                                                   int64_t *out, uint32_t *state, hipStream_t stream);
+extern "C" size_t bpftime_amd_group_scratch_bytes(uint64_t n);
+extern "C" hipError_t bpftime_amd_group_threads(const void *recs, uint64_t n, uint32_t rec_size, void *scratch,
+                                                uint32_t **perm, uint32_t **seg, uint64_t *nseg,
+                                                hipStream_t stream);
 
 namespace {
 
@@ -50,28 +68,40 @@ struct Attach {
   int64_t sys_nr;  // -1: every syscall
   bool enter;      // sys_enter (true) or sys_exit tracepoint
   int flags;       // bpftime_amd::vm_prog_flags
-  struct ebpf_vm *vm;
+  // (shared: a dispatch in flight keeps the VMs it copied alive through a
+  // detach or reset on another thread)
+  std::shared_ptr<struct ebpf_vm> vm;
 };
 
 std::mutex g_mu;
 std::vector<Attach> g_attach;
 int g_next_id = 1;
 
-// per-stream device scratch of a dispatch (the records' override state, a
-// copy of the records for programs that may store into their ctx): a
-// dispatch's batches use it in stream order
+// Per-stream device scratch of a dispatch (the records' override state, a
+// copy of the records for programs that may store into their ctx, the thread
+// grouping), and a per-stream lock that a dispatch holds from taking the
+// scratch until it has queued its last launch: two dispatches on one stream
+// never share the scratch, and a larger allocation frees the old buffer only
+// after the dispatches that used it have queued everything (the stream sync
+// then waits for them)
 std::mutex g_buf_mu;
 struct Buf {
   void *p = nullptr;
   uint64_t bytes = 0;
+  std::shared_ptr<std::mutex> mu = std::make_shared<std::mutex>();
 };
 std::map<hipStream_t, Buf> g_bufs;
 
+std::shared_ptr<std::mutex> stream_lock(hipStream_t s) {
+  std::lock_guard<std::mutex> g(g_buf_mu);
+  return g_bufs[s].mu;
+}
+
+// (called with the stream's lock held)
 uint8_t *scratch(hipStream_t s, uint64_t bytes) {
   std::lock_guard<std::mutex> g(g_buf_mu);
   Buf &b = g_bufs[s];
   if (b.bytes < bytes) {
-    // (the stream may still run a dispatch that uses the old buffer)
     if (b.p && (hipStreamSynchronize(s) != hipSuccess || hipFree(b.p) != hipSuccess)) return nullptr;
     b.p = nullptr;
     b.bytes = 0;
@@ -87,12 +117,151 @@ int fail(const std::string &what, int err) {
   return -1;
 }
 
+// dispatch_syscall's order: enter per-syscall, enter global, exit
+// per-syscall, exit global (attach order inside each group; the reference
+// keeps each group in a std::set of entry pointers, syscall_trace_attach_impl.hpp:
+// 93-96, whose order follows the entries' addresses)
+std::vector<Attach> ordered_attachments() {
+  std::vector<Attach> order;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    order = g_attach;
+  }
+  auto rank = [](const Attach &a) { return (a.enter ? 0 : 2) + (a.sys_nr >= 0 ? 0 : 1); };
+  std::stable_sort(order.begin(), order.end(), [&](const Attach &a, const Attach &b) { return rank(a) < rank(b); });
+  return order;
+}
+
+// Whether the attachments may not commute: two of them reach one map, and one
+// writes it (a store, a fetching / non-add atomic, update / delete / ring
+// calls) or adds to it while the other reads it.  Counter adds commute with
+// counter adds; reads with reads.  Programs whose accesses the loader cannot
+// place reach every map.  -1 when a program is not loaded.
+int conflicts(const std::vector<Attach> &order) {
+  using bpftime_amd::FX_ADD;
+  using bpftime_amd::FX_READ;
+  using bpftime_amd::FX_WRITE;
+  struct Fx {
+    std::map<int32_t, uint8_t> m;
+    uint8_t any;
+  };
+  std::vector<Fx> fx(order.size());
+  for (size_t i = 0; i < order.size(); i++)
+    if (bpftime_amd::vm_map_effects(order[i].vm.get(), fx[i].m, fx[i].any) < 0) return -1;
+  auto clash = [](uint8_t a, uint8_t b) {
+    return ((a & FX_WRITE) && b) || ((b & FX_WRITE) && a) || ((a & FX_ADD) && (b & FX_READ)) ||
+           ((b & FX_ADD) && (a & FX_READ));
+  };
+  for (size_t i = 0; i < fx.size(); i++)
+    for (size_t j = i + 1; j < fx.size(); j++) {
+      if (clash(fx[i].any, fx[j].any)) return 1;
+      for (const auto &kv : fx[i].m) {
+        auto it = fx[j].m.find(kv.first);
+        if (clash(kv.second | fx[i].any, (it == fx[j].m.end() ? 0 : it->second) | fx[j].any)) return 1;
+      }
+      for (const auto &kv : fx[j].m)
+        if (clash(kv.second | fx[j].any, fx[i].any)) return 1;
+    }
+  return 0;
+}
+
+// 1 thread-ordered, 0 program-major, -1 error
+int plan_for(const std::vector<Attach> &order, uint32_t flags) {
+  if (flags & EBPF_BATCH_ORDERED) return 1;  // one lane, record order: the serial run
+  if (flags & BPFTIME_AMD_DISPATCH_PROGRAMS) return 0;
+  if (flags & BPFTIME_AMD_DISPATCH_THREADS) return 1;
+  const int c = conflicts(order);
+  if (c < 0) return fail("an attached program is not loaded", EINVAL);
+  return c;
+}
+
+int64_t dispatch_threads(const std::vector<Attach> &order, const uint8_t *records, uint64_t n, uint32_t record_size,
+                         int64_t *out_rets, uint32_t flags, hipStream_t s) {
+  std::vector<bpftime_amd::SeqAttach> progs;
+  for (const Attach &a : order) progs.push_back({a.vm.get(), a.sys_nr, a.enter});
+  // one thread: an ORDERED dispatch (the serial reference run) or 64-B
+  // records (no recorded caller: every call is the dispatching thread's)
+  const bool one = (flags & EBPF_BATCH_ORDERED) || record_size < 96;
+  const uint64_t gbytes = one ? 0 : bpftime_amd_group_scratch_bytes(n);
+  if (!one && !gbytes) return fail("thread grouping of " + std::to_string(n) + " records", EINVAL);
+  uint8_t *buf = scratch(s, 256 + gbytes);
+  if (!buf) return fail("scratch allocation failed", ENOMEM);
+  uint32_t *perm = nullptr, *seg = nullptr;
+  uint64_t nseg = 1;
+  if (!one) {
+    const hipError_t e = bpftime_amd_group_threads(records, n, record_size, buf + 256, &perm, &seg, &nseg, s);
+    if (e != hipSuccess) return fail(std::string("thread grouping: ") + hipGetErrorString(e), EIO);
+  }
+  const int64_t rc = bpftime_amd::seq_dispatch(progs, records, n, record_size, perm, seg, nseg, out_rets, flags,
+                                               (uint32_t *)buf, s);
+  return rc;
+}
+
+int64_t dispatch_programs(const std::vector<Attach> &order, const uint8_t *records, uint64_t n,
+                          uint32_t record_size, int64_t *out_rets, uint32_t flags, hipStream_t s) {
+  bool enter_ovr = false, any_ovr = false, copies = false;
+  for (const Attach &a : order) {
+    enter_ovr |= a.enter && (a.flags & bpftime_amd::kProgSetsRetval);
+    any_ovr |= (a.flags & bpftime_amd::kProgSetsRetval) != 0;
+    copies |= (a.flags & bpftime_amd::kProgStoresCtx) != 0;
+  }
+  // scratch: per-record override state, then (programs that may store into
+  // their ctx) a copy of the records
+  const bool state = out_rets || any_ovr;
+  const uint64_t sbytes = state ? (4 * n + 255) & ~255ull : 0, rbytes = n * record_size;
+  uint8_t *buf = nullptr;
+  if (state || copies) {
+    buf = scratch(s, sbytes + (copies ? rbytes : 0));
+    if (!buf) return fail("scratch allocation failed", ENOMEM);
+  }
+  uint32_t *st = state ? (uint32_t *)buf : nullptr;
+  uint8_t *copy = copies ? buf + sbytes : nullptr;
+  if (state) {
+    // out_rets[i] = the recorded ret (96- / 128-B records) or 0; state[i] = 0
+    const hipError_t e = bpftime_amd_launch_sys_init(records, n, record_size, out_rets, st, s);
+    if (e != hipSuccess) return fail(std::string("state init: ") + hipGetErrorString(e), EIO);
+  }
+  int64_t failed = 0;
+  for (const Attach &a : order) {
+    const uint8_t *base = records;
+    if (a.flags & bpftime_amd::kProgStoresCtx) {
+      // each reference callback runs on its own ctx copy (:43-45)
+      const hipError_t e = hipMemcpyAsync(copy, records, rbytes, hipMemcpyDeviceToDevice, s);
+      if (e != hipSuccess) return fail(std::string("record copy: ") + hipGetErrorString(e), EIO);
+      base = copy;
+    }
+    struct ebpf_batch b = {};
+    b.ctx_kind = a.enter ? EBPF_CTX_SYSCALL : EBPF_CTX_SYSCALL_EXIT;
+    b.flags = (flags & (EBPF_BATCH_SYNC | EBPF_BATCH_UNCHECKED)) | (a.sys_nr >= 0 ? EBPF_BATCH_SYS_NR : 0u);
+    b.count = n;
+    b.data = const_cast<uint8_t *>(base + (a.enter ? 0 : 64));
+    b.stride = record_size;
+    b.sys_nr = a.sys_nr;
+    b.stream = s;
+    // (96- / 128-B records: the recorded caller's pid_tgid at +88; 128-B: the
+    // recorded clocks at +96 / +104)
+    if (record_size >= BPFTIME_AMD_SYSCALL_RECORD_FULL) b.pid_tgid_off = a.enter ? 88 : 24;
+    if (record_size == BPFTIME_AMD_SYSCALL_RECORD_TIMED) b.ktime_off = a.enter ? 96 : 40;
+    // the state where this program sets it, or (exit programs) where an
+    // enter program may have overridden the record's return
+    const bool sets = (a.flags & bpftime_amd::kProgSetsRetval) != 0;
+    if (state && (sets || (!a.enter && enter_ovr))) {
+      b.sys_state = st;
+      b.sys_ret = sets ? out_rets : nullptr;
+      b.sys_phase = a.enter ? 1 : 2;
+    }
+    const int rc = ebpf_exec_batch(a.vm.get(), &b);
+    if (rc < 0) return -1;
+    failed += rc;
+  }
+  return failed;
+}
+
 }  // namespace
 
 void bpftime_amd::syscall_detach_all() {
   std::lock_guard<std::mutex> g(g_mu);
-  for (Attach &a : g_attach) ebpf_destroy(a.vm);
-  g_attach.clear();
+  g_attach.clear();  // (each VM goes with the last dispatch that holds it)
 }
 
 extern "C" {
@@ -111,10 +280,16 @@ int bpftime_amd_syscall_attach_ex(int prog_fd, int64_t sys_nr, int is_enter) {
     errno = EINVAL;
     return -1;
   }
+  std::shared_ptr<struct ebpf_vm> owned(vm, ebpf_destroy);
   ebpf_set_ctx_kind(vm, is_enter ? EBPF_CTX_SYSCALL : EBPF_CTX_SYSCALL_EXIT);
   const int flags = bpftime_amd::vm_prog_flags(vm);
+  if (flags < 0) {  // (never attach a program whose flags are unknown)
+    bpftime_amd::set_error("syscall attach: the program is not loaded");
+    errno = EINVAL;
+    return -1;
+  }
   std::lock_guard<std::mutex> g(g_mu);
-  g_attach.push_back(Attach{g_next_id, prog_fd, sys_nr, is_enter != 0, flags < 0 ? 0 : flags, vm});
+  g_attach.push_back(Attach{g_next_id, prog_fd, sys_nr, is_enter != 0, flags, std::move(owned)});
   return g_next_id++;
 }
 
@@ -124,7 +299,6 @@ int bpftime_amd_syscall_detach(int id) {
   std::lock_guard<std::mutex> g(g_mu);
   for (auto it = g_attach.begin(); it != g_attach.end(); ++it)
     if (it->id == id) {
-      ebpf_destroy(it->vm);
       g_attach.erase(it);
       return 0;
     }
@@ -132,80 +306,35 @@ int bpftime_amd_syscall_detach(int id) {
   return -1;
 }
 
+int bpftime_amd_syscall_dispatch_plan(uint32_t flags) { return plan_for(ordered_attachments(), flags); }
+
 int64_t bpftime_amd_syscall_dispatch_records(const void *records, uint64_t n, uint32_t record_size,
                                              int64_t *out_rets, uint32_t flags, void *stream) {
-  if (record_size != BPFTIME_AMD_SYSCALL_RECORD && record_size != BPFTIME_AMD_SYSCALL_RECORD_FULL)
-    return fail("record size " + std::to_string(record_size) + " (64 or 96)", EINVAL);
+  if (record_size != BPFTIME_AMD_SYSCALL_RECORD && record_size != BPFTIME_AMD_SYSCALL_RECORD_FULL &&
+      record_size != BPFTIME_AMD_SYSCALL_RECORD_TIMED)
+    return fail("record size " + std::to_string(record_size) + " (64, 96 or 128)", EINVAL);
   if (n && !records) return fail("no records", EINVAL);
-  std::vector<Attach> order;
-  {
-    std::lock_guard<std::mutex> g(g_mu);
-    order = g_attach;
-  }
-  // dispatch_syscall's order: enter per-syscall, enter global, exit
-  // per-syscall, exit global (attach order inside each group)
-  auto rank = [](const Attach &a) { return (a.enter ? 0 : 2) + (a.sys_nr >= 0 ? 0 : 1); };
-  std::stable_sort(order.begin(), order.end(), [&](const Attach &a, const Attach &b) { return rank(a) < rank(b); });
-  bool exits = false, enter_ovr = false, any_ovr = false, copies = false;
-  for (const Attach &a : order) {
-    exits |= !a.enter;
-    enter_ovr |= a.enter && (a.flags & bpftime_amd::kProgSetsRetval);
-    any_ovr |= (a.flags & bpftime_amd::kProgSetsRetval) != 0;
-    copies |= (a.flags & bpftime_amd::kProgStoresCtx) != 0;
-  }
-  if (exits && record_size != BPFTIME_AMD_SYSCALL_RECORD_FULL)
+  if (n > 0xffffffffull) return fail("more than 2^32 records", EINVAL);
+  const std::vector<Attach> order = ordered_attachments();
+  bool exits = false;
+  for (const Attach &a : order) exits |= !a.enter;
+  if (exits && record_size < BPFTIME_AMD_SYSCALL_RECORD_FULL)
     return fail("sys_exit programs are attached: the records need the 96-B form (enter + exit ctx)", EINVAL);
-  if (n == 0) return 0;
+  const int plan = plan_for(order, flags);
+  if (plan < 0) return -1;
+  if (n == 0 || order.empty()) {
+    if (n && out_rets) {  // nothing attached: every call returns its recorded ret
+      hipStream_t s = (hipStream_t)stream;
+      const hipError_t e = bpftime_amd_launch_sys_init(records, n, record_size, out_rets, nullptr, s);
+      if (e != hipSuccess) return fail(std::string("state init: ") + hipGetErrorString(e), EIO);
+    }
+    return 0;
+  }
   hipStream_t s = (hipStream_t)stream;
-  // scratch: per-record override state, then (programs that may store into
-  // their ctx) a copy of the records
-  const bool state = out_rets || any_ovr;
-  const uint64_t sbytes = state ? (4 * n + 255) & ~255ull : 0, rbytes = n * record_size;
-  uint8_t *buf = nullptr;
-  if (state || copies) {
-    buf = scratch(s, sbytes + (copies ? rbytes : 0));
-    if (!buf) return fail("scratch allocation failed", ENOMEM);
-  }
-  uint32_t *st = state ? (uint32_t *)buf : nullptr;
-  uint8_t *copy = copies ? buf + sbytes : nullptr;
-  if (state) {
-    // out_rets[i] = the recorded ret (96-B records) or 0; state[i] = 0
-    const hipError_t e = bpftime_amd_launch_sys_init(records, n, record_size, out_rets, st, s);
-    if (e != hipSuccess) return fail(std::string("state init: ") + hipGetErrorString(e), EIO);
-  }
-  int64_t failed = 0;
-  for (const Attach &a : order) {
-    const uint8_t *base = (const uint8_t *)records;
-    if (a.flags & bpftime_amd::kProgStoresCtx) {
-      // each reference callback runs on its own ctx copy (:43-45)
-      const hipError_t e = hipMemcpyAsync(copy, records, rbytes, hipMemcpyDeviceToDevice, s);
-      if (e != hipSuccess) return fail(std::string("record copy: ") + hipGetErrorString(e), EIO);
-      base = copy;
-    }
-    struct ebpf_batch b = {};
-    b.ctx_kind = a.enter ? EBPF_CTX_SYSCALL : EBPF_CTX_SYSCALL_EXIT;
-    b.flags = (flags & (EBPF_BATCH_SYNC | EBPF_BATCH_ORDERED | EBPF_BATCH_UNCHECKED)) |
-              (a.sys_nr >= 0 ? EBPF_BATCH_SYS_NR : 0u);
-    b.count = n;
-    b.data = const_cast<uint8_t *>(base + (a.enter ? 0 : 64));
-    b.stride = record_size;
-    b.sys_nr = a.sys_nr;
-    b.stream = stream;
-    // (96-B records: the recorded caller's pid_tgid at +88)
-    if (record_size == BPFTIME_AMD_SYSCALL_RECORD_FULL) b.pid_tgid_off = a.enter ? 88 : 24;
-    // the state where this program sets it, or (exit programs) where an
-    // enter program may have overridden the record's return
-    const bool sets = (a.flags & bpftime_amd::kProgSetsRetval) != 0;
-    if (state && (sets || (!a.enter && enter_ovr))) {
-      b.sys_state = st;
-      b.sys_ret = sets ? out_rets : nullptr;
-      b.sys_phase = a.enter ? 1 : 2;
-    }
-    const int rc = ebpf_exec_batch(a.vm, &b);
-    if (rc < 0) return -1;
-    failed += rc;
-  }
-  return failed;
+  const std::shared_ptr<std::mutex> mu = stream_lock(s);
+  std::lock_guard<std::mutex> hold(*mu);
+  return plan ? dispatch_threads(order, (const uint8_t *)records, n, record_size, out_rets, flags, s)
+              : dispatch_programs(order, (const uint8_t *)records, n, record_size, out_rets, flags, s);
 }
 
 int64_t bpftime_amd_syscall_dispatch(const void *records, uint64_t n, uint32_t flags, void *stream) {

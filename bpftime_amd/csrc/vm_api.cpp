@@ -468,6 +468,20 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     error = "descriptor batches need an XDP / raw ctx and umem_bytes";
     return -1;
   }
+  // the recorded caller / clock offsets (include/ebpf-vm.h): syscall kinds
+  // only, 8-aligned, the u64 inside the unit (the kernel reads
+  // it for any nonzero value, in both tiers)
+  {
+    const uint64_t extent = sys_exit && b->stride >= 96 ? b->stride - 64 : b->stride;
+    for (const auto &o : {std::make_pair("pid_tgid_off", b->pid_tgid_off), std::make_pair("ktime_off", b->ktime_off)}) {
+      if (!o.second) continue;
+      if (kind != CTX_SYSCALL || o.second < 0 || o.second % 8 != 0 || (uint64_t)o.second + 8 > extent) {
+        error = std::string(o.first) + " " + std::to_string(o.second) +
+                ": a syscall batch's u64 inside the unit (8-aligned, off + 8 <= " + std::to_string(extent) + ")";
+        return -1;
+      }
+    }
+  }
   hipStream_t s = (hipStream_t)b->stream;
   if (b->count == 0) return 0;
   Runtime &r = rt();
@@ -534,6 +548,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   p.sys_ret = b->sys_ret;
   p.sys_phase = b->sys_phase;
   p.pid_off = b->pid_tgid_off;
+  p.kt_off = b->ktime_off;
   p.pid_tgid = ((uint64_t)(uint32_t)getpid() << 32) | (uint32_t)syscall(SYS_gettid);
   p.arena_lo = (uint64_t)(uintptr_t)r.arena;
   p.arena_hi = p.arena_lo + r.arena_size;
@@ -1070,6 +1085,128 @@ int vm_prog_flags(const ::ebpf_vm *vm) {
   auto im = vm->impl->image();
   if (!im) return -1;
   return (im->prog.sets_retval ? kProgSetsRetval : 0) | (im->fr.stores_unit ? kProgStoresCtx : 0);
+}
+
+int vm_map_effects(const ::ebpf_vm *vm, std::map<int32_t, uint8_t> &fx, uint8_t &any) {
+  if (!vm || !vm->impl->loaded) return -1;
+  auto im = vm->impl->image();
+  if (!im) return -1;
+  fx = im->fr.map_fx;
+  any = im->fr.any_fx;
+  return 0;
+}
+
+extern "C" hipError_t bpftime_amd_launch_sys_seq(const SeqParams *p, hipStream_t stream);
+
+int64_t seq_dispatch(const std::vector<SeqAttach> &progs, const void *recs, uint64_t n, uint32_t rec_size,
+                     const uint32_t *perm, const uint32_t *seg, uint64_t nseg, int64_t *out, uint32_t flags,
+                     uint32_t *err, hipStream_t s) {
+  auto fail = [](const std::string &e) {
+    set_error("thread-ordered dispatch: " + e);
+    return (int64_t)-1;
+  };
+  if (progs.size() > kSeqMaxProgs)
+    return fail(std::to_string(progs.size()) + " programs attached (at most " + std::to_string(kSeqMaxProgs) + ")");
+  Runtime &r = rt();
+  SeqParams p{};
+  // the images stay referenced until the launch is queued (a relink by
+  // another thread never frees what is read: Image, above)
+  std::vector<std::shared_ptr<Image>> keep;
+  const bool ordered = (flags & EBPF_BATCH_ORDERED) != 0;
+  bool may_delete = false, names_lpm = false;
+  std::vector<int> lpm_w;
+  uint32_t lpm_updates = 0;
+  uint64_t steps = 0;
+  for (const SeqAttach &a : progs) {
+    Mi355xVm *vm = a.vm->impl;
+    auto im = vm->image();
+    if (!vm->loaded || !im) return fail("an attached program is not loaded");
+    if (vm->has_tail) return fail("an attached program calls bpf_tail_call (program-major dispatch runs it)");
+    const FInsn *f = im->linked(false, 0, 0, true, -1, 0, 0);
+    if (!f) return fail("device upload failed");
+    SeqProg &q = p.progs[p.nprogs++];
+    q.prog = im->d_prog;
+    q.fast = f;
+    q.sys_nr = a.sys_nr;
+    q.enter = a.enter ? 1 : 0;
+    may_delete |= im->prog.may_delete;
+    names_lpm |= im->fr.names_lpm;
+    for (const auto &w : im->fr.lpm_writes) {
+      if (!ordered)
+        return fail(std::string(w.first == 2 ? "bpf_map_update_elem" : "bpf_map_delete_elem") +
+                    " on LPM_TRIE map fd " + std::to_string(w.second) +
+                    ": program-side LPM trie writes run only in EBPF_BATCH_ORDERED batches");
+      lpm_updates += w.first == 2;
+      if (std::find(lpm_w.begin(), lpm_w.end(), w.second) == lpm_w.end()) lpm_w.push_back(w.second);
+    }
+    steps = std::max(steps, vm->step_limit);
+    keep.push_back(std::move(im));
+  }
+  p.rec_size = rec_size;
+  p.recs = (const uint8_t *)recs;
+  p.n = n;
+  p.perm = perm;
+  p.seg = seg;
+  p.nseg = nseg;
+  p.out = out;
+  p.maps = r.d_maptab;
+  p.ncpu = r.ncpu;
+  p.checked = (flags & EBPF_BATCH_UNCHECKED) ? 0 : 1;
+  p.arena_lo = (uint64_t)(uintptr_t)r.arena;
+  p.arena_hi = p.arena_lo + r.arena_size;
+  p.step_limit = steps;
+  p.pid_tgid = ((uint64_t)(uint32_t)getpid() << 32) | (uint32_t)syscall(SYS_gettid);
+  p.err_count = err;
+  p.exact = ordered ? 1 : 0;
+  // the map upkeep exec_batch does before a launch, for the union of the
+  // programs (a deletion never runs beside a cached launch; LPM launches
+  // under the LPM launch lock; lookup indexes; LRU stamps; host views)
+  if (may_delete && r.lcache_inflight.load()) {
+    if (hipDeviceSynchronize() != hipSuccess) return fail("device synchronize failed");
+    r.lcache_inflight = false;
+    r.deleter_inflight = false;
+  }
+  std::unique_lock<std::mutex> lpm_lk(r.lpm_launch_mu, std::defer_lock);
+  const bool touches_lpm = r.lpm_maps.load() > 0 && names_lpm;
+  if (touches_lpm) {
+    lpm_lk.lock();
+    if ((!lpm_w.empty() && r.lpm_inflight.load()) || r.lpm_writer_inflight.load()) {
+      if (hipDeviceSynchronize() != hipSuccess) return fail("device synchronize failed");
+      r.lpm_inflight = false;
+      r.lpm_writer_inflight = false;
+    }
+  }
+  if (r.prepare_ix(may_delete, n, lpm_w, lpm_updates, names_lpm) < 0) {
+    const std::string le = bpftime_amd_last_error() ? bpftime_amd_last_error() : "";
+    return fail(le.rfind("LPM_TRIE", 0) == 0 ? le : "hash lookup index rebuild failed");
+  }
+  p.lru_seq = r.prepare_lru();
+  if (!p.lru_seq) return fail("LRU table upkeep failed");
+  if (r.host_views_push() < 0) return fail("host view upload failed");
+  hipError_t e = hipMemsetAsync(err, 0, 4, s);
+  if (e == hipSuccess) e = bpftime_amd_launch_sys_seq(&p, s);
+  if (e != hipSuccess) return fail(std::string("kernel launch failed: ") + hipGetErrorString(e));
+  if (may_delete) r.deleter_inflight = true;
+  if (!lpm_w.empty()) {
+    std::lock_guard<std::mutex> g(r.mu);
+    for (const int fd : lpm_w) r.lpm_dev_dirty.insert(fd);
+    r.lpm_writer_inflight = true;
+  }
+  if (touches_lpm) {
+    r.lpm_inflight = true;
+    lpm_lk.unlock();
+  }
+  if (!(flags & EBPF_BATCH_SYNC)) return 0;
+  uint32_t failed = 0;
+  e = hipMemcpyAsync(&failed, err, 4, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess || r.host_views_pull() < 0)
+    return fail(std::string("sync failed: ") + (e != hipSuccess ? hipGetErrorString(e) : "host view pull"));
+  for (const int fd : lpm_w) {
+    std::lock_guard<std::mutex> g(r.mu);
+    if (lpm_pull(fd) < 0) return -1;
+  }
+  return failed;
 }
 }  // namespace bpftime_amd
 

@@ -125,6 +125,25 @@ def syscall_records_full(n: int, seed: int = SEED_CFG5, first: int = 0) -> np.nd
     return recs.view(np.uint8).reshape(n, 96)
 
 
+def syscall_records_timed(n: int, seed: int = SEED_CFG5, first: int = 0, threads: int = 64) -> np.ndarray:
+    """128-B replay records (include/bpftime_amd.h BPFTIME_AMD_SYSCALL_RECORD_TIMED):
+    the 96-B records of :func:`syscall_records_full` with the caller drawn
+    from ``threads`` threads (thread t: tgid 1000 + t // 4, tid 2000 + t,
+    tids unique as a kernel's are), then the clock at sys_enter (1 s + 1 us
+    per record index + [0, 500) ns: monotonic within a thread) and after the
+    call (enter + [50, 100050) ns), then 16 zero bytes."""
+    idx = np.arange(first, first + n, dtype=np.uint64)
+    full = syscall_records_full(n, seed, first).view(np.uint64).reshape(n, 12)
+    recs = np.zeros((n, 16), dtype=np.uint64)
+    recs[:, :12] = full
+    t = sm64(seed ^ 0x9999, idx) % np.uint64(threads)
+    recs[:, 11] = ((np.uint64(1000) + t // np.uint64(4)) << np.uint64(32)) | (np.uint64(2000) + t)
+    rc = sm64(seed ^ 0xAAAA, idx)
+    recs[:, 12] = np.uint64(1_000_000_000) + idx * np.uint64(1000) + rc % np.uint64(500)
+    recs[:, 13] = recs[:, 12] + np.uint64(50) + (rc >> np.uint64(16)) % np.uint64(100000)
+    return recs.view(np.uint8).reshape(n, 128)
+
+
 # ---------------------------------------------------------------------------
 # config 1: 1k-packet pcap (990 x 64 B Eth/IPv4/UDP + 10 runts, seed 1)
 # ---------------------------------------------------------------------------

@@ -18,7 +18,7 @@ from __future__ import annotations
 
 import struct
 
-from .isa import (Asm, BPF_ANY, BPF_FUNC_get_current_pid_tgid, BPF_FUNC_map_lookup_elem,
+from .isa import (Asm, BPF_ANY, BPF_FUNC_get_current_pid_tgid, BPF_FUNC_ktime_get_ns, BPF_FUNC_map_lookup_elem,
                   BPF_FUNC_map_update_elem, BPF_FUNC_override_return, BPF_FUNC_set_retval,
                   BPF_FUNC_ringbuf_output, BPF_NOEXIST, ATOMIC_ADD, XDP_DROP, XDP_PASS, XDP_TX, XDP_ABORTED)
 
@@ -212,24 +212,55 @@ EEXIST = 17
 
 
 def syscount_rodata(count_by_process: bool = False, filter_failed: bool = False, filter_errno: int = 0,
-                    filter_pid: int = 0) -> bytes:
-    return struct.pack("<BBBBii", 0, int(count_by_process), 0, int(filter_failed), filter_errno, filter_pid)
+                    filter_pid: int = 0, measure_latency: bool = False) -> bytes:
+    return struct.pack("<BBBBii", 0, int(count_by_process), int(measure_latency), int(filter_failed),
+                       filter_errno, filter_pid)
 
 
-def syscount_exit(data_fd: int, rodata_fd: int) -> bytes:
+def syscount_enter(start_fd: int, rodata_fd: int) -> bytes:
+    """syscount's sys_enter program (example/tracing/syscount/syscount.bpf.c:
+    33-47): the caller's pid_tgid; filter_pid on the pid (.rodata @8); ``ts =
+    bpf_ktime_get_ns()``; ``bpf_map_update_elem(&start, &tid, &ts, 0)``.
+    start: HASH u32 tid -> u64 ns.  Returns 0."""
+    a = Asm()
+    a.call(BPF_FUNC_get_current_pid_tgid)
+    a.stx(4, 10, -4, "r0")                # u32 tid = id
+    a.mov64(6, "r0").alu64("rsh", 6, 32)  # pid = id >> 32
+    a.ld_map_value(9, rodata_fd, 0)
+    a.ldx(4, 2, 9, 8)                     # filter_pid
+    a.jmp("jeq", 2, 0, "nopid")
+    a.jmp32("jne", 6, "r2", "ret")        # (pid_t) pid != filter_pid
+    a.label("nopid")
+    a.call(BPF_FUNC_ktime_get_ns)
+    a.stx(8, 10, -16, "r0")               # ts
+    a.ld_map_fd(1, start_fd)
+    a.mov64(2, "r10").add64(2, -4)
+    a.mov64(3, "r10").add64(3, -16)
+    a.mov64(4, BPF_ANY)
+    a.call(BPF_FUNC_map_update_elem)
+    a.label("ret")
+    a.mov64(0, 0)
+    a.exit()
+    return a.assemble()
+
+
+def syscount_exit(data_fd: int, rodata_fd: int, start_fd: int = -1) -> bytes:
     """syscount's sys_exit program (example/tracing/syscount/syscount.bpf.c:
     49-87) over ``trace_event_raw_sys_exit`` {ent, id@8, ret@16}: skip id == -1
     (an interrupt), filter_pid on the caller's pid, filter_failed (ret >= 0
     skipped) and filter_errno (ret != -filter_errno skipped) from .rodata;
-    key = count_by_process ? pid : id; ``bpf_map_lookup_or_try_init`` of
-    data (maps.bpf.h: lookup, NOEXIST update of a zeroed data_t, an error
-    other than -EEXIST gives up, lookup again); ``count = count + 1``.
-    measure_latency (ktime, the start map) is not compiled in: SURVEY.md
-    Appendix B.11.  data: HASH u32 -> data_t 32 B {u64 count, u64 total_ns,
-    char comm[16]}.  Returns 0."""
+    with ``start_fd`` (the sys_enter program's start map) the measure_latency
+    path: ``start_ts = lookup(&start, &tid)``, none -> return, ``lat =
+    bpf_ktime_get_ns() - *start_ts``; key = count_by_process ? pid : id;
+    ``bpf_map_lookup_or_try_init`` of data (maps.bpf.h: lookup, NOEXIST update
+    of a zeroed data_t, an error other than -EEXIST gives up, lookup again);
+    ``count = count + 1`` and, measuring latency, ``total_ns = total_ns +
+    lat``.  data: HASH u32 -> data_t 32 B {u64 count, u64 total_ns, char
+    comm[16]}.  Returns 0."""
     a = Asm()
     a.mov64(6, "r1")
     a.call(BPF_FUNC_get_current_pid_tgid)
+    a.stx(4, 10, -8, "r0")                # u32 tid = id
     a.mov64(8, "r0").alu64("rsh", 8, 32)  # pid = id >> 32
     a.ldx(8, 7, 6, 8)                     # args->id
     a.jmp("jeq", 7, -1, "ret")
@@ -248,6 +279,21 @@ def syscount_exit(data_fd: int, rodata_fd: int) -> bytes:
     a.alu64("lsh", 2, 32).alu64("arsh", 2, 32).neg64(2)  # (long) -filter_errno
     a.jmp("jne", 3, "r2", "ret")
     a.label("noerr")
+    a.st(8, 10, -48, 0)                   # lat = 0
+    if start_fd >= 0:
+        a.ldx(1, 2, 9, 2)                 # measure_latency
+        a.jmp("jeq", 2, 0, "nolat")
+        a.ld_map_fd(1, start_fd)
+        a.mov64(2, "r10").add64(2, -8)
+        a.call(BPF_FUNC_map_lookup_elem)  # start_ts = lookup(&start, &tid)
+        a.jmp("jeq", 0, 0, "ret")
+        a.ldx(8, 1, 0, 0)
+        a.stx(8, 10, -48, "r1")
+        a.call(BPF_FUNC_ktime_get_ns)
+        a.ldx(8, 1, 10, -48)
+        a.alu64("sub", 0, "r1")           # lat = now - *start_ts
+        a.stx(8, 10, -48, "r0")
+        a.label("nolat")
     a.ldx(1, 2, 9, 1)                     # count_by_process
     a.mov64(1, "r7")
     a.jmp("jeq", 2, 0, "key")
@@ -278,7 +324,58 @@ def syscount_exit(data_fd: int, rodata_fd: int) -> bytes:
     a.ldx(8, 1, 0, 0)                     # val->count = val->count + 1
     a.add64(1, 1)
     a.stx(8, 0, 0, "r1")
+    if start_fd >= 0:
+        a.ldx(1, 2, 9, 2)                 # measure_latency
+        a.jmp("jeq", 2, 0, "ret")
+        a.ldx(8, 2, 10, -48)
+        a.ldx(8, 1, 0, 8)                 # val->total_ns = val->total_ns + lat
+        a.add64(1, "r2")
+        a.stx(8, 0, 8, "r1")
     a.label("ret")
+    a.mov64(0, 0)
+    a.exit()
+    return a.assemble()
+
+
+def tid_state_enter(start_fd: int) -> bytes:
+    """A sys_enter program that keeps per-thread state: ``start[tid] =
+    args[0]`` (start: HASH u32 tid -> u64), the shape of syscount's latency
+    pair with the argument in place of the clock."""
+    a = Asm()
+    a.mov64(6, "r1")
+    a.call(BPF_FUNC_get_current_pid_tgid)
+    a.stx(4, 10, -4, "r0")
+    a.ldx(8, 1, 6, 16)                    # args[0]
+    a.stx(8, 10, -16, "r1")
+    a.ld_map_fd(1, start_fd)
+    a.mov64(2, "r10").add64(2, -4)
+    a.mov64(3, "r10").add64(3, -16)
+    a.mov64(4, BPF_ANY)
+    a.call(BPF_FUNC_map_update_elem)
+    a.mov64(0, 0)
+    a.exit()
+    return a.assemble()
+
+
+def tid_state_exit(start_fd: int, sum_fd: int) -> bytes:
+    """Its sys_exit partner: ``sum += start[tid]`` (sum: an ARRAY u64 @0),
+    ``sum2 += start[tid] * ret`` (@8): the value the same call's sys_enter
+    stored."""
+    a = Asm()
+    a.mov64(6, "r1")
+    a.call(BPF_FUNC_get_current_pid_tgid)
+    a.stx(4, 10, -4, "r0")
+    a.ld_map_fd(1, start_fd)
+    a.mov64(2, "r10").add64(2, -4)
+    a.call(BPF_FUNC_map_lookup_elem)
+    a.jmp("jeq", 0, 0, "out")
+    a.ldx(8, 3, 0, 0)
+    a.ld_map_value(2, sum_fd, 0)
+    a.atomic(8, ATOMIC_ADD, 2, 0, 3)
+    a.ldx(8, 4, 6, 16)                    # ret
+    a.alu64("mul", 3, "r4")
+    a.atomic(8, ATOMIC_ADD, 2, 8, 3)
+    a.label("out")
     a.mov64(0, 0)
     a.exit()
     return a.assemble()

@@ -17,7 +17,8 @@ from . import isa
 from ._lib import BpfLinkCreateArgs, BpfMapAttr, EbpfBatch, lib
 
 CTX_RAW, CTX_XDP, CTX_SYSCALL, CTX_SYSCALL_EXIT = 0, 1, 2, 3
-SYSCALL_RECORD, SYSCALL_RECORD_FULL = 64, 96  # include/bpftime_amd.h replay records
+SYSCALL_RECORD, SYSCALL_RECORD_FULL, SYSCALL_RECORD_TIMED = 64, 96, 128  # include/bpftime_amd.h replay records
+DISPATCH_THREADS, DISPATCH_PROGRAMS = 0x100, 0x200  # dispatch plans (include/bpftime_amd.h)
 BATCH_SYNC, BATCH_ORDERED, BATCH_UNCHECKED, BATCH_SYS_NR, BATCH_TIMED = 0x1, 0x2, 0x4, 0x8, 0x10
 
 
@@ -278,9 +279,11 @@ class VM:
                    len_out: Optional[DeviceBuffer] = None, flags: int = BATCH_SYNC, first_unit: int = 0,
                    head: int = 0, data_offset: int = 0, ifindex: int = 0, rxq: int = 0,
                    stream: int = 0, descs: Optional[DeviceBuffer] = None, umem_bytes: int = 0,
-                   sys_nr: Optional[int] = None) -> int:
+                   sys_nr: Optional[int] = None, pid_tgid_off: int = 0, ktime_off: int = 0) -> int:
         """descs: AF_XDP descriptor mode ({u64 addr; u32 len; u32 options} per
-        unit, frames at data + addr inside umem_bytes; stride = chunk size)."""
+        unit, frames at data + addr inside umem_bytes; stride = chunk size).
+        pid_tgid_off / ktime_off: the recorded caller / clock of a syscall
+        replay unit (include/ebpf-vm.h)."""
         b = EbpfBatch(ctx_kind=kind, flags=flags, count=count, data=data.ptr + data_offset, stride=stride,
                       lens=lens.ptr if lens else None, fixed_len=fixed_len, ingress_ifindex=ifindex,
                       rx_queue_index=rxq, head=head, verdicts=verdicts.ptr if verdicts else None,
@@ -288,7 +291,8 @@ class VM:
                       data_off_out=data_off_out.ptr if data_off_out else None,
                       len_out=len_out.ptr if len_out else None, first_unit=first_unit,
                       stream=stream or None, descs=descs.ptr if descs else None, umem_bytes=umem_bytes,
-                      sys_nr=-1 if sys_nr is None else sys_nr)
+                      sys_nr=-1 if sys_nr is None else sys_nr, pid_tgid_off=pid_tgid_off,
+                      ktime_off=ktime_off)
         if sys_nr is not None:
             b.flags |= BATCH_SYS_NR
         rc = lib().ebpf_exec_batch(C.c_void_p(self.h), C.byref(b))
@@ -340,12 +344,24 @@ def syscall_detach(i: int) -> int:
 
 def syscall_dispatch(records: DeviceBuffer, n: int, record_size: int = SYSCALL_RECORD_FULL,
                      out: Optional[DeviceBuffer] = None, flags: int = BATCH_SYNC, stream: int = 0) -> int:
-    """dispatch_syscall over n recorded calls (64-B enter or 96-B enter + exit
-    records); out (i64 per record) receives what each call returns."""
+    """dispatch_syscall over n recorded calls (64-B enter, 96-B enter + exit
+    + caller, or 128-B records with the recorded clocks too); out (i64 per
+    record) receives what each call returns.  flags: BATCH_* and the plan
+    (DISPATCH_THREADS / DISPATCH_PROGRAMS; default: chosen from the attached
+    programs' map effects, syscall_dispatch_plan)."""
     rc = lib().bpftime_amd_syscall_dispatch_records(records.ptr, n, record_size, out.ptr if out else None,
                                                      flags, stream or None)
     if rc < 0:
         raise EbpfError(f"syscall dispatch failed: {_err()}")
+    return rc
+
+
+def syscall_dispatch_plan(flags: int = 0) -> int:
+    """1 when a dispatch with these flags runs thread-ordered for the
+    current attachments, 0 program-major."""
+    rc = lib().bpftime_amd_syscall_dispatch_plan(flags)
+    if rc < 0:
+        raise EbpfError(f"syscall dispatch plan failed: {_err()}")
     return rc
 
 

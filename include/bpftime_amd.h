@@ -277,33 +277,64 @@ int64_t bpftime_amd_ringbuf_fetch(int fd, void *out, uint64_t cap, uint64_t *use
  * calling thread's u64 pid_tgid (tgid << 32 | tid) at +88: the enter ctx and
  * the exit ctx as dispatch_syscall builds them (:57-66, :80-85), each the unit
  * its programs run on in place, and what bpf_get_current_pid_tgid returns to
- * them (bpf_helper.cpp:330-348; 64-B records: the dispatching thread's).  Per record
+ * them (bpf_helper.cpp:330-348; 64-B records: the dispatching thread's);
+ * BPFTIME_AMD_SYSCALL_RECORD_TIMED (128 B) = the 96-B record, then the
+ * recorded clock at sys_enter (u64 ns at +96) and after the call (+104), 16
+ * zero bytes: what bpf_ktime_get_ns (bpf_helper.cpp:357-362) returns inside
+ * the record's enter / exit callbacks (the replay definition of the clock;
+ * other records: the device clock).  Per record
  * (dispatch_syscall :18-95): exit (60) / exit_group (231) run nothing and
  * return ret; the per-syscall enter programs, then the global ones; if one of
  * them called bpf_override_return / bpf_set_retval the record returns that
  * value and its exit programs do not run; else the per-syscall exit programs,
  * then the global ones, and the record returns ret, or the value an exit
  * program set.  Ids outside [0, 512) (the reference indexes its callback
- * arrays with them, undefined there) run only global programs.  Each program
- * runs once over the batch (records are not interleaved across programs:
- * equal to the per-record order whenever the programs' map effects commute);
- * a program that may store into its ctx runs on a copy of the records, as
- * each reference callback runs on its own copy (:43-45).
+ * arrays with them, undefined there) run only global programs.
+ *
+ * Order.  The reference runs a call's callbacks on the calling thread, one
+ * call after another; threads run side by side.  Two plans give that result:
+ *  - program-major (BPFTIME_AMD_DISPATCH_PROGRAMS): each program runs once
+ *    over the batch, one lane per record, in the order above; a program that
+ *    may store into its ctx runs on a copy of the records, as each reference
+ *    callback runs on its own copy (:43-45).  Equal to the per-call order
+ *    whenever the attached programs' map effects commute;
+ *  - thread-ordered (BPFTIME_AMD_DISPATCH_THREADS): records are grouped by
+ *    their recorded pid_tgid (64-B records: one thread, the dispatcher), one
+ *    lane per thread walks its records in record order and runs each
+ *    record's enter callbacks, the override check and its exit callbacks
+ *    before the next record, every callback on a fresh ctx copy: the
+ *    reference's own schedule for any programs, threads in parallel.
+ * By default the dispatch picks thread-ordered when two attachments may not
+ * commute (one writes a map the other reads or writes, or adds to a map the
+ * other reads: the loader's map effects, loader.hpp FastForm::map_fx), else
+ * program-major.  EBPF_BATCH_ORDERED runs thread-ordered on one lane over
+ * every record in record order (the serial reference run).  Thread-ordered
+ * dispatch does not run bpf_tail_call (the dispatch fails, named).
+ * bpftime_amd_syscall_dispatch_plan(flags) says which plan a dispatch with
+ * these flags would take for the current attachments: 1 thread-ordered, 0
+ * program-major, -1 on errors.
  *
  * dispatch_records: `out_rets` (device i64 per record, nullable) receives the
  * value dispatch_syscall would return (64-B records have no ret: 0 unless
  * overridden).  64-B records with sys_exit programs attached are refused
- * (EINVAL).  Returns the failed-unit count summed over the programs with
- * EBPF_BATCH_SYNC, else 0; -1 on errors (bpftime_amd_last_error).
+ * (EINVAL).  Returns the failed-unit count summed over the programs (a
+ * failed callback counts once) with EBPF_BATCH_SYNC, else 0; -1 on errors
+ * (bpftime_amd_last_error).  Concurrent dispatches on one stream run one
+ * after the other (the dispatch holds the stream's scratch until it has
+ * queued its last launch).
  * bpftime_amd_syscall_dispatch(r, n, f, s) = dispatch_records(r, n, 64, NULL, f, s). */
 #define BPFTIME_AMD_SYSCALL_RECORD 64
 #define BPFTIME_AMD_SYSCALL_RECORD_FULL 96
+#define BPFTIME_AMD_SYSCALL_RECORD_TIMED 128
+#define BPFTIME_AMD_DISPATCH_THREADS 0x100  /* force the thread-ordered plan */
+#define BPFTIME_AMD_DISPATCH_PROGRAMS 0x200 /* force the program-major plan */
 int bpftime_amd_syscall_attach(int prog_fd, int64_t sys_nr);   /* attach id or -1 */
 int bpftime_amd_syscall_attach_ex(int prog_fd, int64_t sys_nr, int is_enter);
 int bpftime_amd_syscall_detach(int id);
 int64_t bpftime_amd_syscall_dispatch(const void *records, uint64_t n, uint32_t flags, void *stream);
 int64_t bpftime_amd_syscall_dispatch_records(const void *records, uint64_t n, uint32_t record_size,
                                              int64_t *out_rets, uint32_t flags, void *stream);
+int bpftime_amd_syscall_dispatch_plan(uint32_t flags);
 
 /* ---- attach plugins (attach/base_attach_impl/base_attach_impl.hpp:24-71,
  * attach/simple_attach_impl/simple_attach_impl.cpp:7-55; csrc/attach.cpp) ----

@@ -51,7 +51,12 @@ bool ebpf_toggle_bounds_check(struct ebpf_vm *vm, bool enable);
 void ebpf_set_error_print(struct ebpf_vm *vm, int (*error_printf)(FILE *stream, const char *format, ...));
 /* ebpf-vm.h:117.  `index` is the bpftime helper id (BPF_FUNC_*); the host
  * function pointer is recorded for ABI compatibility, the device runs its own
- * implementation of ids 1,2,3,5,7,8,28,44,65,189.  0 / -1. */
+ * implementation of ids 1,2,3 (map lookup / update / delete), 5 (ktime_get_ns),
+ * 7 (get_prandom_u32), 8 (get_smp_processor_id), 12 (tail_call), 14
+ * (get_current_pid_tgid), 28 (csum_diff), 44 (xdp_adjust_head), 58
+ * (override_return), 65 (xdp_adjust_tail), 130-133 (ringbuf output / reserve /
+ * submit / discard), 187 (set_retval) and 189 (xdp_load_bytes)
+ * (loader.cpp device_helper_supported).  0 / -1. */
 int ebpf_register(struct ebpf_vm *vm, unsigned int index, const char *name, void *fn);
 /* ebpf-vm.h:137: copy, patch (compat_ubpf.cpp:61-200), validate, pre-decode
  * and upload.  0 / <0 with *errmsg strdup'd (caller frees). */
@@ -134,6 +139,14 @@ struct ebpf_batch {
 	 * offset from each unit (96-B records: +88 of the record); 0: the thread that
 	 * launches the batch */
 	int32_t pid_tgid_off;
+	/* bpf_ktime_get_ns (5, bpf_helper.cpp:357-362) in a syscall replay: the
+	 * recorded clock, a u64 at this offset from each unit (128-B records: +96 of
+	 * the record at sys_enter, +104 at sys_exit); 0: the device clock.
+	 * Both offsets are syscall-kind only, multiples of 8, and the u64 must lie
+	 * inside the unit (EBPF_CTX_SYSCALL: off + 8 <= stride; EBPF_CTX_SYSCALL_EXIT
+	 * units with stride >= 96 are the tail of a record whose first 64 bytes are
+	 * the enter ctx: off + 8 <= stride - 64); else the batch fails (-1, named). */
+	int32_t ktime_off;
 };
 
 /* linux/if_xdp.h struct xdp_desc */

@@ -180,22 +180,24 @@ static int any_set(int enter, int64_t nr)
 
 int orc_sys_dispatch(const uint8_t *recs, uint64_t n, uint32_t rec_size, int64_t *out)
 {
-	if (rec_size != 64 && rec_size != 96)
+	if (rec_size != 64 && rec_size != 96 && rec_size != 128)
 		return -22;
 	for (uint64_t i = 0; i < n; i++) {
 		const uint8_t *r = recs + i * rec_size;
 		const struct trace_event_raw_sys_enter *er = (const void *)r;
 		const int64_t nr = er->id;
 		/* the "original syscall" is the recorded one: its ret */
-		const int64_t ret = rec_size == 96 ? ((const struct trace_event_raw_sys_exit *)(r + 64))->ret : 0;
+		const int64_t ret = rec_size >= 96 ? ((const struct trace_event_raw_sys_exit *)(r + 64))->ret : 0;
 		if (nr == 231 /*__NR_exit_group*/ || nr == 60 /*__NR_exit*/) { /* :25-26 */
 			if (out)
 				out[i] = ret;
 			continue;
 		}
 		const int64_t pnr = nr >= 0 && nr < 512 ? nr : -2; /* no per-syscall set */
-		if (rec_size == 96) /* the recorded caller (bpf_helper.cpp:330-348) */
+		if (rec_size >= 96) /* the recorded caller (bpf_helper.cpp:330-348) */
 			orc_pid_tgid_recorded(1, *(const uint64_t *)(r + 88));
+		if (rec_size == 128) /* the recorded clock at sys_enter (bpf_helper.cpp:357-362) */
+			orc_ktime_recorded(1, *(const uint64_t *)(r + 96));
 		orc_retval.active = 1; /* :35-40 */
 		orc_retval.overridden = 0;
 		if (any_set(1, pnr)) { /* :55-67 */
@@ -213,6 +215,8 @@ int orc_sys_dispatch(const uint8_t *recs, uint64_t n, uint32_t rec_size, int64_t
 			continue;
 		}
 		orc_retval.active = 1; /* :73-78 */
+		if (rec_size == 128) /* ... and after the call returned */
+			orc_ktime_recorded(1, *(const uint64_t *)(r + 104));
 		if (any_set(0, pnr)) { /* :80-89 */
 			struct trace_event_raw_sys_exit ctx;
 			memset(&ctx, 0, sizeof(ctx));
@@ -226,6 +230,7 @@ int orc_sys_dispatch(const uint8_t *recs, uint64_t n, uint32_t rec_size, int64_t
 			out[i] = orc_retval.overridden ? orc_retval.value : ret;
 	}
 	orc_pid_tgid_recorded(0, 0);
+	orc_ktime_recorded(0, 0);
 	return 0;
 }
 

@@ -53,9 +53,21 @@ static uint64_t h_delete(uint64_t map, uint64_t key, uint64_t a, uint64_t b, uin
 	return (uint64_t)orc_map_delete((int)map, (const void *)(uintptr_t)key);
 }
 
+/* a replayed call's recorded clock (orc_sys_dispatch, 128-B records) */
+static int g_kt_rec_on;
+static uint64_t g_kt_rec;
+
+void orc_ktime_recorded(int on, uint64_t v)
+{
+	g_kt_rec_on = on;
+	g_kt_rec = v;
+}
+
 static uint64_t h_ktime(uint64_t a, uint64_t b, uint64_t c, uint64_t d, uint64_t e)
 {
 	(void)a, (void)b, (void)c, (void)d, (void)e;
+	if (g_kt_rec_on)
+		return g_kt_rec;
 	struct timespec ts;
 	clock_gettime(CLOCK_MONOTONIC, &ts);
 	return (uint64_t)ts.tv_sec * 1000000000ULL + (uint64_t)ts.tv_nsec;

@@ -123,12 +123,16 @@ int orc_run_syscall(struct orc_vm *vm, const uint8_t *recs, uint64_t n, uint64_t
  * the sys_enter (is_enter 1) or sys_exit (0) tracepoint of sys_nr in
  * [0, 512) or of every syscall (-1): an id > 0, or -EINVAL.  dispatch: per
  * record, in record order, dispatch_syscall with the recorded call: records
- * of rec_size 64 (trace_event_raw_sys_enter) or 96 (that, then
- * trace_event_raw_sys_exit {0, id, ret} at +64); out[i] = what
- * dispatch_syscall returns (ret, 0 for 64-B records, or an override).  A
- * callback's failed exec is ignored (:47-52).  bpf_get_current_pid_tgid
- * returns a 96-B record's u64 at +88 (its recorded caller).  Ids outside [0, 512) have no
- * per-syscall callbacks here (the reference indexes its arrays with them). */
+ * of rec_size 64 (trace_event_raw_sys_enter), 96 (that, then
+ * trace_event_raw_sys_exit {0, id, ret} at +64, the caller's pid_tgid at +88)
+ * or 128 (that, then the recorded enter and exit clocks at +96 / +104);
+ * out[i] = what dispatch_syscall returns (ret, 0 for 64-B records, or an
+ * override).  A callback's failed exec is ignored (:47-52).
+ * bpf_get_current_pid_tgid returns a 96- / 128-B record's u64 at +88 (its
+ * recorded caller); bpf_ktime_get_ns inside a 128-B record's enter callbacks
+ * its u64 at +96, inside its exit callbacks the u64 at +104 (the replay
+ * definition of the clock).  Ids outside [0, 512) have no per-syscall
+ * callbacks here (the reference indexes its arrays with them). */
 int orc_sys_attach(struct orc_vm *vm, int64_t sys_nr, int is_enter);
 int orc_sys_detach(int id);
 void orc_sys_reset(void);
@@ -142,6 +146,8 @@ extern struct orc_retval_cb orc_retval;
 extern int orc_helper_abort;
 /* bpf_get_current_pid_tgid of a replayed call (96-B records: the u64 at +88) */
 void orc_pid_tgid_recorded(int on, uint64_t v);
+/* bpf_ktime_get_ns of a replayed call (128-B records: the recorded clock) */
+void orc_ktime_recorded(int on, uint64_t v);
 /* timed XDP loop (steady clock around the packet loop only, like
  * tools/bpftimetool/main.cpp:42-58); returns seconds, pins to `cpu` if >=0 */
 double orc_time_xdp(struct orc_vm *vm, uint8_t *base, uint64_t n, uint64_t stride,
