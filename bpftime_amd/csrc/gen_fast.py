@@ -2205,7 +2205,10 @@ class Gen:
         e = self.e
         fresh, loaded = L("fresh"), self.label("loaded")
         # ---- entry ----
-        e("s_mov_b64 s[78:79], %[prog]",
+        # (M0: s_set_gpr_idx_on writes it; the compiler's value is kept in an
+        # operand register and restored at the exit, so M0 is no clobber)
+        e("s_mov_b32 %[m0s], m0",
+          "s_mov_b64 s[78:79], %[prog]",
           "v_mov_b32 v40, %[rb]",
           "s_lshl_b32 s48, %[pc], 5",
           "s_mov_b64 s[58:59], exec", "s_mov_b64 exec, %[alive]",
@@ -2423,7 +2426,8 @@ class Gen:
           "s_mov_b64 %[aliveout], exec",
           "s_mov_b64 exec, s[58:59]",
           "s_lshr_b32 s52, s48, 5",
-          "s_mov_b32 %[pc], s52", "s_mov_b32 %[why], s68")
+          "s_mov_b32 %[pc], s52", "s_mov_b32 %[why], s68",
+          "s_mov_b32 m0, %[m0s]", "s_nop 0")
         return ids
 
 
@@ -2495,7 +2499,7 @@ def main():
                 f.write('  "%s\\n" \\\n' % line)
             f.write('  ""\n')
         f.write("#define BPFTIME_AMD_FAST_CLOBBERS %s\n" %
-                ", ".join('"%s"' % c for c in clob + ["vcc", "scc", "m0", "memory"]))
+                ", ".join('"%s"' % c for c in clob + ["vcc", "scc", "memory"]))
     with open(os.path.join(HERE, "fast_ops.hpp"), "w") as f:
         f.write("// Generated by gen_fast.py; do not edit.\n#pragma once\n#include <stdint.h>\n\n")
         f.write("namespace bpftime_amd {\n\n// handler ids of the threaded fast path (FInsn::hoff = 4 + 4 * id)\nenum FOp : uint32_t {\n")

@@ -530,11 +530,12 @@ __device__ __forceinline__ uint32_t run_fast(Ctx &c, const FastEnv &f, const Fas
   uint32_t vcpu = __ballot(c.alive && u.vm != vm0) == 0 && f.ncpu <= 0xffff ? vm0 | (f.ncpu << 16) : ~0u;
   uint64_t vaddr = u.vaddr, raddr = u.raddr, laddr = u.laddr;
   uint32_t ulen = u.len, chain = __builtin_amdgcn_readfirstlane(chain_in);
+  uint32_t m0s;  // M0 across the block (gen_fast.py: saved at the entry, restored at the exit)
 #define FAST_OUTS                                                                                             \
   [pc] "+s"(pc), [steps] "+s"(steps), [why] "=s"(why), [aliveout] "=s"(alive_out), [lpc] "=v"(lpc),            \
       [c0a] "+s"(c0a), [c1a] "+s"(c1a), [c0dl] "+s"(c0dl), [c0dh] "+s"(c0dh), [c1dl] "+s"(c1dl),                \
       [c1dh] "+s"(c1dh), [c0s] "+s"(c0s), [c1s] "+s"(c1s), [vaddr] "+v"(vaddr), [raddr] "+v"(raddr),            \
-      [laddr] "+v"(laddr), [ulen] "+v"(ulen), [chain] "+s"(chain), [vcpu] "+s"(vcpu)
+      [laddr] "+v"(laddr), [ulen] "+v"(ulen), [chain] "+s"(chain), [vcpu] "+s"(vcpu), [m0s] "=&s"(m0s)
 #define FAST_INS                                                                                              \
   [prog] "s"(f.fast), [maps] "s"(f.maps), [dlo] "s"(f.dlo), [dhi] "s"(f.dhi), [alo] "s"(f.alo),               \
       [ahi] "s"(f.ahi), [shi] "s"(f.shi), [phi] "s"(f.phi), [limit] "s"(limit), [rb] "v"(f.rb),               \
@@ -601,7 +602,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   SRP(miss_log); SRP(miss_counts); SRV(miss_cap); SRP(tail_slots); SRV(full_q); SRV(full_r); SRV(step_cpu);
   SRP(sys_state); SRP(sys_ret); SRV(sys_phase); SRV(pid_tgid);
   p.pid_off = (int32_t)sreg((uint64_t)(uint32_t)pin.pid_off);
-  p.kt_off = (int32_t)sreg((uint64_t)(uint32_t)pin.kt_off);
+  SRP(pid_base); SRV(pid_stride); SRP(kt_base); SRV(kt_stride);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
   p.unwind_idx = (int32_t)sreg((uint64_t)(uint32_t)pin.unwind_idx);
 #undef SRP
@@ -1082,9 +1083,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         env.ovr_state = p.sys_state ? p.sys_state + unit : nullptr;
         env.ovr_val = p.sys_ret ? p.sys_ret + unit : nullptr;
         env.ovr_bit = p.sys_phase;
-        env.pid_tgid = p.pid_off ? *(const uint64_t *)(slot + (int64_t)p.pid_off) : p.pid_tgid;
-        env.kt_on = p.kt_off != 0;
-        env.ktime = p.kt_off ? *(const uint64_t *)(slot + (int64_t)p.kt_off) : 0;
+        env.pid_tgid = p.pid_base ? *(const uint64_t *)(p.pid_base + unit * p.pid_stride) : p.pid_tgid;
+        env.kt_on = p.kt_base != nullptr;
+        env.ktime = p.kt_base ? *(const uint64_t *)(p.kt_base + unit * p.kt_stride) : 0;
         uint32_t cerr = E_OK;
         uint64_t *R = c.R;
         const uint64_t rv = call_helper(c.call_id, R[1 * kBlock], R[2 * kBlock], R[3 * kBlock], R[4 * kBlock],
@@ -1366,10 +1367,13 @@ __global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
   while (__ballot(k < end) != 0) {
     const bool has = k < end;
     const uint64_t idx = has ? (p.perm ? (uint64_t)p.perm[k] : k) : 0;
-    const uint8_t *rec = p.recs + idx * p.rec_size;
-    const int64_t nr = has ? *(const int64_t *)(rec + 8) : 0;
-    const int64_t ret = has && p.rec_size >= 96 ? *(const int64_t *)(rec + 80) : 0;
-    const uint64_t pid = has && p.rec_size >= 96 ? *(const uint64_t *)(rec + 88) : p.pid_tgid;
+    const SysLayout &L = p.lay;
+    const uint8_t *ent = L.enter ? L.enter + idx * L.estride : nullptr;
+    const uint8_t *ext = L.exit ? L.exit + idx * L.xstride : nullptr;
+    const uint8_t *clk = L.clock ? L.clock + idx * L.cstride : nullptr;
+    const int64_t nr = has ? *(const int64_t *)((ent ? ent : ext) + 8) : 0;
+    const int64_t ret = has && ext ? *(const int64_t *)(ext + 16) : 0;
+    const uint64_t pid = has && L.pid ? *(const uint64_t *)(L.pid + idx * L.pstride) : p.pid_tgid;
     const bool live = has && nr != 60 && nr != 231;  // :23-26
     ovr_st[tid] = 0;
     ovr_v[tid] = 0;
@@ -1385,7 +1389,7 @@ __global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
         ctx[0] = 0;
         ctx[1] = (uint64_t)nr;
         if (enter) {
-          for (int w = 2; w < 8; w++) ctx[w] = *(const uint64_t *)(rec + 8 * w);
+          for (int w = 2; w < 8; w++) ctx[w] = ent ? *(const uint64_t *)(ent + 8 * w) : 0;
         } else {
           ctx[2] = (uint64_t)ret;
           for (int w = 3; w < 8; w++) ctx[w] = 0;
@@ -1433,8 +1437,8 @@ __global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
           env.ovr_val = &ovr_v[tid];
           env.ovr_bit = enter ? 1 : 2;
           env.pid_tgid = pid;
-          env.kt_on = p.rec_size == 128;
-          env.ktime = p.rec_size == 128 ? *(const uint64_t *)(rec + (enter ? 96 : 104)) : 0;
+          env.kt_on = clk != nullptr;
+          env.ktime = clk ? *(const uint64_t *)(clk + (enter ? 0 : 8)) : 0;
           uint32_t cerr = E_OK;
           uint64_t *R = c.R;
           const uint32_t cid = __builtin_amdgcn_readfirstlane(c.call_id);
