@@ -3,7 +3,7 @@ size, device-resident, one GPU:
 
   python bench.py --workload flow-hash     # 2^24 frames in 2048-B slots, HASH map
   python bench.py --workload syscall-agg   # 2^25 trace_event_raw_sys_enter records
-  python bench.py --workload syscount      # 2^25 96-B records, sys_exit through the dispatch
+  python bench.py --workload syscount      # 2^25 32-B exit records (SoA), sys_exit through the dispatch
 
 The headline line (xdp-counter) stays in bench.py.  Inputs are generated on
 the device by csrc/gen.hip from the same seeded streams as bpftime_amd/gen.py;
@@ -231,8 +231,12 @@ def syscall_agg(args, dev, gen, isa, programs):
 def syscount(args, dev, gen, isa, programs):
     """syscount's sys_exit program (example/tracing/syscount/syscount.bpf.c:
     49-87) attached to raw_syscalls:sys_exit, replayed through the dispatch
-    (bpftime_amd_syscall_dispatch_records) over 2^25 device-resident 96-B
-    records (enter ctx, trace_event_raw_sys_exit, caller pid_tgid)."""
+    over 2^25 device-resident calls in struct-of-arrays form
+    (bpftime_amd_syscall_dispatch_soa): the exit array only, 32 B per call
+    {trace_event_raw_sys_exit, caller pid_tgid} -- an exit-only dispatch
+    streams what its program reads (BPFTIME_AMD_SYSCOUNT_AOS=1: the 96-B
+    records through bpftime_amd_syscall_dispatch_records instead, same
+    calls)."""
     n = 1 << (args.log2n if args.log2n_set else 25)
     dev.reset_runtime()
     data = dev.Map(isa.BPF_MAP_TYPE_HASH, 4, 32, 8192, name="data")
@@ -243,12 +247,18 @@ def syscount(args, dev, gen, isa, programs):
     dev.syscall_attach(pfd, -1, enter=False)
     cdf = gen.zipf_cdf(335, 1.2)
     dcdf = dev.DeviceBuffer.from_array(cdf)
-    recs = dev.DeviceBuffer(n * 96)
-    if dev.lib().bpftime_amd_gen_syscall_full(recs.ptr, n, gen.SEED_CFG5, 0, dcdf.ptr, 335, None):
+    aos = os.environ.get("BPFTIME_AMD_SYSCOUNT_AOS") == "1"
+    recs = dev.DeviceBuffer(n * (96 if aos else 32))
+    rc = (dev.lib().bpftime_amd_gen_syscall_full(recs.ptr, n, gen.SEED_CFG5, 0, dcdf.ptr, 335, None) if aos else
+          dev.lib().bpftime_amd_gen_syscall_soa(None, recs.ptr, n, gen.SEED_CFG5, 0, dcdf.ptr, 335, None))
+    if rc:
         raise SystemExit("syscall generator failed")
 
     def step():
-        dev.syscall_dispatch(recs, n, flags=0)
+        if aos:
+            dev.syscall_dispatch(recs, n, flags=0)
+        else:
+            dev.syscall_dispatch_soa(recs, n, flags=0)
 
     wall, kern_s = _timed(dev, step, args.steps, args.warmup)
     runs = args.steps + args.warmup
@@ -277,10 +287,13 @@ def syscount(args, dev, gen, isa, programs):
         "value": round(value, 3), "unit": "Mrec/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "int64",
-        "data": "synthetic (seeded splitmix64 96-B records: id Zipf(1.2) over 0..334 + 1% exit/exit_group + "
+        "data": "synthetic (seeded splitmix64 replay records: id Zipf(1.2) over 0..334 + 1% exit/exit_group + "
                 "0.5% id -1, 20% negative rets, 64 callers; seed 0x5EED0005)",
         "config": {"workload": "syscount sys_exit (BASELINE configs[4]'s attach point) over 2^%d device-resident "
-                               "96-B records, HASH map max 8192" % int(np.log2(n)), "records": n},
+                               "calls, %s, HASH map max 8192"
+                               % (int(np.log2(n)), "96-B records" if aos else
+                                  "struct-of-arrays exit records (32 B: trace_event_raw_sys_exit + caller)"),
+                   "records": n, "layout": "aos96" if aos else "soa"},
         "parity": {"per_id_totals_exact": ok_map, "keys": len(got), "ok": ok_map},
         **_dbg_lcache(dev),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -38,7 +38,12 @@ class EbpfBatch(C.Structure):  # include/ebpf-vm.h struct ebpf_batch
                 ("first_unit", C.c_uint64), ("stream", C.c_void_p), ("descs", C.c_void_p),
                 ("umem_bytes", C.c_uint64), ("sys_nr", C.c_int64), ("sys_state", C.c_void_p),
                 ("sys_ret", C.c_void_p), ("sys_phase", C.c_uint32), ("pid_tgid_off", C.c_int32),
-                ("ktime_off", C.c_int32)]
+                ("ktime_off", C.c_int32), ("pid_tgid_arr", C.c_void_p), ("pid_tgid_stride", C.c_uint64),
+                ("ktime_arr", C.c_void_p), ("ktime_stride", C.c_uint64)]
+
+
+class SysRecords(C.Structure):  # include/bpftime_amd.h struct bpftime_amd_sys_records
+    _fields_ = [("enter", C.c_void_p), ("exit", C.c_void_p), ("clock", C.c_void_p), ("count", C.c_uint64)]
 
 
 class PerfEvent(C.Structure):
@@ -129,6 +134,7 @@ SIGNATURES = [
     ("bpftime_amd_syscall_dispatch_records", C.c_int64, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p,
                                                          C.c_uint32, C.c_void_p]),
     ("bpftime_amd_syscall_dispatch_plan", C.c_int, [C.c_uint32]),
+    ("bpftime_amd_syscall_dispatch_soa", C.c_int64, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
     ("bpftime_amd_handle_sysbpf", C.c_long, [C.c_int, C.c_void_p, C.c_uint32]),
     ("bpftime_map_get_info", C.c_int, [C.c_int, C.POINTER(BpfMapAttr), C.POINTER(C.c_char_p),
                                         C.POINTER(C.c_int)]),
@@ -185,6 +191,8 @@ SIGNATURES = [
     ("bpftime_amd_last_error", C.c_char_p, []),
     ("bpftime_amd_gen_syscall_full", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p,
                                                 C.c_uint32, C.c_void_p]),
+    ("bpftime_amd_gen_syscall_soa", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64,
+                                              C.c_void_p, C.c_uint32, C.c_void_p]),
     ("bpftime_amd_static_lds", C.c_size_t, [C.c_uint32, C.c_bool, C.c_bool, C.c_uint32]),
     ("bpftime_amd_lds_bytes", C.c_size_t, [C.c_uint32, C.c_bool, C.c_uint32, C.c_uint32, C.c_uint32, C.c_bool,
                                            C.c_bool, C.c_uint32]),

@@ -310,9 +310,31 @@ struct KParams {
   // syscalls), or (0) the launching thread's value
   int32_t pid_off;
   uint64_t pid_tgid;
-  // bpf_ktime_get_ns: a u64 at this offset from the unit (the recorded clock
-  // of a syscall replay), or (0) the device clock
-  int32_t kt_off;
+  // the C++ tier's view of both (include/ebpf-vm.h): unit i's recorded
+  // caller at pid_base + i * pid_stride (pid_base null: the launching
+  // thread's), its recorded clock at kt_base + i * kt_stride (null: the
+  // device clock) -- offsets from the unit and struct-of-arrays alike
+  const uint8_t *pid_base;
+  uint64_t pid_stride;
+  const uint8_t *kt_base;
+  uint64_t kt_stride;
+};
+
+// Where a syscall replay's fields live (include/bpftime_amd.h): record i's
+// enter ctx (64 B) at enter + i * estride (null: no enter ctx, the id comes
+// from the exit ctx), its exit ctx (24 B) at exit + i * xstride (null: 64-B
+// enter records, which hold no ret), its caller's pid_tgid at pid + i *
+// pstride (null: the dispatching thread's), its clocks {enter ns, exit ns}
+// at clock + i * cstride (null: the device clock)
+struct SysLayout {
+  const uint8_t *enter;
+  uint64_t estride;
+  const uint8_t *exit;
+  uint64_t xstride;
+  const uint8_t *pid;
+  uint64_t pstride;
+  const uint8_t *clock;
+  uint64_t cstride;
 };
 
 // Thread-ordered syscall dispatch (interp.hip k_sys_seq, syscall_dispatch.cpp):
@@ -332,8 +354,9 @@ static_assert(sizeof(SeqProg) == 32, "SeqProg is read with scalar loads");
 constexpr uint32_t kSeqMaxProgs = 64;  // attached programs a thread-ordered dispatch runs (kernel arguments)
 struct SeqParams {
   uint32_t nprogs;
-  uint32_t rec_size;      // 64, 96 or 128 (include/bpftime_amd.h)
-  const uint8_t *recs;
+  // the records' fields (include/bpftime_amd.h: 64- / 96- / 128-B records or
+  // struct-of-arrays), record i's at base + i * stride:
+  SysLayout lay;
   uint64_t n;
   // thread t's records: perm[seg[t] .. seg[t + 1]) (record indexes in record
   // order); null perm: the identity; null seg: one thread over [0, n)

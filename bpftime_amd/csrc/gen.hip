@@ -102,8 +102,12 @@ __global__ void k_gen_syscall(uint8_t *base, uint64_t n, uint64_t seed, uint64_t
 // interrupt marker syscount skips), then trace_event_raw_sys_exit {0, id,
 // ret}: ret a negative errno in [-133, -1] for 20 % of the records, else in
 // [0, 65535]; then the caller's pid_tgid: tgid 1000 + [0, 64), tid tgid + [0, 4)
-__global__ void k_gen_syscall_full(uint8_t *base, uint64_t n, uint64_t seed, uint64_t first, const double *cdf,
-                                   uint32_t support) {
+// Words 0-7 (the enter ctx) go to enter + unit * estride (enter null: not
+// written), words 8-11 (exit ctx, pid_tgid) to exit + unit * xstride: the
+// 96-B records (enter = base, exit = base + 64, strides 96) or the
+// struct-of-arrays form (strides 64 and 32).
+__global__ void k_gen_syscall_full(uint8_t *enter, uint64_t estride, uint8_t *exit, uint64_t xstride, uint64_t n,
+                                   uint64_t seed, uint64_t first, const double *cdf, uint32_t support) {
   for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n * 12;
        w += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t unit = w / 12, j = w % 12, g = first + unit;
@@ -121,7 +125,10 @@ __global__ void k_gen_syscall_full(uint8_t *base, uint64_t n, uint64_t seed, uin
       const uint64_t r = sm64(seed ^ 0x8888, g), tgid = 1000 + r % 64;
       v = (tgid << 32) | (tgid + (r >> 8) % 4);
     }
-    *(uint64_t *)(base + unit * 96 + j * 8) = v;
+    if (j >= 8)
+      *(uint64_t *)(exit + unit * xstride + (j - 8) * 8) = v;
+    else if (enter)
+      *(uint64_t *)(enter + unit * estride + j * 8) = v;
   }
 }
 
@@ -155,7 +162,16 @@ extern "C" int bpftime_amd_gen_syscall_full(void *dev, uint64_t n, uint64_t seed
   if (!cdf || !support) return -1;
   if (!n) return 0;
   hipLaunchKernelGGL(bpftime_amd::k_gen_syscall_full, dim3(gen_blocks(n * 12)), dim3(256), 0, (hipStream_t)stream,
-                     (uint8_t *)dev, n, seed, first, cdf, support);
+                     (uint8_t *)dev, 96, (uint8_t *)dev + 64, 96, n, seed, first, cdf, support);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int bpftime_amd_gen_syscall_soa(void *enter, void *exit, uint64_t n, uint64_t seed, uint64_t first,
+                                           const double *cdf, uint32_t support, void *stream) {
+  if (!cdf || !support || !exit) return -1;
+  if (!n) return 0;
+  hipLaunchKernelGGL(bpftime_amd::k_gen_syscall_full, dim3(gen_blocks(n * 12)), dim3(256), 0, (hipStream_t)stream,
+                     (uint8_t *)enter, 64, (uint8_t *)exit, 32, n, seed, first, cdf, support);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -2,7 +2,8 @@
 // (common.hpp SeqParams, interp.hip k_sys_seq).
 //
 // A replay record names its calling thread (96- / 128-B records: the u64
-// pid_tgid at +88, include/bpftime_amd.h); the reference runs a thread's
+// pid_tgid at +88; struct-of-arrays records: in the exit array,
+// include/bpftime_amd.h); the reference runs a thread's
 // calls one after another on that thread (syscall_trace_attach_impl.cpp:
 // 18-95 runs on the caller).  Grouping = a stable radix sort of (pid_tgid,
 // record index) pairs: thread t's records are perm[seg[t] .. seg[t + 1]) in
@@ -18,10 +19,10 @@
 
 namespace {
 
-__global__ void k_group_keys(const uint8_t *recs, uint64_t n, uint32_t rec_size, uint64_t *keys, uint32_t *idx) {
+__global__ void k_group_keys(const uint8_t *pid, uint64_t n, uint64_t stride, uint64_t *keys, uint32_t *idx) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  keys[i] = *(const uint64_t *)(recs + i * rec_size + 88);
+  keys[i] = *(const uint64_t *)(pid + i * stride);
   idx[i] = (uint32_t)i;
 }
 
@@ -71,14 +72,14 @@ extern "C" size_t bpftime_amd_group_scratch_bytes(uint64_t n) {
   return l.total;
 }
 
-// Groups n records (rec_size >= 96) by their pid_tgid into `scratch`
-// (bpftime_amd_group_scratch_bytes(n) bytes): *perm / *seg point into it;
-// *nseg = the thread count (a synchronous read of the selected count).
-extern "C" hipError_t bpftime_amd_group_threads(const void *recs, uint64_t n, uint32_t rec_size, void *scratch,
+// Groups n records by their pid_tgid (record i's at pid + i * stride) into
+// `scratch` (bpftime_amd_group_scratch_bytes(n) bytes): *perm / *seg point
+// into it; *nseg = the thread count (a synchronous read of the selected count).
+extern "C" hipError_t bpftime_amd_group_threads(const void *pid, uint64_t stride, uint64_t n, void *scratch,
                                                 uint32_t **perm, uint32_t **seg, uint64_t *nseg,
                                                 hipStream_t stream) {
   Layout l;
-  if (n == 0 || n > 0xffffffffull || rec_size < 96) return hipErrorInvalidValue;
+  if (n == 0 || n > 0xffffffffull || !pid || stride % 8) return hipErrorInvalidValue;
   hipError_t e = layout(n, l);
   if (e != hipSuccess) return e;
   uint8_t *b = (uint8_t *)scratch;
@@ -87,7 +88,7 @@ extern "C" hipError_t bpftime_amd_group_threads(const void *recs, uint64_t n, ui
   uint32_t *nsel = (uint32_t *)(b + l.nsel);
   uint8_t *flags = b + l.flags;
   const uint32_t grid = (uint32_t)((n + 255) / 256);
-  hipLaunchKernelGGL(k_group_keys, dim3(grid), dim3(256), 0, stream, (const uint8_t *)recs, n, rec_size, keys_in,
+  hipLaunchKernelGGL(k_group_keys, dim3(grid), dim3(256), 0, stream, (const uint8_t *)pid, n, stride, keys_in,
                      idx_in);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   size_t tb = l.temp_bytes;

@@ -160,7 +160,7 @@ void syscall_detach_all();
 int vm_map_effects(const ::ebpf_vm *vm, std::map<int32_t, uint8_t> &fx, uint8_t &any);
 // The thread-ordered syscall dispatch's launch (interp.hip k_sys_seq):
 // `progs` in the reference's order (syscall_dispatch.cpp), over n device
-// records of rec_size bytes; thread t's records perm[seg[t] .. seg[t + 1])
+// records laid out as `lay`; thread t's records perm[seg[t] .. seg[t + 1])
 // (null perm / seg: one thread over every record in record order).  `err`: a
 // device u32 (failed callbacks).  Returns the failed-callback count with
 // EBPF_BATCH_SYNC, else 0; -1 on errors (set_error).
@@ -169,8 +169,7 @@ struct SeqAttach {
   int64_t sys_nr;
   bool enter;
 };
-int64_t seq_dispatch(const std::vector<SeqAttach> &progs, const void *recs, uint64_t n, uint32_t rec_size,
-                     const uint32_t *perm, const uint32_t *seg, uint64_t nseg, int64_t *out, uint32_t flags,
-                     uint32_t *err, hipStream_t s);
+int64_t seq_dispatch(const std::vector<SeqAttach> &progs, const SysLayout &lay, uint64_t n, const uint32_t *perm,
+                     const uint32_t *seg, uint64_t nseg, int64_t *out, uint32_t flags, uint32_t *err, hipStream_t s);
 
 }  // namespace bpftime_amd

@@ -50,12 +50,14 @@
 #include "../../include/ebpf-vm.h"
 #include "runtime.hpp"
 
-extern "C" hipError_t bpftime_amd_launch_sys_init(const void *records, uint64_t n, uint32_t record_size,
+extern "C" hipError_t bpftime_amd_launch_sys_init(const void *exits, uint64_t n, uint64_t xstride,
                                                   int64_t *out, uint32_t *state, hipStream_t stream);
 extern "C" size_t bpftime_amd_group_scratch_bytes(uint64_t n);
-extern "C" hipError_t bpftime_amd_group_threads(const void *recs, uint64_t n, uint32_t rec_size, void *scratch,
+extern "C" hipError_t bpftime_amd_group_threads(const void *pid, uint64_t stride, uint64_t n, void *scratch,
                                                 uint32_t **perm, uint32_t **seg, uint64_t *nseg,
                                                 hipStream_t stream);
+
+using bpftime_amd::SysLayout;
 
 namespace {
 
@@ -175,30 +177,41 @@ int plan_for(const std::vector<Attach> &order, uint32_t flags) {
   return c;
 }
 
-int64_t dispatch_threads(const std::vector<Attach> &order, const uint8_t *records, uint64_t n, uint32_t record_size,
-                         int64_t *out_rets, uint32_t flags, hipStream_t s) {
+// The records of a dispatch: their field layout (common.hpp SysLayout) and,
+// per phase, the block a program's ctx lies in -- what a program that may
+// store into its ctx gets a copy of (AoS: the whole records; SoA: the
+// phase's array) and the ctx's offset in it
+struct Records {
+  SysLayout lay;
+  uint64_t n;
+  const uint8_t *block[2];  // [0] enter, [1] exit
+  uint64_t block_bytes[2];
+  uint32_t ctx_off[2];
+};
+
+int64_t dispatch_threads(const std::vector<Attach> &order, const Records &r, int64_t *out_rets, uint32_t flags,
+                         hipStream_t s) {
   std::vector<bpftime_amd::SeqAttach> progs;
   for (const Attach &a : order) progs.push_back({a.vm.get(), a.sys_nr, a.enter});
-  // one thread: an ORDERED dispatch (the serial reference run) or 64-B
-  // records (no recorded caller: every call is the dispatching thread's)
-  const bool one = (flags & EBPF_BATCH_ORDERED) || record_size < 96;
-  const uint64_t gbytes = one ? 0 : bpftime_amd_group_scratch_bytes(n);
-  if (!one && !gbytes) return fail("thread grouping of " + std::to_string(n) + " records", EINVAL);
+  // one thread: an ORDERED dispatch (the serial reference run) or records
+  // without a recorded caller (every call is the dispatching thread's)
+  const bool one = (flags & EBPF_BATCH_ORDERED) || !r.lay.pid;
+  const uint64_t gbytes = one ? 0 : bpftime_amd_group_scratch_bytes(r.n);
+  if (!one && !gbytes) return fail("thread grouping of " + std::to_string(r.n) + " records", EINVAL);
   uint8_t *buf = scratch(s, 256 + gbytes);
   if (!buf) return fail("scratch allocation failed", ENOMEM);
   uint32_t *perm = nullptr, *seg = nullptr;
   uint64_t nseg = 1;
   if (!one) {
-    const hipError_t e = bpftime_amd_group_threads(records, n, record_size, buf + 256, &perm, &seg, &nseg, s);
+    const hipError_t e = bpftime_amd_group_threads(r.lay.pid, r.lay.pstride, r.n, buf + 256, &perm, &seg, &nseg, s);
     if (e != hipSuccess) return fail(std::string("thread grouping: ") + hipGetErrorString(e), EIO);
   }
-  const int64_t rc = bpftime_amd::seq_dispatch(progs, records, n, record_size, perm, seg, nseg, out_rets, flags,
-                                               (uint32_t *)buf, s);
-  return rc;
+  return bpftime_amd::seq_dispatch(progs, r.lay, r.n, perm, seg, nseg, out_rets, flags, (uint32_t *)buf, s);
 }
 
-int64_t dispatch_programs(const std::vector<Attach> &order, const uint8_t *records, uint64_t n,
-                          uint32_t record_size, int64_t *out_rets, uint32_t flags, hipStream_t s) {
+int64_t dispatch_programs(const std::vector<Attach> &order, const Records &r, int64_t *out_rets, uint32_t flags,
+                          hipStream_t s) {
+  const uint64_t n = r.n;
   bool enter_ovr = false, any_ovr = false, copies = false;
   for (const Attach &a : order) {
     enter_ovr |= a.enter && (a.flags & bpftime_amd::kProgSetsRetval);
@@ -208,40 +221,55 @@ int64_t dispatch_programs(const std::vector<Attach> &order, const uint8_t *recor
   // scratch: per-record override state, then (programs that may store into
   // their ctx) a copy of the records
   const bool state = out_rets || any_ovr;
-  const uint64_t sbytes = state ? (4 * n + 255) & ~255ull : 0, rbytes = n * record_size;
+  const uint64_t sbytes = state ? (4 * n + 255) & ~255ull : 0;
+  const uint64_t cbytes = copies ? std::max(r.block_bytes[0], r.block_bytes[1]) : 0;
   uint8_t *buf = nullptr;
   if (state || copies) {
-    buf = scratch(s, sbytes + (copies ? rbytes : 0));
+    buf = scratch(s, sbytes + cbytes);
     if (!buf) return fail("scratch allocation failed", ENOMEM);
   }
   uint32_t *st = state ? (uint32_t *)buf : nullptr;
   uint8_t *copy = copies ? buf + sbytes : nullptr;
   if (state) {
-    // out_rets[i] = the recorded ret (96- / 128-B records) or 0; state[i] = 0
-    const hipError_t e = bpftime_amd_launch_sys_init(records, n, record_size, out_rets, st, s);
+    // out_rets[i] = the recorded ret (or 0 without exit ctxs); state[i] = 0
+    const hipError_t e = bpftime_amd_launch_sys_init(r.lay.exit, n, r.lay.xstride, out_rets, st, s);
     if (e != hipSuccess) return fail(std::string("state init: ") + hipGetErrorString(e), EIO);
   }
+  // a field inside the unit's own record (AoS) is an offset from the unit
+  // (the asm tier reads bpf_get_current_pid_tgid's there); else an array
+  auto field = [](const uint8_t *f, uint64_t fs, const uint8_t *unit, uint64_t us, int32_t &off, const void *&arr,
+                  uint64_t &stride) {
+    if (!f) return;
+    if (fs == us && f >= unit && f + 8 <= unit + us) {
+      off = (int32_t)(f - unit);
+    } else {
+      arr = f;
+      stride = fs;
+    }
+  };
   int64_t failed = 0;
   for (const Attach &a : order) {
-    const uint8_t *base = records;
+    const int ph = a.enter ? 0 : 1;
+    const uint8_t *unit = r.block[ph] + r.ctx_off[ph];
+    const uint64_t ustride = a.enter ? r.lay.estride : r.lay.xstride;
+    struct ebpf_batch b = {};
+    // pid / clock addressed against the records the program reads
+    field(r.lay.pid, r.lay.pstride, unit, ustride, b.pid_tgid_off, b.pid_tgid_arr, b.pid_tgid_stride);
+    field(r.lay.clock ? r.lay.clock + (a.enter ? 0 : 8) : nullptr, r.lay.cstride, unit, ustride, b.ktime_off,
+          b.ktime_arr, b.ktime_stride);
     if (a.flags & bpftime_amd::kProgStoresCtx) {
       // each reference callback runs on its own ctx copy (:43-45)
-      const hipError_t e = hipMemcpyAsync(copy, records, rbytes, hipMemcpyDeviceToDevice, s);
+      const hipError_t e = hipMemcpyAsync(copy, r.block[ph], r.block_bytes[ph], hipMemcpyDeviceToDevice, s);
       if (e != hipSuccess) return fail(std::string("record copy: ") + hipGetErrorString(e), EIO);
-      base = copy;
+      unit = copy + r.ctx_off[ph];
     }
-    struct ebpf_batch b = {};
     b.ctx_kind = a.enter ? EBPF_CTX_SYSCALL : EBPF_CTX_SYSCALL_EXIT;
     b.flags = (flags & (EBPF_BATCH_SYNC | EBPF_BATCH_UNCHECKED)) | (a.sys_nr >= 0 ? EBPF_BATCH_SYS_NR : 0u);
     b.count = n;
-    b.data = const_cast<uint8_t *>(base + (a.enter ? 0 : 64));
-    b.stride = record_size;
+    b.data = const_cast<uint8_t *>(unit);
+    b.stride = ustride;
     b.sys_nr = a.sys_nr;
     b.stream = s;
-    // (96- / 128-B records: the recorded caller's pid_tgid at +88; 128-B: the
-    // recorded clocks at +96 / +104)
-    if (record_size >= BPFTIME_AMD_SYSCALL_RECORD_FULL) b.pid_tgid_off = a.enter ? 88 : 24;
-    if (record_size == BPFTIME_AMD_SYSCALL_RECORD_TIMED) b.ktime_off = a.enter ? 96 : 40;
     // the state where this program sets it, or (exit programs) where an
     // enter program may have overridden the record's return
     const bool sets = (a.flags & bpftime_amd::kProgSetsRetval) != 0;
@@ -255,6 +283,32 @@ int64_t dispatch_programs(const std::vector<Attach> &order, const uint8_t *recor
     failed += rc;
   }
   return failed;
+}
+
+int64_t dispatch(const Records &r, int64_t *out_rets, uint32_t flags, void *stream) {
+  const std::vector<Attach> order = ordered_attachments();
+  bool enters = false, exits = false;
+  for (const Attach &a : order) {
+    exits |= !a.enter;
+    enters |= a.enter;
+  }
+  if (exits && !r.lay.exit)
+    return fail("sys_exit programs are attached: the records need the 96-B form (enter + exit ctx)", EINVAL);
+  if (enters && !r.lay.enter) return fail("sys_enter programs are attached: the records need enter ctxs", EINVAL);
+  const int plan = plan_for(order, flags);
+  if (plan < 0) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  if (r.n == 0) return 0;
+  if (order.empty()) {
+    if (out_rets) {  // nothing attached: every call returns its recorded ret
+      const hipError_t e = bpftime_amd_launch_sys_init(r.lay.exit, r.n, r.lay.xstride, out_rets, nullptr, s);
+      if (e != hipSuccess) return fail(std::string("state init: ") + hipGetErrorString(e), EIO);
+    }
+    return 0;
+  }
+  const std::shared_ptr<std::mutex> mu = stream_lock(s);
+  std::lock_guard<std::mutex> hold(*mu);
+  return plan ? dispatch_threads(order, r, out_rets, flags, s) : dispatch_programs(order, r, out_rets, flags, s);
 }
 
 }  // namespace
@@ -315,26 +369,45 @@ int64_t bpftime_amd_syscall_dispatch_records(const void *records, uint64_t n, ui
     return fail("record size " + std::to_string(record_size) + " (64, 96 or 128)", EINVAL);
   if (n && !records) return fail("no records", EINVAL);
   if (n > 0xffffffffull) return fail("more than 2^32 records", EINVAL);
-  const std::vector<Attach> order = ordered_attachments();
-  bool exits = false;
-  for (const Attach &a : order) exits |= !a.enter;
-  if (exits && record_size < BPFTIME_AMD_SYSCALL_RECORD_FULL)
-    return fail("sys_exit programs are attached: the records need the 96-B form (enter + exit ctx)", EINVAL);
-  const int plan = plan_for(order, flags);
-  if (plan < 0) return -1;
-  if (n == 0 || order.empty()) {
-    if (n && out_rets) {  // nothing attached: every call returns its recorded ret
-      hipStream_t s = (hipStream_t)stream;
-      const hipError_t e = bpftime_amd_launch_sys_init(records, n, record_size, out_rets, nullptr, s);
-      if (e != hipSuccess) return fail(std::string("state init: ") + hipGetErrorString(e), EIO);
-    }
-    return 0;
-  }
-  hipStream_t s = (hipStream_t)stream;
-  const std::shared_ptr<std::mutex> mu = stream_lock(s);
-  std::lock_guard<std::mutex> hold(*mu);
-  return plan ? dispatch_threads(order, (const uint8_t *)records, n, record_size, out_rets, flags, s)
-              : dispatch_programs(order, (const uint8_t *)records, n, record_size, out_rets, flags, s);
+  const uint8_t *b = (const uint8_t *)records;
+  const bool full = record_size >= BPFTIME_AMD_SYSCALL_RECORD_FULL;
+  Records r{};
+  r.n = n;
+  r.lay.enter = b;
+  r.lay.estride = r.lay.xstride = r.lay.pstride = r.lay.cstride = record_size;
+  r.lay.exit = full ? b + 64 : nullptr;
+  r.lay.pid = full ? b + 88 : nullptr;
+  r.lay.clock = record_size == BPFTIME_AMD_SYSCALL_RECORD_TIMED ? b + 96 : nullptr;
+  r.block[0] = r.block[1] = b;
+  r.block_bytes[0] = r.block_bytes[1] = n * record_size;
+  r.ctx_off[0] = 0;
+  r.ctx_off[1] = 64;
+  return dispatch(r, out_rets, flags, stream);
+}
+
+int64_t bpftime_amd_syscall_dispatch_soa(const struct bpftime_amd_sys_records *recs, int64_t *out_rets,
+                                         uint32_t flags, void *stream) {
+  if (!recs) return fail("no records", EINVAL);
+  const uint64_t n = recs->count;
+  if (n && !recs->exit) return fail("struct-of-arrays records need the exit array", EINVAL);
+  if (n > 0xffffffffull) return fail("more than 2^32 records", EINVAL);
+  for (const void *a : {recs->enter, recs->exit, recs->clock})
+    if ((uintptr_t)a % 8) return fail("struct-of-arrays records: arrays must be 8-aligned", EINVAL);
+  Records r{};
+  r.n = n;
+  r.lay.enter = (const uint8_t *)recs->enter;
+  r.lay.estride = 64;
+  r.lay.exit = (const uint8_t *)recs->exit;
+  r.lay.xstride = 32;
+  r.lay.pid = r.lay.exit ? r.lay.exit + 24 : nullptr;
+  r.lay.pstride = 32;
+  r.lay.clock = (const uint8_t *)recs->clock;
+  r.lay.cstride = 16;
+  r.block[0] = r.lay.enter;
+  r.block_bytes[0] = 64 * n;
+  r.block[1] = r.lay.exit;
+  r.block_bytes[1] = 32 * n;
+  return dispatch(r, out_rets, flags, stream);
 }
 
 int64_t bpftime_amd_syscall_dispatch(const void *records, uint64_t n, uint32_t flags, void *stream) {

@@ -468,16 +468,32 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
     error = "descriptor batches need an XDP / raw ctx and umem_bytes";
     return -1;
   }
-  // the recorded caller / clock offsets (include/ebpf-vm.h): syscall kinds
-  // only, 8-aligned, the u64 inside the unit (the kernel reads
-  // it for any nonzero value, in both tiers)
+  // the recorded caller / clock (include/ebpf-vm.h): syscall kinds only; an
+  // offset 8-aligned with the u64 inside the unit (the kernel
+  // reads it for any nonzero value, in both tiers), or an array with an
+  // 8-aligned stride, not both
   {
     const uint64_t extent = sys_exit && b->stride >= 96 ? b->stride - 64 : b->stride;
-    for (const auto &o : {std::make_pair("pid_tgid_off", b->pid_tgid_off), std::make_pair("ktime_off", b->ktime_off)}) {
-      if (!o.second) continue;
-      if (kind != CTX_SYSCALL || o.second < 0 || o.second % 8 != 0 || (uint64_t)o.second + 8 > extent) {
-        error = std::string(o.first) + " " + std::to_string(o.second) +
-                ": a syscall batch's u64 inside the unit (8-aligned, off + 8 <= " + std::to_string(extent) + ")";
+    struct R {
+      const char *name;
+      int32_t off;
+      const void *arr;
+      uint64_t stride;
+    };
+    for (const R &o : {R{"pid_tgid", b->pid_tgid_off, b->pid_tgid_arr, b->pid_tgid_stride},
+                       R{"ktime", b->ktime_off, b->ktime_arr, b->ktime_stride}}) {
+      if (!o.off && !o.arr) continue;
+      std::string bad;
+      if (kind != CTX_SYSCALL || b->descs)
+        bad = "a syscall batch only";
+      else if (o.off && o.arr)
+        bad = "an offset or an array, not both";
+      else if (o.off && (o.off < 0 || o.off % 8 != 0 || (uint64_t)o.off + 8 > extent))
+        bad = "the u64 inside the unit (8-aligned, off + 8 <= " + std::to_string(extent) + ")";
+      else if (o.arr && (o.stride == 0 || o.stride % 8 != 0 || (uintptr_t)o.arr % 8 != 0))
+        bad = "an 8-aligned array with a nonzero stride that is a multiple of 8";
+      if (!bad.empty()) {
+        error = std::string(o.name) + (o.arr ? "_arr" : "_off " + std::to_string(o.off)) + ": " + bad;
         return -1;
       }
     }
@@ -548,7 +564,20 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   p.sys_ret = b->sys_ret;
   p.sys_phase = b->sys_phase;
   p.pid_off = b->pid_tgid_off;
-  p.kt_off = b->ktime_off;
+  if (b->pid_tgid_off) {
+    p.pid_base = (const uint8_t *)b->data + b->pid_tgid_off;
+    p.pid_stride = b->stride;
+  } else if (b->pid_tgid_arr) {
+    p.pid_base = (const uint8_t *)b->pid_tgid_arr;
+    p.pid_stride = b->pid_tgid_stride;
+  }
+  if (b->ktime_off) {
+    p.kt_base = (const uint8_t *)b->data + b->ktime_off;
+    p.kt_stride = b->stride;
+  } else if (b->ktime_arr) {
+    p.kt_base = (const uint8_t *)b->ktime_arr;
+    p.kt_stride = b->ktime_stride;
+  }
   p.pid_tgid = ((uint64_t)(uint32_t)getpid() << 32) | (uint32_t)syscall(SYS_gettid);
   p.arena_lo = (uint64_t)(uintptr_t)r.arena;
   p.arena_hi = p.arena_lo + r.arena_size;
@@ -1098,9 +1127,8 @@ int vm_map_effects(const ::ebpf_vm *vm, std::map<int32_t, uint8_t> &fx, uint8_t 
 
 extern "C" hipError_t bpftime_amd_launch_sys_seq(const SeqParams *p, hipStream_t stream);
 
-int64_t seq_dispatch(const std::vector<SeqAttach> &progs, const void *recs, uint64_t n, uint32_t rec_size,
-                     const uint32_t *perm, const uint32_t *seg, uint64_t nseg, int64_t *out, uint32_t flags,
-                     uint32_t *err, hipStream_t s) {
+int64_t seq_dispatch(const std::vector<SeqAttach> &progs, const SysLayout &lay, uint64_t n, const uint32_t *perm,
+                     const uint32_t *seg, uint64_t nseg, int64_t *out, uint32_t flags, uint32_t *err, hipStream_t s) {
   auto fail = [](const std::string &e) {
     set_error("thread-ordered dispatch: " + e);
     return (int64_t)-1;
@@ -1142,8 +1170,7 @@ int64_t seq_dispatch(const std::vector<SeqAttach> &progs, const void *recs, uint
     steps = std::max(steps, vm->step_limit);
     keep.push_back(std::move(im));
   }
-  p.rec_size = rec_size;
-  p.recs = (const uint8_t *)recs;
+  p.lay = lay;
   p.n = n;
   p.perm = perm;
   p.seg = seg;

@@ -144,6 +144,17 @@ def syscall_records_timed(n: int, seed: int = SEED_CFG5, first: int = 0, threads
     return recs.view(np.uint8).reshape(n, 128)
 
 
+def syscall_records_soa(recs: np.ndarray):
+    """The struct-of-arrays form of 96- / 128-B replay records (include/
+    bpftime_amd.h struct bpftime_amd_sys_records): (enter n x 64 B, exit n x
+    32 B {exit ctx, pid_tgid}, clock n x 16 B or None)."""
+    n, rs = recs.shape
+    enter = np.ascontiguousarray(recs[:, :64])
+    exit_ = np.ascontiguousarray(recs[:, 64:96])
+    clock = np.ascontiguousarray(recs[:, 96:112]) if rs == 128 else None
+    return enter, exit_, clock
+
+
 # ---------------------------------------------------------------------------
 # config 1: 1k-packet pcap (990 x 64 B Eth/IPv4/UDP + 10 runts, seed 1)
 # ---------------------------------------------------------------------------

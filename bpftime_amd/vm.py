@@ -14,7 +14,7 @@ from typing import Optional
 import numpy as np
 
 from . import isa
-from ._lib import BpfLinkCreateArgs, BpfMapAttr, EbpfBatch, lib
+from ._lib import BpfLinkCreateArgs, BpfMapAttr, EbpfBatch, SysRecords, lib
 
 CTX_RAW, CTX_XDP, CTX_SYSCALL, CTX_SYSCALL_EXIT = 0, 1, 2, 3
 SYSCALL_RECORD, SYSCALL_RECORD_FULL, SYSCALL_RECORD_TIMED = 64, 96, 128  # include/bpftime_amd.h replay records
@@ -351,6 +351,21 @@ def syscall_dispatch(records: DeviceBuffer, n: int, record_size: int = SYSCALL_R
     programs' map effects, syscall_dispatch_plan)."""
     rc = lib().bpftime_amd_syscall_dispatch_records(records.ptr, n, record_size, out.ptr if out else None,
                                                      flags, stream or None)
+    if rc < 0:
+        raise EbpfError(f"syscall dispatch failed: {_err()}")
+    return rc
+
+
+def syscall_dispatch_soa(exit: Optional[DeviceBuffer], n: int, enter: Optional[DeviceBuffer] = None,
+                         clock: Optional[DeviceBuffer] = None, out: Optional[DeviceBuffer] = None,
+                         flags: int = BATCH_SYNC, stream: int = 0) -> int:
+    """dispatch_syscall over n recorded calls in struct-of-arrays form
+    (include/bpftime_amd.h struct bpftime_amd_sys_records): exit (n x 32 B
+    {exit ctx, pid_tgid}), enter (n x 64 B, optional), clock (n x 16 B,
+    optional)."""
+    r = SysRecords(enter=enter.ptr if enter else None, exit=exit.ptr if exit else None,
+                   clock=clock.ptr if clock else None, count=n)
+    rc = lib().bpftime_amd_syscall_dispatch_soa(C.byref(r), out.ptr if out else None, flags, stream or None)
     if rc < 0:
         raise EbpfError(f"syscall dispatch failed: {_err()}")
     return rc

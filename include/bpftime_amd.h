@@ -335,6 +335,26 @@ int64_t bpftime_amd_syscall_dispatch(const void *records, uint64_t n, uint32_t f
 int64_t bpftime_amd_syscall_dispatch_records(const void *records, uint64_t n, uint32_t record_size,
                                              int64_t *out_rets, uint32_t flags, void *stream);
 int bpftime_amd_syscall_dispatch_plan(uint32_t flags);
+/* Struct-of-arrays replay records: the same calls as the AoS forms, each
+ * field in its own device array, so a dispatch streams only what its
+ * programs read (an exit-only dispatch: 32 B per call instead of a 96-B
+ * record's three 128-B cache lines' worth).
+ *   enter: count x 64 B trace_event_raw_sys_enter {ent = 0, id, args} (NULL
+ *          when no sys_enter program is attached: the id comes from exit);
+ *   exit:  count x 32 B {trace_event_raw_sys_exit {ent = 0, id, ret} (24 B),
+ *          the caller's u64 pid_tgid};
+ *   clock: count x 16 B {u64 ns at sys_enter, u64 ns after the call} (the
+ *          replayed bpf_ktime_get_ns), or NULL (the device clock).
+ * The dispatch runs as bpftime_amd_syscall_dispatch_records over the
+ * equivalent 96- / 128-B records (same plans, results and errors). */
+struct bpftime_amd_sys_records {
+  const void *enter;
+  const void *exit;
+  const void *clock;
+  uint64_t count;
+};
+int64_t bpftime_amd_syscall_dispatch_soa(const struct bpftime_amd_sys_records *records, int64_t *out_rets,
+                                         uint32_t flags, void *stream);
 
 /* ---- attach plugins (attach/base_attach_impl/base_attach_impl.hpp:24-71,
  * attach/simple_attach_impl/simple_attach_impl.cpp:7-55; csrc/attach.cpp) ----
@@ -419,6 +439,10 @@ int bpftime_amd_gen_syscall(void *dev, uint64_t n, uint64_t seed, uint64_t first
  * (id -1 for 0.5 %), then the exit ctx {0, id, ret}, then a pid_tgid. */
 int bpftime_amd_gen_syscall_full(void *dev, uint64_t n, uint64_t seed, uint64_t first, const double *cdf,
                                  uint32_t support, void *stream);
+/* The same calls as struct-of-arrays records (bpftime_amd_syscall_dispatch_soa):
+ * enter (n x 64 B, may be NULL) and exit (n x 32 B {exit ctx, pid_tgid}). */
+int bpftime_amd_gen_syscall_soa(void *enter, void *exit, uint64_t n, uint64_t seed, uint64_t first,
+                                const double *cdf, uint32_t support, void *stream);
 /* Static LDS bytes of the interpreter kernel for a launch shape (its
  * attribute; the restated sum without a device): with the dynamic part
  * (common.hpp dyn_lds_for) what a block needs of the CU's 160 KiB. */

@@ -87,8 +87,9 @@ ebpf_jit_fn ebpf_load_aot_object(struct ebpf_vm *vm, const void *buf, size_t buf
 #define EBPF_CTX_SYSCALL 2 /* r1 = 64-B trace_event_raw_sys_enter; nr 60/231 skipped */
 /* r1 = 24-B trace_event_raw_sys_exit {ent = 0, id, ret} (syscall_trace_attach_impl.hpp:31-36,
  * built at syscall_trace_attach_impl.cpp:80-85), r2 = 24; nr 60/231 skipped.  The unit is the
- * exit half of a 96-B replay record (data = records + 64, stride 96) or any record with
- * that layout at `stride`. */
+ * exit half of a 96-B replay record (data = records + 64, stride 96), a 32-B
+ * struct-of-arrays exit record {ctx, pid_tgid} (stride 32), or any record with that
+ * layout at `stride`. */
 #define EBPF_CTX_SYSCALL_EXIT 3
 
 #define EBPF_BATCH_SYNC 0x1    /* wait for completion; return the failed-unit count */
@@ -147,6 +148,13 @@ struct ebpf_batch {
 	 * units with stride >= 96 are the tail of a record whose first 64 bytes are
 	 * the enter ctx: off + 8 <= stride - 64); else the batch fails (-1, named). */
 	int32_t ktime_off;
+	/* ... or, for struct-of-arrays replays, each in its own device array: unit
+	 * i's pid_tgid / clock is the u64 at arr + i * stride (non-NULL arrays take
+	 * the place of the offsets; syscall kinds only, stride a multiple of 8) */
+	const void *pid_tgid_arr;
+	uint64_t pid_tgid_stride;
+	const void *ktime_arr;
+	uint64_t ktime_stride;
 };
 
 /* linux/if_xdp.h struct xdp_desc */

@@ -297,3 +297,71 @@ def test_concurrent_dispatches_one_stream(fresh_oracle, fresh_runtime):
     assert not errs
     for recs, d, out in sets:
         assert (out.download(np.int64) == o.dispatch(recs)).all()
+
+
+# ---- struct-of-arrays records (include/bpftime_amd.h struct bpftime_amd_sys_records) ----
+
+def _soa_bufs(dev, recs, with_enter=True):
+    enter, exit_, clock = gen.syscall_records_soa(recs)
+    return (dev.DeviceBuffer.from_array(exit_), dev.DeviceBuffer.from_array(enter) if with_enter else None,
+            dev.DeviceBuffer.from_array(clock) if clock is not None else None)
+
+
+def test_soa_syscount_exit_only(fresh_oracle, fresh_runtime):
+    """syscount's sys_exit program over 32-B exit records (no enter array):
+    every data_t and every return as the oracle's run over the 96-B records;
+    the device generator writes the same arrays."""
+    po, dev = fresh_oracle, fresh_runtime
+    (odata, oro), (ddata, dro) = make_maps([(HASH, 4, 32, 8192), (ARRAY, 4, programs.SYSCOUNT_RODATA, 1)], po, dev)
+    ro = programs.syscount_rodata(filter_failed=True)
+    assert oro.update(b"\0" * 4, ro) == 0 and dro.update(b"\0" * 4, ro) == 0
+    o = po.OracleSyscallDispatch()
+    _attach(dev, o, programs.syscount_exit(ddata.fd, dro.fd), -1, False)
+    n = 1 << 21
+    recs = gen.syscall_records_full(n)
+    x, _, _ = _soa_bufs(dev, recs, with_enter=False)
+    out = dev.DeviceBuffer(8 * n)
+    assert dev.syscall_dispatch_soa(x, n, out=out) == 0
+    want = o.dispatch(recs)
+    assert (out.download(np.int64) == want).all()
+    assert ddata.hash_items() == odata.items()
+    # the device generator: the same calls, both layouts
+    from bpftime_amd import _lib
+    cdf = dev.DeviceBuffer.from_array(gen.zipf_cdf(335, 1.2))
+    e2, x2 = dev.DeviceBuffer(64 * n), dev.DeviceBuffer(32 * n)
+    assert _lib.lib().bpftime_amd_gen_syscall_soa(e2.ptr, x2.ptr, n, gen.SEED_CFG5, 0, cdf.ptr, 335, None) == 0
+    enter, exit_, _ = gen.syscall_records_soa(recs)
+    assert (x2.download().reshape(n, 32) == exit_).all() and (e2.download().reshape(n, 64) == enter).all()
+    # an enter program needs the enter array
+    _attach(dev, o, programs.inject_enter(3), 1, True)
+    with pytest.raises(dev.EbpfError, match="enter ctxs"):
+        dev.syscall_dispatch_soa(x, n)
+
+
+@pytest.mark.parametrize("plan", ["programs", "threads"])
+def test_soa_matches_aos(fresh_oracle, fresh_runtime, plan):
+    """Enter and exit programs reading the recorded caller and clock, with
+    overrides, over SoA records: the oracle's results over the 128-B
+    records, in both plans (pid / clock through the arrays in the enter
+    batches, at an offset of the 32-B exit record in the exit batches)."""
+    po, dev = fresh_oracle, fresh_runtime
+    (ocnt,), (dcnt,) = make_maps([(ARRAY, 4, 64, 1)], po, dev)
+    pid_sum = lambda slot: (Asm().call(isa.BPF_FUNC_get_current_pid_tgid).ld_map_value(2, dcnt.fd, 8 * slot)
+                            .atomic(8, isa.ATOMIC_ADD, 2, 0, 0).mov64(0, 0).exit().assemble())
+    o = po.OracleSyscallDispatch()
+    for code, nr, enter in [(programs.inject_enter(3, -1), 1, True), (pid_sum(0), -1, True),
+                            (_ktime_sum(dcnt.fd, 1), 0, True), (pid_sum(2), -1, False),
+                            (_ktime_sum(dcnt.fd, 3), -1, False), (programs.exit_clamp(0), -1, False)]:
+        _attach(dev, o, code, nr, enter)
+    n = 1 << 19
+    recs = gen.syscall_records_timed(n, threads=512)
+    w = recs.view(np.int64).reshape(n, 16)
+    w[::7, 1] = w[::7, 9] = 1
+    x, e, c = _soa_bufs(dev, recs)
+    out = dev.DeviceBuffer(8 * n)
+    flags = dev.BATCH_SYNC | (dev.DISPATCH_PROGRAMS if plan == "programs" else dev.DISPATCH_THREADS)
+    assert dev.syscall_dispatch_soa(x, n, enter=e, clock=c, out=out, flags=flags) == 0
+    want = o.dispatch(recs)
+    assert (out.download(np.int64) == want).all()
+    assert dcnt.lookup(b"\0" * 4) == ocnt.lookup(b"\0" * 4)
+    assert all(struct.unpack("<8Q", ocnt.lookup(b"\0" * 4))[:4])
