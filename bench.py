@@ -28,7 +28,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log2n", type=int, default=None, help="units per GPU = 2^log2n (xdp-counter: 24)")
-    ap.add_argument("--workload", default="xdp-counter", choices=["xdp-counter", "flow-hash", "syscall-agg", "lpm-route", "ringbuf-sample", "tail-call", "syscount"],
+    ap.add_argument("--workload", default="xdp-counter", choices=["xdp-counter", "flow-hash", "syscall-agg", "lpm-route", "ringbuf-sample", "tail-call", "syscount",
+                             "syscount-latency"],
                     help="xdp-counter is the headline (BASELINE metric); the others are configs[2]/[4] "
                          "(bench_workloads.py)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0,

@@ -4,6 +4,7 @@ size, device-resident, one GPU:
   python bench.py --workload flow-hash     # 2^24 frames in 2048-B slots, HASH map
   python bench.py --workload syscall-agg   # 2^25 trace_event_raw_sys_enter records
   python bench.py --workload syscount      # 2^25 32-B exit records (SoA), sys_exit through the dispatch
+  python bench.py --workload syscount-latency  # syscount -L: enter + exit, thread-ordered dispatch
 
 The headline line (xdp-counter) stays in bench.py.  Inputs are generated on
 the device by csrc/gen.hip from the same seeded streams as bpftime_amd/gen.py;
@@ -505,11 +506,92 @@ def tail_call(args, dev, gen, isa, programs):
     }
 
 
+def syscount_latency(args, dev, gen, isa, programs):
+    """syscount -L: its sys_enter program (start[tid] = bpf_ktime_get_ns())
+    and its sys_exit program with measure_latency (lat = now - start[tid])
+    attached together (example/tracing/syscount/syscount.bpf.c:33-87).  The
+    exit program reads what the same call's enter program wrote, so the
+    dispatch runs thread-ordered (include/bpftime_amd.h "Order"): the records
+    grouped by their recorded caller, one lane per thread, each call's enter
+    and exit programs back to back; the clock is the recorded one.  Records:
+    2^22 struct-of-arrays calls (64-B enter, 32-B exit + caller, 16-B clocks)
+    from 4096 threads (BPFTIME_AMD_THREADS); the step is the whole dispatch
+    (grouping sort included).  Parity at full size: per-id count and
+    total_ns against the host recomputation (each call's exit - enter clock),
+    and every thread's start entry."""
+    n = 1 << (args.log2n if args.log2n_set else 22)
+    threads = int(os.environ.get("BPFTIME_AMD_THREADS", "4096"))
+    dev.reset_runtime()
+    start = dev.Map(isa.BPF_MAP_TYPE_HASH, 4, 8, max(10240, 2 * threads), name="start")
+    data = dev.Map(isa.BPF_MAP_TYPE_HASH, 4, 32, 10240, name="data")
+    ro = dev.Map(isa.BPF_MAP_TYPE_ARRAY, 4, programs.SYSCOUNT_RODATA, 1, name="syscount.rodata")
+    ro.update(b"\0" * 4, programs.syscount_rodata(measure_latency=True))
+    dev.syscall_attach(dev.prog_create(programs.syscount_enter(start.fd, ro.fd), "sys_enter", 5), -1, True)
+    dev.syscall_attach(dev.prog_create(programs.syscount_exit(data.fd, ro.fd, start.fd), "sys_exit", 5), -1, False)
+    plan = dev.syscall_dispatch_plan()
+    recs = gen.syscall_records_timed(n, threads=threads)
+    enter, exit_, clock = gen.syscall_records_soa(recs)
+    de, dx, dc = (dev.DeviceBuffer.from_array(a) for a in (enter, exit_, clock))
+
+    def step():
+        dev.syscall_dispatch_soa(dx, n, enter=de, clock=dc, flags=0)
+
+    wall, kern_s = _timed(dev, step, args.steps, args.warmup)
+    runs = args.steps + args.warmup
+    w = recs.view(np.int64).reshape(n, 16)
+    ids, rets = w[:, 1], w[:, 10]
+    live = ~np.isin(ids, [60, 231, -1])
+    lat = (w[:, 13] - w[:, 12]).astype(np.uint64)
+    cnt = np.bincount(ids[live], minlength=335).astype(np.uint64)
+    tot = np.zeros(335, dtype=np.uint64)
+    np.add.at(tot, ids[live], lat[live])
+    got = data.hash_items()
+    ok_map = len(got) == int((cnt > 0).sum()) and all(
+        struct.unpack("<QQ", got.get(struct.pack("<I", int(k)), b"\0" * 32)[:16]) ==
+        (int(cnt[k]) * runs, int(tot[k]) * runs % (1 << 64)) for k in np.nonzero(cnt)[0])
+    # start[tid] = the enter clock of each thread's last call (exit / exit_group run nothing)
+    ent = ~np.isin(ids, [60, 231])
+    tid = (w[:, 11] & 0xFFFFFFFF).astype(np.uint64)
+    last = {}
+    for t, c in zip(tid[ent].tolist(), w[ent, 12].tolist()):
+        last[t] = c
+    st = start.hash_items()
+    ok_start = len(st) == len(last) and all(struct.unpack("<Q", st[struct.pack("<I", t)])[0] == c
+                                            for t, c in last.items())
+    del rets
+    cpu = None
+    if not args.no_cpu_baseline:
+        from bench import cpu_baseline
+        cpu = cpu_baseline(args.cpu_seconds, "syscount-latency")
+    algo = 64.0 + 32.0 + 16.0  # per call: the enter ctx, the exit ctx + caller, the clocks
+    achieved = algo * n / kern_s / 1e9
+    return {
+        "metric": "device-resident Mrec/s, syscount -L (sys_enter + sys_exit, measure_latency) through the "
+                  "thread-ordered syscall dispatch",
+        "value": round(n * args.steps / wall / 1e6, 3), "unit": "Mrec/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic (seeded splitmix64 replay calls from %d threads, recorded clocks; seed 0x5EED0005)"
+                % threads,
+        "config": {"workload": "syscount -L over 2^%d device-resident calls (struct-of-arrays, 112 B per call), "
+                               "%d threads, thread-ordered dispatch" % (int(np.log2(n)), threads),
+                   "records": n, "threads": threads, "plan": "threads" if plan == 1 else "programs"},
+        "parity": {"per_id_count_and_latency_exact": ok_map, "start_per_thread_exact": ok_start,
+                   "ok": bool(ok_map and ok_start and plan == 1)},
+        "roofline": {"bound": "latency (one lane per thread: a thread's calls run in order)",
+                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "kernel_avg_ms": round(kern_s * 1e3, 4), "algo_bytes_per_rec": algo},
+        "cpu_baseline": cpu,
+    }
+
+
 def run(args):
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         raise SystemExit("--workload %s runs on one GPU (BASELINE configs[2]/[4])" % args.workload)
     from bpftime_amd import gen, isa, programs
     from bpftime_amd import vm as dev
     fn = {"flow-hash": flow_hash, "syscall-agg": syscall_agg, "lpm-route": lpm_route,
-          "ringbuf-sample": ringbuf_sample, "tail-call": tail_call, "syscount": syscount}[args.workload]
+          "ringbuf-sample": ringbuf_sample, "tail-call": tail_call, "syscount": syscount,
+          "syscount-latency": syscount_latency}[args.workload]
     print(json.dumps(fn(args, dev, gen, isa, programs)))

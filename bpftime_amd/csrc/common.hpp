@@ -318,6 +318,8 @@ struct KParams {
   uint64_t pid_stride;
   const uint8_t *kt_base;
   uint64_t kt_stride;
+  // per-lane LDS strides of the XDP ctx and the stack (lane_stride)
+  uint32_t ctx_stride, stack_stride;
 };
 
 // Where a syscall replay's fields live (include/bpftime_amd.h): record i's
@@ -404,6 +406,14 @@ BA_HD constexpr uint32_t wave_cache_entries(uint32_t block) { return (block / 64
 BA_HD constexpr uint32_t comb_tag_pos(uint32_t e, uint32_t entries) {
   return (e & 7) < 4 ? (e >> 3) * 4 + (e & 3) : entries / 2 + (e >> 3) * 4 + (e & 3);
 }
+// The delta granules after the tags, a row of 8 x 16 B per set padded to
+// kCombRowBytes: way k of set s starts at bank ((s * 36 + k * 4) mod 32), so
+// lanes adding to the first ways of different sets no longer queue on the
+// same banks (with 128-B rows every set's way 0 sat on banks 0-3: flow-hash
+// 9.6 conflict cycles per LDS instruction)
+constexpr uint32_t kCombRowBytes = 144;
+BA_HD constexpr size_t comb_bytes(uint32_t entries) { return 4 * (size_t)entries + (size_t)(entries / 8) * kCombRowBytes; }
+BA_HD constexpr uint32_t comb_granule_off(uint32_t e) { return (e >> 3) * kCombRowBytes + (e & 7) * 16; }
 constexpr uint32_t kMergeGroup = 16;
 constexpr uint32_t kMergeEntries = 4096;  // merge table entries (64 KiB of LDS)
 // (a combining-table entry flushes up to four counters: gen_fast.py comb_add)
@@ -423,7 +433,7 @@ constexpr size_t kCuLds = 160 * 1024;  // LDS per CU (gfx950)
 // Dynamic LDS of an interpreter block: the lanes' XDP ctx (48 B each), their
 // stacks (LDS-stack programs), 48 B of launch constants (interp.hip
 // tenv; the asm finds them 48 B before the combining table), the combining
-// table (a u32 tag + a 16-byte delta granule per entry).
+// table (a u32 tag per entry, then the delta rows: comb_bytes).
 // tenv: 8 u64 launch constants (tail calls, the register copy base, the
 // block's miss-log region and its capacity), then kMissParts u32 miss counters,
 // then the block's ring staging area (u64, 0 = none) and the LDS address of
@@ -445,12 +455,26 @@ BA_HD inline size_t lcache_bytes(uint32_t sets) { return (size_t)(32 + 8) * sets
 // ... and after the table, the LDS tail-call frames of an XDP image
 // (tail_lds: depths | words per frame << 8; [depth][word][lane] u64)
 BA_HD constexpr uint32_t tail_lds_lane_bytes(uint32_t tail_lds) { return (tail_lds & 0xff) * (tail_lds >> 8) * 8; }
+// Per-lane LDS areas (the XDP ctx, the stack) at a lane stride of 8 x an odd
+// number of bytes (BPFTIME_AMD_LANE_PAD=1; off by default, vm_api.cpp
+// lane_pad): the same offset in 16 lanes' areas then falls on 16 different
+// bank pairs (dword d of lane t at bank (stride / 4 * t + d) mod 32, stride
+// / 4 = 2 x odd), where a power-of-two stride puts every fourth lane on one
+// bank (flow-hash's 32-B stacks: 4-way conflicts on every stack access).
+// Host side; the kernel takes the strides from KParams.
+bool lane_pad();
+inline uint32_t lane_stride(uint32_t bytes) {
+  return !lane_pad() || ((bytes / 8) & 1) || bytes == 0 ? bytes : bytes + 8;
+}
+constexpr uint32_t kXdpCtxBytes = 48;  // xdp_md_userspace (runtime/extension/userspace_xdp.h:6-17)
+
 inline size_t dyn_lds_for(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
                           uint32_t lcache_sets = 0, bool ctx_lds = true, uint32_t block = kBlock,
                           uint32_t tail_lds = 0) {
-  return (size_t)block * ((kind == CTX_XDP && ctx_lds ? 48 : 0) + (big_stack ? 0 : stack_size) +
+  return (size_t)block * ((kind == CTX_XDP && ctx_lds ? lane_stride(kXdpCtxBytes) : 0) +
+                          (big_stack ? 0 : lane_stride(stack_size)) +
                           tail_lds_lane_bytes(tail_lds)) +
-         lcache_bytes(lcache_sets) + kTenvBytes + 20 * (size_t)comb_entries;
+         lcache_bytes(lcache_sets) + kTenvBytes + comb_bytes(comb_entries);
 }
 
 // Error codes recorded per unit (err_count counts units with any error)

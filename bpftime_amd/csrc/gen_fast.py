@@ -119,6 +119,7 @@ PIP = ["s86", "s87", "s93"]
 PM = ["s[88:89]", "s[90:91]", "s[94:95]"]
 KP = 3
 WAYS = 8  # combining-table associativity
+COMB_ROW = 144  # bytes per set of delta granules (common.hpp kCombRowBytes)
 MISS_PARTS = 256  # miss-log partitions (common.hpp kMissParts)
 RB_TENV = 64 + 4 * MISS_PARTS  # the block's ring staging slots in the launch constants (common.hpp kTenvRb)
 LF_TENV = RB_TENV + 16  # the LDS tail-call frames' offset and shape (common.hpp kTenvLf)
@@ -309,7 +310,9 @@ class Gen:
     def comb_add(self, sz, direct_only=False, pair=False):
         """Per-lane add of Y (v46, v[46:47] for 8 B) at the global address Z
         through the workgroup's LDS combining table (interp.hip: %[combn] u32
-        tags, then %[combn] 16-byte delta granules, flushed when the block
+        tags, then a row of eight 16-byte delta granules per set, padded to
+        COMB_ROW bytes so the sets' first ways spread over the banks
+        (common.hpp kCombRowBytes), flushed when the block
         ends; the tags of ways 0-3 of every set, [set][4], then those of ways
         4-7, so a set's first four tags are one 16-byte slot and sets spread
         over all sixteen slots of a bank row, common.hpp comb_tag_pos): Zipf-hot counters cost an LDS add instead of a same-address
@@ -364,7 +367,7 @@ class Gen:
                "v_lshrrev_b32 v41, 4, v54", "s_mov_b32 s69, 0x9e3779b1", "v_mul_lo_u32 v41, v41, s69",
                f"s_lshr_b32 s69, %[combn], {WAYS.bit_length() - 1}",             # sets (any count)
                "v_mul_hi_u32 v41, v41, s69",                                     # the set: multiply-shift
-               f"v_lshlrev_b32 v55, {WAYS.bit_length() - 1 + 4}, v41",           # its first way's delta
+               f"v_mul_u32_u24 v55, {COMB_ROW}, v41",                             # its first way's delta
                "v_lshlrev_b32 v41, 4, v41",
                "v_add_u32 v41, %[comb], v41",                                   # ways 0-3's tags
                "s_lshl_b32 s70, %[combn], 2", "s_add_u32 s70, s70, %[comb]",

@@ -602,7 +602,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   SRP(miss_log); SRP(miss_counts); SRV(miss_cap); SRP(tail_slots); SRV(full_q); SRV(full_r); SRV(step_cpu);
   SRP(sys_state); SRP(sys_ret); SRV(sys_phase); SRV(pid_tgid);
   p.pid_off = (int32_t)sreg((uint64_t)(uint32_t)pin.pid_off);
-  SRP(pid_base); SRV(pid_stride); SRP(kt_base); SRV(kt_stride);
+  SRP(pid_base); SRV(pid_stride); SRP(kt_base); SRV(kt_stride); SRV(ctx_stride); SRV(stack_stride);
   p.sys_nr = (int64_t)sreg((uint64_t)pin.sys_nr);
   p.unwind_idx = (int32_t)sreg((uint64_t)(uint32_t)pin.unwind_idx);
 #undef SRP
@@ -620,23 +620,25 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   // the lane's XDP ctx: in LDS, or (p.gctx: a program that only reads
   // data / data_end, whose ctx only the C++ tier touches) in global memory
   const uint32_t tid = threadIdx.x;
-  const uint32_t ctxb = KIND == CTX_XDP && !p.gctx ? 48 : 0;
+  // (lane strides: common.hpp lane_stride)
+  const uint32_t ctxb = KIND == CTX_XDP && !p.gctx ? p.ctx_stride : 0;
+  const uint32_t sstride = p.stack_stride;
   uint8_t *my_ctx = KIND == CTX_XDP && p.gctx ? p.gctx + ((uint64_t)blockIdx.x * BS + tid) * 48 : dyn + tid * ctxb;
-  uint8_t *my_stack = dyn + BS * ctxb + tid * p.stack_size;
+  uint8_t *my_stack = dyn + BS * ctxb + tid * sstride;
   // combining table for per-lane counter adds (gen_fast.py comb_add), after
   // the ctx and stack areas: comb_entries u32 tags {16-byte granule's arena
   // offset (8-byte aligned for 8-byte counters) | 2 | (4-byte ? 1 : 0)}
   // (8-way sets), then comb_entries 16-byte
   // delta granules (2 x u64 or 4 x u32), flushed when the block ends; sized 0
   // for programs that never need it
-  uint32_t *lcache = (uint32_t *)(dyn + BS * (ctxb + (BIGSTACK ? 0 : p.stack_size)));
+  uint32_t *lcache = (uint32_t *)(dyn + BS * (ctxb + (BIGSTACK ? 0 : sstride)));
   uint64_t *tenv = (uint64_t *)((uint8_t *)lcache + lcache_bytes(p.lcache));
   uint32_t *comb = (uint32_t *)((uint8_t *)tenv + kTenvBytes);
-  uint64_t *comb_d = (uint64_t *)(comb + p.comb_entries);
+  uint8_t *const comb_d = (uint8_t *)(comb + p.comb_entries);  // delta rows (common.hpp comb_granule_off)
   // XDP images: the LDS tail-call frames of the first depths (common.hpp
   // kTailLdsMax), [depth][word][lane]
-  uint64_t *const lfr = (uint64_t *)((uint8_t *)comb + 20 * (size_t)p.comb_entries);
-  for (uint32_t i = tid; i < 5 * p.comb_entries; i += BS) comb[i] = 0;
+  uint64_t *const lfr = (uint64_t *)((uint8_t *)comb + comb_bytes(p.comb_entries));
+  for (uint32_t i = tid; i < comb_bytes(p.comb_entries) / 4; i += BS) comb[i] = 0;
   for (uint32_t i = tid; i < lcache_bytes(p.lcache) / 4; i += BS) lcache[i] = 0;
   // ring-buffer staging (dev_helpers.hpp RbStage): LDS counters of the block
   __shared__ RbLds rb_lds;
@@ -657,11 +659,12 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (!t) return;
     // 4-byte granules are 16-byte aligned; 8-byte ones 8-byte aligned (pairs)
     const uint64_t g = p.arena_lo + (t & ((t & 1) ? ~15u : ~7u));
+    const uint8_t *gr = comb_d + comb_granule_off(e);
     if (t & 1) {
-      delta = ((const uint32_t *)comb_d)[4 * e + j];
+      delta = ((const uint32_t *)gr)[j];
       tag = (g + 4 * j) | 1;
     } else if (j < 2) {
-      delta = comb_d[2 * e + j];
+      delta = ((const uint64_t *)gr)[j];
       tag = g + 8 * j;
     }
   };

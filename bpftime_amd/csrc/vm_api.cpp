@@ -38,6 +38,15 @@ extern "C" hipError_t bpftime_amd_launch_miss_merge(const uint64_t *log, const u
                                                      uint32_t nblocks, const KParams *p, uint32_t *bad,
                                                      hipStream_t stream);
 
+// Off by default: measured on one box (profiles/r06_ab_lane_pad.txt) the
+// padding halves flow-hash's LDS bank conflicts but costs the lines LDS
+// (residency, table reach, LDS tail-call frames): tail-call 1.186 -> 1.277
+// ms, lpm-route 0.454 -> 0.471, flow-hash 0.670 -> 0.682, syscount equal
+bool lane_pad() {
+  static const bool on = getenv("BPFTIME_AMD_LANE_PAD") && atoi(getenv("BPFTIME_AMD_LANE_PAD")) != 0;
+  return on;
+}
+
 // experiment counters (BPFTIME_AMD_DBG 512), a device buffer made on first use
 static std::mutex g_dbg_mu;
 static uint64_t *g_dbg = nullptr;  // lookup-cache hit / miss lanes (gen_fast.py lcache_count)
@@ -435,7 +444,8 @@ class Mi355xVm {
 // of its dynamic LDS (common.hpp dyn_lds_for) and the kernel's static LDS
 std::string lds_fit_error(uint32_t kind, bool big_stack, uint32_t stack_size, uint32_t comb_entries,
                           uint32_t lcache, bool ctx_lds, bool greg, uint32_t block, bool image, uint32_t tail_lds) {
-  const size_t lanes = (size_t)block * ((kind == CTX_XDP && ctx_lds ? 48 : 0) + (big_stack ? 0 : stack_size) +
+  const size_t lanes = (size_t)block * ((kind == CTX_XDP && ctx_lds ? lane_stride(kXdpCtxBytes) : 0) +
+                                        (big_stack ? 0 : lane_stride(stack_size)) +
                                         tail_lds_lane_bytes(tail_lds));
   const size_t dyn = dyn_lds_for(kind, big_stack, stack_size, comb_entries, lcache, ctx_lds, block, tail_lds);
   const size_t stat = bpftime_amd_static_lds_image(kind, big_stack, greg, block, image);
@@ -443,7 +453,7 @@ std::string lds_fit_error(uint32_t kind, bool big_stack, uint32_t stack_size, ui
          std::to_string(block) + "-lane block (lanes' ctx, stacks and tail-call frames " + std::to_string(lanes) +
          ", lookup cache " + std::to_string(lcache) + " sets " + std::to_string(lcache_bytes(lcache)) +
          ", launch constants " + std::to_string(kTenvBytes) + ", combining table " + std::to_string(comb_entries) +
-         " entries " + std::to_string(20 * (size_t)comb_entries) + ", static " + std::to_string(stat) + ") > " +
+         " entries " + std::to_string(comb_bytes(comb_entries)) + ", static " + std::to_string(stat) + ") > " +
          std::to_string(kCuLds) + " (check BPFTIME_AMD_COMB_ENTRIES / BPFTIME_AMD_LCACHE_SETS)";
 }
 
@@ -585,6 +595,8 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   // (syscall kinds: r2 = sizeof the ctx, syscall_trace_attach_impl.cpp:46)
   p.fixed_len = kind != CTX_SYSCALL ? b->fixed_len : sys_exit ? 24 : 64;
   p.stack_size = prog.stack_size;
+  p.stack_stride = lane_stride(prog.stack_size);
+  p.ctx_stride = lane_stride(kXdpCtxBytes);
   // ORDERED: every counter add goes straight to memory (link_fast), no table
   p.comb_entries = (b->flags & EBPF_BATCH_ORDERED) ? 0 : prog.comb_entries;
   // launches holding a combining table or lookup cache keep the C++ tier's

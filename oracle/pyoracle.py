@@ -240,6 +240,14 @@ class OracleMap:
             off += 4 + ln
         return out
 
+    def ringbuf_drain(self, cap: int = 1 << 22) -> int:
+        """Consume committed records (ringbuf::fetch_data) into a reused
+        buffer without decoding them: the record count."""
+        if getattr(self, "_drain", None) is None or len(self._drain) < cap:
+            self._drain = C.create_string_buffer(cap)
+        used = C.c_uint64(0)
+        return int(lib().orc_ringbuf_fetch(self.fd, self._drain, cap, C.byref(used)))
+
     @staticmethod
     def errno() -> int:
         return lib().orc_last_errno()

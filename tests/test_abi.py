@@ -121,13 +121,17 @@ def test_lds_sizing_of_launch_shapes():
     # kind, big_stack, stack, comb entries, lcache sets, ctx in LDS, gregs, block
     bad = l.bpftime_amd_lds_bytes(xdp, False, 32, 2000, 2048, False, True, 1024)
     assert bad > cu
-    flow = l.bpftime_amd_lds_bytes(xdp, False, 32, 4000, 1024, False, True, 1024)
+    flow = l.bpftime_amd_lds_bytes(xdp, False, 32, 2800, 1024, False, True, 1024)
     assert flow <= cu
     head = l.bpftime_amd_lds_bytes(xdp, False, 8, 0, 0, False, False, 256)
     assert head <= cu // 4           # four headline blocks per CU
-    # the parts add up: each entry of the combining table 20 B, each lookup
-    # set 40 B, each lane's stack its bytes
-    assert l.bpftime_amd_lds_bytes(xdp, False, 32, 2008, 2048, False, True, 1024) - bad == 8 * 20
+    # the parts add up: each 8 entries of the combining table 8 tags + a
+    # 144-B delta row (common.hpp kCombRowBytes), each lookup set 40 B, each
+    # lane's stack its bytes at a stride of 8 x an odd number (lane_stride:
+    # with BPFTIME_AMD_LANE_PAD=1: 32 and 40 -> 40, 48 -> 56; unpadded by default)
+    assert l.bpftime_amd_lds_bytes(xdp, False, 32, 2008, 2048, False, True, 1024) - bad == 8 * 4 + 144
     assert l.bpftime_amd_lds_bytes(xdp, False, 32, 2000, 2049, False, True, 1024) - bad == 40
-    assert l.bpftime_amd_lds_bytes(xdp, False, 40, 2000, 2048, False, True, 1024) - bad == 8 * 1024
+    pad = os.environ.get("BPFTIME_AMD_LANE_PAD", "0") not in ("", "0")
+    assert l.bpftime_amd_lds_bytes(xdp, False, 40, 2000, 2048, False, True, 1024) - bad == (0 if pad else 8 * 1024)
+    assert l.bpftime_amd_lds_bytes(xdp, False, 48, 2000, 2048, False, True, 1024) - bad == (16 if pad else 16) * 1024
     assert l.bpftime_amd_lds_bytes(syscall, False, 32, 512, 2048, True, True, 1024) < cu

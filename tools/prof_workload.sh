@@ -27,13 +27,16 @@ run() {  # name, counters...
   return $rc
 }
 mkdir -p $D
-run kt || exit $?
-run sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY || exit $?
-run sq2 SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_WAVES || exit $?
-run fetch FETCH_SIZE || exit $?
-run write WRITE_SIZE || exit $?
-run l2 TCC_HIT_sum TCC_MISS_sum || exit $?
-run tcp TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum || true
+# PASSES (default all): a subset, e.g. PASSES="kt sq1 sq2"
+P=" ${PASSES:-kt sq1 sq2 fetch write l2 tcp} "
+on() { [[ "$P" == *" $1 "* ]]; }
+if on kt; then run kt || exit $?; fi
+if on sq1; then run sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY || exit $?; fi
+if on sq2; then run sq2 SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_WAVES || exit $?; fi
+if on fetch; then run fetch FETCH_SIZE || exit $?; fi
+if on write; then run write WRITE_SIZE || exit $?; fi
+if on l2; then run l2 TCC_HIT_sum TCC_MISS_sum || exit $?; fi
+if on tcp; then run tcp TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum || true; fi
 U=${UNITS:-16777216}
 python3 tools/pmc_table.py $D $U $D.pmc.json > $D.summary.txt 2>&1 || true
 cat $D.summary.txt
