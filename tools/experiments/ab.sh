@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B timing of library builds under ab/: bash tools/ab.sh variant... (workloads via WL)
+# A/B timing of library builds under ab/: bash tools/experiments/ab.sh variant... (workloads via WL)
 set -u
 mkdir -p gpurun_out
 WL=${WL:-"main flow-hash tail-call"}

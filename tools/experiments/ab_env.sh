@@ -1,5 +1,5 @@
 #!/bin/bash
-# one build, several environments: bash tools/ab_env.sh build workload "ENV1" "ENV2" ...
+# one build, several environments: bash tools/experiments/ab_env.sh build workload "ENV1" "ENV2" ...
 set -u
 v=$1; w=$2; shift 2
 for round in 1 2; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # one build, several environments, failures reported and skipped:
-#   bash tools/ab_env_k.sh build workload "ENV1" "ENV2" ...
+#   bash tools/experiments/ab_env_k.sh build workload "ENV1" "ENV2" ...
 set -u
 v=$1; w=$2; shift 2
 for round in 1 2; do

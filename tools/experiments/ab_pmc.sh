@@ -1,5 +1,5 @@
 #!/bin/bash
-# SQ counters of the headline kernel for library builds under ab/: bash tools/ab_pmc.sh variant...
+# SQ counters of the headline kernel for library builds under ab/: bash tools/experiments/ab_pmc.sh variant...
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp

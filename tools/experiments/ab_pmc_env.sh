@@ -1,5 +1,5 @@
 #!/bin/bash
-# SQ counters of one workload under several environments: bash tools/ab_pmc_env.sh build workload "ENV1" "ENV2"
+# SQ counters of one workload under several environments: bash tools/experiments/ab_pmc_env.sh build workload "ENV1" "ENV2"
 set -u
 export TMPDIR=/tmp
 v=$1; w=$2; shift 2

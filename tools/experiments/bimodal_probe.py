@@ -1,11 +1,11 @@
 """Headline kernel time per fresh packet-buffer allocation in one process
 (is the fast / slow mode a property of the buffer's placement?).
-    python tools/bimodal_probe.py [allocs] [steps]"""
+    python tools/experiments/bimodal_probe.py [allocs] [steps]"""
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from bpftime_amd import gen, isa, programs  # noqa: E402
 from bpftime_amd import vm as dev  # noqa: E402
 

@@ -1,11 +1,11 @@
 """Headline kernel time over wall time in one process, one allocation
 (does the rate change as the GPU keeps running?).
-    python tools/bimodal_time.py [blocks] [steps]"""
+    python tools/experiments/bimodal_time.py [blocks] [steps]"""
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from bpftime_amd import gen, isa, programs  # noqa: E402
 from bpftime_amd import vm as dev  # noqa: E402
 

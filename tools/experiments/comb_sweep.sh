@@ -1,6 +1,6 @@
 #!/bin/bash
 # Kernel time of one workload per combining-table size (BPFTIME_AMD_COMB_ENTRIES; "auto": the library's choice):
-#   bash tools/comb_sweep.sh <workload> "<entries...>" [extra env]
+#   bash tools/experiments/comb_sweep.sh <workload> "<entries...>" [extra env]
 set -u
 mkdir -p gpurun_out
 w=$1

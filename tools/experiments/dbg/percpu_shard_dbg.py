@@ -1,7 +1,7 @@
 """Debug: per-CPU flow-hash, 8 shards vs one batch vs the oracle (first differences)."""
 import os
 import sys
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", ".."))
 import numpy as np
 from bpftime_amd import vm as dev, isa, gen, programs, shard
 from oracle import pyoracle as po

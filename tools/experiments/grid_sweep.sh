@@ -1,6 +1,6 @@
 #!/bin/bash
 # Headline kernel time per grid multiplier (BPFTIME_AMD_GRID_MULT; resident blocks x mult):
-#   bash tools/grid_sweep.sh "<mults...>"
+#   bash tools/experiments/grid_sweep.sh "<mults...>"
 set -u
 mkdir -p gpurun_out
 for m in $1; do

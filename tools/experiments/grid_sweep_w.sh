@@ -1,6 +1,6 @@
 #!/bin/bash
 # One bench workload per grid multiplier (BPFTIME_AMD_GRID_MULT):
-#   bash tools/grid_sweep_w.sh <workload> "<mults...>"
+#   bash tools/experiments/grid_sweep_w.sh <workload> "<mults...>"
 set -u
 mkdir -p gpurun_out
 w=$1

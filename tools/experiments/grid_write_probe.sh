@@ -1,7 +1,7 @@
 #!/bin/bash
 # Headline per grid multiplier: bench time and the median launch's
 # WRITE_SIZE / FETCH_SIZE per packet (raw KiB counters, 2^24 packets)
-#   bash tools/grid_write_probe.sh "<mults...>"
+#   bash tools/experiments/grid_write_probe.sh "<mults...>"
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out

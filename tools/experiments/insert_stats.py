@@ -1,11 +1,11 @@
 """Insert-path counters of flow-hash's cold launch (an experiment build made
 with -DBPFTIME_AMD_INSERT_STATS, dev_helpers.hpp ISTAT):
-    BPFTIME_AMD_LIB=ab/istats.so python tools/insert_stats.py [log2n]"""
+    BPFTIME_AMD_LIB=ab/istats.so python tools/experiments/insert_stats.py [log2n]"""
 import ctypes as C
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from bpftime_amd import gen, isa, programs  # noqa: E402
 from bpftime_amd import vm as dev  # noqa: E402
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # latency / occupancy PMC passes (rocprofv3 derived metrics, one per pass)
-# of one bench workload: bash tools/lat_pmc.sh <workload> [tag]
+# of one bench workload: bash tools/experiments/lat_pmc.sh <workload> [tag]
 set -u
 export TMPDIR=/tmp
 W=${1:-flow-hash}; T=${2:-lat}

@@ -1,10 +1,10 @@
 """Interpreter cost model on the GPU: kernel time of tiny XDP programs over
 2^24 64-B frames (fixed per-unit cost, cost per dispatched instruction of a
-few handler classes).  python tools/micro.py [log2n]"""
+few handler classes).  python tools/experiments/micro.py [log2n]"""
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import bench_workloads as bw  # noqa: E402
 from bpftime_amd import gen, isa, programs  # noqa: E402
 from bpftime_amd import vm as dev  # noqa: E402

@@ -2,7 +2,7 @@
 import os
 import sys
 
-ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "..")
 sys.path.insert(0, ROOT)
 os.environ["BPFTIME_AMD_DUMP_FAST"] = "1"
 from bpftime_amd import gen, isa, programs  # noqa: E402

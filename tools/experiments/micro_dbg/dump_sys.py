@@ -3,7 +3,7 @@ syscount's sys_exit program (BPFTIME_AMD_DUMP_FAST)."""
 import os
 import sys
 
-ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "..")
 sys.path.insert(0, ROOT)
 os.environ["BPFTIME_AMD_DUMP_FAST"] = "1"
 import numpy as np  # noqa: E402

@@ -1,11 +1,11 @@
 """flow-hash steady-state kernel time by flow count (the lookup cache's
 reach): the bench's program and frames with 256 .. 65536 Zipf(1.1) flows in a
 65536-entry table; BPFTIME_AMD_DBG=512 lookup-cache hit rate beside.
-python tools/micro_dbg/flow_nflows.py [log2n]"""
+python tools/experiments/micro_dbg/flow_nflows.py [log2n]"""
 import os
 import sys
 
-ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "..")
 sys.path.insert(0, ROOT)
 import bench_workloads as bw  # noqa: E402
 from bpftime_amd import gen, isa, programs  # noqa: E402

@@ -1,7 +1,7 @@
 """Tail-call parity per first-byte index at n=1 (debug)."""
 import os, struct, sys
 import numpy as np
-ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "..")
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 from bpftime_amd import vm as dev, isa, gen

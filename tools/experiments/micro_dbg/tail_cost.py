@@ -2,14 +2,14 @@
 64-B frames whose first byte (the slot) is the same for every frame (u0..u3),
 the same within each wave but random across waves (wave), or random per frame
 (rand, the bench).  Kernel ms per launch (HIP events).
-python tools/micro_dbg/tail_cost.py [log2n]"""
+python tools/experiments/micro_dbg/tail_cost.py [log2n]"""
 import os
 import struct
 import sys
 
 import numpy as np
 
-ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "..")
 sys.path.insert(0, ROOT)
 import bench_workloads as bw  # noqa: E402
 from bpftime_amd import isa, programs  # noqa: E402

@@ -1,6 +1,6 @@
-"""Summarise a tools/prof.sh run into profiles/ (tracked).
+"""Summarise a tools/experiments/prof.sh run into profiles/ (tracked).
 
-    python tools/prof_summary.py gpurun_out/prof_r01 r01 [packets_per_launch]
+    python tools/experiments/prof_summary.py gpurun_out/prof_r01 r01 [packets_per_launch]
 
 Writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
@@ -19,7 +19,7 @@ import statistics
 import sys
 from collections import defaultdict
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 HOT = "k_interp"
 
 
@@ -54,7 +54,7 @@ def main():
         for k, cs in pmc_means(os.path.join(src, f"{name}_counter_collection.csv")).items():
             pmc.setdefault(k, {}).update(cs)
     lines = [f"# rocprofv3 summary ({tag})", "",
-             "Command: `tools/prof.sh` (bench.py --steps 10 --warmup 2 --no-cpu-baseline), "
+             "Command: `tools/experiments/prof.sh` (bench.py --steps 10 --warmup 2 --no-cpu-baseline), "
              "one pass per counter group.", "",
              "| kernel | calls | avg ns | min ns | max ns | % |", "|---|---|---|---|---|---|"]
     for r in rows:

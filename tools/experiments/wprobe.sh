@@ -1,7 +1,7 @@
 #!/bin/bash
 # One bench line's raw WRITE_SIZE / FETCH_SIZE per unit of the median
 # interpreter launch under several environments (write attribution):
-#   bash tools/wprobe.sh <workload> <units> "ENV1" "ENV2" ...   ("X=1": none)
+#   bash tools/experiments/wprobe.sh <workload> <units> "ENV1" "ENV2" ...   ("X=1": none)
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
