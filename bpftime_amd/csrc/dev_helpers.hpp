@@ -1120,9 +1120,29 @@ __device__ __forceinline__ uint64_t lru_next_stamp(LaneEnv &env) {
   return env.lru_stamp | op;
 }
 
+// A map's descriptor for a helper call: through the scalar cache when every
+// calling lane names the same map (the usual case: an lddw constant), else
+// per lane.  The table only changes between launches.
+__device__ __forceinline__ DMap load_dmap(const DMap *maps, uint64_t fd) {
+  const uint32_t f0 = __builtin_amdgcn_readfirstlane((uint32_t)fd);
+  if (__ballot(fd != f0) == 0) {
+    typedef unsigned int u32x4c __attribute__((ext_vector_type(4)));
+    typedef const u32x4c __attribute__((address_space(4))) *cvec;
+    const cvec q = (cvec)(maps + f0);
+    const u32x4c w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
+    DMap m;
+    __builtin_memcpy((uint8_t *)&m, &w0, 16);
+    __builtin_memcpy((uint8_t *)&m + 16, &w1, 16);
+    __builtin_memcpy((uint8_t *)&m + 32, &w2, 16);
+    __builtin_memcpy((uint8_t *)&m + 48, &w3, 16);
+    return m;
+  }
+  return maps[fd];
+}
+
 __device__ uint64_t helper_lookup(const DMap *maps, uint64_t fd, uint64_t key, LaneEnv &env) {
   if (fd >= kMaxFds) return 0;
-  const DMap m = maps[fd];
+  const DMap m = load_dmap(maps, fd);
   switch (m.type) {
     case MT_ARRAY: {
       uint32_t k = *(const u32u *)key;
@@ -1176,7 +1196,7 @@ __device__ uint64_t helper_lookup(const DMap *maps, uint64_t fd, uint64_t key, L
 __device__ uint64_t helper_update(const DMap *maps, uint64_t fd, uint64_t key, uint64_t val,
                                   uint64_t flags, LaneEnv &env) {
   if (fd >= kMaxFds) return (uint64_t)-1;
-  const DMap m = maps[fd];
+  const DMap m = load_dmap(maps, fd);
   uint64_t base = flags & 0xffffffffull;
   bool flags_ok = base == 0 || base == 1 || base == 2;  // map_common_def.hpp:83-94
   switch (m.type) {
@@ -1237,7 +1257,7 @@ __device__ uint64_t helper_update(const DMap *maps, uint64_t fd, uint64_t key, u
 
 __device__ uint64_t helper_delete(const DMap *maps, uint64_t fd, uint64_t key, LaneEnv &env) {
   if (fd >= kMaxFds) return (uint64_t)-1;
-  const DMap m = maps[fd];
+  const DMap m = load_dmap(maps, fd);
   switch (m.type) {
     case MT_ARRAY:
     case MT_PERCPU_ARRAY:

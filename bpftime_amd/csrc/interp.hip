@@ -1377,6 +1377,8 @@ __global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
     const int64_t nr = has ? *(const int64_t *)((ent ? ent : ext) + 8) : 0;
     const int64_t ret = has && ext ? *(const int64_t *)(ext + 16) : 0;
     const uint64_t pid = has && L.pid ? *(const uint64_t *)(L.pid + idx * L.pstride) : p.pid_tgid;
+    // (the recorded clocks at sys_enter and after the call)
+    const uint64_t kt_e = has && clk ? *(const uint64_t *)clk : 0, kt_x = has && clk ? *(const uint64_t *)(clk + 8) : 0;
     const bool live = has && nr != 60 && nr != 231;  // :23-26
     ovr_st[tid] = 0;
     ovr_v[tid] = 0;
@@ -1427,7 +1429,13 @@ __global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
         }
         // R_CALL: the helper (dev_helpers.hpp) for the lanes at the call
         const bool csel = uni ? c.alive : (c.alive && c.lpc == c.call_pc);
-        if (csel) {
+        const uint32_t fid = __builtin_amdgcn_readfirstlane(c.call_id);
+        if (fid == 5 || fid == 14) {
+          // the replay's clock and caller: register values, no helper
+          // dispatch (each pass through call_helper costs a lone wave
+          // several microseconds of spill traffic: profiles/r06_seq_pmc.txt)
+          if (csel) c.R[0] = fid == 14 ? pid : clk ? (enter ? kt_e : kt_x) : (uint64_t)__builtin_amdgcn_s_memrealtime() * 10ull;
+        } else if (csel) {
           LaneEnv env;
           env.vcpu = idx / 64;
           env.scratch = 0;
@@ -1441,7 +1449,7 @@ __global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
           env.ovr_bit = enter ? 1 : 2;
           env.pid_tgid = pid;
           env.kt_on = clk != nullptr;
-          env.ktime = clk ? *(const uint64_t *)(clk + (enter ? 0 : 8)) : 0;
+          env.ktime = enter ? kt_e : kt_x;
           uint32_t cerr = E_OK;
           uint64_t *R = c.R;
           const uint32_t cid = __builtin_amdgcn_readfirstlane(c.call_id);
