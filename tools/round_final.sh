@@ -17,4 +17,4 @@ for w in $WS; do
 done
 [ -n "${NO_BENCH:-}" ] && exit 0
 bash tools/bench_all.sh || exit 1
-for w in $WS; do cat gpurun_out/bench_$w.json; done > gpurun_out/${TAG}_bench_lines.jsonl
+for w in $WS syscount-latency; do cat gpurun_out/bench_$w.json; done > gpurun_out/${TAG}_bench_lines.jsonl
