@@ -354,6 +354,10 @@ struct SeqProg {
 };
 static_assert(sizeof(SeqProg) == 32, "SeqProg is read with scalar loads");
 constexpr uint32_t kSeqMaxProgs = 64;  // attached programs a thread-ordered dispatch runs (kernel arguments)
+// k_sys_seq's per-lane ctx copy: the 64-B ctx, then the record's caller
+// (pid_tgid) and the clock of the callback's phase, read by the asm tier's
+// CALL_REC handler (loader.cpp link_fast rec_helpers)
+constexpr uint32_t kSeqPidOff = 64, kSeqClockOff = 72, kSeqCtxWords = 10;
 struct SeqParams {
   uint32_t nprogs;
   // the records' fields (include/bpftime_amd.h: 64- / 96- / 128-B records or
@@ -375,6 +379,10 @@ struct SeqParams {
   uint64_t pid_tgid;      // 64-B records: the dispatching thread's
   uint32_t *err_count;    // failed callbacks
   uint32_t exact;         // one lane over every record (EBPF_BATCH_ORDERED)
+  // 1: every program keeps its stack within kLdsStackMax bytes: the stacks
+  // live in LDS and the callbacks run in the asm tier (seq_lds_bytes); 0:
+  // private stacks, the C++ tier only
+  uint32_t fast;
   SeqProg progs[kSeqMaxProgs];  // in the kernel arguments: scalar loads, no upload
 };
 static_assert(sizeof(SeqParams) <= 4096, "kernel arguments");
@@ -444,6 +452,12 @@ constexpr uint32_t kTenvRb = 64 + 4 * kMissParts;     // (u64 index kTenvRb / 8)
 // (KParams tail_lds; gen_fast.py tail_env)
 constexpr uint32_t kTenvLf = kTenvRb + 16;
 constexpr uint32_t kTenvBytes = kTenvLf + 16;          // gen_fast.py TENV
+// k_sys_seq's dynamic LDS with the asm tier on: the lanes' stacks, then the
+// asm's launch constants (tenv, zero: no tail calls, staging or tables) in
+// front of an empty combining table
+inline size_t seq_lds_bytes(uint32_t block, bool fast) {
+  return fast ? (size_t)block * kLdsStackMax + kTenvBytes : 0;
+}
 // Hash-lookup cache of a block (programs whose hash lookups the loader marks
 // FW_LCACHE: no deletions): `sets` 2-way sets, the ways' 16-B keys
 // ([set][way]) then their u32 entries {(slot + 1) | fd << 22}, right below

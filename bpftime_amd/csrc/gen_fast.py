@@ -178,6 +178,7 @@ def handler_ids():
     ids += ["CALL_LOOKUP_STK3", "CALL_LOOKUP_AK3"]
     for sz in (1, 2, 4, 8):  # the lane's own LDS XDP ctx at a static offset
         ids += [f"LDX{sz}_CTX", f"STX{sz}_CTX", f"ST{sz}_CTX"]
+    ids += ["CALL_REC"]  # thread-ordered dispatch: the caller / clock beside the ctx copy
     return ids
 
 
@@ -933,6 +934,19 @@ class Gen:
                "v_addc_co_u32_e32 v49, vcc, 0, v53, vcc",
                f"global_load_dwordx2 v[{R0}:{R0 + 1}], v[48:49], off",
                "s_waitcnt vmcnt(0)")
+        self.next_seq()
+
+    def call_rec(self):
+        """bpf_get_current_pid_tgid / bpf_ktime_get_ns of a thread-ordered
+        callback (interp.hip k_sys_seq, loader.cpp link_fast rec_helpers):
+        r0 = the u64 at slot + w7, the caller or the recorded clock the
+        kernel put beside the lane's LDS ctx copy (a flat load: the slot is
+        that copy).  r1-r5 are left as they are, as the C++ tier's helper
+        call leaves them."""
+        self.e("v_add_co_u32_e32 v48, vcc, s47, v52",
+               "v_addc_co_u32_e32 v49, vcc, 0, v53, vcc",
+               f"flat_load_dwordx2 v[{R0}:{R0 + 1}], v[48:49]",
+               "s_waitcnt vmcnt(0) lgkmcnt(0)")
         self.next_seq()
 
     def ldxk(self):
@@ -2389,6 +2403,8 @@ class Gen:
                 self.tail_ret()
             elif name == "CALL_PID":
                 self.call_pid()
+            elif name == "CALL_REC":
+                self.call_rec()
             elif name == "KLDX":
                 self.ldxk()
             elif name.startswith("RMWD"):

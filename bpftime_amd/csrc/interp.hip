@@ -1337,16 +1337,61 @@ __global__ __launch_bounds__(kBigBlock) void k_miss_merge(const uint64_t *log, c
 // counter add reaches memory at once (the ORDERED links), so a thread's
 // later callbacks see its earlier ones.  Threads are as independent as the
 // reference's: different lanes, no order between them.
+#ifdef BPFTIME_AMD_SEQ_PROF
+// (experiment build only: per-region clock64 sums of k_sys_seq's waves,
+// tools/experiments/seq_prof.py)
+__device__ unsigned long long g_seqprof[32];
+#define SP_NOW() ((uint64_t)clock64())
+#define SP_ADD(i, v) sp_acc[i] += (v)
+#else
+#define SP_NOW() ((uint64_t)0)
+#define SP_ADD(i, v) ((void)0)
+#endif
 __global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
+#ifdef BPFTIME_AMD_SEQ_PROF
+  uint64_t sp_acc[16] = {};
+  const uint64_t sp_t0 = SP_NOW();
+#endif
   __shared__ uint64_t Rf[12 * kBlock];   // r0..r10 columns, the dummy slot
-  __shared__ uint64_t cx[8 * kBlock];    // the lane's ctx copy (64 B)
+  __shared__ uint64_t cx[kSeqCtxWords * kBlock];  // the lane's ctx copy (64 B), its caller and clock
   __shared__ uint32_t ovr_st[kBlock];    // override bits of the lane's record (1 enter, 2 exit)
   __shared__ int64_t ovr_v[kBlock];      // ... and the value
   const uint32_t tid = threadIdx.x;
   const uint64_t t = (uint64_t)blockIdx.x * kBlock + tid;
-  uint64_t stk[kStackSize / 8];          // 512-B stack (private memory)
-  const uint64_t stack_top = (uint64_t)(uintptr_t)(stk + kStackSize / 8);
-  uint64_t *const ctx = &cx[8 * tid];
+  // the callbacks' stacks: private memory (512 B, the C++ tier), or (p.fast)
+  // kLdsStackMax bytes of LDS per lane, which the asm tier addresses, followed
+  // by the asm's launch constants (common.hpp seq_lds_bytes)
+  extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+  const bool fast = __builtin_amdgcn_readfirstlane(p.fast) != 0;
+  uint64_t stk[kStackSize / 8];
+  const uint64_t stack_top = fast ? (uint64_t)(uintptr_t)(dyn + (tid + 1) * kLdsStackMax)
+                                  : (uint64_t)(uintptr_t)(stk + kStackSize / 8);
+  uint64_t *const ctx = &cx[kSeqCtxWords * tid];
+  FastEnv fe{};
+  if (fast) {
+    // tenv all zero (no tail-call frames, ring staging, lookup-cache
+    // counters or miss log), no combining table: every asm path that would
+    // read them leaves for the C++ tier, and the ORDERED links add to memory
+    uint64_t *const tenv = (uint64_t *)(dyn + kBlock * kLdsStackMax);
+    for (uint32_t i = tid; i < kTenvBytes / 8; i += kBlock) tenv[i] = 0;
+    fe.maps = p.maps;
+    fe.comb = sreg((uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(tenv + kTenvBytes / 8)));
+    fe.combn = 0;
+    fe.head = 0;
+    fe.oflags = 0;  // callbacks' return values are not stored (the dispatch ignores them)
+    fe.dlo = sreg((uint64_t)0);
+    const uint32_t dh = __builtin_amdgcn_readfirstlane(p.checked ? 0u : ~0u);
+    fe.dhi = sreg(((uint64_t)dh << 32) | dh);
+    fe.alo = p.arena_lo;
+    fe.ahi = p.arena_hi;
+    fe.shi = sreg((uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)(uintptr_t)&Rf[0] >> 32)));
+    fe.phi = fe.shi;
+    fe.rb = (uint32_t)(uintptr_t)&Rf[0] + 8 * tid;
+    fe.stage = 0;
+    fe.ncpu = p.ncpu ? p.ncpu : 1;
+    fe.sstep = fe.ustep = 0;
+  }
+  __syncthreads();
   Ctx c;
   c.R = &Rf[tid];
   // the programs see their ctx copy (LDS), their stack and the map arena
@@ -1368,6 +1413,8 @@ __global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
   };
   while (__ballot(k < end) != 0) {
+    uint64_t sp_r = SP_NOW();
+    (void)sp_r;
     const bool has = k < end;
     const uint64_t idx = has ? (p.perm ? (uint64_t)p.perm[k] : k) : 0;
     const SysLayout &L = p.lay;
@@ -1399,7 +1446,11 @@ __global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
           ctx[2] = (uint64_t)ret;
           for (int w = 3; w < 8; w++) ctx[w] = 0;
         }
+        // the asm tier's bpf_get_current_pid_tgid / bpf_ktime_get_ns (CALL_REC)
+        ctx[kSeqPidOff / 8] = pid;
+        ctx[kSeqClockOff / 8] = clk ? (enter ? kt_e : kt_x) : (uint64_t)__builtin_amdgcn_s_memrealtime() * 10ull;
       }
+      SP_ADD(1, SP_NOW() - sp_r);  // record fields + ctx build (first use waits on the loads)
       c.prog = (prog_ptr)rfl64((uint64_t)(uintptr_t)sp->prog);
       c.fast = (const FInsn *)rfl64((uint64_t)(uintptr_t)sp->fast);
       for (int r = 0; r <= 10; r++) c.R[r * kBlock] = 0;
@@ -1416,8 +1467,49 @@ __global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
       uint64_t miss_hash = 0;
       uint32_t lru_ops = 0;
       bool uni = true;
+      // the asm tier's view of the callback: a fresh entry (r1 = the ctx
+      // copy, r2 = its size, r10 = the LDS stack top), its ctx loads from the
+      // copy through the generic path (no staging), no verdict / ret stores
+      FastUnit fu{};
+      if (fast) {
+        fe.fast = (const FInsn *)rfl64((uint64_t)(uintptr_t)sp->fast);
+        fu.r1 = fu.slot = (uint64_t)(uintptr_t)ctx;
+        fu.r2 = fu.len = enter ? 64 : 24;
+        fu.r10 = stack_top;
+        fu.entry = 1u | 4u;  // fresh, lane groups scheduled in asm
+        const uint64_t vcpu = idx / 64;
+        fu.vm = (uint32_t)(vcpu % fe.ncpu);
+      }
+      SP_ADD(8, 1);
       while (__ballot(c.alive) != 0) {
-        const uint32_t r = uni ? run_loop<true>(c) : run_loop<false>(c);
+        uint64_t sp_i = SP_NOW();
+        (void)sp_i;
+        uint32_t r;
+        if (fast && uni) {
+          uint32_t adv = 0;
+          const uint32_t why = run_fast<false>(c, fe, fu, 0u, adv);
+          fu.entry &= ~1u;  // re-entries read the registers from their LDS columns
+          if (why == FAST_EXIT) {  // every running lane ran exit
+            c.alive = false;
+            break;
+          }
+          if (why == FAST_SPLIT) {  // lane groups at different pcs (c.lpc): the C++ divergent loop
+            uni = false;
+            continue;
+          }
+          if (why == FAST_STEPS) {
+            c.err = c.alive ? E_STEPS : c.err;
+            c.alive = false;
+            break;
+          }
+          r = run_loop<true, true>(c);  // the instruction the asm does not run
+        } else {
+          r = uni ? run_loop<true>(c) : run_loop<false>(c);
+        }
+        SP_ADD(2, SP_NOW() - sp_i);
+        SP_ADD(uni ? 9 : 10, 1);
+        sp_i = SP_NOW();
+        if (r == R_STEP) continue;
         if (r == R_DONE) break;
         if (r == R_DIVERGE) {
           uni = false;
@@ -1471,14 +1563,42 @@ __global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
           c.pc = c.call_pc + 1;
         else
           c.lpc = csel ? c.call_pc + 1 : c.lpc;
+        {
+          const uint64_t sp_d = SP_NOW() - sp_i;
+          (void)sp_d;
+          SP_ADD(fid == 1 ? 3 : fid == 2 ? 4 : (fid == 5 || fid == 14) ? 5 : 6, sp_d);
+          SP_ADD(fid == 1 ? 11 : fid == 2 ? 12 : (fid == 5 || fid == 14) ? 13 : 14, 1);
+        }
       }
       // a failed callback is ignored by the dispatch (:47-52) and counted
       if (run && c.err != E_OK) atomicAdd(p.err_count, 1u);
+      sp_r = SP_NOW();
     }
+    SP_ADD(7, SP_NOW() - sp_r);  // the record's tail (out store, loop)
     if (has && p.out) p.out[idx] = ovr_st[tid] ? ovr_v[tid] : ret;
     if (has) k++;
   }
+#ifdef BPFTIME_AMD_SEQ_PROF
+  sp_acc[0] = SP_NOW() - sp_t0;
+  sp_acc[15] = c.steps;
+  if ((tid & 63) == 0 && __ballot(t < p.nseg) != 0) {
+    for (int i = 0; i < 16; i++) atomicAdd(&g_seqprof[i], (unsigned long long)sp_acc[i]);
+    atomicAdd(&g_seqprof[16], 1ull);
+  }
+#endif
 }
+
+#ifdef BPFTIME_AMD_SEQ_PROF
+extern "C" int bpftime_amd_seq_prof(unsigned long long *out, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seqprof), sizeof(g_seqprof)) != hipSuccess) return -1;
+  if (reset) {
+    static unsigned long long z[32];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_seqprof), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // Host-side launch wrappers
@@ -1514,7 +1634,7 @@ extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind,
 extern "C" hipError_t bpftime_amd_launch_sys_seq(const SeqParams *p, hipStream_t stream) {
   const uint64_t grid = (p->nseg + kBlock - 1) / kBlock;
   if (grid == 0 || grid > 0x7fffffffull || p->nprogs > kSeqMaxProgs) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_sys_seq, dim3((uint32_t)grid), dim3(kBlock), 0, stream, *p);
+  hipLaunchKernelGGL(k_sys_seq, dim3((uint32_t)grid), dim3(kBlock), seq_lds_bytes(kBlock, p->fast != 0), stream, *p);
   return hipGetLastError();
 }
 

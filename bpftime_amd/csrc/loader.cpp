@@ -1736,8 +1736,29 @@ static void link_staged(const FastForm &f, uint32_t head, uint32_t stage, bool o
                         const std::vector<DInsn> &prog, std::vector<FInsn> &out);
 
 void link_fast(const FastForm &f, uint32_t head, uint32_t stage, bool ordered, const std::vector<DInsn> &prog,
-               std::vector<FInsn> &out, int32_t unwind_idx, uint32_t lc_sets, uint32_t pid_off) {
+               std::vector<FInsn> &out, int32_t unwind_idx, uint32_t lc_sets, uint32_t pid_off, bool no_kldx,
+               bool rec_helpers) {
   link_staged(f, head, stage, ordered, prog, out);
+  // rec_helpers (the thread-ordered kernel): bpf_get_current_pid_tgid and
+  // bpf_ktime_get_ns read the caller / clock the kernel keeps beside the
+  // lane's ctx copy (interp.hip k_sys_seq: ctx + kSeqPidOff / kSeqClockOff)
+  if (rec_helpers)
+    for (size_t i = 0; i < prog.size() && i < out.size(); i++)
+      if (prog[i].op == X_CALL && (prog[i].hi == 14 || prog[i].hi == 5) && unwind_idx != prog[i].hi) {
+        out[i].hoff = 4 + 4 * F_CALL_REC;
+        out[i].aux = (int32_t)(prog[i].hi == 14 ? kSeqPidOff : kSeqClockOff);
+      }
+  // no_kldx: the launch runs other programs that may write the array
+  // storage this one reads at constant addresses (the thread-ordered
+  // kernel: const_loads proves the absence of writes per program only), so
+  // those loads go through the vector memory path again, as unspecialised
+  if (no_kldx)
+    for (size_t i = 0; i < prog.size() && i < out.size(); i++)
+      if (out[i].hoff == 4 + 4 * F_KLDX) {
+        out[i].hoff = 4 + 4 * fast_id(prog[i]);
+        out[i].imm = (int64_t)prog[i].off;
+        out[i].aux = prog[i].imm;
+      }
   // bpf_get_current_pid_tgid of a recorded syscall: a load from the unit
   if (pid_off && pid_off < 256)
     for (size_t i = 0; i < prog.size() && i < out.size(); i++)
@@ -1748,9 +1769,15 @@ void link_fast(const FastForm &f, uint32_t head, uint32_t stage, bool ordered, c
         const bool staged = pid_off % 4 == 0 && pid_off + 8 <= stage;
         out[i].imm = staged ? (int64_t)(pid_off / 4) | (1ll << 32) : 0;
       }
-  // the launch's lookup-cache set count (vm_api.cpp) into the lookups that use it
+  // the launch's lookup-cache set count (vm_api.cpp) into the lookups that
+  // use it; a launch without a cache (0: the thread-ordered kernel) turns it off
   for (FInsn &x : out)
-    if ((x.w1 & FW_LCACHE) && lc_sets) x.dst_x2 = lc_sets;
+    if (x.w1 & FW_LCACHE) {
+      if (lc_sets)
+        x.dst_x2 = lc_sets;
+      else
+        x.w1 &= ~(uint32_t)FW_LCACHE;
+    }
   // an unwind helper (ebpf_set_unwind_function_index) is called from the
   // C++ tier, which ends the unit when it returns 0: map_lookup_elem leaves
   // its asm handlers then

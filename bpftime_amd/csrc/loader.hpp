@@ -112,8 +112,13 @@ uint32_t stage_need(const FastForm &f, uint32_t head);
 // `unwind_idx`: the VM's unwind helper (-1 none); its calls run in C++.
 // `pid_off` (1..255): bpf_get_current_pid_tgid reads the u64 at the unit +
 // pid_off in asm (recorded syscalls, KParams pid_off); else it runs in C++.
+// `lc_sets` 0: no lookup cache in the launch (FW_LCACHE cleared).
+// `no_kldx`: constant-address loads through the vector path (the launch
+// runs other programs that may write them).  `rec_helpers`: caller and
+// clock from beside the ctx copy (the thread-ordered kernel).
 void link_fast(const FastForm &f, uint32_t head, uint32_t stage, bool ordered, const std::vector<DInsn> &prog,
-               std::vector<FInsn> &out, int32_t unwind_idx = -1, uint32_t lc_sets = 0, uint32_t pid_off = 0);
+               std::vector<FInsn> &out, int32_t unwind_idx = -1, uint32_t lc_sets = 0, uint32_t pid_off = 0,
+               bool no_kldx = false, bool rec_helpers = false);
 
 // Runs the compat_ubpf.cpp:61-200 patching (call remap check, lddw pseudo
 // sources), ubpf-style validation, pre-decoding and the dataflow analyses

@@ -86,7 +86,7 @@ struct Image {
   // linked FInsn arrays per launch configuration (entry form, ORDERED,
   // staged bytes, batch head): a few per program, built on first use
   std::mutex link_mu;
-  std::map<uint64_t, FInsn *> links;
+  std::map<std::pair<uint64_t, uint32_t>, FInsn *> links;
 
   ~Image() {
     if (d_prog) hipFree(d_prog);
@@ -95,7 +95,7 @@ struct Image {
     for (auto &kv : links) hipFree(kv.second);
   }
   const FInsn *linked(bool xdp, uint32_t head, uint32_t stage, bool ordered, int32_t unwind_idx, uint32_t lc_sets,
-                      int32_t pid_off) {
+                      int32_t pid_off, bool no_kldx = false, bool rec_helpers = false) {
     std::lock_guard<std::mutex> g(link_mu);
     // (the helpers with asm handlers an unwind index changes: lookup, pid_tgid)
     const bool uw = unwind_idx == 1, uwp = unwind_idx == 14;
@@ -103,10 +103,11 @@ struct Image {
     const uint64_t key = ((uint64_t)xdp << 63) | ((uint64_t)ordered << 62) | ((uint64_t)uw << 61) |
                          ((uint64_t)(lc_sets & 0x1fff) << 47) | ((uint64_t)stage << 40) | ((uint64_t)po << 32) |
                          (stage ? head : 0);
-    auto it = links.find(key);
+    const auto lk = std::make_pair(key, (uint32_t)no_kldx | ((uint32_t)rec_helpers << 1));
+    auto it = links.find(lk);
     if (it != links.end()) return it->second;
     std::vector<FInsn> out;
-    link_fast(xdp ? fx : fr, head, stage, ordered, prog.prog, out, uw ? 1 : -1, lc_sets, po);
+    link_fast(xdp ? fx : fr, head, stage, ordered, prog.prog, out, uw ? 1 : -1, lc_sets, po, no_kldx, rec_helpers);
     if (getenv("BPFTIME_AMD_DUMP_FAST"))  // the linked threaded form, one FInsn a line
       for (size_t i = 0; i < out.size(); i++)
         fprintf(stderr, "bpftime_amd: fast %3zu %-18s w1 %08x imm %llx dst %u src %u tgt %u aux %x\n", i,
@@ -119,7 +120,7 @@ struct Image {
       hipFree(d);
       return nullptr;
     }
-    links[key] = d;
+    links[lk] = d;
     return d;
   }
   // device copy of the decoded program + both threaded forms
@@ -1157,12 +1158,31 @@ int64_t seq_dispatch(const std::vector<SeqAttach> &progs, const SysLayout &lay, 
   std::vector<int> lpm_w;
   uint32_t lpm_updates = 0;
   uint64_t steps = 0;
+  // the asm tier runs the callbacks when every stack fits the LDS stacks
+  // (BPFTIME_AMD_SEQ_ASM=0: the C++ tier, for comparison)
+  const char *asm_env = getenv("BPFTIME_AMD_SEQ_ASM");
+  bool fast = !(asm_env && asm_env[0] == '0');
+  // constant-address loads (loader.cpp const_loads: array storage nothing in
+  // THAT program writes) stay scalar-cache loads only while no attached
+  // program writes or adds to an array map: one launch runs them all
+  bool array_writes = false;
+  for (const SeqAttach &a : progs) {
+    auto im = a.vm->impl->image();
+    if (!im) continue;
+    fast = fast && !im->prog.big_stack && im->prog.stack_size <= kLdsStackMax;
+    const uint8_t w = FX_WRITE | FX_ADD;
+    array_writes = array_writes || (im->fr.any_fx & w);
+    for (const auto &kv : im->fr.map_fx)
+      if ((kv.second & w) && kv.first >= 0 && kv.first < (int32_t)kMaxFds &&
+          (r.maps[kv.first].type == MT_ARRAY || r.maps[kv.first].type == MT_PERCPU_ARRAY))
+        array_writes = true;
+  }
   for (const SeqAttach &a : progs) {
     Mi355xVm *vm = a.vm->impl;
     auto im = vm->image();
     if (!vm->loaded || !im) return fail("an attached program is not loaded");
     if (vm->has_tail) return fail("an attached program calls bpf_tail_call (program-major dispatch runs it)");
-    const FInsn *f = im->linked(false, 0, 0, true, -1, 0, 0);
+    const FInsn *f = im->linked(false, 0, 0, true, -1, 0, 0, array_writes && progs.size() > 1, fast);
     if (!f) return fail("device upload failed");
     SeqProg &q = p.progs[p.nprogs++];
     q.prog = im->d_prog;
@@ -1197,6 +1217,7 @@ int64_t seq_dispatch(const std::vector<SeqAttach> &progs, const SysLayout &lay, 
   p.pid_tgid = ((uint64_t)(uint32_t)getpid() << 32) | (uint32_t)syscall(SYS_gettid);
   p.err_count = err;
   p.exact = ordered ? 1 : 0;
+  p.fast = fast ? 1 : 0;
   // the map upkeep exec_batch does before a launch, for the union of the
   // programs (a deletion never runs beside a cached launch; LPM launches
   // under the LPM launch lock; lookup indexes; LRU stamps; host views)

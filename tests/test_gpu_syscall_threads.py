@@ -80,6 +80,50 @@ def test_syscount_latency_pair_bit_exact(fresh_oracle, fresh_runtime, filter_pid
         assert len(ostart.items()) == 4  # tgid 1003: threads 12..15
 
 
+@pytest.mark.parametrize("tier", ["asm", "cpp"])
+def test_syscount_pair_both_tiers(fresh_oracle, fresh_runtime, monkeypatch, tier):
+    """The callbacks run in the asm tier when every stack fits the LDS stacks
+    (vm_api.cpp seq_dispatch), else -- or with BPFTIME_AMD_SEQ_ASM=0 -- in
+    the C++ tier: both bit-exact, over 256 threads."""
+    po, dev = fresh_oracle, fresh_runtime
+    monkeypatch.setenv("BPFTIME_AMD_SEQ_ASM", "1" if tier == "asm" else "0")
+    o, (ostart, odata), (dstart, ddata) = _syscount(po, dev)
+    n = 1 << 18
+    recs = gen.syscall_records_timed(n, threads=256)
+    d = dev.DeviceBuffer.from_array(recs)
+    out = dev.DeviceBuffer(8 * n)
+    assert dev.syscall_dispatch(d, n, record_size=dev.SYSCALL_RECORD_TIMED, out=out) == 0
+    assert (out.download(np.int64) == o.dispatch(recs)).all()
+    assert ddata.hash_items() == odata.items()
+    assert dstart.hash_items() == ostart.items()
+
+
+def test_big_stack_callbacks_run_in_cpp(fresh_oracle, fresh_runtime):
+    """A callback whose stack exceeds the LDS stacks (kLdsStackMax) keeps the
+    C++ tier and its private stack: a start[tid] pair keyed through fp-200."""
+    po, dev = fresh_oracle, fresh_runtime
+    (ostart, osum), (dstart, dsum) = make_maps([(HASH, 4, 8, 1024), (ARRAY, 4, 16, 1)], po, dev)
+    enter = (Asm().call(isa.BPF_FUNC_get_current_pid_tgid).stx(4, 10, -200, "r0").ldx(8, 3, 1, 16)
+             .stx(8, 10, -192, "r3").ld_map_fd(1, dstart.fd).mov64(2, "r10").add64(2, -200)
+             .mov64(3, "r10").add64(3, -192).mov64(4, 0).call(isa.BPF_FUNC_map_update_elem)
+             .mov64(0, 0).exit().assemble())
+    exit_ = (Asm().call(isa.BPF_FUNC_get_current_pid_tgid).stx(4, 10, -200, "r0").ld_map_fd(1, dstart.fd)
+             .mov64(2, "r10").add64(2, -200).call(isa.BPF_FUNC_map_lookup_elem).jmp("jeq", 0, 0, "out")
+             .ldx(8, 3, 0, 0).ld_map_value(2, dsum.fd, 0).atomic(8, isa.ATOMIC_ADD, 2, 0, 3)
+             .label("out").mov64(0, 0).exit().assemble())
+    o = po.OracleSyscallDispatch()
+    _attach(dev, o, enter, -1, True)
+    _attach(dev, o, exit_, -1, False)
+    assert dev.syscall_dispatch_plan() == 1
+    n = 1 << 16
+    recs = gen.syscall_records_timed(n, threads=128)
+    d = dev.DeviceBuffer.from_array(recs)
+    assert dev.syscall_dispatch(d, n, record_size=dev.SYSCALL_RECORD_TIMED) == 0
+    o.dispatch(recs)
+    assert dsum.lookup(b"\0" * 4) == osum.lookup(b"\0" * 4)
+    assert dstart.hash_items() == ostart.items()
+
+
 def test_tid_state_pair_threads_vs_programs(fresh_oracle, fresh_runtime):
     po, dev = fresh_oracle, fresh_runtime
     (ostart, osum), (dstart, dsum) = make_maps([(HASH, 4, 8, 1024), (ARRAY, 4, 16, 1)], po, dev)
