@@ -1412,20 +1412,47 @@ __global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
     return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
   };
+  // A record's fields, loaded one record ahead: a lane's records are a chain
+  // of dependent memory round trips otherwise (its index, then the fields),
+  // which nothing else on the CU hides when the threads are few.  The index
+  // is loaded two records ahead.
+  const SysLayout &L = p.lay;
+  struct Rec {
+    uint64_t idx, pid, kt_e, kt_x;
+    int64_t nr, ret;
+    uint64_t args[6];
+  };
+  auto perm_at = [&](uint64_t kk) -> uint64_t { return kk < end ? (p.perm ? (uint64_t)p.perm[kk] : kk) : 0; };
+  auto fetch = [&](uint64_t kk, uint64_t idx) {
+    Rec f;
+    const bool h = kk < end;
+    const uint8_t *en = L.enter ? L.enter + idx * L.estride : nullptr;
+    const uint8_t *ex = L.exit ? L.exit + idx * L.xstride : nullptr;
+    const uint8_t *ck = L.clock ? L.clock + idx * L.cstride : nullptr;
+    f.idx = idx;
+    f.nr = h ? *(const int64_t *)((en ? en : ex) + 8) : 0;
+    f.ret = h && ex ? *(const int64_t *)(ex + 16) : 0;
+    f.pid = h && L.pid ? *(const uint64_t *)(L.pid + idx * L.pstride) : p.pid_tgid;
+    // (the recorded clocks at sys_enter and after the call)
+    f.kt_e = h && ck ? *(const uint64_t *)ck : 0;
+    f.kt_x = h && ck ? *(const uint64_t *)(ck + 8) : 0;
+    for (int w = 0; w < 6; w++) f.args[w] = h && en ? *(const uint64_t *)(en + 16 + 8 * w) : 0;
+    return f;
+  };
+  uint64_t idx_next = perm_at(k + 1);
+  Rec cur = fetch(k, perm_at(k));
   while (__ballot(k < end) != 0) {
     uint64_t sp_r = SP_NOW();
     (void)sp_r;
     const bool has = k < end;
-    const uint64_t idx = has ? (p.perm ? (uint64_t)p.perm[k] : k) : 0;
-    const SysLayout &L = p.lay;
-    const uint8_t *ent = L.enter ? L.enter + idx * L.estride : nullptr;
-    const uint8_t *ext = L.exit ? L.exit + idx * L.xstride : nullptr;
-    const uint8_t *clk = L.clock ? L.clock + idx * L.cstride : nullptr;
-    const int64_t nr = has ? *(const int64_t *)((ent ? ent : ext) + 8) : 0;
-    const int64_t ret = has && ext ? *(const int64_t *)(ext + 16) : 0;
-    const uint64_t pid = has && L.pid ? *(const uint64_t *)(L.pid + idx * L.pstride) : p.pid_tgid;
-    // (the recorded clocks at sys_enter and after the call)
-    const uint64_t kt_e = has && clk ? *(const uint64_t *)clk : 0, kt_x = has && clk ? *(const uint64_t *)(clk + 8) : 0;
+    // the next record's fields and the index after it, issued before this
+    // record's callbacks run
+    const uint64_t idx_next2 = perm_at(k + 2);
+    const Rec nxt = fetch(k + 1, idx_next);
+    const uint64_t idx = cur.idx;
+    const int64_t nr = cur.nr, ret = cur.ret;
+    const uint64_t pid = cur.pid, kt_e = cur.kt_e, kt_x = cur.kt_x;
+    const bool clk = L.clock != nullptr;
     const bool live = has && nr != 60 && nr != 231;  // :23-26
     ovr_st[tid] = 0;
     ovr_v[tid] = 0;
@@ -1441,7 +1468,7 @@ __global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
         ctx[0] = 0;
         ctx[1] = (uint64_t)nr;
         if (enter) {
-          for (int w = 2; w < 8; w++) ctx[w] = ent ? *(const uint64_t *)(ent + 8 * w) : 0;
+          for (int w = 2; w < 8; w++) ctx[w] = cur.args[w - 2];
         } else {
           ctx[2] = (uint64_t)ret;
           for (int w = 3; w < 8; w++) ctx[w] = 0;
@@ -1540,7 +1567,7 @@ __global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
           env.ovr_val = &ovr_v[tid];
           env.ovr_bit = enter ? 1 : 2;
           env.pid_tgid = pid;
-          env.kt_on = clk != nullptr;
+          env.kt_on = clk;
           env.ktime = enter ? kt_e : kt_x;
           uint32_t cerr = E_OK;
           uint64_t *R = c.R;
@@ -1576,7 +1603,11 @@ __global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
     }
     SP_ADD(7, SP_NOW() - sp_r);  // the record's tail (out store, loop)
     if (has && p.out) p.out[idx] = ovr_st[tid] ? ovr_v[tid] : ret;
-    if (has) k++;
+    if (has) {
+      k++;
+      cur = nxt;
+      idx_next = idx_next2;
+    }
   }
 #ifdef BPFTIME_AMD_SEQ_PROF
   sp_acc[0] = SP_NOW() - sp_t0;
