@@ -484,15 +484,18 @@ class Gen:
         every lane adds the same value (a counter += constant), lanes that
         share the first lane's address are folded into one add of
         popcount * value by that lane, up to four distinct addresses per
-        wave (Zipf-hot keys put most of a wave on a few map values); the
-        rest add lane by lane (comb_add).  Masks survive comb_add in lanes
-        of v56."""
+        wave (Zipf-hot keys put most of a wave on a few map values); when
+        the values differ (a sum of latencies), the lanes sharing an address
+        fold their values' sum the same way, summed lane by lane in SGPRs;
+        the rest add lane by lane (comb_add).  Masks survive comb_add in
+        lanes of v56."""
         loop, rest, out = self.label("pl"), self.label("pr"), self.label("po")
+        dloop, dsum = self.label("pdl"), self.label("pds")
         self.e("v_writelane_b32 v56, exec_lo, 2", "v_writelane_b32 v56, exec_hi, 3",
                "v_readfirstlane_b32 s64, v46", "v_readfirstlane_b32 s65, v47",
                "v_cmp_ne_u64 s[54:55], s[64:65], v[46:47]",
-               "s_cmp_lg_u64 s[54:55], 0", f"s_cbranch_scc1 {rest}",       # values differ
                "s_mov_b32 s85, 0",
+               "s_cmp_lg_u64 s[54:55], 0", f"s_cbranch_scc1 {dloop}",      # values differ
                f"{loop}:",
                "s_ff1_i32_b64 s69, exec",
                "v_readlane_b32 s62, v48, s69", "v_readlane_b32 s63, v49, s69",
@@ -510,6 +513,32 @@ class Gen:
                "s_mov_b64 exec, s[56:57]",
                f"s_cbranch_execz {out}",
                "s_add_u32 s85, s85, 1", "s_cmp_lt_u32 s85, 4", f"s_cbranch_scc1 {loop}",
+               f"s_branch {rest}")
+        # values differ: the first lane's address group adds the sum of its
+        # lanes' values (s[66:67], a scalar loop over the group), up to four
+        # groups; groups of one lane end the folding
+        self.e(f"{dloop}:",
+               "s_ff1_i32_b64 s69, exec",
+               "v_readlane_b32 s62, v48, s69", "v_readlane_b32 s63, v49, s69",
+               "v_cmp_eq_u64 s[54:55], s[62:63], v[48:49]",
+               "s_bcnt1_i32_b64 s70, s[54:55]",
+               "s_cmp_lt_u32 s70, 2", f"s_cbranch_scc1 {rest}",             # no sharing left
+               "s_andn2_b64 s[56:57], exec, s[54:55]",
+               "v_writelane_b32 v56, s56, 0", "v_writelane_b32 v56, s57, 1",
+               "s_mov_b32 s66, 0", "s_mov_b32 s67, 0",
+               f"{dsum}:",
+               "s_ff1_i32_b64 s70, s[54:55]",
+               "v_readlane_b32 s64, v46, s70", "v_readlane_b32 s65, v47, s70",
+               "s_add_u32 s66, s66, s64", "s_addc_u32 s67, s67, s65",
+               "s_bitset0_b64 s[54:55], s70",
+               "s_cmp_lg_u64 s[54:55], 0", f"s_cbranch_scc1 {dsum}",
+               "s_lshl_b64 exec, 1, s69",                                   # the first lane adds for all
+               "v_mov_b32 v46, s66", "v_mov_b32 v47, s67")
+        self.comb_add(sz, direct_only)
+        self.e("v_readlane_b32 s56, v56, 0", "v_readlane_b32 s57, v56, 1",
+               "s_mov_b64 exec, s[56:57]",
+               f"s_cbranch_execz {out}",
+               "s_add_u32 s85, s85, 1", "s_cmp_lt_u32 s85, 4", f"s_cbranch_scc1 {dloop}",
                f"{rest}:")
         self.comb_add(sz, direct_only)
         self.e(f"{out}:", "v_readlane_b32 s56, v56, 2", "v_readlane_b32 s57, v56, 3",
