@@ -358,6 +358,9 @@ constexpr uint32_t kSeqMaxProgs = 64;  // attached programs a thread-ordered dis
 // (pid_tgid) and the clock of the callback's phase, read by the asm tier's
 // CALL_REC handler (loader.cpp link_fast rec_helpers)
 constexpr uint32_t kSeqPidOff = 64, kSeqClockOff = 72, kSeqCtxWords = 10;
+// threads up to which the thread-ordered dispatch runs its callbacks in the
+// asm tier (vm_api.cpp seq_dispatch)
+constexpr uint64_t kSeqAsmThreads = 16384;
 struct SeqParams {
   uint32_t nprogs;
   // the records' fields (include/bpftime_amd.h: 64- / 96- / 128-B records or

@@ -1158,10 +1158,14 @@ int64_t seq_dispatch(const std::vector<SeqAttach> &progs, const SysLayout &lay, 
   std::vector<int> lpm_w;
   uint32_t lpm_updates = 0;
   uint64_t steps = 0;
-  // the asm tier runs the callbacks when every stack fits the LDS stacks
-  // (BPFTIME_AMD_SEQ_ASM=0: the C++ tier, for comparison)
+  // the asm tier runs the callbacks when every stack fits the LDS stacks and
+  // the threads are at most kSeqAsmThreads: measured (profiles/
+  // r06_seq_xover.txt, syscount's pair) 2-3.7x the C++ tier up to 8192
+  // threads, even at 16384, and behind it from 32768 on, where the waves no
+  // longer wait on their own latency chains and the map helpers' coherent
+  // atomics set the rate.  BPFTIME_AMD_SEQ_ASM=1 / 0 forces a tier.
   const char *asm_env = getenv("BPFTIME_AMD_SEQ_ASM");
-  bool fast = !(asm_env && asm_env[0] == '0');
+  bool fast = asm_env && asm_env[0] ? asm_env[0] != '0' : nseg <= kSeqAsmThreads;
   // constant-address loads (loader.cpp const_loads: array storage nothing in
   // THAT program writes) stay scalar-cache loads only while no attached
   // program writes or adds to an array map: one launch runs them all

