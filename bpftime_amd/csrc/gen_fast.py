@@ -179,6 +179,7 @@ def handler_ids():
     for sz in (1, 2, 4, 8):  # the lane's own LDS XDP ctx at a static offset
         ids += [f"LDX{sz}_CTX", f"STX{sz}_CTX", f"ST{sz}_CTX"]
     ids += ["CALL_REC"]  # thread-ordered dispatch: the caller / clock beside the ctx copy
+    ids += ["CALL_UPDATE_STK"]  # HASH update of a key every lane finds, key and value on the stack
     return ids
 
 
@@ -1038,7 +1039,35 @@ class Gen:
                f"v_cmp_ne_u64 s[54:55], s[{slo}:{shi_}], v[{lo}:{hi}]",
                "s_cmp_lg_u64 s[54:55], 0", f"s_cbranch_scc1 {L('slow')}")
 
-    def call_lookup(self, stack_key=False):
+    def call_update_stk(self):
+        """bpf_map_update_elem of a HASH map, key and value on the stack
+        (loader.cpp: w6 / w2 their offsets from the stack top, w7 the value's
+        dwords): when every lane finds its key (the lookup's probe), the
+        value is overwritten in place and r0 = 0 (fix_hash_map.cpp:34-39:
+        the flags are not looked at; dev_helpers.hpp helper_update).  A new
+        key, an in-flight insert, and a wave with a lane whose lookup of a
+        key just missed (entry bit 8: the lookup-or-init race rule, which
+        the C++ helper keeps) leave for C++ before anything is written."""
+        self.e("s_bitcmp1_b32 %[entry], 8", f"s_cbranch_scc1 {L('slow')}")
+        self.call_lookup(stack_key=True, update=True)
+
+    def update_tail(self):
+        """r0 = the found element's value in every lane: the value's dwords
+        from the stack over it, then r0 = 0."""
+        loop = self.label("upd")
+        self.e("v_add_u32 v41, s42, %[stklo]",                             # the value on the stack
+               f"v_mov_b32 v48, v{R0}", f"v_mov_b32 v49, v{R0 + 1}",
+               "s_mov_b32 s69, s47",
+               f"{loop}:",
+               "ds_read_b32 v44, v41", "s_waitcnt lgkmcnt(0)",
+               "global_store_dword v[48:49], v44, off",
+               "v_add_u32 v41, 4, v41",
+               "v_add_co_u32 v48, vcc, 4, v48", "v_addc_co_u32 v49, vcc, 0, v49, vcc",
+               "s_sub_u32 s69, s69, 1", "s_cmp_lg_u32 s69, 0", f"s_cbranch_scc1 {loop}",
+               "s_waitcnt vmcnt(0)",
+               f"v_mov_b32 v{R0}, 0", f"v_mov_b32 v{R0 + 1}, 0")
+
+    def call_lookup(self, stack_key=False, update=False):
         """bpf_map_lookup_elem with a wave-uniform map fd.
         ARRAY (array_map.cpp:27-40): r0 = key < max_entries ? &data[key * vsz] : 0.
         HASH with its key on the stack (stack_key: the loader proved r2 =
@@ -1069,6 +1098,10 @@ class Gen:
                    "ds_read_b32 v44, v41", "ds_read_b32 v45, v41 offset:4",
                    "ds_read_b32 v46, v41 offset:8", "ds_read_b32 v47, v41 offset:12")
         self.e("s_waitcnt lgkmcnt(0)")
+        if update:
+            self.e("s_cmp_lg_u32 s72, 1", f"s_cbranch_scc1 {L('slow')}")       # BPF_MAP_TYPE_HASH only
+            self.hash_lookup(update=True)
+            return
         if stack_key:
             hsh, lpm = self.label("hash"), self.label("lpm")
             self.e("s_cmp_eq_u32 s72, 1", f"s_cbranch_scc1 {hsh}",          # BPF_MAP_TYPE_HASH
@@ -1387,7 +1420,7 @@ class Gen:
         self.e(f"s_branch {bail}",
                f"{fail}:", "s_mov_b64 exec, s[60:61]")
 
-    def hash_lookup(self):
+    def hash_lookup(self, update=False):
         done, bail = self.label("hdone"), self.label("hbail")
         # DMap words 4-11 (s[64:71], loaded by call_lookup): data,
         # nbuckets, ix_mask, slot_size, key_off, val_off, ncpu; words 14-15
@@ -1443,6 +1476,8 @@ class Gen:
         self.e(f"s_branch {L('slow')}",
                f"{bail}:", "s_mov_b64 exec, s[76:77]", f"s_branch {L('slow')}",
                f"{done}:", "s_mov_b64 exec, s[76:77]")
+        if update:
+            self.update_tail()
         self.next_seq()
 
     def counter_cache(self, sz, done):
@@ -2434,6 +2469,8 @@ class Gen:
                 self.call_pid()
             elif name == "CALL_REC":
                 self.call_rec()
+            elif name == "CALL_UPDATE_STK":
+                self.call_update_stk()
             elif name == "KLDX":
                 self.ldxk()
             elif name.startswith("RMWD"):

@@ -923,6 +923,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
       if (uni) {
         // chain only from a unit every lane of the wave runs without a failure
         const bool whole = __ballot(c.alive) == ~0ull && __ballot(c.err != E_OK) == 0 && __ballot(parked) == 0;
+        // entry bit 8: a lane's lookup just missed (the lookup-or-init race
+        // rule of helper_update): its map updates stay in the C++ helper
+        fu.entry = (fu.entry & ~256u) | (__ballot(miss_fd >= 0) != 0 ? 256u : 0u);
         uint32_t adv = 0;
         const uint32_t why = run_fast<G>(c, fe, fu, whole ? fu.chain : 0u, adv);
         fu.entry &= ~1u;
@@ -1514,6 +1517,7 @@ __global__ __launch_bounds__(kBlock) void k_sys_seq(SeqParams p) {
         uint32_t r;
         if (fast && uni) {
           uint32_t adv = 0;
+          fu.entry = (fu.entry & ~256u) | (__ballot(miss_fd >= 0) != 0 ? 256u : 0u);  // (k_interp)
           const uint32_t why = run_fast<false>(c, fe, fu, 0u, adv);
           fu.entry &= ~1u;  // re-entries read the registers from their LDS columns
           if (why == FAST_EXIT) {  // every running lane ran exit

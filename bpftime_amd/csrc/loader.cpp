@@ -1514,6 +1514,26 @@ void build_fast(const LoadOut &lo, bool xdp, FastForm &out) {
         }
         continue;
       }
+      if (d.hi == 2) {
+        // update of a HASH map with key and value on the stack (gen_fast.py
+        // call_update_stk): an element every lane finds is overwritten in
+        // asm; anything else (a new key, a lane whose lookup of the key just
+        // missed: the lookup-or-init race rule) runs the C++ helper
+        const PVal key = st[2], val = st[3];
+        const MapRec *m = st[1].kind == P_MAPFD ? map_rec(st[1].id) : nullptr;
+        const int64_t ka = (int64_t)key.k, va = (int64_t)val.k;
+        if (m && m->type == MT_HASH && !big_stack && m->key_size % 4 == 0 && m->key_size <= 16 &&
+            m->value_size % 4 == 0 && m->value_size > 0 && m->value_size <= 64 && key.kind == P_STK &&
+            ka >= -stack_size && ka + m->key_size <= 0 && ka % 4 == 0 && val.kind == P_STK &&
+            va >= -stack_size && va + m->value_size <= 0 && va % 4 == 0 && !getenv("BPFTIME_AMD_NO_ASM_UPDATE")) {
+          f.hoff = 4 + 4 * F_CALL_UPDATE_STK;
+          f.target = (uint32_t)(int32_t)ka;  // (w6: the key's offset from the stack top)
+          f.imm = va;                         // (w2: the value's)
+          f.aux = (int32_t)(m->value_size / 4);
+          nspec++;
+        }
+        continue;
+      }
       if (d.hi != 1) continue;
       // lookup with its key on the stack: key read straight from LDS; an
       // ARRAY map bound at load needs no map-table read at all
@@ -1781,6 +1801,9 @@ void link_fast(const FastForm &f, uint32_t head, uint32_t stage, bool ordered, c
   // an unwind helper (ebpf_set_unwind_function_index) is called from the
   // C++ tier, which ends the unit when it returns 0: map_lookup_elem leaves
   // its asm handlers then
+  if (unwind_idx == 2)
+    for (size_t i = 0; i < prog.size() && i < out.size(); i++)
+      if (prog[i].op == X_CALL && prog[i].hi == 2) out[i].hoff = 4 + 4 * F_SLOW;
   if (unwind_idx == 1)
     for (size_t i = 0; i < prog.size() && i < out.size(); i++)
       if (prog[i].op == X_CALL && prog[i].hi == 1) {

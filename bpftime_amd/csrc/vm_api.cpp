@@ -103,11 +103,13 @@ struct Image {
     const uint64_t key = ((uint64_t)xdp << 63) | ((uint64_t)ordered << 62) | ((uint64_t)uw << 61) |
                          ((uint64_t)(lc_sets & 0x1fff) << 47) | ((uint64_t)stage << 40) | ((uint64_t)po << 32) |
                          (stage ? head : 0);
-    const auto lk = std::make_pair(key, (uint32_t)no_kldx | ((uint32_t)rec_helpers << 1));
+    const bool uwu = unwind_idx == 2;  // (map_update_elem's asm handler)
+    const auto lk = std::make_pair(key, (uint32_t)no_kldx | ((uint32_t)rec_helpers << 1) | ((uint32_t)uwu << 2));
     auto it = links.find(lk);
     if (it != links.end()) return it->second;
     std::vector<FInsn> out;
-    link_fast(xdp ? fx : fr, head, stage, ordered, prog.prog, out, uw ? 1 : -1, lc_sets, po, no_kldx, rec_helpers);
+    link_fast(xdp ? fx : fr, head, stage, ordered, prog.prog, out, uw ? 1 : uwu ? 2 : -1, lc_sets, po, no_kldx,
+              rec_helpers);
     if (getenv("BPFTIME_AMD_DUMP_FAST"))  // the linked threaded form, one FInsn a line
       for (size_t i = 0; i < out.size(); i++)
         fprintf(stderr, "bpftime_amd: fast %3zu %-18s w1 %08x imm %llx dst %u src %u tgt %u aux %x\n", i,

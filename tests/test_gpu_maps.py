@@ -536,3 +536,48 @@ def test_keyed_index_inserts_and_lookups(fresh_oracle, fresh_runtime, ksz):
         np.testing.assert_array_equal(dv.download(np.uint32), want)
         assert dm.hash_items() == om.items()
     assert len(om.items()) == len(set(pick.tolist())) and (pick == 0).sum() > 1000
+
+
+@pytest.mark.parametrize("present", [1.0, 0.5])
+def test_hash_update_existing_keys_in_asm(fresh_oracle, fresh_runtime, present):
+    """bpf_map_update_elem of a HASH map with key and value on the stack
+    (gen_fast.py call_update_stk): a wave whose lanes all find their key
+    overwrites the values in asm; new keys, and a lane whose lookup of the
+    key just missed (the lookup-or-init race rule), take the C++ helper.
+    Each unit updates its own key (unit index % keys) with 16 bytes of its
+    data, then looks the key up, reads the value back and returns it: every
+    map value and every return bit-exact against the oracle.  present: the
+    fraction of keys inserted by the host first."""
+    po, dev = fresh_oracle, fresh_runtime
+    n = 4096
+    (om,), (dm,) = make_maps([(isa.BPF_MAP_TYPE_HASH, 4, 16, 2 * n)], po, dev)
+    for k in range(int(n * present)):
+        key, val = struct.pack("<I", k), struct.pack("<QQ", 7 * k, k)
+        assert om.update(key, val) == 0 and dm.update(key, val) == 0
+    a = Asm()
+    a.ldx(4, 2, 1, 0).stx(4, 10, -4, "r2")                 # key = unit word 0
+    a.ldx(8, 3, 1, 8).stx(8, 10, -24, "r3")                # value = unit bytes 8..23
+    a.ldx(8, 3, 1, 16).stx(8, 10, -16, "r3")
+    a.ld_map_fd(1, dm.fd).mov64(2, "r10").add64(2, -4).mov64(3, "r10").add64(3, -24).mov64(4, 0)
+    a.call(isa.BPF_FUNC_map_update_elem)
+    a.mov64(6, "r0")
+    a.ld_map_fd(1, dm.fd).mov64(2, "r10").add64(2, -4).call(isa.BPF_FUNC_map_lookup_elem)
+    a.jmp("jeq", 0, 0, "miss")
+    a.ldx(8, 0, 0, 8).alu64("add", 0, "r6").exit()
+    a.label("miss").mov64(0, 99).exit()
+    code = a.assemble()
+    units = np.zeros((n, 32), dtype=np.uint8)
+    w = units.view(np.uint32)
+    w[:, 0] = np.arange(n, dtype=np.uint32)
+    units.view(np.uint64)[:, 1] = gen.sm64(11, np.arange(n, dtype=np.uint64))
+    units.view(np.uint64)[:, 2] = gen.sm64(12, np.arange(n, dtype=np.uint64))
+    ovm = po.OracleVM()
+    ovm.load(code)
+    orets = ovm.run_raw(units.copy(), 32)
+    vm = dev.VM()
+    vm.load(code)
+    d = dev.DeviceBuffer.from_array(units)
+    dr = dev.DeviceBuffer(8 * n)
+    assert vm.exec_batch(dev.CTX_RAW, d, n, 32, fixed_len=32, rets=dr, flags=dev.BATCH_SYNC) == 0
+    np.testing.assert_array_equal(dr.download(np.uint64), orets)
+    assert dm.hash_items() == om.items()
