@@ -317,9 +317,17 @@ def main():
     nall = max(1, min(args.cores or len(cores), len(cores)))
     unit = "Mrec/s" if args.workload in ("syscall-agg", "syscount", "syscount-latency") else "Mpps"
     bits = SAMPLE[args.workload].bit_length() - 1
-    # (i) one pinned core
-    done1, secs1, ok1, _ = _worker((args.workload, 0, cores[0], args.seconds, RING_LOG2))
-    single = done1 / secs1 / 1e6
+    # (i) one pinned core: the better of two (the first core of the affinity
+    # and the last of the 16-process leg, half the time each), so that one
+    # core busy with the host's own work does not set the per-core rate the
+    # other legs are checked against
+    c1 = [cores[0]] + ([cores[min(16, nall) - 1]] if min(16, nall) > 1 else [])
+    single, secs1, ok1, core1 = 0.0, 0.0, True, cores[0]
+    for c in c1:
+        done_c, secs_c, ok_c, _ = _worker((args.workload, 0, c, args.seconds / len(c1), RING_LOG2))
+        ok1 = ok1 and ok_c
+        if done_c / secs_c / 1e6 > single:
+            single, secs1, core1 = done_c / secs_c / 1e6, secs_c, c
     # (ii) 16 pinned processes (the GPU box's CPU share per GPU), (iii) one per
     # core this process may use (nproc; tools/bpftimetool/main.cpp:42-58 runs
     # the CPU path on every core)
@@ -361,7 +369,8 @@ def main():
                       "sample": "one pinned oracle process per core in the affinity, %.1f s of timed loops (union), "
                                 "%.1f s wall" % (loopn, walln)},
         "single_core": {"value": round(single, 3), "unit": unit, "cores": 1,
-                        "sample": "1 oracle thread pinned to core %d, %.1f s" % (cores[0], secs1)},
+                        "sample": "1 oracle thread pinned to core %d (the better of cores %s), %.1f s"
+                                  % (core1, "/".join(str(c) for c in c1), secs1)},
         "ok": ok,
     }
     print(json.dumps(out))
