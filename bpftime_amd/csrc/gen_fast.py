@@ -2368,8 +2368,11 @@ class Gen:
         e(f"{loaded}:",
           "s_getpc_b64 s[50:51]",          # = address of the s_branch below
           f"s_branch {L('start')}")
+        # (BPFTIME_AMD_EXTRA_HOP=1 at generation: a second branch per dispatch,
+        # an A/B of what the table's hop costs; never the default)
+        hop = os.environ.get("BPFTIME_AMD_EXTRA_HOP") == "1"
         for name in ids:                   # table: entry i at TB + 4 + 4*i
-            e(f"s_branch {L('h_' + name)}")
+            e(f"s_branch {L(('x_' if hop else 'h_') + name)}")
         for name in ids:                   # divergent table: TB + 4N + 4 + 4*i
             e(f"s_branch {L('d_' + name)}")
         # divergent dispatch: the running group has reached the first
@@ -2377,6 +2380,9 @@ class Gen:
         for name in ids:
             e(f"{L('d_' + name)}:", "s_cmp_ge_u32 s48, s86", f"s_cbranch_scc1 {L('dswitch')}",
               f"s_branch {L('h_' + name)}")
+        if hop:
+            for name in ids:
+                e(f"{L('x_' + name)}:", f"s_branch {L('h_' + name)}")
         e(f"{L('start')}:")
         self.dispatch()
         # ---- handlers ----
