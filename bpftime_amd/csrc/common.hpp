@@ -17,6 +17,9 @@ constexpr uint32_t kMaxInsts = 65536;   // vm/vm-core/include/ebpf-vm.h:33-35
 constexpr uint32_t kStackSize = 512;    // ebpf-vm.h:47-49
 constexpr uint32_t kMaxFds = 1024;      // device map table size
 constexpr uint32_t kBlock = 256;        // threads per workgroup (4 waves)
+// KParams::dbg bit of the host linker's query launch (bpftime_amd_launch_fast_xlat):
+// the kernel writes the asm tier's handler offsets and returns
+constexpr uint32_t kDbgXlat = 1u << 30;
 constexpr uint32_t kLdsStackMax = 64;   // per-lane stack bytes kept in LDS
 constexpr uint32_t kComb = 256;         // per-block LDS combining entries (counter adds), minimum
 constexpr uint32_t kCombMax = 4096;     // ... and maximum (a multiple of 8 in between, vm_api.cpp)

@@ -68,7 +68,7 @@ budget (v40..v101 -> v66..v127):
                target IP / static offset / continuation IP, w7 imm32 (ST, RMW)
                or byte mask (staged stores)
   s48 IP (byte offset of the current FInsn from PROG)   s49 scratch
-  s[50:51] TB  table base - 4                    s[52:53] T scratch / target
+  s[50:51] TB  handler base + 8 (divergent: + 0)   s[52:53] T scratch / target
   s[54:55], s[56:57], s[60:61] masks             s[58:59] saved exec
   s[62:63] A0 (wave-uniform address)             s[64:65] V0 (uniform value)
   s[66:67] TOT (wave total)                      s68 exit reason
@@ -2184,11 +2184,12 @@ class Gen:
     # the asm does not run, hands every group's pc to the C++ divergent loop
     # (exit reason 3).
     def set_table(self, divergent):
-        n4 = 4 * len(handler_ids())
+        """Dispatch into the handlers' divergent stubs (8 bytes in front of
+        each handler) or straight into the handlers."""
         if divergent:
-            self.e(f"s_add_u32 s50, s50, {n4}", "s_addc_u32 s51, s51, 0")
+            self.e("s_sub_u32 s50, s50, 8", "s_subb_u32 s51, s51, 0")
         else:
-            self.e(f"s_sub_u32 s50, s50, {n4}", "s_subb_u32 s51, s51, 0")
+            self.e("s_add_u32 s50, s50, 8", "s_addc_u32 s51, s51, 0")
 
     def pop0(self):
         keep = self.label("keep")
@@ -2292,8 +2293,18 @@ class Gen:
           "s_mov_b64 s[78:79], %[prog]",
           "v_mov_b32 v40, %[rb]",
           "s_lshl_b32 s48, %[pc], 5",
-          "s_mov_b64 s[58:59], exec", "s_mov_b64 exec, %[alive]",
-          "s_mov_b32 s80, 0", "s_mov_b32 s81, 0", "s_mov_b32 s84, 0", "s_mov_b32 s92, 0",
+          "s_mov_b64 s[58:59], exec", "s_mov_b64 exec, %[alive]")
+        # the host linker's query (entry = ~0, which no unit's entry is: its
+        # RAW and SYSCALL bits exclude each other): every handler's offset
+        # from the handler base, u32 per id at the vaddr operand
+        # (vm_api.cpp fast_xlat), then out
+        nq = self.label("nq")
+        e("s_cmp_eq_u32 %[entry], -1", f"s_cbranch_scc0 {nq}")
+        for i, name in enumerate(handler_ids()):
+            e(f"v_mov_b32 v56, ({L('d_' + name)} - {L('hbase')})",
+              f"global_store_dword %[vaddr], v56, off offset:{4 * i}")
+        e("s_mov_b32 s48, 0", "s_mov_b32 s68, 0", f"s_branch {L('done')}", f"{nq}:")
+        e("s_mov_b32 s80, 0", "s_mov_b32 s81, 0", "s_mov_b32 s84, 0", "s_mov_b32 s92, 0",
           "s_mov_b32 s86, -1", "s_mov_b32 s87, -1", "s_mov_b32 s93, -1",
           "v_mov_b32 v52, %[slotlo]", "v_mov_b32 v53, %[slothi]",
           "s_bitcmp1_b32 %[entry], 0", f"s_cbranch_scc1 {fresh}")
@@ -2365,30 +2376,29 @@ class Gen:
           "s_mov_b64 exec, s[60:61]",
           f"s_cbranch_execnz {loaded}",
           "s_mov_b32 s84, 0", f"s_branch {L('chain')}")                  # every lane an exit record
+        # Direct dispatch: an FInsn's handler offset (and the next one's, in
+        # w1) is its handler's divergent stub's distance from the 64-aligned
+        # handler base (the host linker learns the distances from the asm
+        # itself: the query above); each stub is 8 bytes in front of its
+        # handler, so s[50:51] = base + 8 jumps straight into handlers and
+        # base + 0 (set_table, while lane groups are pending) into the stubs.
+        here = self.label("here")
         e(f"{loaded}:",
-          "s_getpc_b64 s[50:51]",          # = address of the s_branch below
+          "s_getpc_b64 s[50:51]",
+          f"{here}:",
+          f"s_add_u32 s50, s50, ({L('hbase')} - {here} + 8)",
+          "s_addc_u32 s51, s51, 0",
           f"s_branch {L('start')}")
-        # (BPFTIME_AMD_EXTRA_HOP=1 at generation: a second branch per dispatch,
-        # an A/B of what the table's hop costs; never the default)
-        hop = os.environ.get("BPFTIME_AMD_EXTRA_HOP") == "1"
-        for name in ids:                   # table: entry i at TB + 4 + 4*i
-            e(f"s_branch {L(('x_' if hop else 'h_') + name)}")
-        for name in ids:                   # divergent table: TB + 4N + 4 + 4*i
-            e(f"s_branch {L('d_' + name)}")
-        # divergent dispatch: the running group has reached the first
-        # pending group's IP (s86) -> dswitch; else straight to the handler
-        for name in ids:
-            e(f"{L('d_' + name)}:", "s_cmp_ge_u32 s48, s86", f"s_cbranch_scc1 {L('dswitch')}",
-              f"s_branch {L('h_' + name)}")
-        if hop:
-            for name in ids:
-                e(f"{L('x_' + name)}:", f"s_branch {L('h_' + name)}")
         e(f"{L('start')}:")
         self.dispatch()
-        # ---- handlers ----
+        # ---- handlers, each behind its divergent stub: the running group
+        # has reached the first pending group's IP (s86) -> dswitch, else on
+        # into the handler ----
+        e(".p2align 6", f"{L('hbase')}:")
         for name in ids:
             if HANDLER_ALIGN:
                 e(f".p2align {HANDLER_ALIGN}")
+            e(f"{L('d_' + name)}:", "s_cmp_ge_u32 s48, s86", f"s_cbranch_scc1 {L('dswitch')}")
             e(f"{L('h_' + name)}:", "s_waitcnt lgkmcnt(0)")  # W of a fall-through fetch
             if name == "SLOW":
                 e(f"s_branch {L('slow')}")

@@ -782,6 +782,11 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const uint32_t chain_bits = (KIND != CTX_XDP ? 8u : 0u) | (KIND == CTX_RAW ? 16u : 0u) | (p.lens ? 32u : 0u) |
                               (KIND == CTX_SYSCALL ? 64u : 0u) | (IMAGE ? 128u : 0u) |
                               (p.step_cpu << 16);
+  // the host linker's query (vm_api.cpp fast_xlat, one unit): the asm block
+  // writes its handlers' offsets (u32 per handler id) at p.verdicts and the
+  // kernel ends (through the one run_fast site, so the block is not inlined
+  // twice)
+  const bool xlat = (p.dbg & kDbgXlat) != 0;
   uint64_t it = 0;
   for (uint64_t u0 = ordered ? 0 : (uint64_t)blockIdx.x * BS; u0 < p.n; u0 += ustep, it++) {
     uint64_t unit, slot, chunk, vcpu;
@@ -927,7 +932,12 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         // rule of helper_update): its map updates stay in the C++ helper
         fu.entry = (fu.entry & ~256u) | (__ballot(miss_fd >= 0) != 0 ? 256u : 0u);
         uint32_t adv = 0;
+        if (xlat) {
+          fu.entry = ~0u;
+          fu.vaddr = (uint64_t)(uintptr_t)p.verdicts;
+        }
         const uint32_t why = run_fast<G>(c, fe, fu, whole ? fu.chain : 0u, adv);
+        if (xlat) return;
         fu.entry &= ~1u;
         if (adv) {  // the asm tier finished `adv` units of this wave and is in the next
           it += adv;
@@ -1664,6 +1674,32 @@ extern "C" hipError_t bpftime_amd_launch_interp(const KParams *p, uint32_t kind,
 #undef LK
 #undef L
   return hipGetLastError();
+}
+
+// One block of the k_interp instance a launch of these parameters runs, in
+// query mode: the asm tier's handler offsets (F_COUNT u32) into d_out
+// (kind, big_stack, greg, image select the instance, as in a launch; the
+// pointers that select it are never read)
+extern "C" hipError_t bpftime_amd_launch_fast_xlat(uint32_t kind, bool big_stack, bool greg, bool image,
+                                                   uint32_t *d_out, hipStream_t stream) {
+  KParams q{};
+  q.dbg = kDbgXlat;
+  q.verdicts = d_out;
+  q.n = 1;  // (one unit, over the output buffer: nothing reads it)
+  q.data = (uint8_t *)d_out;
+  q.data_lo = (uint64_t)(uintptr_t)d_out;
+  q.data_hi = q.data_lo + 64;
+  q.sys_nr = -1;
+  q.unwind_idx = -1;
+  q.pid_off = 0;
+  q.step_limit = 1;
+  q.gregs = greg ? (uint64_t *)d_out : nullptr;
+  q.tail_entry = image ? (const int32_t *)d_out : nullptr;
+  q.stack_size = 8;
+  q.stack_stride = lane_stride(8);
+  q.ctx_stride = lane_stride(kXdpCtxBytes);
+  q.ncpu = 1;
+  return bpftime_amd_launch_interp(&q, kind, big_stack, 1, 0, kBlock, stream);
 }
 
 extern "C" hipError_t bpftime_amd_launch_sys_seq(const SeqParams *p, hipStream_t stream) {

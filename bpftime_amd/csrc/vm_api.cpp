@@ -47,6 +47,37 @@ bool lane_pad() {
   return on;
 }
 
+extern "C" hipError_t bpftime_amd_launch_fast_xlat(uint32_t kind, bool big_stack, bool greg, bool image,
+                                                   uint32_t *d_out, hipStream_t stream);
+
+// The asm tier dispatches straight into its handlers (gen_fast.py: direct
+// dispatch): an FInsn names its handler by the handler's offset from the
+// asm's handler base, not by its id.  The offsets are assembly-time
+// constants of each of the two asm variants (the C++ tier's register copy in
+// LDS or in global memory, k_interp G); the kernel reports them once per
+// process (its query entry), and every linked program is translated from
+// handler ids to them.  Handlers are laid out in id order, so the offsets
+// must rise: anything else fails the link.
+static std::mutex g_xlat_mu;
+static std::vector<uint32_t> g_xlat[2];
+static const std::vector<uint32_t> *fast_xlat(bool greg) {
+  std::lock_guard<std::mutex> g(g_xlat_mu);
+  std::vector<uint32_t> &t = g_xlat[greg ? 1 : 0];
+  if (!t.empty()) return &t;
+  uint32_t *d = nullptr;
+  std::vector<uint32_t> h(F_COUNT, ~0u);
+  bool ok = hipMalloc((void **)&d, 4 * F_COUNT) == hipSuccess &&
+            hipMemset(d, 0xff, 4 * F_COUNT) == hipSuccess &&
+            bpftime_amd_launch_fast_xlat(CTX_RAW, false, greg, false, d, nullptr) == hipSuccess &&
+            hipDeviceSynchronize() == hipSuccess &&
+            hipMemcpy(h.data(), d, 4 * F_COUNT, hipMemcpyDeviceToHost) == hipSuccess;
+  if (d) hipFree(d);
+  for (uint32_t i = 1; ok && i < F_COUNT; i++) ok = h[i] > h[i - 1] && h[i] < (1u << 24);
+  if (!ok) return nullptr;
+  t = std::move(h);
+  return &t;
+}
+
 // experiment counters (BPFTIME_AMD_DBG 512), a device buffer made on first use
 static std::mutex g_dbg_mu;
 static uint64_t *g_dbg = nullptr;  // lookup-cache hit / miss lanes (gen_fast.py lcache_count)
@@ -94,8 +125,10 @@ struct Image {
     if (d_tail_slots) hipFree(d_tail_slots);
     for (auto &kv : links) hipFree(kv.second);
   }
-  const FInsn *linked(bool xdp, uint32_t head, uint32_t stage, bool ordered, int32_t unwind_idx, uint32_t lc_sets,
-                      int32_t pid_off, bool no_kldx = false, bool rec_helpers = false) {
+  // greg: the asm variant of the launch (k_interp G), whose handler offsets
+  // the form is translated to
+  const FInsn *linked(bool greg, bool xdp, uint32_t head, uint32_t stage, bool ordered, int32_t unwind_idx,
+                      uint32_t lc_sets, int32_t pid_off, bool no_kldx = false, bool rec_helpers = false) {
     std::lock_guard<std::mutex> g(link_mu);
     // (the helpers with asm handlers an unwind index changes: lookup, pid_tgid)
     const bool uw = unwind_idx == 1, uwp = unwind_idx == 14;
@@ -104,7 +137,8 @@ struct Image {
                          ((uint64_t)(lc_sets & 0x1fff) << 47) | ((uint64_t)stage << 40) | ((uint64_t)po << 32) |
                          (stage ? head : 0);
     const bool uwu = unwind_idx == 2;  // (map_update_elem's asm handler)
-    const auto lk = std::make_pair(key, (uint32_t)no_kldx | ((uint32_t)rec_helpers << 1) | ((uint32_t)uwu << 2));
+    const auto lk = std::make_pair(key, (uint32_t)no_kldx | ((uint32_t)rec_helpers << 1) | ((uint32_t)uwu << 2) |
+                                            ((uint32_t)greg << 3));
     auto it = links.find(lk);
     if (it != links.end()) return it->second;
     std::vector<FInsn> out;
@@ -115,6 +149,16 @@ struct Image {
         fprintf(stderr, "bpftime_amd: fast %3zu %-18s w1 %08x imm %llx dst %u src %u tgt %u aux %x\n", i,
                 fop_name((out[i].hoff - 4) / 4), out[i].w1, (unsigned long long)out[i].imm, out[i].dst_x2 / 2,
                 out[i].src_x2 / 2, out[i].target / kFastInsnBytes, (unsigned)out[i].aux);
+    // handler ids -> the variant's handler offsets (this FInsn's and, in
+    // w1 bits 8.., the next one's)
+    const std::vector<uint32_t> *xl = fast_xlat(greg);
+    if (!xl) return nullptr;
+    for (FInsn &x : out) {
+      const uint32_t id = (x.hoff - 4) / 4, nid = ((x.w1 >> 8) - 4) / 4;
+      if (x.hoff < 4 || id >= F_COUNT || (x.w1 >> 8) < 4 || nid >= F_COUNT) return nullptr;
+      x.hoff = (*xl)[id];
+      x.w1 = (x.w1 & 0xffu) | ((*xl)[nid] << 8);
+    }
     FInsn *d = nullptr;
     const size_t bytes = out.size() * sizeof(FInsn);
     if (hipMalloc((void **)&d, bytes) != hipSuccess) return nullptr;
@@ -660,7 +704,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
         if (!getenv("BPFTIME_AMD_LCACHE_SETS")) p.lcache = p.lcache ? lcache_sets() : 0;
       }
     }
-    p.fast = im.linked(kind == CTX_XDP, kind == CTX_XDP ? b->head : 0, p.stage, ordered, unwind_helper,
+    p.fast = im.linked(greg, kind == CTX_XDP, kind == CTX_XDP ? b->head : 0, p.stage, ordered, unwind_helper,
                        p.lcache, b->pid_tgid_off);
     if (!p.fast) {
       error = "device upload failed";
@@ -722,7 +766,7 @@ int Mi355xVm::exec_batch(const ebpf_batch *b) {
   p.rxq = b->rx_queue_index;
   p.head = b->head;
   p.checked = (b->flags & EBPF_BATCH_UNCHECKED) ? 0 : 1;
-  if (const char *d = getenv("BPFTIME_AMD_DBG")) p.dbg = (uint32_t)strtoul(d, nullptr, 0);
+  if (const char *d = getenv("BPFTIME_AMD_DBG")) p.dbg = (uint32_t)strtoul(d, nullptr, 0) & ~kDbgXlat;
   if (p.dbg & 512) p.dbg_counts = dbg_counts();
   // every block of the launch must fit the CU's LDS (env overrides of the
   // table / cache sizes included): a launch that needs more fails, named,
@@ -1188,7 +1232,7 @@ int64_t seq_dispatch(const std::vector<SeqAttach> &progs, const SysLayout &lay, 
     auto im = vm->image();
     if (!vm->loaded || !im) return fail("an attached program is not loaded");
     if (vm->has_tail) return fail("an attached program calls bpf_tail_call (program-major dispatch runs it)");
-    const FInsn *f = im->linked(false, 0, 0, true, -1, 0, 0, array_writes && progs.size() > 1, fast);
+    const FInsn *f = im->linked(false, false, 0, 0, true, -1, 0, 0, array_writes && progs.size() > 1, fast);
     if (!f) return fail("device upload failed");
     SeqProg &q = p.progs[p.nprogs++];
     q.prog = im->d_prog;
