@@ -228,13 +228,21 @@ class Gen:
                "s_addc_u32 s53, s51, 0",
                "s_setpc_b64 s[52:53]")
 
-    def jump_taken(self):
+    def jump_taken(self, hsrc):
         """IP = target; a taken jump is the only way back, so the step limit
-        is enforced here."""
+        is enforced here.  The target's handler offset is in this FInsn
+        (`hsrc`: w2 for JA and register jumps, w5 for immediate ones;
+        vm_api.cpp Image::linked), so the jump does not wait for the
+        target's fetch: the handler waits for it on entry, as after
+        next_seq."""
         self.e("s_mov_b32 s48, s46",
                "s_add_u32 %[steps], %[steps], 1",
-               "s_cmp_gt_u32 %[steps], %[limit]", f"s_cbranch_scc1 {L('steps')}")
-        self.dispatch()
+               "s_cmp_gt_u32 %[steps], %[limit]", f"s_cbranch_scc1 {L('steps')}",
+               f"s_mov_b32 s52, {hsrc}",
+               "s_load_dwordx8 s[40:47], s[78:79], s48",
+               "s_add_u32 s52, s50, s52",
+               "s_addc_u32 s53, s51, 0",
+               "s_setpc_b64 s[52:53]")
 
     # ---- register file (VGPRs, indexed by a wave-uniform SGPR) ----
     def idx(self, sreg, modes):
@@ -1027,7 +1035,7 @@ class Gen:
         nt = self.label("nt")
         self.e(f"s_cbranch_vccz {nt}",
                "s_cmp_eq_u64 vcc, exec", f"s_cbranch_scc0 {L('split')}")
-        self.jump_taken()
+        self.jump_taken("s42" if k == "R" else "s45")
         self.e(f"{nt}:")
         self.next_seq()
 
@@ -2452,7 +2460,7 @@ class Gen:
             elif name == "LDDW":
                 self.lddw()
             elif name == "JA":
-                self.jump_taken()
+                self.jump_taken("s42")
             elif name == "CALL_LOOKUP":
                 self.call_lookup()
             elif name in ("CALL_LOOKUP_STK3", "CALL_LOOKUP_AK3"):

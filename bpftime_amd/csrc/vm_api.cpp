@@ -153,11 +153,30 @@ struct Image {
     // w1 bits 8.., the next one's)
     const std::vector<uint32_t> *xl = fast_xlat(greg);
     if (!xl) return nullptr;
+    // jumps also carry their target's handler offset (gen_fast.py
+    // jump_taken): w2 for JA and register compares (their imm is unused),
+    // w5 for immediate compares (their src is unused)
+    std::vector<uint32_t> jt(out.size(), ~0u);
+    for (size_t i = 0; i < out.size(); i++) {
+      const uint32_t id = (out[i].hoff - 4) / 4;
+      if (id != F_JA && (id < F_J64_EQ_R || id > F_J32_SLE_I)) continue;
+      const size_t t = out[i].target / kFastInsnBytes;
+      jt[i] = t < out.size() ? (out[t].hoff - 4) / 4 : (uint32_t)F_SLOW;
+      if (jt[i] >= F_COUNT) return nullptr;
+    }
     for (FInsn &x : out) {
       const uint32_t id = (x.hoff - 4) / 4, nid = ((x.w1 >> 8) - 4) / 4;
       if (x.hoff < 4 || id >= F_COUNT || (x.w1 >> 8) < 4 || nid >= F_COUNT) return nullptr;
       x.hoff = (*xl)[id];
       x.w1 = (x.w1 & 0xffu) | ((*xl)[nid] << 8);
+      const size_t i = &x - out.data();
+      if (jt[i] == ~0u) continue;
+      static_assert((F_J64_EQ_I - F_J64_EQ_R) == 1 && (F_J32_SLE_I - F_J64_EQ_R) % 2 == 1,
+                    "jump handlers alternate register / immediate forms");
+      if (id != F_JA && (id - F_J64_EQ_R) % 2 == 1)
+        x.src_x2 = (*xl)[jt[i]];
+      else
+        x.imm = (int64_t)(*xl)[jt[i]];
     }
     FInsn *d = nullptr;
     const size_t bytes = out.size() * sizeof(FInsn);
