@@ -20,8 +20,9 @@ producer and consumer:
 
 Every instruction counts one wait state, `s_nop N` counts N + 1.  The check
 walks the control-flow graph backwards from each consumer over every path
-(fall-through, branches to labels, the dispatch table's entries after any
-s_setpc_b64), so a producer before a branch is seen from the branch target.
+(fall-through, branches to labels, every handler entry and divergent stub
+after any s_setpc_b64), so a producer before a branch is seen from the
+branch target.
 The block's entry is taken as a VALU write of every asm operand (%[name]:
 the compiler may have produced an "s" operand with v_readfirstlane right
 before the block) and its end as a VMEM read of them.  Index mode
@@ -152,14 +153,11 @@ def parse(lines: List[str]) -> Tuple[List[Insn], Dict[str, int]]:
         if t.startswith("s_set_gpr_idx_off"):
             idx_dst = idx_src = False
         insns.append(ins)
-    # the dispatch table: the s_branch entries right after `s_getpc_b64` and
-    # the branch around the table, reached through any s_setpc_b64
-    for k, ins in enumerate(insns):
-        if ins.mn == "s_getpc_b64":
-            j = k + 2
-            while j < len(insns) and insns[j].mn == "s_branch":
-                insns[j].is_table = True
-                j += 1
+    # direct dispatch: every handler's divergent stub (`.._d_<name>`) and
+    # the handler itself (`.._h_<name>`) are reached through any s_setpc_b64
+    for name, k in labels.items():
+        if re.search(r"_[dh]_[A-Z0-9_]+$", name) and k < len(insns):
+            insns[k].is_table = True
     return insns, labels
 
 

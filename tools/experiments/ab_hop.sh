@@ -1,5 +1,6 @@
 #!/bin/bash
-# A/B of the dispatch table's branch hop (gen_fast.py BPFTIME_AMD_EXTRA_HOP):
+# A/B of the dispatch table's branch hop (gen_fast.py BPFTIME_AMD_EXTRA_HOP, at commit aabfa90:
+# the knob went with the table when dispatch became direct, 54c3d9e):
 # the default library against one built with a second branch per dispatch
 # (bpftime_amd/lib_hop), alternating, every line without CPU legs.
 set -o pipefail
